@@ -1,0 +1,48 @@
+# Builds the gfx950 checksum engine and the (test-only) CPU oracle.
+#   tcp_amd/libtcpcsum.so      product: HIP kernels + C ABI (include/tcpcsum.h)
+#   oracle/build/liboracle.so  test infrastructure: C restatement, -O2 -g
+#   oracle/build/liboracle_O0.so  same at -O0 -g (the reference Makefile's flags)
+#   tests/c/abi_smoke          C program that links the ABI (C-callable proof)
+ROCM ?= /opt/rocm
+HIPCC ?= $(ROCM)/bin/hipcc
+CC ?= gcc
+ARCH ?= gfx950
+HIPFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Wno-unused-parameter -Wno-unused-value -Wno-unused-result
+CFLAGS_LIB ?= -O2 -fPIC -Wall -Wextra
+
+LIB := tcp_amd/libtcpcsum.so
+HIP_SRCS := tcp_amd/csrc/tcpcsum_kernels.hip tcp_amd/csrc/tcpcsum_api.hip
+HDRS := include/tcpcsum.h tcp_amd/csrc/tcpcsum_internal.h
+OBJDIR := build/obj
+
+all: $(LIB) oracle tests/c/abi_smoke
+
+$(OBJDIR)/%.o: tcp_amd/csrc/%.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -Iinclude -c $< -o $@
+
+$(OBJDIR)/scalar_dropin.o: tcp_amd/csrc/scalar_dropin.c include/tcpcsum.h
+	@mkdir -p $(OBJDIR)
+	$(CC) $(CFLAGS_LIB) -Iinclude -c $< -o $@
+
+$(LIB): $(OBJDIR)/tcpcsum_kernels.o $(OBJDIR)/tcpcsum_api.o $(OBJDIR)/scalar_dropin.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@.tmp $^ -Wl,-soname,libtcpcsum.so
+	mv $@.tmp $@
+
+oracle: oracle/build/liboracle.so oracle/build/liboracle_O0.so
+
+oracle/build/liboracle.so: oracle/csum_oracle.c oracle/oracle.h oracle/cpu_bench.inc.c
+	@mkdir -p oracle/build
+	$(CC) -O2 -g -fPIC -shared -pthread -Wall -Wextra -o $@ $<
+
+oracle/build/liboracle_O0.so: oracle/csum_oracle.c oracle/oracle.h oracle/cpu_bench.inc.c
+	@mkdir -p oracle/build
+	$(CC) -O0 -g -fPIC -shared -pthread -Wall -Wextra -o $@ $<
+
+tests/c/abi_smoke: tests/c/abi_smoke.c include/tcpcsum.h $(LIB)
+	$(CC) -O2 -Wall -Wextra -Iinclude -o $@ $< -Ltcp_amd -ltcpcsum -Wl,-rpath,'$$ORIGIN/../../tcp_amd'
+
+clean:
+	rm -rf build oracle/build $(LIB) tests/c/abi_smoke
+
+.PHONY: all oracle clean

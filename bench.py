@@ -1,0 +1,273 @@
+#!/usr/bin/env python3
+"""bench.py — GiB/s checksummed (device-resident) on MI355X, bit-exact TCP checksum.
+
+BASELINE.json metric, measured on its configs[1]: 1M x 1500-byte synthetic
+segments per GPU (SURVEY.md Appendix B generator), inputs resident in HBM
+before the timed region. One step = one launch of the batch checksum
+(tcpcsum_batch_uniform_dev: /root/reference/context.c:104-145 for every segment
+of the batch) over the GPU's whole shard.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config 1500|64|64k]
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+Multi-GPU: one process per GPU, each owns a contiguous shard of segments
+(weak scaling: 1M segments per GPU; N=8 is BASELINE's 8M x 1500 config). No
+collective touches the data path; torch.distributed (RCCL) is used only for the
+barriers around the timed region and the max-over-ranks of its duration.
+
+Rank 0 prints one JSON line. ``roofline.achieved`` = algorithmic bytes per
+launch (segments x segment bytes) / the kernel's average duration, measured
+with HIP events on the stream the kernels are launched on. ``cpu_baseline``
+times the oracle's C restatement of the reference's scalar checksum on this
+host (rank 0, N=1 only), the only use of oracle/ in this file.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+METRIC = "GiB/s checksummed (device-resident), 1500B & 64KiB segment batches; bit-exact"
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+CONFIGS = {
+    # name: (segments per GPU, segment bytes, description)
+    "1500": (1 << 20, 1500, "1M x 1500-byte synthetic segments per GPU, device-resident"),
+    "64": (1 << 20, 64, "1M x 64-byte header-only segments per GPU, device-resident (L3-rotated)"),
+    "64k": (1 << 18, 65536, "256K x 64KiB jumbo segments per GPU, device-resident"),
+}
+
+
+def shard_range(total: int, world: int, rank: int) -> tuple[int, int]:
+    """Contiguous shard [s0, s0+cnt) of `total` segments for `rank` of `world`."""
+    s0 = total * rank // world
+    s1 = total * (rank + 1) // world
+    return s0, s1 - s0
+
+
+def dist_env() -> tuple[int, int, int]:
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def max_over_ranks(x: float, dist, device) -> float:
+    if dist is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def timed_region(step, steps: int, warmup: int, dist, sync, on_start=None, on_end=None) -> float:
+    """W untimed steps, then EXACTLY `steps` steps between barrier+sync on both sides.
+    on_start/on_end run right after/before the syncs (HIP event records).
+    Returns this rank's wall seconds for the timed steps."""
+    for _ in range(warmup):
+        step()
+    sync()
+    if dist is not None:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    if on_start:
+        on_start()
+    for _ in range(steps):
+        step()
+    if on_end:
+        on_end()
+    sync()
+    t1 = time.perf_counter()
+    if dist is not None:
+        dist.barrier()
+    return t1 - t0
+
+
+def load_traffic(config: str):
+    """HBM bytes per launch from the committed PMC summary (profiles/traffic.json), if present."""
+    p = os.path.join(REPO, "profiles", "traffic.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        v = d.get(config, {}).get("hbm_bytes_per_launch")
+        return float(v) if v is not None else None
+    except Exception:
+        return None
+
+
+def cpu_baseline(seg_len: int, seconds: float) -> dict:
+    """The reference's scalar checksum (C restatement, oracle/) on this host, bounded sample."""
+    import oracle
+    nseg = max(1, (96 << 20) // seg_len)   # ~96 MiB host-resident sample of the same workload
+    threads = min(16, os.cpu_count() or 1)
+    res = {}
+    for key, th, opt, secs in (("o2_all", threads, "O2", seconds * 0.4), ("o2_1", 1, "O2", seconds * 0.35),
+                               ("o0_1", 1, "O0", seconds * 0.25)):
+        gibs, _, passes = oracle.cpu_bench(th, seg_len, nseg, secs, opt)
+        res[key] = (gibs, th, passes)
+    gibs, th, _ = res["o2_all"]
+    return {
+        "value": round(gibs, 3), "unit": "GiB/s", "cores": th, "kind": "port",
+        "sample": f"{nseg} x {seg_len}-byte segments (Appendix B stream, host-resident), gcc -O2, "
+                  f"{th} pthreads, best pass of >=3 over ~{seconds * 0.4:.0f}s",
+        "single_core_O2": round(res["o2_1"][0], 3),
+        "single_core_O0_makefile_flags": round(res["o0_1"][0], 3),
+    }
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="1500")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--probe", action="store_true", help="also time the read-only stream probe")
+    ap.add_argument("--max-blocks", type=int, default=0)
+    ap.add_argument("--unroll", type=int, default=0)
+    args = ap.parse_args(argv)
+
+    import numpy as np
+    import torch
+    import tcp_amd
+
+    rank, world, local = dist_env()
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            print("bench.py: --gpus > 1 needs torch.distributed.run with one process per GPU", file=sys.stderr)
+            return 2
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as tdist
+        tdist.init_process_group("nccl", device_id=device)
+        dist = tdist
+    rc, arch = tcp_amd.device_check()
+    if rc != 0:
+        raise SystemExit(f"bench.py: no usable gfx950 device ({rc}, '{arch}')")
+    tcp_amd.set_tuning(args.max_blocks, args.unroll)
+
+    per_gpu, L, desc = CONFIGS[args.config]
+    total = per_gpu * world
+    s0, cnt = shard_range(total, world, rank)
+    batch_bytes = cnt * L
+    # Batches under ~1 GiB would be served from the 256 MiB Infinity Cache on
+    # repeat launches; rotate enough distinct batches that every launch reads HBM.
+    rot = max(1, math.ceil((1 << 30) / batch_bytes)) if batch_bytes < (1 << 30) else 1
+    stream = torch.cuda.current_stream()
+    bufs, sss = [], []
+    for r in range(rot):
+        data = torch.empty(batch_bytes, dtype=torch.uint8, device=device)
+        ss = torch.empty(cnt, dtype=torch.int32, device=device)
+        # rotation r holds the same segment indices with the stream bytes of a later block
+        tcp_amd.synth_fill(data, (s0 + r * total) * L, batch_bytes)
+        tcp_amd.synth_pseudo(ss, s0, cnt, L)
+        bufs.append(data)
+        sss.append(ss)
+    out = torch.empty(cnt, dtype=torch.int16, device=device)
+    torch.cuda.synchronize()
+
+    # Sanity (not a parity test — tests/ does that): rotation 0 of each shard is
+    # exactly the Appendix B batch whose digest the reference produced.
+    tcp_amd.batch_uniform(bufs[0], L, L, cnt, sss[0], out=out)
+    torch.cuda.synchronize()
+    res = out.cpu().numpy().view(np.uint16)
+    check = None
+    try:
+        gold = json.load(open(os.path.join(REPO, "tests", "golden", "reference_vectors.json")))["digests"]
+        key = {("1500", 1): "1Mx1500", ("64", 1): "1Mx64", ("64k", 1): "256Kx64KiB"}.get((args.config, world))
+        if args.config == "1500" and world == 8:
+            key = f"8Mx1500_shard{rank}"
+        elif args.config == "1500" and world > 1 and per_gpu == 1 << 20:
+            key = f"8Mx1500_shard{rank}" if rank < 8 else None
+        if key:
+            g = gold[key]
+            check = bool(int(res.astype(np.uint64).sum()) == g["sum"]
+                         and f"{int(np.bitwise_xor.reduce(res)):04x}" == g["xor"]
+                         and [f"{v:04x}" for v in res[:4]] == g["first4"] and f"{res[-1]:04x}" == g["last"])
+    except Exception:
+        check = None
+
+    k = [0]
+
+    def step():
+        r = k[0] % rot
+        k[0] += 1
+        tcp_amd.batch_uniform(bufs[r], L, L, cnt, sss[r], out=out)
+
+    # HIP events on the launch stream bracket the kernels of the timed region
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    wall = timed_region(step, args.steps, args.warmup, dist, torch.cuda.synchronize,
+                        on_start=lambda: ev0.record(stream), on_end=lambda: ev1.record(stream))
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps
+    wall_max = max_over_ranks(wall, dist, device)
+    kernel_ms_max = max_over_ranks(kernel_ms, dist, device)
+
+    probe = None
+    if args.probe:
+        pout = torch.zeros(1, dtype=torch.int64, device=device)
+        nb = (batch_bytes // 16) * 16
+        for _ in range(3):
+            tcp_amd.stream_probe(bufs[0], nb, pout)
+        torch.cuda.synchronize()
+        pe0, pe1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        pe0.record(stream)
+        for i in range(args.steps):
+            tcp_amd.stream_probe(bufs[i % rot], nb, pout)
+        pe1.record(stream)
+        torch.cuda.synchronize()
+        pms = pe0.elapsed_time(pe1) / args.steps
+        probe = {"kernel": "k_probe (read-only 16-B stream, same access shape)", "avg_ms": round(pms, 5),
+                 "GB/s": round(nb / (pms * 1e-3) / 1e9, 1)}
+
+    if rank == 0:
+        total_bytes = batch_bytes * world * args.steps
+        value = total_bytes / wall_max / (1 << 30)
+        achieved = batch_bytes / (kernel_ms * 1e-3) / 1e9   # rank 0's kernel, GB/s
+        traffic = load_traffic(args.config)
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(wall_max * 1e3 / args.steps, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u16",
+            "data": "synthetic (SURVEY.md Appendix B generator, generated in HBM before timing)",
+            "config": {"workload": desc, "segments_per_gpu": cnt, "segment_bytes": L,
+                       "parallelism": f"shard{world} (contiguous segment ranges, no collective)",
+                       "rotating_batches": rot, "arch": arch},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic,
+                         "kernel": "tcpcsum::k_uniform (tcpcsum_batch_uniform_dev)",
+                         "kernel_avg_ms": round(kernel_ms, 5), "kernel_avg_ms_max_rank": round(kernel_ms_max, 5),
+                         "algorithmic_bytes_per_launch": batch_bytes},
+            "digest_check": check,
+        }
+        if probe:
+            line["stream_probe"] = probe
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(L, args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

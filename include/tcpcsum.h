@@ -1,0 +1,177 @@
+/*
+ * tcpcsum.h — C ABI of the MI355X (gfx950) TCP checksum engine.
+ *
+ * Drop-in boundary for the one per-byte hot path of uNetworking/tcp: the
+ * 16-bit one's-complement TCP checksum that the reference computes per
+ * outgoing segment in
+ *     /root/reference/context.c:104-119  getPseudoHeaderSum
+ *     /root/reference/context.c:121-145  csum_continue
+ *     /root/reference/context.c:208-209  the single call site (send_packet)
+ * and flushes in batches of <= 1024 IP packets at
+ *     /root/reference/loop.c:27-94       releaseSend -> sendmmsg (loop.c:75)
+ *
+ * Every batch entry point computes, per segment, exactly
+ *     csum_continue(sum_start, segment, nbytes)
+ * bit for bit (exact 64-bit sum, the reference's two folds, 16-bit
+ * complement, odd trailing byte as the low byte of a zeroed word).
+ *
+ * Conventions
+ *   - Plain C: pointers, sizes, integer status codes; no C++ or torch types.
+ *   - "stream" is a hipStream_t passed as void* (NULL = the default stream).
+ *     Batch calls are asynchronous on that stream; the caller synchronises.
+ *   - d_* pointers are device (or device-accessible) memory; h_* are host.
+ *   - Return 0 on success or a negative TCPCSUM_E* code. No global state
+ *     beyond what tcpcsum_ctx_* owns; no call keeps a pointer after it returns
+ *     (async calls: until the stream reaches that point).
+ *   - The caller owns every buffer.
+ *   - The batch API covers sum_start < 2^32 (getPseudoHeaderSum returns at
+ *     most 6 * 0xFFFF) and segment lengths <= INT32_MAX (csum_continue's
+ *     nbytes is an int).
+ */
+#ifndef TCPCSUM_H
+#define TCPCSUM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TCPCSUM_OK 0
+#define TCPCSUM_EINVAL (-1)   /* bad argument */
+#define TCPCSUM_ENODEV (-2)   /* no usable gfx950 device / HIP runtime */
+#define TCPCSUM_EHIP (-3)     /* a HIP call failed (tcpcsum_last_hip_error) */
+#define TCPCSUM_ENOMEM (-4)   /* allocation failed */
+
+#define TCPCSUM_ABI_VERSION 1
+
+/* Ragged-batch descriptor: segment = d_base[offset .. offset+len). 16 bytes. */
+typedef struct tcpcsum_desc {
+    uint64_t offset;
+    uint32_t len;
+    uint32_t sum_start; /* pseudo-header sum (tcpcsum_pseudo) or any start value */
+} tcpcsum_desc_t;
+
+/* Wire-batch modes (tcpcsum_ipv4_batch_dev). */
+#define TCPCSUM_IPV4_FILL 0   /* tx: checksum with check=0, store it at TCP+16 */
+#define TCPCSUM_IPV4_VERIFY 1 /* rx: checksum incl. check; 0 means the segment verifies */
+
+/* Wire-batch per-packet status. */
+#define TCPCSUM_PKT_OK 0
+#define TCPCSUM_PKT_SKIPPED 1 /* not IPv4/TCP, ihl < 5, or tot_len outside [ihl*4+20, cap] */
+
+/* ---------------------------------------------------------------- library */
+int tcpcsum_abi_version(void);
+const char *tcpcsum_strerror(int code);
+int tcpcsum_last_hip_error(void);      /* hipError_t of the last failing HIP call */
+/* 0 if a gfx950 device is usable; TCPCSUM_ENODEV otherwise. Fills the name
+ * of the current device's gfx arch into arch (may be NULL). */
+int tcpcsum_device_check(char *arch, size_t arch_len);
+
+/* ------------------------------------------------------ scalar drop-ins
+ * Synchronous, reference-identical per-segment helpers for code that needs a
+ * single result immediately (e.g. the SYN-ACK retransmit at context.c:94).
+ * They run on the calling CPU thread; they are NOT used by any batch entry
+ * point below, which always run on the GPU. */
+
+/* == getPseudoHeaderSum, context.c:104-119. saddr/daddr in network order as
+ * stored in struct iphdr; len_be = htons(tcp header + payload length). */
+unsigned long tcpcsum_pseudo(uint32_t saddr_be, uint32_t daddr_be, uint16_t len_be);
+
+/* == csum_continue, context.c:121-145. */
+unsigned short tcpcsum_continue(unsigned long sum_start, const char *p, int nbytes);
+
+/* ------------------------------------------------------ device batches (GPU) */
+
+/* Uniform layout: segment i = d_base[i*stride .. i*stride+len), i < n.
+ * Start value: d_sum_start[i] if d_sum_start != NULL, else sum_start.
+ * Result:      d_out[i] = csum_continue(start_i, segment_i, len).
+ * Replaces the per-packet call at context.c:208-209 for a whole batch. */
+int tcpcsum_batch_uniform_dev(const void *d_base, uint64_t stride, uint32_t len,
+                              const uint32_t *d_sum_start, uint32_t sum_start,
+                              uint16_t *d_out, uint64_t n, void *stream);
+
+/* Ragged layout: segment i = d_base[d_desc[i].offset .. +d_desc[i].len).
+ * max_len: an upper bound on every d_desc[i].len (picks the kernel shape;
+ * segments longer than max_len are still summed correctly, only slower).
+ * d_out[i] = csum_continue(d_desc[i].sum_start, segment_i, d_desc[i].len). */
+int tcpcsum_batch_desc_dev(const void *d_base, const tcpcsum_desc_t *d_desc, uint64_t n,
+                           uint32_t max_len, uint16_t *d_out, void *stream);
+
+/* Wire layout (the loop's out-buffers, loop.c:107-116 / releaseSend
+ * loop.c:27-94): packet i is a raw IPv4 packet at d_pkts + d_pkt_off[i], of
+ * at most cap bytes. The pseudo header comes from the IP header (saddr @12,
+ * daddr @16, tcp length = tot_len - ihl*4), the TCP segment starts at ihl*4.
+ *   FILL:   the sum is taken with the check field (TCP+16) as zero, as
+ *           context.c:182 leaves it; the result is stored at TCP+16 in place
+ *           (and in d_out[i] when d_out != NULL).
+ *   VERIFY: d_out[i] = csum over the segment including check (0 == valid).
+ * d_status[i] (may be NULL) = TCPCSUM_PKT_OK or TCPCSUM_PKT_SKIPPED; skipped
+ * packets are left untouched and d_out[i] = 0. */
+int tcpcsum_ipv4_batch_dev(void *d_pkts, const uint64_t *d_pkt_off, uint64_t n, uint32_t cap,
+                           int mode, uint16_t *d_out, uint8_t *d_status, void *stream);
+
+/* ------------------------------------------------------ host-memory batches
+ * The path as the reference sees it: segments start and end in host memory
+ * (raw-socket buffers). A context owns one device, pinned staging and device
+ * scratch, and pipelines H2D copy, checksum and D2H copy in chunks. */
+typedef struct tcpcsum_ctx tcpcsum_ctx_t;
+
+/* scratch_bytes: device staging size per pipeline slot (0 = 64 MiB). */
+int tcpcsum_ctx_create(int device, size_t scratch_bytes, tcpcsum_ctx_t **out);
+void tcpcsum_ctx_destroy(tcpcsum_ctx_t *ctx);
+
+/* Page-locked host memory for packet pools: copies from it are plain DMA
+ * (pageable memory is staged by the runtime). NULL on failure. */
+void *tcpcsum_host_alloc(size_t bytes);
+void tcpcsum_host_free(void *p);
+
+/* Uniform layout in host memory; h_out[i] as tcpcsum_batch_uniform_dev.
+ * h_sum_start may be NULL (then sum_start is used for every segment).
+ * Synchronous: returns when h_out is complete. */
+int tcpcsum_batch_uniform_host(tcpcsum_ctx_t *ctx, const void *h_base, uint64_t stride,
+                               uint32_t len, const uint32_t *h_sum_start, uint32_t sum_start,
+                               uint16_t *h_out, uint64_t n);
+
+/* Wire layout in host memory: n packets at h_pkts + h_pkt_off[i] (offsets
+ * within one host region of region_bytes). FILL patches check in place in
+ * host memory. Synchronous. */
+int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t *ctx, void *h_pkts, size_t region_bytes,
+                            const uint64_t *h_pkt_off, uint64_t n, uint32_t cap, int mode,
+                            uint16_t *h_out, uint8_t *h_status);
+
+/* ------------------------------------------------------ synthetic workload
+ * Device-side generation of the SURVEY.md Appendix B batches, so benchmarks
+ * start with inputs already resident in HBM (no H2D in the timed region). */
+
+/* d_dst[k] = byte (off+k) of the Appendix B stream, k < nbytes. */
+int tcpcsum_synth_fill_dev(void *d_dst, uint64_t stream_off, uint64_t nbytes, void *stream);
+
+/* d_sum_start[k] = getPseudoHeaderSum(saddr(seg0+k), daddr(seg0+k), htons((u16)seg_len)). */
+int tcpcsum_synth_pseudo_dev(uint32_t *d_sum_start, uint64_t seg0, uint64_t n, uint32_t seg_len,
+                             void *stream);
+
+/* ------------------------------------------------------ measurement helpers */
+
+/* Read-only streaming probe: d_out[0] = sum of all u32 words of d_src
+ * (nbytes multiple of 16, d_src 16-B aligned). The chip's practical HBM read
+ * ceiling for this access pattern; reported beside the checksum kernel. */
+int tcpcsum_stream_probe_dev(const void *d_src, uint64_t nbytes, uint64_t *d_out, void *stream);
+
+/* Host-side planning only (no device work): the kernel the library would use
+ * for a uniform batch at device address base. mode: 0 = 16-B aligned, 1 =
+ * 4-B aligned, 2 = byte-granular; shape: 0..8 = lane-group shapes covering
+ * 4,8,16,32,64,96,128,256,512 chunks, 9 = one wave per long segment;
+ * unroll: segments in flight per lane group. */
+int tcpcsum_plan_uniform(uint64_t base, uint64_t stride, uint32_t len, uint64_t n, int *mode,
+                         int *shape, int *unroll);
+
+/* Launch-shape override for tuning (0 = built-in default). Affects batch
+ * calls issued afterwards from any thread. */
+int tcpcsum_set_tuning(int max_blocks, int unroll);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TCPCSUM_H */

@@ -1,0 +1,44 @@
+"""tcp_amd — MI355X-native (gfx950) TCP checksum engine for uNetworking/tcp's hot path.
+
+This package is the Python front end of ``libtcpcsum.so`` (C ABI:
+``include/tcpcsum.h``). The checksum itself runs only in the library's HIP
+kernels; nothing here computes a checksum. If the library is missing, every
+entry point raises — there is no fallback.
+
+Reference path (``/root/reference``):
+  * ``context.c:104-119`` getPseudoHeaderSum -> :func:`getPseudoHeaderSum`
+  * ``context.c:121-145`` csum_continue      -> :func:`csum_continue` (scalar) and
+    the batch entry points (:func:`batch_uniform`, :func:`batch_desc`,
+    :func:`ipv4_batch`) that replace the per-packet call at ``context.c:208-209``
+    with one GPU launch per batch (the ``releaseSend`` seam, ``loop.c:27-94``).
+"""
+from __future__ import annotations
+
+from .api import (  # noqa: F401
+    DESC_DTYPE,
+    IPV4_FILL,
+    IPV4_VERIFY,
+    PKT_OK,
+    PKT_SKIPPED,
+    TcpCsumError,
+    HostContext,
+    batch_desc,
+    batch_uniform,
+    csum_continue,
+    device_check,
+    getPseudoHeaderSum,
+    ipv4_batch,
+    lib,
+    lib_path,
+    set_tuning,
+    stream_probe,
+    synth_fill,
+    synth_pseudo,
+)
+
+__all__ = [
+    "DESC_DTYPE", "IPV4_FILL", "IPV4_VERIFY", "PKT_OK", "PKT_SKIPPED", "TcpCsumError",
+    "HostContext", "batch_desc", "batch_uniform", "csum_continue", "device_check",
+    "getPseudoHeaderSum", "ipv4_batch", "lib", "lib_path", "set_tuning", "stream_probe",
+    "synth_fill", "synth_pseudo",
+]

@@ -1,0 +1,287 @@
+"""ctypes bindings of include/tcpcsum.h and torch-tensor conveniences.
+
+Device buffers are torch tensors on ``cuda`` (HIP); kernels are launched on
+``torch.cuda.current_stream()`` unless a stream is given, so torch events and
+synchronisation see them. torch is imported before the library is loaded so
+that both use the one HIP runtime already in the process (torch ships a
+``libamdhip64.so.7`` with the same SONAME the library links against).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Optional
+
+import numpy as np
+
+try:  # torch first: its HIP runtime must be the one the library binds to
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is always present in this image
+    torch = None
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_NAME = "libtcpcsum.so"
+
+OK = 0
+EINVAL = -1
+ENODEV = -2
+EHIP = -3
+ENOMEM = -4
+IPV4_FILL = 0
+IPV4_VERIFY = 1
+PKT_OK = 0
+PKT_SKIPPED = 1
+
+# tcpcsum_desc_t {u64 offset; u32 len; u32 sum_start}
+DESC_DTYPE = np.dtype([("offset", "<u8"), ("len", "<u4"), ("sum_start", "<u4")])
+
+_ERRNAMES = {EINVAL: "EINVAL", ENODEV: "ENODEV", EHIP: "EHIP", ENOMEM: "ENOMEM"}
+
+
+class TcpCsumError(RuntimeError):
+    def __init__(self, code: int, where: str):
+        self.code = code
+        msg = f"{where}: {_ERRNAMES.get(code, code)}"
+        try:
+            msg += f" ({lib().tcpcsum_strerror(code).decode()})"
+            if code == EHIP:
+                msg += f" hipError={lib().tcpcsum_last_hip_error()}"
+        except Exception:
+            pass
+        super().__init__(msg)
+
+
+_lib = None
+_lock = threading.Lock()
+
+c_u8p = ctypes.POINTER(ctypes.c_uint8)
+c_u16p = ctypes.POINTER(ctypes.c_uint16)
+c_u32p = ctypes.POINTER(ctypes.c_uint32)
+c_u64p = ctypes.POINTER(ctypes.c_uint64)
+vp = ctypes.c_void_p
+u32 = ctypes.c_uint32
+u64 = ctypes.c_uint64
+
+# name -> (restype, argtypes); must cover every function in include/tcpcsum.h
+SIGNATURES = {
+    "tcpcsum_abi_version": (ctypes.c_int, []),
+    "tcpcsum_strerror": (ctypes.c_char_p, [ctypes.c_int]),
+    "tcpcsum_last_hip_error": (ctypes.c_int, []),
+    "tcpcsum_device_check": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t]),
+    "tcpcsum_pseudo": (ctypes.c_ulong, [u32, u32, ctypes.c_uint16]),
+    "tcpcsum_continue": (ctypes.c_ushort, [ctypes.c_ulong, ctypes.c_char_p, ctypes.c_int]),
+    "tcpcsum_batch_uniform_dev": (ctypes.c_int, [vp, u64, u32, vp, u32, vp, u64, vp]),
+    "tcpcsum_batch_desc_dev": (ctypes.c_int, [vp, vp, u64, u32, vp, vp]),
+    "tcpcsum_ipv4_batch_dev": (ctypes.c_int, [vp, vp, u64, u32, ctypes.c_int, vp, vp, vp]),
+    "tcpcsum_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_size_t, ctypes.POINTER(vp)]),
+    "tcpcsum_ctx_destroy": (None, [vp]),
+    "tcpcsum_host_alloc": (vp, [ctypes.c_size_t]),
+    "tcpcsum_host_free": (None, [vp]),
+    "tcpcsum_batch_uniform_host": (ctypes.c_int, [vp, vp, u64, u32, vp, u32, vp, u64]),
+    "tcpcsum_ipv4_batch_host": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp, u64, u32, ctypes.c_int, vp, vp]),
+    "tcpcsum_synth_fill_dev": (ctypes.c_int, [vp, u64, u64, vp]),
+    "tcpcsum_synth_pseudo_dev": (ctypes.c_int, [vp, u64, u64, u32, vp]),
+    "tcpcsum_stream_probe_dev": (ctypes.c_int, [vp, u64, vp, vp]),
+    "tcpcsum_set_tuning": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    "tcpcsum_plan_uniform": (ctypes.c_int, [u64, u64, u32, u64, ctypes.POINTER(ctypes.c_int),
+                                            ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+}
+
+
+def lib_path() -> str:
+    return os.environ.get("TCPCSUM_LIB", os.path.join(_HERE, _LIB_NAME))
+
+
+def lib() -> ctypes.CDLL:
+    """Load libtcpcsum.so (raises if it is missing: there is no CPU fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            path = lib_path()
+            if not os.path.exists(path):
+                raise ImportError(
+                    f"tcp_amd: {path} not found — build it with `make` (or __graft_entry__.build()); "
+                    "the checksum path has no CPU fallback")
+            L = ctypes.CDLL(path)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = L
+    return _lib
+
+
+def _check(rc: int, where: str) -> None:
+    if rc != OK:
+        raise TcpCsumError(rc, where)
+
+
+# ------------------------------------------------------------------ scalar
+def getPseudoHeaderSum(saddr: int, daddr: int, tcpLength: int) -> int:
+    """context.c:104-119: saddr/daddr in network order (as in struct iphdr), tcpLength = htons(len)."""
+    return int(lib().tcpcsum_pseudo(saddr & 0xFFFFFFFF, daddr & 0xFFFFFFFF, tcpLength & 0xFFFF))
+
+
+def csum_continue(sumStart: int, p: bytes, nbytes: Optional[int] = None) -> int:
+    """context.c:121-145, synchronous scalar form (one segment, calling thread)."""
+    if nbytes is None:
+        nbytes = len(p)
+    if nbytes > len(p):
+        raise ValueError("nbytes exceeds buffer")
+    return int(lib().tcpcsum_continue(sumStart & 0xFFFFFFFFFFFFFFFF, bytes(p), int(nbytes)))
+
+
+def device_check() -> tuple[int, str]:
+    buf = ctypes.create_string_buffer(64)
+    rc = lib().tcpcsum_device_check(buf, 64)
+    return rc, buf.value.decode()
+
+
+def set_tuning(max_blocks: int = 0, unroll: int = 0) -> None:
+    _check(lib().tcpcsum_set_tuning(int(max_blocks), int(unroll)), "tcpcsum_set_tuning")
+
+
+def plan_uniform(base_addr: int, stride: int, length: int, n: int) -> tuple[int, int, int]:
+    """(mode, shape, unroll) the library picks for a uniform batch — host logic only."""
+    mode, shape, unroll = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    _check(lib().tcpcsum_plan_uniform(base_addr, stride, length, n, ctypes.byref(mode), ctypes.byref(shape),
+                                      ctypes.byref(unroll)), "tcpcsum_plan_uniform")
+    return mode.value, shape.value, unroll.value
+
+
+# ------------------------------------------------------------------ device batches (torch tensors)
+def _stream_handle(stream) -> int:
+    if stream is None:
+        return torch.cuda.current_stream().cuda_stream
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream
+
+
+def _dev_ptr(t, what: str) -> int:
+    if t is None:
+        return 0
+    if not t.is_cuda:
+        raise ValueError(f"{what} must be a device tensor")
+    return t.data_ptr()
+
+
+def batch_uniform(data, stride: int, length: int, n: int, sum_start=0, out=None, offset: int = 0,
+                  stream=None):
+    """d_out[i] = csum_continue(start_i, data[offset+i*stride : +length], length) on the GPU.
+
+    ``sum_start``: an int (same start for every segment) or a device int32 tensor of n entries.
+    Returns ``out`` (device int16 tensor holding the u16 results)."""
+    if out is None:
+        out = torch.empty(n, dtype=torch.int16, device=data.device)
+    if n:
+        last = offset + (n - 1) * stride + length
+        if last > data.numel() * data.element_size():
+            raise ValueError("batch runs past the end of data")
+    if isinstance(sum_start, int):
+        ss_ptr, ss0 = 0, sum_start
+    else:
+        if sum_start.numel() < n:
+            raise ValueError("sum_start too short")
+        ss_ptr, ss0 = _dev_ptr(sum_start, "sum_start"), 0
+    rc = lib().tcpcsum_batch_uniform_dev(_dev_ptr(data, "data") + offset, stride, length, ss_ptr, ss0,
+                                         _dev_ptr(out, "out"), n, _stream_handle(stream))
+    _check(rc, "tcpcsum_batch_uniform_dev")
+    return out
+
+
+def batch_desc(data, desc, n: int, max_len: int, out=None, stream=None):
+    """Ragged batch; ``desc`` is a device uint8/int64 tensor holding n tcpcsum_desc_t records."""
+    if out is None:
+        out = torch.empty(n, dtype=torch.int16, device=data.device)
+    rc = lib().tcpcsum_batch_desc_dev(_dev_ptr(data, "data"), _dev_ptr(desc, "desc"), n, max_len,
+                                      _dev_ptr(out, "out"), _stream_handle(stream))
+    _check(rc, "tcpcsum_batch_desc_dev")
+    return out
+
+
+def ipv4_batch(pkts, pkt_off, n: int, cap: int, mode: int, out=None, status=None, stream=None):
+    rc = lib().tcpcsum_ipv4_batch_dev(_dev_ptr(pkts, "pkts"), _dev_ptr(pkt_off, "pkt_off"), n, cap, mode,
+                                      _dev_ptr(out, "out"), _dev_ptr(status, "status"), _stream_handle(stream))
+    _check(rc, "tcpcsum_ipv4_batch_dev")
+    return out, status
+
+
+def synth_fill(dst, stream_off: int, nbytes: int, dst_offset: int = 0, stream=None) -> None:
+    if dst_offset + nbytes > dst.numel() * dst.element_size():
+        raise ValueError("synth_fill past end of dst")
+    _check(lib().tcpcsum_synth_fill_dev(_dev_ptr(dst, "dst") + dst_offset, stream_off, nbytes,
+                                        _stream_handle(stream)), "tcpcsum_synth_fill_dev")
+
+
+def synth_pseudo(dst, seg0: int, n: int, seg_len: int, stream=None) -> None:
+    if n > dst.numel():
+        raise ValueError("synth_pseudo past end of dst")
+    _check(lib().tcpcsum_synth_pseudo_dev(_dev_ptr(dst, "dst"), seg0, n, seg_len, _stream_handle(stream)),
+           "tcpcsum_synth_pseudo_dev")
+
+
+def stream_probe(src, nbytes: int, out, stream=None) -> None:
+    _check(lib().tcpcsum_stream_probe_dev(_dev_ptr(src, "src"), nbytes, _dev_ptr(out, "out"),
+                                          _stream_handle(stream)), "tcpcsum_stream_probe_dev")
+
+
+# ------------------------------------------------------------------ host-memory batches
+def _np_ptr(a: Optional[np.ndarray]) -> int:
+    return 0 if a is None else a.ctypes.data
+
+
+class HostContext:
+    """tcpcsum_ctx_t: host-memory batches (H2D -> kernel -> D2H), synchronous."""
+
+    def __init__(self, device: int = 0, scratch_bytes: int = 0):
+        h = vp()
+        _check(lib().tcpcsum_ctx_create(device, scratch_bytes, ctypes.byref(h)), "tcpcsum_ctx_create")
+        self._h = h
+
+    def close(self) -> None:
+        if self._h:
+            lib().tcpcsum_ctx_destroy(self._h)
+            self._h = vp()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def batch_uniform(self, data: np.ndarray, stride: int, length: int, n: int, sum_start=0,
+                      offset: int = 0) -> np.ndarray:
+        data = np.ascontiguousarray(data).view(np.uint8)
+        if n and offset + (n - 1) * stride + length > data.nbytes:
+            raise ValueError("batch runs past the end of data")
+        out = np.empty(n, np.uint16)
+        if isinstance(sum_start, (int, np.integer)):
+            ss, ss0 = None, int(sum_start)
+        else:
+            ss, ss0 = np.ascontiguousarray(sum_start, np.uint32), 0
+        rc = lib().tcpcsum_batch_uniform_host(self._h, data.ctypes.data + offset, stride, length, _np_ptr(ss), ss0,
+                                              out.ctypes.data, n)
+        _check(rc, "tcpcsum_batch_uniform_host")
+        return out
+
+    def ipv4_batch(self, region: np.ndarray, pkt_off: np.ndarray, cap: int, mode: int):
+        """region: writable uint8 array holding the packets (FILL patches it in place)."""
+        assert region.dtype == np.uint8 and region.flags.c_contiguous and region.flags.writeable
+        off = np.ascontiguousarray(pkt_off, np.uint64)
+        n = off.size
+        out = np.empty(n, np.uint16)
+        status = np.empty(n, np.uint8)
+        rc = lib().tcpcsum_ipv4_batch_host(self._h, region.ctypes.data, region.nbytes, off.ctypes.data, n, cap,
+                                           mode, out.ctypes.data, status.ctypes.data)
+        _check(rc, "tcpcsum_ipv4_batch_host")
+        return out, status

@@ -1,0 +1,437 @@
+// tcpcsum_api.hip — the C ABI declared in include/tcpcsum.h.
+//
+// Argument checking, device checks, error mapping, the host-memory pipeline
+// (tcpcsum_ctx_*) and the synthetic-workload entry points. All checksum
+// arithmetic on the batch paths runs in the gfx950 kernels of
+// tcpcsum_kernels.hip; this file never computes a checksum itself.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <atomic>
+#include <climits>
+#include <mutex>
+#include <new>
+
+#include "tcpcsum.h"
+#include "tcpcsum_internal.h"
+
+namespace {
+
+std::atomic<int> g_last_hip_error{0};
+std::atomic<int> g_max_blocks{0};
+std::atomic<int> g_unroll{0};
+
+constexpr int kMaxDevices = 64;
+std::atomic<int> g_dev_ok[kMaxDevices];   // 0 unknown, 1 gfx950, -1 unusable
+
+int hip_fail(hipError_t e) {
+    g_last_hip_error.store((int)e);
+    return TCPCSUM_EHIP;
+}
+
+tcpcsum::Tuning tuning() {
+    tcpcsum::Tuning t;
+    t.max_blocks = g_max_blocks.load(std::memory_order_relaxed);
+    t.unroll = g_unroll.load(std::memory_order_relaxed);
+    return t;
+}
+
+// The current device must be a gfx950 (the only code object in this library).
+int require_device(char* arch, size_t arch_len) {
+    int dev = -1;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess || dev < 0) {
+        g_last_hip_error.store((int)e);
+        return TCPCSUM_ENODEV;
+    }
+    if (dev < kMaxDevices && !arch) {
+        const int v = g_dev_ok[dev].load(std::memory_order_relaxed);
+        if (v == 1) return TCPCSUM_OK;
+        if (v == -1) return TCPCSUM_ENODEV;
+    }
+    hipDeviceProp_t prop;
+    e = hipGetDeviceProperties(&prop, dev);
+    if (e != hipSuccess) {
+        g_last_hip_error.store((int)e);
+        return TCPCSUM_ENODEV;
+    }
+    if (arch && arch_len) {
+        strncpy(arch, prop.gcnArchName, arch_len - 1);
+        arch[arch_len - 1] = 0;
+    }
+    const bool ok = strncmp(prop.gcnArchName, "gfx950", 6) == 0;
+    if (dev < kMaxDevices) g_dev_ok[dev].store(ok ? 1 : -1);
+    return ok ? TCPCSUM_OK : TCPCSUM_ENODEV;
+}
+
+int check_launch() {
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? TCPCSUM_OK : hip_fail(e);
+}
+
+}  // namespace
+
+extern "C" {
+
+int tcpcsum_abi_version(void) { return TCPCSUM_ABI_VERSION; }
+
+const char* tcpcsum_strerror(int code) {
+    switch (code) {
+        case TCPCSUM_OK: return "ok";
+        case TCPCSUM_EINVAL: return "invalid argument";
+        case TCPCSUM_ENODEV: return "no usable gfx950 device";
+        case TCPCSUM_EHIP: return "HIP runtime error";
+        case TCPCSUM_ENOMEM: return "out of memory";
+        default: return "unknown error";
+    }
+}
+
+int tcpcsum_last_hip_error(void) { return g_last_hip_error.load(); }
+
+int tcpcsum_device_check(char* arch, size_t arch_len) {
+    int count = 0;
+    hipError_t e = hipGetDeviceCount(&count);
+    if (e != hipSuccess || count <= 0) {
+        g_last_hip_error.store((int)e);
+        if (arch && arch_len) arch[0] = 0;
+        return TCPCSUM_ENODEV;
+    }
+    return require_device(arch, arch_len);
+}
+
+int tcpcsum_set_tuning(int max_blocks, int unroll) {
+    if (max_blocks < 0 || !(unroll == 0 || unroll == 1 || unroll == 2 || unroll == 4)) return TCPCSUM_EINVAL;
+    g_max_blocks.store(max_blocks);
+    g_unroll.store(unroll);
+    return TCPCSUM_OK;
+}
+
+int tcpcsum_plan_uniform(uint64_t base, uint64_t stride, uint32_t len, uint64_t n, int* mode, int* shape,
+                         int* unroll) {
+    if (!mode || !shape || !unroll || len > (uint32_t)INT_MAX) return TCPCSUM_EINVAL;
+    const tcpcsum::UniformPlan p = tcpcsum::plan_uniform((uintptr_t)base, stride, len, n, g_unroll.load());
+    *mode = p.mode;
+    *shape = p.shape;
+    *unroll = p.unroll;
+    return TCPCSUM_OK;
+}
+
+int tcpcsum_batch_uniform_dev(const void* d_base, uint64_t stride, uint32_t len, const uint32_t* d_sum_start,
+                              uint32_t sum_start, uint16_t* d_out, uint64_t n, void* stream) {
+    if (n == 0) return TCPCSUM_OK;
+    if (!d_base || !d_out || len > (uint32_t)INT_MAX) return TCPCSUM_EINVAL;
+    int rc = require_device(nullptr, 0);
+    if (rc) return rc;
+    tcpcsum::launch_uniform((const uint8_t*)d_base, stride, len, d_sum_start, sum_start, d_out, n,
+                            (hipStream_t)stream, tuning());
+    return check_launch();
+}
+
+int tcpcsum_batch_desc_dev(const void* d_base, const tcpcsum_desc_t* d_desc, uint64_t n, uint32_t max_len,
+                           uint16_t* d_out, void* stream) {
+    if (n == 0) return TCPCSUM_OK;
+    if (!d_base || !d_desc || !d_out || max_len > (uint32_t)INT_MAX) return TCPCSUM_EINVAL;
+    if (((uintptr_t)d_desc) & 15u) return TCPCSUM_EINVAL;   // descriptors are read as one 16-B load
+    int rc = require_device(nullptr, 0);
+    if (rc) return rc;
+    tcpcsum::launch_desc((const uint8_t*)d_base, d_desc, n, max_len, d_out, (hipStream_t)stream, tuning());
+    return check_launch();
+}
+
+int tcpcsum_ipv4_batch_dev(void* d_pkts, const uint64_t* d_pkt_off, uint64_t n, uint32_t cap, int mode,
+                           uint16_t* d_out, uint8_t* d_status, void* stream) {
+    if (n == 0) return TCPCSUM_OK;
+    if (!d_pkts || !d_pkt_off || (mode != TCPCSUM_IPV4_FILL && mode != TCPCSUM_IPV4_VERIFY)) return TCPCSUM_EINVAL;
+    if (cap > 65535u) cap = 65535u;   // tot_len is a u16
+    int rc = require_device(nullptr, 0);
+    if (rc) return rc;
+    tcpcsum::launch_ipv4((uint8_t*)d_pkts, d_pkt_off, n, cap, UINT64_MAX, mode, d_out, d_status, (hipStream_t)stream,
+                         tuning());
+    return check_launch();
+}
+
+int tcpcsum_synth_fill_dev(void* d_dst, uint64_t stream_off, uint64_t nbytes, void* stream) {
+    if (nbytes == 0) return TCPCSUM_OK;
+    if (!d_dst) return TCPCSUM_EINVAL;
+    int rc = require_device(nullptr, 0);
+    if (rc) return rc;
+    tcpcsum::launch_synth_fill((uint8_t*)d_dst, stream_off, nbytes, (hipStream_t)stream);
+    return check_launch();
+}
+
+int tcpcsum_synth_pseudo_dev(uint32_t* d_sum_start, uint64_t seg0, uint64_t n, uint32_t seg_len, void* stream) {
+    if (n == 0) return TCPCSUM_OK;
+    if (!d_sum_start) return TCPCSUM_EINVAL;
+    int rc = require_device(nullptr, 0);
+    if (rc) return rc;
+    tcpcsum::launch_synth_pseudo(d_sum_start, seg0, n, seg_len, (hipStream_t)stream);
+    return check_launch();
+}
+
+int tcpcsum_stream_probe_dev(const void* d_src, uint64_t nbytes, uint64_t* d_out, void* stream) {
+    if (!d_src || !d_out || (nbytes & 15u) || (((uintptr_t)d_src) & 15u)) return TCPCSUM_EINVAL;
+    int rc = require_device(nullptr, 0);
+    if (rc) return rc;
+    hipError_t e = hipMemsetAsync(d_out, 0, sizeof(uint64_t), (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e);
+    tcpcsum::launch_probe((const uint8_t*)d_src, nbytes, d_out, (hipStream_t)stream, tuning());
+    return check_launch();
+}
+
+// ------------------------------------------------------------------ host path
+
+struct tcpcsum_ctx {
+    int device = 0;
+    size_t scratch = 0;
+    hipStream_t st[2] = {nullptr, nullptr};
+    uint8_t* d_buf[2] = {nullptr, nullptr};
+    size_t d_buf_bytes = 0;
+    uint32_t* d_ss[2] = {nullptr, nullptr};
+    uint16_t* d_out[2] = {nullptr, nullptr};
+    size_t d_seg_cap = 0;   // entries of d_ss / d_out per slot
+    // wire path
+    uint8_t* d_region = nullptr;
+    size_t d_region_bytes = 0;
+    uint64_t* d_off = nullptr;
+    uint16_t* d_wout = nullptr;
+    uint8_t* d_wstat = nullptr;
+    size_t d_pkt_cap = 0;
+    std::mutex mu;
+};
+
+namespace {
+
+void ctx_free_buffers(tcpcsum_ctx* c) {
+    for (int i = 0; i < 2; ++i) {
+        if (c->d_buf[i]) hipFree(c->d_buf[i]);
+        if (c->d_ss[i]) hipFree(c->d_ss[i]);
+        if (c->d_out[i]) hipFree(c->d_out[i]);
+        c->d_buf[i] = nullptr;
+        c->d_ss[i] = nullptr;
+        c->d_out[i] = nullptr;
+    }
+    c->d_buf_bytes = 0;
+    c->d_seg_cap = 0;
+}
+
+int ctx_ensure(tcpcsum_ctx* c, size_t buf_bytes, size_t segs) {
+    if (buf_bytes > c->d_buf_bytes || segs > c->d_seg_cap) {
+        for (int i = 0; i < 2; ++i) hipStreamSynchronize(c->st[i]);
+        const size_t nb = buf_bytes > c->d_buf_bytes ? buf_bytes : c->d_buf_bytes;
+        const size_t ns = segs > c->d_seg_cap ? segs : c->d_seg_cap;
+        ctx_free_buffers(c);
+        for (int i = 0; i < 2; ++i) {
+            hipError_t e = hipMalloc(&c->d_buf[i], nb);
+            if (e == hipSuccess) e = hipMalloc(&c->d_ss[i], ns * sizeof(uint32_t));
+            if (e == hipSuccess) e = hipMalloc(&c->d_out[i], ns * sizeof(uint16_t));
+            if (e != hipSuccess) {
+                ctx_free_buffers(c);
+                g_last_hip_error.store((int)e);
+                return TCPCSUM_ENOMEM;
+            }
+        }
+        c->d_buf_bytes = nb;
+        c->d_seg_cap = ns;
+    }
+    return TCPCSUM_OK;
+}
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) hipSetDevice(prev);
+    }
+};
+
+}  // namespace
+
+int tcpcsum_ctx_create(int device, size_t scratch_bytes, tcpcsum_ctx_t** out) {
+    if (!out) return TCPCSUM_EINVAL;
+    *out = nullptr;
+    int count = 0;
+    hipError_t e = hipGetDeviceCount(&count);
+    if (e != hipSuccess || device < 0 || device >= count) {
+        g_last_hip_error.store((int)e);
+        return TCPCSUM_ENODEV;
+    }
+    DeviceGuard g(device);
+    int rc = require_device(nullptr, 0);
+    if (rc) return rc;
+    tcpcsum_ctx* c = new (std::nothrow) tcpcsum_ctx();
+    if (!c) return TCPCSUM_ENOMEM;
+    c->device = device;
+    c->scratch = scratch_bytes ? scratch_bytes : (64u << 20);
+    for (int i = 0; i < 2; ++i) {
+        e = hipStreamCreateWithFlags(&c->st[i], hipStreamNonBlocking);
+        if (e != hipSuccess) {
+            tcpcsum_ctx_destroy(c);
+            return hip_fail(e);
+        }
+    }
+    *out = c;
+    return TCPCSUM_OK;
+}
+
+void tcpcsum_ctx_destroy(tcpcsum_ctx_t* c) {
+    if (!c) return;
+    DeviceGuard g(c->device);
+    for (int i = 0; i < 2; ++i)
+        if (c->st[i]) hipStreamSynchronize(c->st[i]);
+    ctx_free_buffers(c);
+    if (c->d_region) hipFree(c->d_region);
+    if (c->d_off) hipFree(c->d_off);
+    if (c->d_wout) hipFree(c->d_wout);
+    if (c->d_wstat) hipFree(c->d_wstat);
+    for (int i = 0; i < 2; ++i)
+        if (c->st[i]) hipStreamDestroy(c->st[i]);
+    delete c;
+}
+
+void* tcpcsum_host_alloc(size_t bytes) {
+    void* p = nullptr;
+    if (!bytes) return nullptr;
+    hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        g_last_hip_error.store((int)e);
+        return nullptr;
+    }
+    return p;
+}
+
+void tcpcsum_host_free(void* p) {
+    if (p) hipHostFree(p);
+}
+
+// Chunks of segments alternate between two slots (stream + device buffers):
+// the H2D copy of chunk k+1 overlaps the kernel and D2H of chunk k.
+int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t stride, uint32_t len,
+                               const uint32_t* h_sum_start, uint32_t sum_start, uint16_t* h_out, uint64_t n) {
+    if (!c) return TCPCSUM_EINVAL;
+    if (n == 0) return TCPCSUM_OK;
+    if (!h_base || !h_out || len > (uint32_t)INT_MAX) return TCPCSUM_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    // segments per chunk: (cnt-1)*stride + len <= scratch (at least one segment)
+    uint64_t per = 1;
+    if (stride == 0) per = n;
+    else if (c->scratch > len) per = (c->scratch - len) / stride + 1;
+    if (per > n) per = n;
+    const uint64_t chunk_bytes = (per - 1) * stride + len;
+    int rc = ctx_ensure(c, (size_t)chunk_bytes + 16, (size_t)per);
+    if (rc) return rc;
+    const tcpcsum::Tuning tu = tuning();
+    uint64_t k = 0;
+    for (uint64_t s0 = 0; s0 < n; s0 += per, ++k) {
+        const int slot = (int)(k & 1);
+        hipStream_t st = c->st[slot];
+        const uint64_t cnt = (n - s0) < per ? (n - s0) : per;
+        const uint64_t bytes = (cnt - 1) * stride + len;
+        const uint8_t* src = (const uint8_t*)h_base + s0 * stride;
+        // keep the device-side start alignment mod 16 equal to the host's so the
+        // kernel shape matches what the same batch gets on device memory
+        const size_t mis = (uintptr_t)src & 15u;
+        hipError_t e = hipMemcpyAsync(c->d_buf[slot] + mis, src, bytes, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess && h_sum_start)
+            e = hipMemcpyAsync(c->d_ss[slot], h_sum_start + s0, cnt * sizeof(uint32_t), hipMemcpyHostToDevice, st);
+        if (e != hipSuccess) return hip_fail(e);
+        tcpcsum::launch_uniform(c->d_buf[slot] + mis, stride, len, h_sum_start ? c->d_ss[slot] : nullptr, sum_start,
+                                c->d_out[slot], cnt, st, tu);
+        rc = check_launch();
+        if (rc) return rc;
+        e = hipMemcpyAsync(h_out + s0, c->d_out[slot], cnt * sizeof(uint16_t), hipMemcpyDeviceToHost, st);
+        if (e != hipSuccess) return hip_fail(e);
+        // before slot is reused two chunks later, its previous work must be done
+        if (s0 + per < n) {
+            e = hipStreamSynchronize(c->st[slot ^ 1]);
+            if (e != hipSuccess) return hip_fail(e);
+        }
+    }
+    for (int i = 0; i < 2; ++i) {
+        hipError_t e = hipStreamSynchronize(c->st[i]);
+        if (e != hipSuccess) return hip_fail(e);
+    }
+    return TCPCSUM_OK;
+}
+
+int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t* c, void* h_pkts, size_t region_bytes, const uint64_t* h_pkt_off,
+                            uint64_t n, uint32_t cap, int mode, uint16_t* h_out, uint8_t* h_status) {
+    if (!c) return TCPCSUM_EINVAL;
+    if (n == 0) return TCPCSUM_OK;
+    if (!h_pkts || !h_pkt_off || !region_bytes || (mode != TCPCSUM_IPV4_FILL && mode != TCPCSUM_IPV4_VERIFY))
+        return TCPCSUM_EINVAL;
+    if (cap > 65535u) cap = 65535u;
+    // every packet (up to cap bytes, clipped to the region) must lie inside the region
+    for (uint64_t i = 0; i < n; ++i)
+        if (h_pkt_off[i] + 20u > region_bytes) return TCPCSUM_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    hipStream_t st = c->st[0];
+    const size_t mis = (uintptr_t)h_pkts & 15u;
+    const size_t need = region_bytes + mis + 65536u;   // slack: a packet's cap may run past the region end
+    hipError_t e = hipSuccess;
+    if (need > c->d_region_bytes) {
+        hipStreamSynchronize(st);
+        if (c->d_region) hipFree(c->d_region);
+        c->d_region = nullptr;
+        c->d_region_bytes = 0;
+        e = hipMalloc(&c->d_region, need);
+        if (e != hipSuccess) { g_last_hip_error.store((int)e); return TCPCSUM_ENOMEM; }
+        c->d_region_bytes = need;
+    }
+    if (n > c->d_pkt_cap) {
+        hipStreamSynchronize(st);
+        if (c->d_off) hipFree(c->d_off);
+        if (c->d_wout) hipFree(c->d_wout);
+        if (c->d_wstat) hipFree(c->d_wstat);
+        c->d_off = nullptr; c->d_wout = nullptr; c->d_wstat = nullptr; c->d_pkt_cap = 0;
+        e = hipMalloc(&c->d_off, n * sizeof(uint64_t));
+        if (e == hipSuccess) e = hipMalloc(&c->d_wout, n * sizeof(uint16_t));
+        if (e == hipSuccess) e = hipMalloc(&c->d_wstat, n);
+        if (e != hipSuccess) { g_last_hip_error.store((int)e); return TCPCSUM_ENOMEM; }
+        c->d_pkt_cap = n;
+    }
+    // zero the slack so a malformed tot_len past the region reads zeros, not stale bytes
+    e = hipMemsetAsync(c->d_region + mis + region_bytes, 0, 65536u, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(c->d_region + mis, h_pkts, region_bytes, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(c->d_off, h_pkt_off, n * sizeof(uint64_t), hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) return hip_fail(e);
+    // packets whose tot_len runs past the region end are SKIPPED by the kernel
+    tcpcsum::launch_ipv4(c->d_region + mis, c->d_off, n, cap, (uint64_t)region_bytes, mode, c->d_wout, c->d_wstat, st, tuning());
+    int rc = check_launch();
+    if (rc) return rc;
+    uint16_t* out = h_out;
+    uint8_t* stat = h_status;
+    // FILL needs out+status on the host to patch checks in place
+    uint16_t* tmp_out = nullptr;
+    uint8_t* tmp_stat = nullptr;
+    if (mode == TCPCSUM_IPV4_FILL) {
+        if (!out) out = tmp_out = new (std::nothrow) uint16_t[n];
+        if (!stat) stat = tmp_stat = new (std::nothrow) uint8_t[n];
+        if (!out || !stat) { delete[] tmp_out; delete[] tmp_stat; return TCPCSUM_ENOMEM; }
+    }
+    if (out) e = hipMemcpyAsync(out, c->d_wout, n * sizeof(uint16_t), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess && stat) e = hipMemcpyAsync(stat, c->d_wstat, n, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) { delete[] tmp_out; delete[] tmp_stat; return hip_fail(e); }
+    if (mode == TCPCSUM_IPV4_FILL) {
+        // store each result at TCP+16 (native u16, as context.c:208) — no arithmetic here
+        uint8_t* base = (uint8_t*)h_pkts;
+        for (uint64_t i = 0; i < n; ++i) {
+            if (stat[i] != TCPCSUM_PKT_OK) continue;
+            uint8_t* ip = base + h_pkt_off[i];
+            uint8_t* tcp = ip + (ip[0] & 15u) * 4u;
+            memcpy(tcp + 16, &out[i], 2);
+        }
+    }
+    delete[] tmp_out;
+    delete[] tmp_stat;
+    return TCPCSUM_OK;
+}
+
+}  // extern "C"

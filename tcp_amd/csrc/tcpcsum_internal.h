@@ -1,0 +1,37 @@
+// tcpcsum_internal.h — launchers shared between the kernel TU and the C ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "tcpcsum.h"
+
+namespace tcpcsum {
+
+// 256 CUs x 8 workgroups of 256 threads = 32 waves per CU: the whole grid is
+// resident at once and grid-strides over the batch.
+constexpr int kDefaultMaxBlocks = 2048;
+
+struct Tuning {
+    int max_blocks = 0;   // 0 = kDefaultMaxBlocks
+    int unroll = 0;       // 0 = per-shape default; else 1, 2 or 4
+};
+
+struct UniformPlan {
+    int mode;     // 0: 16-B aligned starts/len, 1: 4-B aligned, 2: byte granular
+    int shape;    // 0..8 segment-group shapes, 9 = one wave per long segment
+    int unroll;   // segments in flight per lane group
+};
+UniformPlan plan_uniform(uintptr_t base, uint64_t stride, uint32_t len, uint64_t n, int unroll_override);
+
+void launch_uniform(const uint8_t* base, uint64_t stride, uint32_t len, const uint32_t* ss, uint32_t ss0,
+                    uint16_t* out, uint64_t n, hipStream_t s, const Tuning& tu);
+void launch_desc(const uint8_t* base, const tcpcsum_desc_t* d, uint64_t n, uint32_t max_len, uint16_t* out,
+                 hipStream_t s, const Tuning& tu);
+void launch_ipv4(uint8_t* pkts, const uint64_t* off, uint64_t n, uint32_t cap, uint64_t limit, int mode,
+                 uint16_t* out, uint8_t* status, hipStream_t s, const Tuning& tu);
+void launch_synth_fill(uint8_t* dst, uint64_t off, uint64_t nbytes, hipStream_t s);
+void launch_synth_pseudo(uint32_t* ss, uint64_t seg0, uint64_t n, uint32_t seg_len, hipStream_t s);
+void launch_probe(const uint8_t* src, uint64_t nbytes, uint64_t* out, hipStream_t s, const Tuning& tu);
+
+}  // namespace tcpcsum

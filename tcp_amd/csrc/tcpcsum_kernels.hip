@@ -1,0 +1,557 @@
+// tcpcsum_kernels.hip — gfx950 (MI355X / CDNA4) kernels for the TCP checksum
+// hot path of uNetworking/tcp (context.c:104-145, called at context.c:208-209).
+//
+// Arithmetic contract, for every segment:
+//   S   = sum_start + sum_{k < len} byte[k] * (k even ? 1 : 256)      (exact)
+//   s1  = (S >> 16) + (S & 0xffff);  s2 = s1 + (s1 >> 16);  out = ~s2 & 0xffff
+// The first line is csum_continue's loop (context.c:130-133) over native
+// little-endian u16 words plus its odd-byte rule (context.c:134-138: a trailing
+// byte sits at an even offset and is added as a low byte). The second line is
+// its fold (context.c:140-144). S is never reduced early, so results are bit
+// exact for every length, including sums >= 2^32 where the two-fold differs
+// from a full RFC 1071 fold.
+//
+// How the bytes are read (all kernels): a segment is covered by the 16-byte
+// aligned chunks that overlap it. Lanes of a "group" (G lanes per segment)
+// load consecutive chunks with one 16-B non-temporal load each
+// (global_load_dwordx4 nt), so every wave-instruction reads contiguous memory.
+// Bytes outside the segment are masked in registers. Per chunk the sum of its
+// four dwords' u16 halves is taken with v_sad_u16 (|a.lo-0| + |a.hi-0| + acc),
+// one VALU op per dword. Word parity is absolute-address parity; for a segment
+// starting at an odd address the relative even/odd roles swap, which is exact
+// with E = W - 256*O (W: sum of absolute-aligned words, O: sum of odd-address
+// bytes): S = sum_start + O + 256*E.
+//
+// Groups are reduced with DPP row ops (<=16 lanes) and ds_swizzle / bpermute
+// (32/64 lanes). No LDS staging and no MFMA: this is an HBM-bound integer
+// reduction (~1 VALU op per 4 bytes) and each byte is read exactly once.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "tcpcsum.h"
+#include "tcpcsum_internal.h"
+
+namespace tcpcsum {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+enum : int { M16 = 0, M4 = 1, M1 = 2 };
+
+__device__ __forceinline__ u32x4 ld16(const uint8_t* p) {
+    return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+}
+
+// context.c:140-144, on the exact sum.
+__device__ __forceinline__ uint16_t fold_ref(uint64_t S) {
+    uint64_t s = (S >> 16) + (S & 0xffffu);
+    s = s + (s >> 16);
+    return (uint16_t)(~s & 0xffffu);
+}
+
+__device__ __forceinline__ uint32_t sad16(uint32_t d, uint32_t acc) {
+    return __builtin_amdgcn_sad_u16(d, 0u, acc);   // lo16(d) + hi16(d) + acc
+}
+__device__ __forceinline__ uint32_t sad8(uint32_t d, uint32_t acc) {
+    return __builtin_amdgcn_sad_u8(d, 0u, acc);    // sum of the 4 bytes + acc
+}
+
+// ---------------------------------------------------------------- reductions
+// Sum over the G lanes of an aligned lane group; result valid in every lane
+// of the group. DPP for 2..16 lanes, swizzle/bpermute above.
+template <int G>
+__device__ __forceinline__ uint32_t group_sum32(uint32_t x) {
+    if constexpr (G >= 2)  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
+    if constexpr (G >= 4)  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);  // quad_perm 2,3,0,1
+    if constexpr (G >= 8)  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xF, 0xF, false); // row_half_mirror
+    if constexpr (G >= 16) x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x140, 0xF, 0xF, false); // row_mirror
+    if constexpr (G >= 32) x += (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x401F);                    // xor 16 within 32
+    if constexpr (G >= 64) x += (uint32_t)__shfl_xor((int)x, 32, 64);
+    return x;
+}
+
+template <int G>
+__device__ __forceinline__ uint64_t group_sum64(uint64_t x) {
+#pragma unroll
+    for (int s = G / 2; s >= 1; s >>= 1) x += __shfl_xor(x, s, 64);
+    return x;
+}
+
+// ---------------------------------------------------------------- chunk sums
+// One 16-B chunk whose first byte sits at segment-relative offset rel
+// (negative for the leading partial chunk; two's complement in a u32).
+// M16: chunk entirely inside the segment (masking done by the load predicate).
+// M4 : segment start and length are multiples of 4 — dword-granular mask.
+template <int MODE>
+__device__ __forceinline__ uint32_t chunk_w(u32x4 v, uint32_t rel, uint32_t len) {
+    if constexpr (MODE == M16) {
+        uint32_t w = sad16(v.x, 0u);
+        w = sad16(v.y, w);
+        w = sad16(v.z, w);
+        return sad16(v.w, w);
+    } else {
+        uint32_t w = sad16((rel + 0u) < len ? v.x : 0u, 0u);
+        w = sad16((rel + 4u) < len ? v.y : 0u, w);
+        w = sad16((rel + 8u) < len ? v.z : 0u, w);
+        return sad16((rel + 12u) < len ? v.w : 0u, w);
+    }
+}
+
+__device__ __forceinline__ uint64_t bytemask64(int64_t nbytes) {   // low nbytes bytes set, nbytes in [0,8]
+    return nbytes >= 8 ? ~0ull : ((1ull << (8 * nbytes)) - 1ull);
+}
+
+// Byte-granular: valid bytes of the chunk are [lo, hi) with lo = -rel and
+// hi = len - rel clamped to [0,16]. Adds the aligned-word sum to W and the
+// odd-address byte sum to O (O only when want_odd).
+__device__ __forceinline__ void chunk_wo_bytes(u32x4 v, int64_t rel, int64_t len, bool want_odd,
+                                               uint32_t& W, uint32_t& O) {
+    int64_t lo = -rel;       lo = lo < 0 ? 0 : (lo > 16 ? 16 : lo);
+    int64_t hi = len - rel;  hi = hi < 0 ? 0 : (hi > 16 ? 16 : hi);
+    int64_t lo0 = lo < 8 ? lo : 8, hi0 = hi < 8 ? hi : 8;
+    int64_t lo1 = lo > 8 ? lo - 8 : 0, hi1 = hi > 8 ? hi - 8 : 0;
+    const uint64_t m0 = bytemask64(hi0) & ~bytemask64(lo0);
+    const uint64_t m1 = bytemask64(hi1) & ~bytemask64(lo1);
+    const uint32_t d0 = v.x & (uint32_t)m0, d1 = v.y & (uint32_t)(m0 >> 32);
+    const uint32_t d2 = v.z & (uint32_t)m1, d3 = v.w & (uint32_t)(m1 >> 32);
+    W = sad16(d0, W); W = sad16(d1, W); W = sad16(d2, W); W = sad16(d3, W);
+    if (want_odd) {
+        O = sad8(d0 & 0xff00ff00u, O); O = sad8(d1 & 0xff00ff00u, O);
+        O = sad8(d2 & 0xff00ff00u, O); O = sad8(d3 & 0xff00ff00u, O);
+    }
+}
+
+__device__ __forceinline__ uint64_t combine(uint64_t start, uint64_t W, uint64_t O, bool odd_start) {
+    // even start: relative parity == absolute parity -> S = start + W.
+    // odd start : relative even bytes are the absolute odd ones.
+    return odd_start ? start + O + 256ull * (W - 256ull * O) : start + W;
+}
+
+// ---------------------------------------------------------------- uniform
+// Segment i at base + i*stride, all of length len; n segments.
+// G lanes per segment, C chunk loads per lane per segment (G*C >= chunks a
+// segment can touch), U segments per group in flight per iteration.
+// A wave tile = (64/G)*U consecutive segments; load instruction (u, k) of the
+// wave reads chunk k*G+gl of segments tile+u*(64/G)+q — consecutive segments
+// across groups, i.e. one contiguous run of memory.
+template <int G, int C, int U, int MODE>
+__global__ __launch_bounds__(256) void k_uniform(const uint8_t* __restrict__ base, uint64_t stride,
+                                                 uint32_t len, const uint32_t* __restrict__ ss,
+                                                 uint32_t ss_scalar, uint16_t* __restrict__ out,
+                                                 uint64_t n) {
+    constexpr int GPW = 64 / G;
+    constexpr int SPT = GPW * U;
+    const int lane = threadIdx.x & 63;
+    const int q = lane / G, gl = lane % G;
+    const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
+    const uint64_t ntiles = (n + SPT - 1) / SPT;
+    for (uint64_t t = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6); t < ntiles; t += nwaves) {
+        u32x4 v[U][C];
+        uint32_t st[U], mm[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t seg = t * SPT + (uint64_t)(u * GPW + q);
+            const bool live = seg < n;
+            const uint8_t* p = base + seg * stride;
+            const uint32_t m = (uint32_t)((uintptr_t)p & 15u);
+            const uint8_t* a0 = p - m;
+            const uint32_t nch = (m + len + 15u) >> 4;
+            mm[u] = m;
+            st[u] = (live && gl == 0) ? (ss ? ss[seg] : ss_scalar) : 0u;
+#pragma unroll
+            for (int k = 0; k < C; ++k) {
+                const uint32_t idx = (uint32_t)(k * G + gl);
+                v[u][k] = (live && idx < nch) ? ld16(a0 + (uint64_t)idx * 16u) : u32x4{0u, 0u, 0u, 0u};
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t seg = t * SPT + (uint64_t)(u * GPW + q);
+            uint32_t w = 0, o = 0;
+            bool odd = false;
+            if constexpr (MODE == M1) odd = ((uintptr_t)(base + seg * stride)) & 1u;
+#pragma unroll
+            for (int k = 0; k < C; ++k) {
+                const uint32_t rel = (uint32_t)((k * G + gl) * 16) - mm[u];
+                if constexpr (MODE == M1)
+                    chunk_wo_bytes(v[u][k], (int64_t)(int32_t)rel, (int64_t)len, odd, w, o);
+                else
+                    w += chunk_w<MODE>(v[u][k], rel, len);
+            }
+            w = group_sum32<G>(w);
+            if constexpr (MODE == M1) o = group_sum32<G>(o);
+            if (gl == 0 && seg < n) out[seg] = fold_ref(combine(st[u], w, o, odd));
+        }
+    }
+}
+
+// Long segments (more than 512 chunks): one wave per segment, 8 chunk loads
+// per lane per round (8 KiB per wave-round), u32 lane partials flushed to u64
+// every round so any length <= INT32_MAX is exact.
+template <int MODE>
+__global__ __launch_bounds__(256) void k_uniform_long(const uint8_t* __restrict__ base, uint64_t stride,
+                                                      uint32_t len, const uint32_t* __restrict__ ss,
+                                                      uint32_t ss_scalar, uint16_t* __restrict__ out,
+                                                      uint64_t n) {
+    constexpr int C = 8;
+    const int lane = threadIdx.x & 63;
+    const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
+    for (uint64_t seg = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6); seg < n; seg += nwaves) {
+        const uint8_t* p = base + seg * stride;
+        const uint32_t m = (uint32_t)((uintptr_t)p & 15u);
+        const uint8_t* a0 = p - m;
+        const uint32_t nch = (uint32_t)(((uint64_t)m + len + 15u) >> 4);
+        const bool odd = (MODE == M1) && ((uintptr_t)p & 1u);
+        const uint32_t st = ss ? ss[seg] : ss_scalar;
+        uint64_t W = 0, O = 0;
+        for (uint32_t r = 0; r < nch; r += 64u * C) {
+            u32x4 v[C];
+#pragma unroll
+            for (int k = 0; k < C; ++k) {
+                const uint32_t idx = r + (uint32_t)(k * 64 + lane);
+                v[k] = idx < nch ? ld16(a0 + (uint64_t)idx * 16u) : u32x4{0u, 0u, 0u, 0u};
+            }
+            uint32_t w = 0, o = 0;
+#pragma unroll
+            for (int k = 0; k < C; ++k) {
+                const uint32_t idx = r + (uint32_t)(k * 64 + lane);
+                const uint32_t rel = idx * 16u - m;
+                if constexpr (MODE == M1)
+                    chunk_wo_bytes(v[k], (int64_t)idx * 16 - (int64_t)m, (int64_t)len, odd, w, o);
+                else
+                    w += chunk_w<MODE>(v[k], rel, len);
+            }
+            W += w;
+            O += o;
+        }
+        W = group_sum64<64>(W);
+        if constexpr (MODE == M1) O = group_sum64<64>(O);
+        if (lane == 0) out[seg] = fold_ref(combine(st, W, O, odd));
+    }
+}
+
+// ---------------------------------------------------------------- ragged
+// Exact sum of one segment [p, p+len) by the G lanes of a group, C chunk
+// loads per lane per round. Returns the group total S - start (i.e. with the
+// parity rule applied) in every lane of the group.
+template <int G, int C>
+__device__ __forceinline__ uint64_t group_segment_sum(const uint8_t* p, uint32_t len, int gl) {
+    const uint32_t m = (uint32_t)((uintptr_t)p & 15u);
+    const uint8_t* a0 = p - m;
+    const uint32_t nch = (uint32_t)(((uint64_t)m + len + 15u) >> 4);
+    const bool a4 = (((uintptr_t)p | len) & 3u) == 0;
+    const bool odd = ((uintptr_t)p & 1u) != 0;
+    uint64_t W = 0, O = 0;
+    for (uint32_t r = 0; r < nch; r += (uint32_t)(G * C)) {
+        u32x4 v[C];
+#pragma unroll
+        for (int k = 0; k < C; ++k) {
+            const uint32_t idx = r + (uint32_t)(k * G + gl);
+            v[k] = idx < nch ? ld16(a0 + (uint64_t)idx * 16u) : u32x4{0u, 0u, 0u, 0u};
+        }
+        uint32_t w = 0, o = 0;
+        if (a4) {
+#pragma unroll
+            for (int k = 0; k < C; ++k) {
+                const uint32_t idx = r + (uint32_t)(k * G + gl);
+                w += chunk_w<M4>(v[k], idx * 16u - m, len);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < C; ++k) {
+                const uint32_t idx = r + (uint32_t)(k * G + gl);
+                chunk_wo_bytes(v[k], (int64_t)idx * 16 - (int64_t)m, (int64_t)len, odd, w, o);
+            }
+        }
+        W += w;
+        O += o;
+    }
+    W = group_sum64<G>(W);
+    O = odd ? group_sum64<G>(O) : 0;
+    return combine(0, W, O, odd);
+}
+
+template <int G, int C>
+__global__ __launch_bounds__(256) void k_desc(const uint8_t* __restrict__ base,
+                                              const tcpcsum_desc_t* __restrict__ desc, uint64_t n,
+                                              uint16_t* __restrict__ out) {
+    constexpr int GPW = 64 / G;
+    const int lane = threadIdx.x & 63;
+    const int q = lane / G, gl = lane % G;
+    const uint64_t ngroups = (uint64_t)gridDim.x * 4u * GPW;
+    for (uint64_t seg = ((uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6)) * GPW + q; seg < n;
+         seg += ngroups) {
+        const u32x4 d = *reinterpret_cast<const u32x4*>(desc + seg);   // one 16-B load
+        const uint64_t off = (uint64_t)d.x | ((uint64_t)d.y << 32);
+        const uint64_t S = group_segment_sum<G, C>(base + off, d.z, gl) + (uint64_t)d.w;
+        if (gl == 0) out[seg] = fold_ref(S);
+    }
+}
+
+// ---------------------------------------------------------------- wire (IPv4)
+// Packet i at pkts + off[i]. Header fields are read by every lane of the
+// group (same addresses: one broadcast request per group). See tcpcsum.h.
+template <int G, int C>
+__global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const uint64_t* __restrict__ off,
+                                              uint64_t n, uint32_t cap, uint64_t limit, int mode,
+                                              uint16_t* __restrict__ out, uint8_t* __restrict__ status) {
+    constexpr int GPW = 64 / G;
+    const int lane = threadIdx.x & 63;
+    const int q = lane / G, gl = lane % G;
+    const uint64_t ngroups = (uint64_t)gridDim.x * 4u * GPW;
+    for (uint64_t i = ((uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6)) * GPW + q; i < n; i += ngroups) {
+        const uint64_t o = off[i];
+        uint8_t* ip = pkts + o;
+        const uint32_t b0 = ip[0];
+        const uint32_t ver = b0 >> 4, ihl = b0 & 15u;
+        const uint32_t tot = ((uint32_t)ip[2] << 8) | ip[3];
+        const uint32_t proto = ip[9];
+        const bool ok = ver == 4u && proto == 6u && ihl >= 5u && tot >= ihl * 4u + 20u && tot <= cap &&
+                        o + tot <= limit;
+        if (!ok) {   // group-uniform
+            if (gl == 0) {
+                if (out) out[i] = 0;
+                if (status) status[i] = TCPCSUM_PKT_SKIPPED;
+            }
+            continue;
+        }
+        // saddr/daddr as stored (network order), read as native u32 (bytewise:
+        // the IP header start need not be 4-byte aligned).
+        const uint32_t sa = (uint32_t)ip[12] | ((uint32_t)ip[13] << 8) | ((uint32_t)ip[14] << 16) | ((uint32_t)ip[15] << 24);
+        const uint32_t da = (uint32_t)ip[16] | ((uint32_t)ip[17] << 8) | ((uint32_t)ip[18] << 16) | ((uint32_t)ip[19] << 24);
+        uint8_t* tcp = ip + ihl * 4u;
+        const uint32_t tcp_len = tot - ihl * 4u;
+        const uint32_t len_be = ((tcp_len & 0xffu) << 8) | ((tcp_len >> 8) & 0xffu);   // htons
+        // context.c:104-119 closed form: six native u16 words of the pseudo header.
+        const uint64_t ps = (sa & 0xffffu) + (sa >> 16) + (da & 0xffffu) + (da >> 16) + 0x0600u + len_be;
+        const uint32_t check_word = (uint32_t)tcp[16] | ((uint32_t)tcp[17] << 8);
+        uint64_t S = group_segment_sum<G, C>(tcp, tcp_len, gl) + ps;
+        // FILL: the reference sums with check == 0 (context.c:182); TCP+16 is an
+        // even relative offset, so its native word contributes exactly check_word.
+        if (mode == TCPCSUM_IPV4_FILL) S -= check_word;
+        const uint16_t c = fold_ref(S);
+        if (gl == 0) {
+            if (mode == TCPCSUM_IPV4_FILL) {   // native u16 store, as context.c:208
+                tcp[16] = (uint8_t)(c & 0xffu);
+                tcp[17] = (uint8_t)(c >> 8);
+            }
+            if (out) out[i] = c;
+            if (status) status[i] = TCPCSUM_PKT_OK;
+        }
+    }
+}
+
+// ---------------------------------------------------------------- synthetic
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// SURVEY.md Appendix B stream: byte b = byte (b % 8) of mix(SEED + (b/8 + 1) * gamma).
+__global__ __launch_bounds__(256) void k_synth_fill(uint8_t* __restrict__ dst, uint64_t off, uint64_t nbytes) {
+    const uint64_t w0 = off >> 3, w1 = (off + nbytes + 7) >> 3;
+    const uint64_t nthr = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t w = w0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < w1; w += nthr) {
+        const uint64_t v = mix64(0x5EEDC0DEull + (w + 1) * 0x9E3779B97F4A7C15ull);
+        const uint64_t b0 = w << 3;
+        uint8_t* d = dst + (int64_t)(b0 - off);
+        if (b0 >= off && b0 + 8 <= off + nbytes && (((uintptr_t)d) & 7u) == 0) {
+            *reinterpret_cast<uint64_t*>(d) = v;
+        } else {
+            for (int k = 0; k < 8; ++k) {
+                const uint64_t b = b0 + k;
+                if (b >= off && b < off + nbytes) dst[b - off] = (uint8_t)(v >> (8 * k));
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_synth_pseudo(uint32_t* __restrict__ ss, uint64_t seg0, uint64_t n,
+                                                      uint32_t len_be) {
+    const uint64_t nthr = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += nthr) {
+        const uint64_t i = seg0 + k;
+        const uint32_t sa = __builtin_bswap32(0x0A000000u | (uint32_t)(i & 0xFFFFFFu));
+        const uint32_t da = __builtin_bswap32(0xC0A80000u | (uint32_t)((i * 7u) & 0xFFFFu));
+        ss[k] = (sa & 0xffffu) + (sa >> 16) + (da & 0xffffu) + (da >> 16) + 0x0600u + len_be;
+    }
+}
+
+// ---------------------------------------------------------------- probe
+// Read-only stream with the checksum kernel's access shape (each wave reads
+// contiguous 1 KiB per load instruction, 8 in flight), summed so it cannot be
+// dead-code eliminated; one 64-bit atomic per wave.
+__global__ __launch_bounds__(256) void k_probe(const uint8_t* __restrict__ src, uint64_t nchunks,
+                                               unsigned long long* __restrict__ out) {
+    constexpr int C = 8;
+    const int lane = threadIdx.x & 63;
+    const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
+    const uint64_t ntiles = (nchunks + 64 * C - 1) / (64 * C);
+    uint64_t acc = 0;
+    for (uint64_t t = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6); t < ntiles; t += nwaves) {
+        u32x4 v[C];
+#pragma unroll
+        for (int k = 0; k < C; ++k) {
+            const uint64_t idx = t * (64 * C) + (uint64_t)(k * 64 + lane);
+            v[k] = idx < nchunks ? ld16(src + idx * 16u) : u32x4{0u, 0u, 0u, 0u};
+        }
+        uint32_t w = 0;
+#pragma unroll
+        for (int k = 0; k < C; ++k) w += chunk_w<M16>(v[k], 0u, 0u);
+        acc += w;
+    }
+    acc = group_sum64<64>(acc);
+    if (lane == 0) atomicAdd(out, (unsigned long long)acc);
+}
+
+}  // namespace tcpcsum
+
+// ============================================================== launchers
+using namespace tcpcsum;
+
+namespace {
+
+inline unsigned grid_for(uint64_t waves_needed, int max_blocks) {
+    uint64_t blocks = (waves_needed + 3) / 4;
+    if (blocks < 1) blocks = 1;
+    if (blocks > (uint64_t)max_blocks) blocks = (uint64_t)max_blocks;
+    return (unsigned)blocks;
+}
+
+template <int G, int C, int U, int MODE>
+void launch_uniform_t(const uint8_t* base, uint64_t stride, uint32_t len, const uint32_t* ss,
+                      uint32_t ss0, uint16_t* out, uint64_t n, hipStream_t s, int max_blocks) {
+    constexpr int SPT = (64 / G) * U;
+    const uint64_t ntiles = (n + SPT - 1) / SPT;
+    hipLaunchKernelGGL((k_uniform<G, C, U, MODE>), dim3(grid_for(ntiles, max_blocks)), dim3(256), 0, s,
+                       base, stride, len, ss, ss0, out, n);
+}
+
+template <int MODE>
+void launch_uniform_mode(int shape, int unroll, const uint8_t* base, uint64_t stride, uint32_t len,
+                         const uint32_t* ss, uint32_t ss0, uint16_t* out, uint64_t n, hipStream_t s,
+                         int max_blocks) {
+#define TC_U(G, C, U) launch_uniform_t<G, C, U, MODE>(base, stride, len, ss, ss0, out, n, s, max_blocks)
+#define TC_U3(G, C)                          \
+    do {                                     \
+        if (unroll == 1) TC_U(G, C, 1);      \
+        else if (unroll == 2) TC_U(G, C, 2); \
+        else TC_U(G, C, 4);                  \
+    } while (0)
+    switch (shape) {
+        case 0: TC_U3(4, 1); break;    // <= 4 chunks   (64 B)
+        case 1: TC_U3(8, 1); break;    // <= 8
+        case 2: TC_U3(16, 1); break;   // <= 16
+        case 3: TC_U3(32, 1); break;   // <= 32
+        case 4: TC_U3(64, 1); break;   // <= 64
+        case 5: TC_U3(32, 3); break;   // <= 96         (1500 B)
+        case 6: TC_U3(64, 2); break;   // <= 128
+        case 7: TC_U3(64, 4); break;   // <= 256
+        case 8: TC_U3(64, 8); break;   // <= 512
+        default:
+            hipLaunchKernelGGL((k_uniform_long<MODE>), dim3(grid_for(n, max_blocks)), dim3(256), 0, s,
+                               base, stride, len, ss, ss0, out, n);
+    }
+#undef TC_U3
+#undef TC_U
+}
+
+}  // namespace
+
+namespace tcpcsum {
+
+// Segment-group shapes: shape k covers up to kShapeChunks[k] 16-B chunks per
+// segment; kShapeUnroll[k] is the default segments-in-flight per group.
+static const uint32_t kShapeChunks[9] = {4, 8, 16, 32, 64, 96, 128, 256, 512};
+static const int kShapeUnroll[10] = {4, 4, 4, 4, 4, 2, 2, 1, 1, 1};
+
+UniformPlan plan_uniform(uintptr_t b, uint64_t stride, uint32_t len, uint64_t n, int unroll_override) {
+    UniformPlan p;
+    p.mode = (((b | stride | len) & 15u) == 0) ? M16 : (((b | stride | len) & 3u) == 0) ? M4 : M1;
+    // The chunks a segment touches depend on its start mod 16, which repeats
+    // with period <= 16 over i: take the max over one period.
+    uint64_t nch = 0;
+    for (uint64_t i = 0; i < 16 && i < n; ++i) {
+        const uint64_t m = (b + i * stride) & 15u;
+        const uint64_t c = (m + len + 15u) >> 4;
+        if (c > nch) nch = c;
+    }
+    p.shape = 9;
+    for (int k = 0; k < 9; ++k)
+        if (nch <= kShapeChunks[k]) { p.shape = k; break; }
+    p.unroll = p.shape == 9 ? 1 : (unroll_override ? unroll_override : kShapeUnroll[p.shape]);
+    return p;
+}
+
+void launch_uniform(const uint8_t* base, uint64_t stride, uint32_t len, const uint32_t* ss, uint32_t ss0,
+                    uint16_t* out, uint64_t n, hipStream_t s, const Tuning& tu) {
+    const UniformPlan p = plan_uniform((uintptr_t)base, stride, len, n, tu.unroll);
+    const int max_blocks = tu.max_blocks > 0 ? tu.max_blocks : kDefaultMaxBlocks;
+    if (p.mode == M16) launch_uniform_mode<M16>(p.shape, p.unroll, base, stride, len, ss, ss0, out, n, s, max_blocks);
+    else if (p.mode == M4) launch_uniform_mode<M4>(p.shape, p.unroll, base, stride, len, ss, ss0, out, n, s, max_blocks);
+    else launch_uniform_mode<M1>(p.shape, p.unroll, base, stride, len, ss, ss0, out, n, s, max_blocks);
+}
+
+template <int G, int C>
+static void launch_desc_t(const uint8_t* base, const tcpcsum_desc_t* d, uint64_t n, uint16_t* out,
+                          hipStream_t s, int max_blocks) {
+    const uint64_t groups = n, waves = (groups + (64 / G) - 1) / (64 / G);
+    hipLaunchKernelGGL((k_desc<G, C>), dim3(grid_for(waves, max_blocks)), dim3(256), 0, s, base, d, n, out);
+}
+
+void launch_desc(const uint8_t* base, const tcpcsum_desc_t* d, uint64_t n, uint32_t max_len, uint16_t* out,
+                 hipStream_t s, const Tuning& tu) {
+    const uint64_t nch = ((uint64_t)max_len + 30u) >> 4;   // worst-case start alignment
+    const int max_blocks = tu.max_blocks > 0 ? tu.max_blocks : kDefaultMaxBlocks;
+    if (nch <= 4) launch_desc_t<4, 1>(base, d, n, out, s, max_blocks);
+    else if (nch <= 8) launch_desc_t<8, 1>(base, d, n, out, s, max_blocks);
+    else if (nch <= 16) launch_desc_t<16, 1>(base, d, n, out, s, max_blocks);
+    else if (nch <= 32) launch_desc_t<32, 1>(base, d, n, out, s, max_blocks);
+    else if (nch <= 96) launch_desc_t<32, 3>(base, d, n, out, s, max_blocks);
+    else if (nch <= 256) launch_desc_t<64, 4>(base, d, n, out, s, max_blocks);
+    else launch_desc_t<64, 8>(base, d, n, out, s, max_blocks);
+}
+
+void launch_ipv4(uint8_t* pkts, const uint64_t* off, uint64_t n, uint32_t cap, uint64_t limit, int mode,
+                 uint16_t* out, uint8_t* status, hipStream_t s, const Tuning& tu) {
+    const int max_blocks = tu.max_blocks > 0 ? tu.max_blocks : kDefaultMaxBlocks;
+    const uint64_t nch = ((uint64_t)cap + 30u) >> 4;
+    if (nch <= 8) {
+        hipLaunchKernelGGL((k_ipv4<8, 1>), dim3(grid_for((n + 7) / 8, max_blocks)), dim3(256), 0, s, pkts, off,
+                           n, cap, limit, mode, out, status);
+    } else if (nch <= 96) {
+        hipLaunchKernelGGL((k_ipv4<32, 3>), dim3(grid_for((n + 1) / 2, max_blocks)), dim3(256), 0, s, pkts, off,
+                           n, cap, limit, mode, out, status);
+    } else {
+        hipLaunchKernelGGL((k_ipv4<64, 8>), dim3(grid_for(n, max_blocks)), dim3(256), 0, s, pkts, off, n, cap,
+                           limit, mode, out, status);
+    }
+}
+
+void launch_synth_fill(uint8_t* dst, uint64_t off, uint64_t nbytes, hipStream_t s) {
+    const uint64_t words = ((off + nbytes + 7) >> 3) - (off >> 3);
+    uint64_t blocks = (words + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(k_synth_fill, dim3((unsigned)blocks), dim3(256), 0, s, dst, off, nbytes);
+}
+
+void launch_synth_pseudo(uint32_t* ss, uint64_t seg0, uint64_t n, uint32_t seg_len, hipStream_t s) {
+    const uint32_t l16 = seg_len & 0xffffu;
+    const uint32_t len_be = ((l16 & 0xffu) << 8) | (l16 >> 8);
+    uint64_t blocks = (n + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(k_synth_pseudo, dim3((unsigned)blocks), dim3(256), 0, s, ss, seg0, n, len_be);
+}
+
+void launch_probe(const uint8_t* src, uint64_t nbytes, uint64_t* out, hipStream_t s, const Tuning& tu) {
+    const int max_blocks = tu.max_blocks > 0 ? tu.max_blocks : kDefaultMaxBlocks;
+    const uint64_t nchunks = nbytes / 16;
+    const uint64_t tiles = (nchunks + 511) / 512;
+    hipLaunchKernelGGL(k_probe, dim3(grid_for(tiles, max_blocks)), dim3(256), 0, s, src, nchunks,
+                       (unsigned long long*)out);
+}
+
+}  // namespace tcpcsum

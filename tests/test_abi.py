@@ -1,0 +1,136 @@
+"""CPU: the C-ABI library loads, exports every symbol include/tcpcsum.h declares,
+its host-side logic behaves, and the scalar drop-ins equal the oracle.
+No GPU compute here."""
+import os
+import random
+import re
+import socket
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle
+import tcp_amd
+from tcp_amd import api
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "tcpcsum.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    names = re.findall(r"\b(tcpcsum_[a-z0-9_]+)\s*\(", text)
+    return sorted(set(names))
+
+
+def test_library_exports_every_declared_symbol():
+    L = tcp_amd.lib()
+    names = declared_functions()
+    assert len(names) >= 20
+    for n in names:
+        assert hasattr(L, n), n
+    # the ctypes signature table covers the whole header
+    assert set(names) == set(api.SIGNATURES)
+
+
+def test_nm_exports_match_header():
+    out = subprocess.run(["nm", "-D", "--defined-only", tcp_amd.lib_path()], capture_output=True, text=True,
+                         check=True).stdout
+    exported = set(re.findall(r" T (tcpcsum_[a-z0-9_]+)", out))
+    assert set(declared_functions()) <= exported
+
+
+def test_header_constants_match_python():
+    text = open(HEADER).read()
+    consts = dict(re.findall(r"#define (TCPCSUM_[A-Z0-9_]+) \(?(-?\d+)\)?", text))
+    assert int(consts["TCPCSUM_OK"]) == api.OK
+    assert int(consts["TCPCSUM_EINVAL"]) == api.EINVAL
+    assert int(consts["TCPCSUM_ENODEV"]) == api.ENODEV
+    assert int(consts["TCPCSUM_EHIP"]) == api.EHIP
+    assert int(consts["TCPCSUM_ENOMEM"]) == api.ENOMEM
+    assert int(consts["TCPCSUM_IPV4_FILL"]) == api.IPV4_FILL
+    assert int(consts["TCPCSUM_IPV4_VERIFY"]) == api.IPV4_VERIFY
+    assert int(consts["TCPCSUM_PKT_SKIPPED"]) == api.PKT_SKIPPED
+    assert int(consts["TCPCSUM_ABI_VERSION"]) == tcp_amd.lib().tcpcsum_abi_version()
+    assert api.DESC_DTYPE.itemsize == 16
+
+
+def test_scalar_dropins_equal_oracle():
+    rng = random.Random(99)
+    for _ in range(300):
+        n = rng.randrange(0, 3000)
+        p = bytes(rng.getrandbits(8) for _ in range(n))
+        ss = rng.choice([0, 393210, rng.getrandbits(32), rng.getrandbits(48)])
+        nb = rng.choice([n, max(n - 1, 0), -1])
+        assert tcp_amd.csum_continue(ss, p, nb if nb >= 0 else 0) == oracle.csum_continue(ss, p, nb if nb >= 0 else 0)
+        sa, da, ln = rng.getrandbits(32), rng.getrandbits(32), rng.getrandbits(16)
+        assert tcp_amd.getPseudoHeaderSum(sa, da, ln) == oracle.pseudo(sa, da, ln)
+    # negative nbytes is a no-op loop in the reference
+    assert tcp_amd.lib().tcpcsum_continue(5, b"abc", -3) == oracle.csum_continue(5, b"abc", -3)
+
+
+def test_scalar_kats(golden):
+    for k in golden["kat_csum_continue"]:
+        assert tcp_amd.csum_continue(k["sum_start"], bytes.fromhex(k["bytes"]), k["nbytes"]) == int(k["out"], 16)
+    for k in golden["kat_pseudo"]:
+        sa = socket.htonl(int(k["saddr_host"], 16))
+        da = socket.htonl(int(k["daddr_host"], 16))
+        assert tcp_amd.getPseudoHeaderSum(sa, da, socket.htons(k["len_host"] & 0xFFFF)) == k["out"]
+
+
+def test_argument_errors_need_no_device():
+    L = tcp_amd.lib()
+    assert L.tcpcsum_batch_uniform_dev(None, 0, 0, None, 0, None, 0, None) == api.OK      # n == 0
+    assert L.tcpcsum_batch_uniform_dev(None, 0, 10, None, 0, None, 5, None) == api.EINVAL
+    assert L.tcpcsum_batch_uniform_dev(1 << 20, 0, 2**31, None, 0, 1 << 20, 5, None) == api.EINVAL
+    assert L.tcpcsum_batch_desc_dev(1 << 20, (1 << 20) + 8, 5, 64, 1 << 20, None) == api.EINVAL   # unaligned desc
+    assert L.tcpcsum_ipv4_batch_dev(1 << 20, 1 << 20, 5, 1500, 7, None, None, None) == api.EINVAL  # bad mode
+    assert L.tcpcsum_stream_probe_dev(1 << 20, 17, 1 << 20, None) == api.EINVAL
+    assert L.tcpcsum_set_tuning(-1, 0) == api.EINVAL
+    assert L.tcpcsum_set_tuning(0, 3) == api.EINVAL
+    assert L.tcpcsum_set_tuning(0, 0) == api.OK
+    assert L.tcpcsum_batch_uniform_host(None, None, 0, 0, None, 0, None, 0) == api.EINVAL
+    assert L.tcpcsum_strerror(api.EHIP) == b"HIP runtime error"
+
+
+def test_no_device_is_reported_not_faked():
+    """On a box without a gfx950 GPU every device entry point fails loudly."""
+    rc, arch = tcp_amd.device_check()
+    if rc == api.OK:
+        pytest.skip(f"a {arch} GPU is present")
+    assert rc == api.ENODEV
+    L = tcp_amd.lib()
+    assert L.tcpcsum_batch_uniform_dev(1 << 20, 1500, 1500, None, 0, 1 << 20, 4, None) == api.ENODEV
+    with pytest.raises(tcp_amd.TcpCsumError):
+        tcp_amd.HostContext(0)
+
+
+@pytest.mark.parametrize("base,stride,length,n,expect", [
+    (0, 1500, 1500, 1 << 20, (1, 5, 2)),       # 1M x 1500: 4-B aligned, 95 chunks -> 32 lanes x 3
+    (0, 64, 64, 1 << 20, (0, 0, 4)),           # 1M x 64: 16-B aligned, 4 lanes
+    (0, 65536, 65536, 1 << 18, (0, 9, 1)),     # 64 KiB: one wave per segment
+    (3, 1501, 1501, 100, (2, 5, 2)),           # byte-granular
+    (0, 1500, 1500, 1, (1, 5, 2)),
+    (12, 64, 64, 8, (1, 1, 4)),                # misaligned 64 B touches 5 chunks
+])
+def test_plan_uniform(base, stride, length, n, expect):
+    assert api.plan_uniform(base, stride, length, n) == expect
+
+
+def test_plan_respects_unroll_override():
+    try:
+        api.set_tuning(0, 1)
+        assert api.plan_uniform(0, 1500, 1500, 1000)[2] == 1
+    finally:
+        api.set_tuning(0, 0)
+
+
+def test_c_program_links_the_abi():
+    exe = os.path.join(REPO, "tests", "c", "abi_smoke")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", REPO, "tests/c/abi_smoke"], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "OK" in r.stdout

@@ -1,0 +1,277 @@
+"""GPU parity: the gfx950 kernels vs the oracle, bit for bit (integer path: exact).
+
+Small/medium cases compare every output with the oracle on the same seeded
+bytes; the BASELINE configs at full size compare against the reference's own
+Appendix B digests (tests/golden/reference_vectors.json); properties
+(verify-to-zero, fill/verify round trip) cover the wire path. Every call goes
+through the C ABI (libtcpcsum.so) — there is no CPU fallback to pass through.
+"""
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    import tcp_amd
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rc, arch = tcp_amd.device_check()
+    assert rc == 0, f"tcpcsum_device_check -> {rc} ({arch}); the HIP path must run on gfx950"
+    return torch.device("cuda:0")
+
+
+def to_dev(a: np.ndarray, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def u16(t) -> np.ndarray:
+    return t.cpu().numpy().view(np.uint16)
+
+
+def test_native_library_is_loaded(dev):
+    import tcp_amd
+    path = tcp_amd.lib_path()
+    with open("/proc/self/maps") as f:
+        assert path in f.read() or "libtcpcsum.so" in open("/proc/self/maps").read()
+
+
+LENGTHS = [0, 1, 2, 3, 4, 5, 7, 8, 15, 16, 17, 24, 31, 32, 33, 44, 63, 64, 65, 100, 255, 256, 257, 511, 512,
+           513, 1023, 1024, 1025, 1479, 1480, 1499, 1500, 1501, 1503, 1504, 2048, 4095, 4096, 4097, 8191, 8192,
+           8193, 9000, 16383, 32767, 65535, 65536, 65537]
+
+
+@pytest.mark.parametrize("length", LENGTHS)
+def test_uniform_vs_oracle_lengths(dev, length):
+    import tcp_amd
+    rng = np.random.default_rng(length + 11)
+    for base_off in (0, 1, 4, 12):
+        for stride in sorted({max(length, 1), length + 3 if length else 7, length + 16}):
+            n = int(min(300, max(8, (1 << 21) // max(stride, 1))))
+            size = base_off + (n - 1) * stride + length + 64
+            host = rng.integers(0, 256, size, dtype=np.uint8)
+            ss = rng.integers(0, 6 * 0xFFFF + 1, n, dtype=np.uint32)
+            d = to_dev(host, dev)
+            got = u16(tcp_amd.batch_uniform(d, stride, length, n, to_dev(ss.view(np.int32), dev), offset=base_off))
+            want = oracle.batch_uniform(host, stride, length, n, ss, offset=base_off)
+            assert np.array_equal(got, want), (length, base_off, stride)
+            # scalar start value
+            got = u16(tcp_amd.batch_uniform(d, stride, length, n, 393210, offset=base_off))
+            want = oracle.batch_uniform(host, stride, length, n, 393210, offset=base_off)
+            assert np.array_equal(got, want), (length, base_off, stride, "scalar")
+
+
+def test_uniform_overlapping_and_zero_stride(dev):
+    import tcp_amd
+    rng = np.random.default_rng(5)
+    host = rng.integers(0, 256, 1 << 16, dtype=np.uint8)
+    d = to_dev(host, dev)
+    for stride, length, n in [(0, 1500, 50), (7, 1500, 500), (1, 64, 1000), (100, 1500, 400)]:
+        got = u16(tcp_amd.batch_uniform(d, stride, length, n, 17))
+        assert np.array_equal(got, oracle.batch_uniform(host, stride, length, n, 17)), (stride, length)
+
+
+def test_uniform_all_unrolls_and_grids(dev):
+    import tcp_amd
+    rng = np.random.default_rng(9)
+    host = rng.integers(0, 256, 3 << 20, dtype=np.uint8)
+    d = to_dev(host, dev)
+    try:
+        for unroll in (1, 2, 4):
+            for max_blocks in (1, 7, 0):
+                tcp_amd.set_tuning(max_blocks, unroll)
+                for length in (64, 60, 1500, 1501, 2000, 8192, 20000):
+                    n = (3 << 20) // (length + 1) - 1
+                    got = u16(tcp_amd.batch_uniform(d, length, length, n, 99))
+                    want = oracle.batch_uniform(host, length, length, n, 99)
+                    assert np.array_equal(got, want), (unroll, max_blocks, length)
+    finally:
+        tcp_amd.set_tuning(0, 0)
+
+
+def test_two_fold_semantics_above_4g(dev):
+    """S = 0x1_0000_FFFF: the reference's exactly-two folds, not a full fold."""
+    import tcp_amd
+    seg = np.frombuffer(b"\xff\xff" * 65538 + b"\x01\x00", np.uint8)
+    host = np.concatenate([seg, seg, np.zeros(64, np.uint8)])
+    d = to_dev(host, dev)
+    got = u16(tcp_amd.batch_uniform(d, seg.size, seg.size, 2, 0))
+    want = oracle.batch_uniform(host, seg.size, seg.size, 2, 0)
+    assert np.array_equal(got, want)
+    assert want[0] == oracle.csum_continue(0, seg.tobytes())
+    # all-zero segment with start 0 -> 0xFFFF (never conflated with 0x0000)
+    z = torch.zeros(4096, dtype=torch.uint8, device=dev)
+    assert np.all(u16(tcp_amd.batch_uniform(z, 64, 64, 64, 0)) == 0xFFFF)
+
+
+def test_long_segments_and_big_sums(dev):
+    import tcp_amd
+    rng = np.random.default_rng(21)
+    for length in (131072, 200003, 1 << 20):
+        n = 6
+        host = rng.integers(200, 256, n * length + 64, dtype=np.uint8)   # large bytes -> S well above 2^32
+        d = to_dev(host, dev)
+        for off in (0, 1, 2):
+            got = u16(tcp_amd.batch_uniform(d, length, length - off, n, 0xFFFFFFFF, offset=off))
+            want = oracle.batch_uniform(host, length, length - off, n, 0xFFFFFFFF, offset=off)
+            assert np.array_equal(got, want), (length, off)
+
+
+def _desc(off, lens, ss):
+    from tcp_amd import DESC_DTYPE
+    d = np.zeros(len(off), DESC_DTYPE)
+    d["offset"], d["len"], d["sum_start"] = off, lens, ss
+    return d.view(np.uint8)
+
+
+@pytest.mark.parametrize("max_len", [64, 1500, 9000, 70000])
+def test_desc_ragged_vs_oracle(dev, max_len):
+    import tcp_amd
+    rng = np.random.default_rng(max_len)
+    size = 4 << 20
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    n = 3000
+    lens = rng.integers(0, max_len + 1, n).astype(np.uint32)
+    lens[:10] = [0, 1, 2, 3, max_len, max_len - 1, 0, 5, 1, max_len]
+    off = np.array([rng.integers(0, size - l) for l in lens], np.uint64)
+    ss = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    d = to_dev(host, dev)
+    dd = to_dev(_desc(off, lens, ss), dev)
+    got = u16(tcp_amd.batch_desc(d, dd, n, max_len))
+    assert np.array_equal(got, oracle.batch_desc(host, off, lens, ss))
+    # a max_len hint that is too small is slower, never wrong
+    got = u16(tcp_amd.batch_desc(d, dd, n, 16))
+    assert np.array_equal(got, oracle.batch_desc(host, off, lens, ss))
+
+
+@pytest.mark.parametrize("odd", [False, True])
+def test_ipv4_fill_and_verify(dev, odd):
+    import tcp_amd
+    from tests.packets import build_batch
+    rng = np.random.default_rng(31 + odd)
+    region, off, _ = build_batch(rng, 1024, malformed=True, odd_offsets=odd)
+    ref_region = region.copy()
+    want_out, want_st = oracle.ipv4_batch(ref_region, off, 32768, tcp_amd.IPV4_FILL)
+    dreg = to_dev(region, dev)
+    doff = to_dev(off.view(np.int64), dev)
+    out = torch.empty(off.size, dtype=torch.int16, device=dev)
+    st = torch.empty(off.size, dtype=torch.uint8, device=dev)
+    tcp_amd.ipv4_batch(dreg, doff, off.size, 32768, tcp_amd.IPV4_FILL, out, st)
+    assert np.array_equal(st.cpu().numpy(), want_st)
+    assert np.array_equal(u16(out), want_out)
+    assert np.array_equal(dreg.cpu().numpy(), ref_region)     # checks patched in place, nothing else touched
+    # rx side: every filled segment verifies to zero (loop.c:314-399 has no verify; new behaviour)
+    tcp_amd.ipv4_batch(dreg, doff, off.size, 32768, tcp_amd.IPV4_VERIFY, out, st)
+    v = u16(out)
+    ok = st.cpu().numpy() == tcp_amd.PKT_OK
+    assert np.all(v[ok] == 0)
+    want_v, _ = oracle.ipv4_batch(ref_region.copy(), off, 32768, tcp_amd.IPV4_VERIFY)
+    assert np.array_equal(v, want_v)
+    # corrupt one payload byte per packet -> verification fails exactly there
+    bad = ref_region.copy()
+    idx = [int(o) + 44 for o, s in zip(off, want_st) if s == 0 and int(o) + 60 < bad.size]
+    bad[idx] ^= 0x5A
+    dbad = to_dev(bad, dev)
+    tcp_amd.ipv4_batch(dbad, doff, off.size, 32768, tcp_amd.IPV4_VERIFY, out, st)
+    want_b, _ = oracle.ipv4_batch(bad.copy(), off, 32768, tcp_amd.IPV4_VERIFY)
+    assert np.array_equal(u16(out), want_b)
+
+
+@pytest.mark.parametrize("name", ["1Mx1500", "1Mx64", "256Kx64KiB"])
+def test_baseline_configs_match_reference_digests(dev, golden, name):
+    """Full-size BASELINE configs, generated on device, vs the reference's own Appendix B digests."""
+    import tcp_amd
+    g = golden["digests"][name]
+    n, L = g["n"], g["seg_len"]
+    data = torch.empty(n * L, dtype=torch.uint8, device=dev)
+    tcp_amd.synth_fill(data, g["seg0"] * L, n * L)
+    ss = torch.empty(n, dtype=torch.int32, device=dev)
+    tcp_amd.synth_pseudo(ss, g["seg0"], n, L)
+    out = u16(tcp_amd.batch_uniform(data, L, L, n, ss))
+    assert oracle.digest(out) == (g["fnv1a64"], g["sum"], g["xor"])
+    assert [f"{v:04x}" for v in out[:4]] == g["first4"] and f"{out[-1]:04x}" == g["last"]
+    # the device generator equals the oracle's generator
+    assert np.array_equal(data[:4096].cpu().numpy(), oracle.gen_stream(g["seg0"] * L, 4096))
+    del data
+
+
+def test_8gpu_config_shard_by_shard(dev, golden):
+    """8M x 1500 as eight contiguous 1M shards, as bench.py --gpus 8 partitions it."""
+    import tcp_amd
+    from bench import shard_range
+    L = 1500
+    parts = []
+    data = torch.empty((1 << 20) * L, dtype=torch.uint8, device=dev)
+    ss = torch.empty(1 << 20, dtype=torch.int32, device=dev)
+    for k in range(8):
+        s0, cnt = shard_range(8 << 20, 8, k)
+        g = golden["digests"][f"8Mx1500_shard{k}"]
+        assert (s0, cnt) == (g["seg0"], g["n"])
+        tcp_amd.synth_fill(data, s0 * L, cnt * L)
+        tcp_amd.synth_pseudo(ss, s0, cnt, L)
+        out = u16(tcp_amd.batch_uniform(data, L, L, cnt, ss))
+        assert oracle.digest(out) == (g["fnv1a64"], g["sum"], g["xor"]), k
+        parts.append(out)
+    g = golden["digests"]["8Mx1500"]
+    assert oracle.digest(np.concatenate(parts)) == (g["fnv1a64"], g["sum"], g["xor"])
+
+
+def test_synth_fill_unaligned(dev):
+    import tcp_amd
+    buf = torch.zeros(5000, dtype=torch.uint8, device=dev)
+    for off, nb, dst in [(3, 100, 1), (8, 64, 0), (13, 4000, 7)]:
+        buf.zero_()
+        tcp_amd.synth_fill(buf, off, nb, dst_offset=dst)
+        h = buf.cpu().numpy()
+        assert np.array_equal(h[dst:dst + nb], oracle.gen_stream(off, nb))
+        assert not h[:dst].any() and not h[dst + nb:].any()
+
+
+def test_stream_probe_sums(dev):
+    import tcp_amd
+    rng = np.random.default_rng(4)
+    host = rng.integers(0, 2**32, (1 << 20) // 4, dtype=np.uint64).astype(np.uint32)
+    d = to_dev(host.view(np.uint8), dev)
+    out = torch.zeros(1, dtype=torch.int64, device=dev)
+    tcp_amd.stream_probe(d, host.nbytes, out)
+    want = int((host & 0xFFFF).astype(np.uint64).sum() + (host >> 16).astype(np.uint64).sum())
+    assert int(out.item()) == want
+
+
+def test_nondefault_stream(dev):
+    import tcp_amd
+    rng = np.random.default_rng(8)
+    host = rng.integers(0, 256, 1500 * 1000, dtype=np.uint8)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        d = to_dev(host, dev)
+        out = tcp_amd.batch_uniform(d, 1500, 1500, 1000, 5)
+    s.synchronize()
+    assert np.array_equal(u16(out), oracle.batch_uniform(host, 1500, 1500, 1000, 5))
+
+
+def test_host_context_uniform_and_wire(dev):
+    import tcp_amd
+    from tests.packets import build_batch
+    rng = np.random.default_rng(12)
+    host = rng.integers(0, 256, 3 << 20, dtype=np.uint8)
+    ss = rng.integers(0, 393211, 2000, dtype=np.uint32)
+    with tcp_amd.HostContext(0, scratch_bytes=256 << 10) as ctx:   # small scratch -> many pipelined chunks
+        for stride, length, n in [(1500, 1500, 2000), (1501, 1480, 2000), (64, 64, 2000), (70000, 65536, 40)]:
+            s = ss if n <= ss.size else 7
+            got = ctx.batch_uniform(host, stride, length, n, s[:n] if isinstance(s, np.ndarray) else s)
+            assert np.array_equal(got, oracle.batch_uniform(host, stride, length, n,
+                                                            s[:n] if isinstance(s, np.ndarray) else s))
+        region, off, _ = build_batch(rng, 512, malformed=True, odd_offsets=True)
+        ref = region.copy()
+        want_out, want_st = oracle.ipv4_batch(ref, off, 32768, tcp_amd.IPV4_FILL)
+        out, st = ctx.ipv4_batch(region, off, 32768, tcp_amd.IPV4_FILL)
+        assert np.array_equal(st, want_st) and np.array_equal(out, want_out)
+        assert np.array_equal(region, ref)
+        out, st = ctx.ipv4_batch(region, off, 32768, tcp_amd.IPV4_VERIFY)
+        assert np.all(out[st == 0] == 0)
