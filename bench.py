@@ -133,6 +133,7 @@ def main(argv=None) -> int:
     ap.add_argument("--probe", action="store_true", help="also time the read-only stream probe")
     ap.add_argument("--max-blocks", type=int, default=0)
     ap.add_argument("--unroll", type=int, default=0)
+    ap.add_argument("--shape", type=int, default=-1)
     args = ap.parse_args(argv)
 
     import numpy as np
@@ -154,7 +155,7 @@ def main(argv=None) -> int:
     rc, arch = tcp_amd.device_check()
     if rc != 0:
         raise SystemExit(f"bench.py: no usable gfx950 device ({rc}, '{arch}')")
-    tcp_amd.set_tuning(args.max_blocks, args.unroll)
+    tcp_amd.set_tuning(args.max_blocks, args.unroll, args.shape)
 
     per_gpu, L, desc = CONFIGS[args.config]
     total = per_gpu * world
@@ -215,7 +216,8 @@ def main(argv=None) -> int:
 
     probe = None
     if args.probe:
-        pout = torch.zeros(1, dtype=torch.int64, device=device)
+        pout = torch.zeros(tcp_amd.api.PROBE_SLOTS, dtype=torch.int64, device=device)
+        tcp_amd.set_tuning(0, 0, -1)
         nb = (batch_bytes // 16) * 16
         for _ in range(3):
             tcp_amd.stream_probe(bufs[0], nb, pout)

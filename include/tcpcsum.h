@@ -154,22 +154,29 @@ int tcpcsum_synth_pseudo_dev(uint32_t *d_sum_start, uint64_t seg0, uint64_t n, u
 
 /* ------------------------------------------------------ measurement helpers */
 
-/* Read-only streaming probe: d_out[0] = sum of all u32 words of d_src
- * (nbytes multiple of 16, d_src 16-B aligned). The chip's practical HBM read
- * ceiling for this access pattern; reported beside the checksum kernel. */
-int tcpcsum_stream_probe_dev(const void *d_src, uint64_t nbytes, uint64_t *d_out, void *stream);
+/* Read-only streaming probe: the chip's practical HBM read ceiling for the
+ * checksum kernels' access pattern (16-B non-temporal loads, each wave
+ * reading contiguous 1 KiB per instruction), reported beside them.
+ * d_partials: TCPCSUM_PROBE_SLOTS u64 entries; on completion the sum over the
+ * first *n_partials entries equals the sum of the lo16+hi16 halves of every
+ * u32 word of d_src. nbytes multiple of 16, d_src 16-B aligned. */
+#define TCPCSUM_PROBE_SLOTS 8192
+int tcpcsum_stream_probe_dev(const void *d_src, uint64_t nbytes, uint64_t *d_partials,
+                             int *n_partials, void *stream);
 
 /* Host-side planning only (no device work): the kernel the library would use
  * for a uniform batch at device address base. mode: 0 = 16-B aligned, 1 =
  * 4-B aligned, 2 = byte-granular; shape: 0..8 = lane-group shapes covering
  * 4,8,16,32,64,96,128,256,512 chunks, 9 = one wave per long segment;
- * unroll: segments in flight per lane group. */
+ * unroll: segments in flight per lane group; max_blocks: resident grid. */
 int tcpcsum_plan_uniform(uint64_t base, uint64_t stride, uint32_t len, uint64_t n, int *mode,
-                         int *shape, int *unroll);
+                         int *shape, int *unroll, int *max_blocks);
 
-/* Launch-shape override for tuning (0 = built-in default). Affects batch
- * calls issued afterwards from any thread. */
-int tcpcsum_set_tuning(int max_blocks, int unroll);
+/* Launch-shape override for tuning (tools/sweep.py). 0 / -1 = built-in
+ * per-shape defaults. unroll in {0,1,2,4,8}; shape in {-1, 0..9} (a forced
+ * shape that cannot cover the segments is ignored). Affects batch calls
+ * issued afterwards from any thread. */
+int tcpcsum_set_tuning(int max_blocks, int unroll, int shape);
 
 #ifdef __cplusplus
 }

@@ -82,10 +82,11 @@ SIGNATURES = {
     "tcpcsum_ipv4_batch_host": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp, u64, u32, ctypes.c_int, vp, vp]),
     "tcpcsum_synth_fill_dev": (ctypes.c_int, [vp, u64, u64, vp]),
     "tcpcsum_synth_pseudo_dev": (ctypes.c_int, [vp, u64, u64, u32, vp]),
-    "tcpcsum_stream_probe_dev": (ctypes.c_int, [vp, u64, vp, vp]),
-    "tcpcsum_set_tuning": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    "tcpcsum_stream_probe_dev": (ctypes.c_int, [vp, u64, vp, ctypes.POINTER(ctypes.c_int), vp]),
+    "tcpcsum_set_tuning": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "tcpcsum_plan_uniform": (ctypes.c_int, [u64, u64, u32, u64, ctypes.POINTER(ctypes.c_int),
-                                            ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+                                            ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                                            ctypes.POINTER(ctypes.c_int)]),
 }
 
 
@@ -140,16 +141,19 @@ def device_check() -> tuple[int, str]:
     return rc, buf.value.decode()
 
 
-def set_tuning(max_blocks: int = 0, unroll: int = 0) -> None:
-    _check(lib().tcpcsum_set_tuning(int(max_blocks), int(unroll)), "tcpcsum_set_tuning")
+PROBE_SLOTS = 8192
 
 
-def plan_uniform(base_addr: int, stride: int, length: int, n: int) -> tuple[int, int, int]:
-    """(mode, shape, unroll) the library picks for a uniform batch — host logic only."""
-    mode, shape, unroll = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+def set_tuning(max_blocks: int = 0, unroll: int = 0, shape: int = -1) -> None:
+    _check(lib().tcpcsum_set_tuning(int(max_blocks), int(unroll), int(shape)), "tcpcsum_set_tuning")
+
+
+def plan_uniform(base_addr: int, stride: int, length: int, n: int) -> tuple[int, int, int, int]:
+    """(mode, shape, unroll, max_blocks) the library picks for a uniform batch — host logic only."""
+    mode, shape, unroll, mb = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
     _check(lib().tcpcsum_plan_uniform(base_addr, stride, length, n, ctypes.byref(mode), ctypes.byref(shape),
-                                      ctypes.byref(unroll)), "tcpcsum_plan_uniform")
-    return mode.value, shape.value, unroll.value
+                                      ctypes.byref(unroll), ctypes.byref(mb)), "tcpcsum_plan_uniform")
+    return mode.value, shape.value, unroll.value, mb.value
 
 
 # ------------------------------------------------------------------ device batches (torch tensors)
@@ -224,9 +228,15 @@ def synth_pseudo(dst, seg0: int, n: int, seg_len: int, stream=None) -> None:
            "tcpcsum_synth_pseudo_dev")
 
 
-def stream_probe(src, nbytes: int, out, stream=None) -> None:
-    _check(lib().tcpcsum_stream_probe_dev(_dev_ptr(src, "src"), nbytes, _dev_ptr(out, "out"),
-                                          _stream_handle(stream)), "tcpcsum_stream_probe_dev")
+def stream_probe(src, nbytes: int, partials, stream=None) -> int:
+    """Launch the read-only probe; ``partials`` is a device int64 tensor of >= PROBE_SLOTS.
+    Returns how many leading partials the launch writes (their sum = lo16+hi16 word sum)."""
+    if partials.numel() < PROBE_SLOTS:
+        raise ValueError("partials needs PROBE_SLOTS entries")
+    n = ctypes.c_int()
+    _check(lib().tcpcsum_stream_probe_dev(_dev_ptr(src, "src"), nbytes, _dev_ptr(partials, "partials"),
+                                          ctypes.byref(n), _stream_handle(stream)), "tcpcsum_stream_probe_dev")
+    return n.value
 
 
 # ------------------------------------------------------------------ host-memory batches

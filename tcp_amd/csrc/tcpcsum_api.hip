@@ -22,6 +22,7 @@ namespace {
 std::atomic<int> g_last_hip_error{0};
 std::atomic<int> g_max_blocks{0};
 std::atomic<int> g_unroll{0};
+std::atomic<int> g_shape{-1};
 
 constexpr int kMaxDevices = 64;
 std::atomic<int> g_dev_ok[kMaxDevices];   // 0 unknown, 1 gfx950, -1 unusable
@@ -35,6 +36,7 @@ tcpcsum::Tuning tuning() {
     tcpcsum::Tuning t;
     t.max_blocks = g_max_blocks.load(std::memory_order_relaxed);
     t.unroll = g_unroll.load(std::memory_order_relaxed);
+    t.shape = g_shape.load(std::memory_order_relaxed);
     return t;
 }
 
@@ -101,20 +103,24 @@ int tcpcsum_device_check(char* arch, size_t arch_len) {
     return require_device(arch, arch_len);
 }
 
-int tcpcsum_set_tuning(int max_blocks, int unroll) {
-    if (max_blocks < 0 || !(unroll == 0 || unroll == 1 || unroll == 2 || unroll == 4)) return TCPCSUM_EINVAL;
+int tcpcsum_set_tuning(int max_blocks, int unroll, int shape) {
+    if (max_blocks < 0 || !(unroll == 0 || unroll == 1 || unroll == 2 || unroll == 4 || unroll == 8) ||
+        shape < -1 || shape > 9)
+        return TCPCSUM_EINVAL;
     g_max_blocks.store(max_blocks);
     g_unroll.store(unroll);
+    g_shape.store(shape);
     return TCPCSUM_OK;
 }
 
 int tcpcsum_plan_uniform(uint64_t base, uint64_t stride, uint32_t len, uint64_t n, int* mode, int* shape,
-                         int* unroll) {
-    if (!mode || !shape || !unroll || len > (uint32_t)INT_MAX) return TCPCSUM_EINVAL;
-    const tcpcsum::UniformPlan p = tcpcsum::plan_uniform((uintptr_t)base, stride, len, n, g_unroll.load());
+                         int* unroll, int* max_blocks) {
+    if (!mode || !shape || !unroll || !max_blocks || len > (uint32_t)INT_MAX) return TCPCSUM_EINVAL;
+    const tcpcsum::UniformPlan p = tcpcsum::plan_uniform((uintptr_t)base, stride, len, n, tuning());
     *mode = p.mode;
     *shape = p.shape;
     *unroll = p.unroll;
+    *max_blocks = p.max_blocks;
     return TCPCSUM_OK;
 }
 
@@ -170,13 +176,13 @@ int tcpcsum_synth_pseudo_dev(uint32_t* d_sum_start, uint64_t seg0, uint64_t n, u
     return check_launch();
 }
 
-int tcpcsum_stream_probe_dev(const void* d_src, uint64_t nbytes, uint64_t* d_out, void* stream) {
-    if (!d_src || !d_out || (nbytes & 15u) || (((uintptr_t)d_src) & 15u)) return TCPCSUM_EINVAL;
+int tcpcsum_stream_probe_dev(const void* d_src, uint64_t nbytes, uint64_t* d_partials, int* n_partials,
+                             void* stream) {
+    if (!d_src || !d_partials || !n_partials || (nbytes & 15u) || (((uintptr_t)d_src) & 15u))
+        return TCPCSUM_EINVAL;
     int rc = require_device(nullptr, 0);
     if (rc) return rc;
-    hipError_t e = hipMemsetAsync(d_out, 0, sizeof(uint64_t), (hipStream_t)stream);
-    if (e != hipSuccess) return hip_fail(e);
-    tcpcsum::launch_probe((const uint8_t*)d_src, nbytes, d_out, (hipStream_t)stream, tuning());
+    *n_partials = tcpcsum::launch_probe((const uint8_t*)d_src, nbytes, d_partials, (hipStream_t)stream, tuning());
     return check_launch();
 }
 

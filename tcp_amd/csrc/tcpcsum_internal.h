@@ -12,17 +12,22 @@ namespace tcpcsum {
 // resident at once and grid-strides over the batch.
 constexpr int kDefaultMaxBlocks = 2048;
 
+// Slots of tcpcsum_stream_probe_dev's partials array (= its maximum grid).
+constexpr int kProbeSlots = TCPCSUM_PROBE_SLOTS;
+
 struct Tuning {
-    int max_blocks = 0;   // 0 = kDefaultMaxBlocks
-    int unroll = 0;       // 0 = per-shape default; else 1, 2 or 4
+    int max_blocks = 0;   // 0 = per-shape default
+    int unroll = 0;       // 0 = per-shape default; else 1, 2, 4 or 8
+    int shape = -1;       // -1 = auto; else a forced lane-group shape (0..9)
 };
 
 struct UniformPlan {
-    int mode;     // 0: 16-B aligned starts/len, 1: 4-B aligned, 2: byte granular
-    int shape;    // 0..8 segment-group shapes, 9 = one wave per long segment
-    int unroll;   // segments in flight per lane group
+    int mode;        // 0: 16-B aligned starts/len, 1: 4-B aligned, 2: byte granular
+    int shape;       // 0..8 segment-group shapes, 9 = one wave per long segment
+    int unroll;      // segments in flight per lane group (shape 9: 8*unroll chunks per lane per round)
+    int max_blocks;  // resident grid (workgroups of 256 threads)
 };
-UniformPlan plan_uniform(uintptr_t base, uint64_t stride, uint32_t len, uint64_t n, int unroll_override);
+UniformPlan plan_uniform(uintptr_t base, uint64_t stride, uint32_t len, uint64_t n, const Tuning& tu);
 
 void launch_uniform(const uint8_t* base, uint64_t stride, uint32_t len, const uint32_t* ss, uint32_t ss0,
                     uint16_t* out, uint64_t n, hipStream_t s, const Tuning& tu);
@@ -32,6 +37,7 @@ void launch_ipv4(uint8_t* pkts, const uint64_t* off, uint64_t n, uint32_t cap, u
                  uint16_t* out, uint8_t* status, hipStream_t s, const Tuning& tu);
 void launch_synth_fill(uint8_t* dst, uint64_t off, uint64_t nbytes, hipStream_t s);
 void launch_synth_pseudo(uint32_t* ss, uint64_t seg0, uint64_t n, uint32_t seg_len, hipStream_t s);
-void launch_probe(const uint8_t* src, uint64_t nbytes, uint64_t* out, hipStream_t s, const Tuning& tu);
+// returns the grid size (= partials written)
+int launch_probe(const uint8_t* src, uint64_t nbytes, uint64_t* partials, hipStream_t s, const Tuning& tu);
 
 }  // namespace tcpcsum

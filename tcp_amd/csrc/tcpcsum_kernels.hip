@@ -185,15 +185,14 @@ __global__ __launch_bounds__(256) void k_uniform(const uint8_t* __restrict__ bas
     }
 }
 
-// Long segments (more than 512 chunks): one wave per segment, 8 chunk loads
-// per lane per round (8 KiB per wave-round), u32 lane partials flushed to u64
+// Long segments (more than 512 chunks): one wave per segment, C chunk loads
+// per lane per round (C KiB per wave-round), u32 lane partials flushed to u64
 // every round so any length <= INT32_MAX is exact.
-template <int MODE>
+template <int C, int MODE>
 __global__ __launch_bounds__(256) void k_uniform_long(const uint8_t* __restrict__ base, uint64_t stride,
                                                       uint32_t len, const uint32_t* __restrict__ ss,
                                                       uint32_t ss_scalar, uint16_t* __restrict__ out,
                                                       uint64_t n) {
-    constexpr int C = 8;
     const int lane = threadIdx.x & 63;
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
     for (uint64_t seg = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6); seg < n; seg += nwaves) {
@@ -379,12 +378,14 @@ __global__ __launch_bounds__(256) void k_synth_pseudo(uint32_t* __restrict__ ss,
 }
 
 // ---------------------------------------------------------------- probe
-// Read-only stream with the checksum kernel's access shape (each wave reads
-// contiguous 1 KiB per load instruction, 8 in flight), summed so it cannot be
-// dead-code eliminated; one 64-bit atomic per wave.
+// Read-only stream with the checksum kernels' access shape (each wave reads
+// contiguous 1 KiB per load instruction, C in flight per lane), summed so it
+// cannot be dead-code eliminated. One plain store of a per-block partial at
+// the end (no atomics: 2048 same-address atomics cost ~25 us on this chip).
+template <int C>
 __global__ __launch_bounds__(256) void k_probe(const uint8_t* __restrict__ src, uint64_t nchunks,
-                                               unsigned long long* __restrict__ out) {
-    constexpr int C = 8;
+                                               uint64_t* __restrict__ partials) {
+    __shared__ uint64_t wsum[4];
     const int lane = threadIdx.x & 63;
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
     const uint64_t ntiles = (nchunks + 64 * C - 1) / (64 * C);
@@ -402,7 +403,9 @@ __global__ __launch_bounds__(256) void k_probe(const uint8_t* __restrict__ src, 
         acc += w;
     }
     acc = group_sum64<64>(acc);
-    if (lane == 0) atomicAdd(out, (unsigned long long)acc);
+    if (lane == 0) wsum[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) partials[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
 }
 
 }  // namespace tcpcsum
@@ -422,9 +425,11 @@ inline unsigned grid_for(uint64_t waves_needed, int max_blocks) {
 template <int G, int C, int U, int MODE>
 void launch_uniform_t(const uint8_t* base, uint64_t stride, uint32_t len, const uint32_t* ss,
                       uint32_t ss0, uint16_t* out, uint64_t n, hipStream_t s, int max_blocks) {
-    constexpr int SPT = (64 / G) * U;
+    // keep at most 32 chunk registers-quads in flight per lane (VGPR budget)
+    constexpr int UE = (C * U > 32) ? (32 / C) : U;
+    constexpr int SPT = (64 / G) * UE;
     const uint64_t ntiles = (n + SPT - 1) / SPT;
-    hipLaunchKernelGGL((k_uniform<G, C, U, MODE>), dim3(grid_for(ntiles, max_blocks)), dim3(256), 0, s,
+    hipLaunchKernelGGL((k_uniform<G, C, UE, MODE>), dim3(grid_for(ntiles, max_blocks)), dim3(256), 0, s,
                        base, stride, len, ss, ss0, out, n);
 }
 
@@ -433,27 +438,34 @@ void launch_uniform_mode(int shape, int unroll, const uint8_t* base, uint64_t st
                          const uint32_t* ss, uint32_t ss0, uint16_t* out, uint64_t n, hipStream_t s,
                          int max_blocks) {
 #define TC_U(G, C, U) launch_uniform_t<G, C, U, MODE>(base, stride, len, ss, ss0, out, n, s, max_blocks)
-#define TC_U3(G, C)                          \
+#define TC_U4(G, C)                          \
     do {                                     \
         if (unroll == 1) TC_U(G, C, 1);      \
         else if (unroll == 2) TC_U(G, C, 2); \
-        else TC_U(G, C, 4);                  \
+        else if (unroll == 4) TC_U(G, C, 4); \
+        else TC_U(G, C, 8);                  \
     } while (0)
     switch (shape) {
-        case 0: TC_U3(4, 1); break;    // <= 4 chunks   (64 B)
-        case 1: TC_U3(8, 1); break;    // <= 8
-        case 2: TC_U3(16, 1); break;   // <= 16
-        case 3: TC_U3(32, 1); break;   // <= 32
-        case 4: TC_U3(64, 1); break;   // <= 64
-        case 5: TC_U3(32, 3); break;   // <= 96         (1500 B)
-        case 6: TC_U3(64, 2); break;   // <= 128
-        case 7: TC_U3(64, 4); break;   // <= 256
-        case 8: TC_U3(64, 8); break;   // <= 512
-        default:
-            hipLaunchKernelGGL((k_uniform_long<MODE>), dim3(grid_for(n, max_blocks)), dim3(256), 0, s,
-                               base, stride, len, ss, ss0, out, n);
+        case 0: TC_U4(4, 1); break;    // <= 4 chunks   (64 B)
+        case 1: TC_U4(8, 1); break;    // <= 8
+        case 2: TC_U4(16, 1); break;   // <= 16
+        case 3: TC_U4(32, 1); break;   // <= 32
+        case 4: TC_U4(64, 1); break;   // <= 64
+        case 5: TC_U4(32, 3); break;   // <= 96         (1500 B)
+        case 6: TC_U4(64, 2); break;   // <= 128
+        case 7: TC_U4(64, 4); break;   // <= 256
+        case 8: TC_U4(64, 8); break;   // <= 512
+        default: {                     // one wave per segment, 8*unroll chunks per lane per round
+            const unsigned g = grid_for(n, max_blocks);
+            if (unroll <= 1)
+                hipLaunchKernelGGL((k_uniform_long<8, MODE>), dim3(g), dim3(256), 0, s, base, stride, len, ss, ss0, out, n);
+            else if (unroll == 2)
+                hipLaunchKernelGGL((k_uniform_long<16, MODE>), dim3(g), dim3(256), 0, s, base, stride, len, ss, ss0, out, n);
+            else
+                hipLaunchKernelGGL((k_uniform_long<32, MODE>), dim3(g), dim3(256), 0, s, base, stride, len, ss, ss0, out, n);
+        }
     }
-#undef TC_U3
+#undef TC_U4
 #undef TC_U
 }
 
@@ -462,11 +474,13 @@ void launch_uniform_mode(int shape, int unroll, const uint8_t* base, uint64_t st
 namespace tcpcsum {
 
 // Segment-group shapes: shape k covers up to kShapeChunks[k] 16-B chunks per
-// segment; kShapeUnroll[k] is the default segments-in-flight per group.
+// segment. Defaults per shape (measured on MI355X, tools/sweep.py; see
+// DESIGN.md): segments-in-flight per group and the resident grid.
 static const uint32_t kShapeChunks[9] = {4, 8, 16, 32, 64, 96, 128, 256, 512};
-static const int kShapeUnroll[10] = {4, 4, 4, 4, 4, 2, 2, 1, 1, 1};
+static const int kShapeUnroll[10] = {4, 4, 4, 4, 4, 4, 2, 1, 1, 1};
+static const int kShapeBlocks[10] = {2048, 2048, 2048, 1024, 1024, 512, 512, 512, 512, 256};
 
-UniformPlan plan_uniform(uintptr_t b, uint64_t stride, uint32_t len, uint64_t n, int unroll_override) {
+UniformPlan plan_uniform(uintptr_t b, uint64_t stride, uint32_t len, uint64_t n, const Tuning& tu) {
     UniformPlan p;
     p.mode = (((b | stride | len) & 15u) == 0) ? M16 : (((b | stride | len) & 3u) == 0) ? M4 : M1;
     // The chunks a segment touches depend on its start mod 16, which repeats
@@ -480,23 +494,25 @@ UniformPlan plan_uniform(uintptr_t b, uint64_t stride, uint32_t len, uint64_t n,
     p.shape = 9;
     for (int k = 0; k < 9; ++k)
         if (nch <= kShapeChunks[k]) { p.shape = k; break; }
-    p.unroll = p.shape == 9 ? 1 : (unroll_override ? unroll_override : kShapeUnroll[p.shape]);
+    // a forced shape is honoured only if it covers the segment
+    if (tu.shape >= 0 && tu.shape <= 9 && (tu.shape == 9 || nch <= kShapeChunks[tu.shape])) p.shape = tu.shape;
+    p.unroll = tu.unroll ? tu.unroll : kShapeUnroll[p.shape];
+    p.max_blocks = tu.max_blocks > 0 ? tu.max_blocks : kShapeBlocks[p.shape];
     return p;
 }
 
 void launch_uniform(const uint8_t* base, uint64_t stride, uint32_t len, const uint32_t* ss, uint32_t ss0,
                     uint16_t* out, uint64_t n, hipStream_t s, const Tuning& tu) {
-    const UniformPlan p = plan_uniform((uintptr_t)base, stride, len, n, tu.unroll);
-    const int max_blocks = tu.max_blocks > 0 ? tu.max_blocks : kDefaultMaxBlocks;
-    if (p.mode == M16) launch_uniform_mode<M16>(p.shape, p.unroll, base, stride, len, ss, ss0, out, n, s, max_blocks);
-    else if (p.mode == M4) launch_uniform_mode<M4>(p.shape, p.unroll, base, stride, len, ss, ss0, out, n, s, max_blocks);
-    else launch_uniform_mode<M1>(p.shape, p.unroll, base, stride, len, ss, ss0, out, n, s, max_blocks);
+    const UniformPlan p = plan_uniform((uintptr_t)base, stride, len, n, tu);
+    if (p.mode == M16) launch_uniform_mode<M16>(p.shape, p.unroll, base, stride, len, ss, ss0, out, n, s, p.max_blocks);
+    else if (p.mode == M4) launch_uniform_mode<M4>(p.shape, p.unroll, base, stride, len, ss, ss0, out, n, s, p.max_blocks);
+    else launch_uniform_mode<M1>(p.shape, p.unroll, base, stride, len, ss, ss0, out, n, s, p.max_blocks);
 }
 
 template <int G, int C>
 static void launch_desc_t(const uint8_t* base, const tcpcsum_desc_t* d, uint64_t n, uint16_t* out,
                           hipStream_t s, int max_blocks) {
-    const uint64_t groups = n, waves = (groups + (64 / G) - 1) / (64 / G);
+    const uint64_t waves = (n + (64 / G) - 1) / (64 / G);
     hipLaunchKernelGGL((k_desc<G, C>), dim3(grid_for(waves, max_blocks)), dim3(256), 0, s, base, d, n, out);
 }
 
@@ -546,12 +562,15 @@ void launch_synth_pseudo(uint32_t* ss, uint64_t seg0, uint64_t n, uint32_t seg_l
     hipLaunchKernelGGL(k_synth_pseudo, dim3((unsigned)blocks), dim3(256), 0, s, ss, seg0, n, len_be);
 }
 
-void launch_probe(const uint8_t* src, uint64_t nbytes, uint64_t* out, hipStream_t s, const Tuning& tu) {
-    const int max_blocks = tu.max_blocks > 0 ? tu.max_blocks : kDefaultMaxBlocks;
+int launch_probe(const uint8_t* src, uint64_t nbytes, uint64_t* partials, hipStream_t s, const Tuning& tu) {
+    const int max_blocks = tu.max_blocks > 0 ? (tu.max_blocks < kProbeSlots ? tu.max_blocks : kProbeSlots) : 512;
     const uint64_t nchunks = nbytes / 16;
-    const uint64_t tiles = (nchunks + 511) / 512;
-    hipLaunchKernelGGL(k_probe, dim3(grid_for(tiles, max_blocks)), dim3(256), 0, s, src, nchunks,
-                       (unsigned long long*)out);
+    const int unroll = tu.unroll ? tu.unroll : 2;
+    const unsigned g = grid_for((nchunks + 64 * 8 * unroll - 1) / (64 * 8 * unroll), max_blocks);
+    if (unroll <= 1) hipLaunchKernelGGL(k_probe<8>, dim3(g), dim3(256), 0, s, src, nchunks, partials);
+    else if (unroll == 2) hipLaunchKernelGGL(k_probe<16>, dim3(g), dim3(256), 0, s, src, nchunks, partials);
+    else hipLaunchKernelGGL(k_probe<32>, dim3(g), dim3(256), 0, s, src, nchunks, partials);
+    return (int)g;
 }
 
 }  // namespace tcpcsum

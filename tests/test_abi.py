@@ -1,6 +1,7 @@
 """CPU: the C-ABI library loads, exports every symbol include/tcpcsum.h declares,
 its host-side logic behaves, and the scalar drop-ins equal the oracle.
 No GPU compute here."""
+import ctypes
 import os
 import random
 import re
@@ -87,10 +88,12 @@ def test_argument_errors_need_no_device():
     assert L.tcpcsum_batch_uniform_dev(1 << 20, 0, 2**31, None, 0, 1 << 20, 5, None) == api.EINVAL
     assert L.tcpcsum_batch_desc_dev(1 << 20, (1 << 20) + 8, 5, 64, 1 << 20, None) == api.EINVAL   # unaligned desc
     assert L.tcpcsum_ipv4_batch_dev(1 << 20, 1 << 20, 5, 1500, 7, None, None, None) == api.EINVAL  # bad mode
-    assert L.tcpcsum_stream_probe_dev(1 << 20, 17, 1 << 20, None) == api.EINVAL
-    assert L.tcpcsum_set_tuning(-1, 0) == api.EINVAL
-    assert L.tcpcsum_set_tuning(0, 3) == api.EINVAL
-    assert L.tcpcsum_set_tuning(0, 0) == api.OK
+    ng = ctypes.c_int()
+    assert L.tcpcsum_stream_probe_dev(1 << 20, 17, 1 << 20, ctypes.byref(ng), None) == api.EINVAL
+    assert L.tcpcsum_set_tuning(-1, 0, -1) == api.EINVAL
+    assert L.tcpcsum_set_tuning(0, 3, -1) == api.EINVAL
+    assert L.tcpcsum_set_tuning(0, 0, 10) == api.EINVAL
+    assert L.tcpcsum_set_tuning(0, 0, -1) == api.OK
     assert L.tcpcsum_batch_uniform_host(None, None, 0, 0, None, 0, None, 0) == api.EINVAL
     assert L.tcpcsum_strerror(api.EHIP) == b"HIP runtime error"
 
@@ -108,23 +111,31 @@ def test_no_device_is_reported_not_faked():
 
 
 @pytest.mark.parametrize("base,stride,length,n,expect", [
-    (0, 1500, 1500, 1 << 20, (1, 5, 2)),       # 1M x 1500: 4-B aligned, 95 chunks -> 32 lanes x 3
-    (0, 64, 64, 1 << 20, (0, 0, 4)),           # 1M x 64: 16-B aligned, 4 lanes
-    (0, 65536, 65536, 1 << 18, (0, 9, 1)),     # 64 KiB: one wave per segment
-    (3, 1501, 1501, 100, (2, 5, 2)),           # byte-granular
-    (0, 1500, 1500, 1, (1, 5, 2)),
-    (12, 64, 64, 8, (1, 1, 4)),                # misaligned 64 B touches 5 chunks
+    (0, 1500, 1500, 1 << 20, (1, 5)),       # 1M x 1500: 4-B aligned, 95 chunks -> 32 lanes x 3
+    (0, 64, 64, 1 << 20, (0, 0)),           # 1M x 64: 16-B aligned, 4 lanes
+    (0, 65536, 65536, 1 << 18, (0, 9)),     # 64 KiB: one wave per segment
+    (3, 1501, 1501, 100, (2, 5)),           # byte-granular
+    (0, 1500, 1500, 1, (1, 5)),
+    (12, 64, 64, 8, (1, 1)),                # misaligned 64 B touches 5 chunks
+    (0, 8192, 8192, 10, (0, 8)),
+    (0, 8208, 8193, 10, (2, 9)),            # 514 chunks -> long kernel
 ])
 def test_plan_uniform(base, stride, length, n, expect):
-    assert api.plan_uniform(base, stride, length, n) == expect
+    mode, shape, unroll, blocks = api.plan_uniform(base, stride, length, n)
+    assert (mode, shape) == expect
+    assert unroll in (1, 2, 4, 8) and 1 <= blocks <= 8192
 
 
-def test_plan_respects_unroll_override():
+def test_plan_respects_overrides():
     try:
-        api.set_tuning(0, 1)
-        assert api.plan_uniform(0, 1500, 1500, 1000)[2] == 1
+        api.set_tuning(100, 1, -1)
+        assert api.plan_uniform(0, 1500, 1500, 1000)[2:] == (1, 100)
+        api.set_tuning(0, 0, 6)                       # G=64 x C=2 covers 95 chunks: honoured
+        assert api.plan_uniform(0, 1500, 1500, 1000)[1] == 6
+        api.set_tuning(0, 0, 0)                       # 4 chunks cannot cover 1500 B: ignored
+        assert api.plan_uniform(0, 1500, 1500, 1000)[1] == 5
     finally:
-        api.set_tuning(0, 0)
+        api.set_tuning(0, 0, -1)
 
 
 def test_c_program_links_the_abi():

@@ -36,9 +36,10 @@ def u16(t) -> np.ndarray:
 
 def test_native_library_is_loaded(dev):
     import tcp_amd
-    path = tcp_amd.lib_path()
+    tcp_amd.lib()
     with open("/proc/self/maps") as f:
-        assert path in f.read() or "libtcpcsum.so" in open("/proc/self/maps").read()
+        maps = f.read()
+    assert "libtcpcsum.so" in maps
 
 
 LENGTHS = [0, 1, 2, 3, 4, 5, 7, 8, 15, 16, 17, 24, 31, 32, 33, 44, 63, 64, 65, 100, 255, 256, 257, 511, 512,
@@ -82,7 +83,7 @@ def test_uniform_all_unrolls_and_grids(dev):
     host = rng.integers(0, 256, 3 << 20, dtype=np.uint8)
     d = to_dev(host, dev)
     try:
-        for unroll in (1, 2, 4):
+        for unroll in (1, 2, 4, 8):
             for max_blocks in (1, 7, 0):
                 tcp_amd.set_tuning(max_blocks, unroll)
                 for length in (64, 60, 1500, 1501, 2000, 8192, 20000):
@@ -91,7 +92,25 @@ def test_uniform_all_unrolls_and_grids(dev):
                     want = oracle.batch_uniform(host, length, length, n, 99)
                     assert np.array_equal(got, want), (unroll, max_blocks, length)
     finally:
-        tcp_amd.set_tuning(0, 0)
+        tcp_amd.set_tuning(0, 0, -1)
+
+
+def test_forced_shapes(dev):
+    import tcp_amd
+    rng = np.random.default_rng(19)
+    host = rng.integers(0, 256, 1 << 21, dtype=np.uint8)
+    d = to_dev(host, dev)
+    try:
+        for shape in range(10):
+            for unroll in (1, 8):
+                tcp_amd.set_tuning(0, unroll, shape)
+                for length, off in ((1500, 0), (1499, 1), (64, 4), (3000, 2)):
+                    n = (1 << 21) // (length + 8) - 1
+                    got = u16(tcp_amd.batch_uniform(d, length + 1, length, n, 3, offset=off))
+                    want = oracle.batch_uniform(host, length + 1, length, n, 3, offset=off)
+                    assert np.array_equal(got, want), (shape, unroll, length, off)
+    finally:
+        tcp_amd.set_tuning(0, 0, -1)
 
 
 def test_two_fold_semantics_above_4g(dev):
@@ -237,10 +256,15 @@ def test_stream_probe_sums(dev):
     rng = np.random.default_rng(4)
     host = rng.integers(0, 2**32, (1 << 20) // 4, dtype=np.uint64).astype(np.uint32)
     d = to_dev(host.view(np.uint8), dev)
-    out = torch.zeros(1, dtype=torch.int64, device=dev)
-    tcp_amd.stream_probe(d, host.nbytes, out)
+    parts = torch.zeros(tcp_amd.api.PROBE_SLOTS, dtype=torch.int64, device=dev)
     want = int((host & 0xFFFF).astype(np.uint64).sum() + (host >> 16).astype(np.uint64).sum())
-    assert int(out.item()) == want
+    for blocks, unroll in ((0, 0), (7, 1), (3000, 4)):
+        tcp_amd.set_tuning(blocks, unroll, -1)
+        try:
+            k = tcp_amd.stream_probe(d, host.nbytes, parts)
+        finally:
+            tcp_amd.set_tuning(0, 0, -1)
+        assert int(parts[:k].sum().item()) == want
 
 
 def test_nondefault_stream(dev):
