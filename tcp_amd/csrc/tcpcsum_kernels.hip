@@ -477,8 +477,8 @@ namespace tcpcsum {
 // segment. Defaults per shape (measured on MI355X, tools/sweep.py; see
 // DESIGN.md): segments-in-flight per group and the resident grid.
 static const uint32_t kShapeChunks[9] = {4, 8, 16, 32, 64, 96, 128, 256, 512};
-static const int kShapeUnroll[10] = {4, 4, 4, 4, 4, 4, 2, 1, 1, 1};
-static const int kShapeBlocks[10] = {2048, 2048, 2048, 1024, 1024, 512, 512, 512, 512, 256};
+static const int kShapeUnroll[10] = {4, 8, 8, 8, 8, 8, 8, 8, 4, 2};
+static const int kShapeBlocks[10] = {4096, 512, 4096, 4096, 4096, 512, 4096, 1024, 2048, 256};
 
 UniformPlan plan_uniform(uintptr_t b, uint64_t stride, uint32_t len, uint64_t n, const Tuning& tu) {
     UniformPlan p;

@@ -20,6 +20,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="1500")
+    ap.add_argument("--len", type=int, default=0, help="custom segment length (total ~1.5 GB)")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--blocks", default="256,512,1024,2048,4096,8192,0")
@@ -30,7 +31,12 @@ def main():
     import torch
     import tcp_amd
     from bench import CONFIGS
-    per, L, _ = CONFIGS[args.config]
+    if args.len:
+        L = args.len
+        per = (1572864000 // L)
+        args.config = f"len{L}"
+    else:
+        per, L, _ = CONFIGS[args.config]
     nbytes = per * L
     rot = max(1, math.ceil((1 << 30) / nbytes)) if nbytes < (1 << 30) else 1
     dev = torch.device("cuda:0")
