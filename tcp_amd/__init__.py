@@ -30,6 +30,7 @@ from .api import (  # noqa: F401
     ipv4_batch,
     lib,
     lib_path,
+    pinned_empty,
     set_tuning,
     stream_probe,
     synth_fill,
@@ -39,6 +40,6 @@ from .api import (  # noqa: F401
 __all__ = [
     "DESC_DTYPE", "IPV4_FILL", "IPV4_VERIFY", "PKT_OK", "PKT_SKIPPED", "TcpCsumError",
     "HostContext", "batch_desc", "batch_uniform", "csum_continue", "device_check",
-    "getPseudoHeaderSum", "ipv4_batch", "lib", "lib_path", "set_tuning", "stream_probe",
+    "getPseudoHeaderSum", "ipv4_batch", "lib", "lib_path", "pinned_empty", "set_tuning", "stream_probe",
     "synth_fill", "synth_pseudo",
 ]

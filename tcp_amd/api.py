@@ -244,6 +244,33 @@ def _np_ptr(a: Optional[np.ndarray]) -> int:
     return 0 if a is None else a.ctypes.data
 
 
+class _Pinned:
+    """Owner of one tcpcsum_host_alloc block; freed when the last view dies."""
+
+    def __init__(self, nbytes: int):
+        self.ptr = lib().tcpcsum_host_alloc(nbytes)
+        if not self.ptr:
+            raise TcpCsumError(ENOMEM, "tcpcsum_host_alloc")
+        self.nbytes = nbytes
+
+    def __del__(self):
+        try:
+            if self.ptr:
+                lib().tcpcsum_host_free(self.ptr)
+                self.ptr = None
+        except Exception:
+            pass
+
+
+def pinned_empty(nbytes: int, dtype=np.uint8) -> np.ndarray:
+    """A numpy array in page-locked host memory (tcpcsum_host_alloc). Host-path
+    calls on such memory run zero-copy: the kernel reads it over PCIe."""
+    owner = _Pinned(max(int(nbytes), 1))
+    raw = (ctypes.c_uint8 * owner.nbytes).from_address(owner.ptr)
+    raw._owner = owner
+    return np.frombuffer(raw, np.uint8)[:nbytes].view(dtype)
+
+
 class HostContext:
     """tcpcsum_ctx_t: host-memory batches (H2D -> kernel -> D2H), synchronous."""
 

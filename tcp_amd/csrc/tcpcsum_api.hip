@@ -314,8 +314,44 @@ void tcpcsum_host_free(void* p) {
     if (p) hipHostFree(p);
 }
 
-// Chunks of segments alternate between two slots (stream + device buffers):
-// the H2D copy of chunk k+1 overlaps the kernel and D2H of chunk k.
+namespace {
+
+// Device-visible address of page-locked (hipHostMalloc / hipHostRegister'ed)
+// host memory, or nullptr for pageable memory. Kernels read and write such
+// memory directly over PCIe ("zero-copy"): no staging copy, only the bytes the
+// kernel touches cross the link.
+void* pinned_dev_ptr(const void* p) {
+    if (!p) return nullptr;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();   // pageable memory: not an error for us
+        return nullptr;
+    }
+    if (a.type == hipMemoryTypeHost && a.devicePointer) return a.devicePointer;
+    return nullptr;
+}
+
+int ensure_pkt_scratch(tcpcsum_ctx* c, uint64_t n, hipStream_t st) {
+    if (n <= c->d_pkt_cap) return TCPCSUM_OK;
+    (void)hipStreamSynchronize(st);
+    if (c->d_off) (void)hipFree(c->d_off);
+    if (c->d_wout) (void)hipFree(c->d_wout);
+    if (c->d_wstat) (void)hipFree(c->d_wstat);
+    c->d_off = nullptr; c->d_wout = nullptr; c->d_wstat = nullptr; c->d_pkt_cap = 0;
+    hipError_t e = hipMalloc(&c->d_off, n * sizeof(uint64_t));
+    if (e == hipSuccess) e = hipMalloc(&c->d_wout, n * sizeof(uint16_t));
+    if (e == hipSuccess) e = hipMalloc(&c->d_wstat, n);
+    if (e != hipSuccess) { g_last_hip_error.store((int)e); return TCPCSUM_ENOMEM; }
+    c->d_pkt_cap = n;
+    return TCPCSUM_OK;
+}
+
+}  // namespace
+
+// Pinned input: one launch reads the segments in host memory directly.
+// Pageable input: chunks of segments alternate between two slots (stream +
+// device buffers), so the H2D copy of chunk k+1 overlaps the kernel and D2H of
+// chunk k.
 int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t stride, uint32_t len,
                                const uint32_t* h_sum_start, uint32_t sum_start, uint16_t* h_out, uint64_t n) {
     if (!c) return TCPCSUM_EINVAL;
@@ -323,15 +359,41 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t st
     if (!h_base || !h_out || len > (uint32_t)INT_MAX) return TCPCSUM_EINVAL;
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard g(c->device);
+    const tcpcsum::Tuning tu = tuning();
+    hipError_t e;
+    int rc;
+    if (const uint8_t* zb = (const uint8_t*)pinned_dev_ptr(h_base)) {
+        hipStream_t st = c->st[0];
+        const uint32_t* zss = nullptr;
+        if (h_sum_start) zss = (const uint32_t*)pinned_dev_ptr(h_sum_start);
+        uint16_t* zout = (uint16_t*)pinned_dev_ptr(h_out);
+        if ((h_sum_start && !zss) || !zout) {   // stage the small arrays
+            rc = ctx_ensure(c, 16, (size_t)n);
+            if (rc) return rc;
+        }
+        if (h_sum_start && !zss) {
+            e = hipMemcpyAsync(c->d_ss[0], h_sum_start, n * sizeof(uint32_t), hipMemcpyHostToDevice, st);
+            if (e != hipSuccess) return hip_fail(e);
+            zss = c->d_ss[0];
+        }
+        tcpcsum::launch_uniform(zb, stride, len, zss, sum_start, zout ? zout : c->d_out[0], n, st, tu);
+        rc = check_launch();
+        if (rc) return rc;
+        if (!zout) {
+            e = hipMemcpyAsync(h_out, c->d_out[0], n * sizeof(uint16_t), hipMemcpyDeviceToHost, st);
+            if (e != hipSuccess) return hip_fail(e);
+        }
+        e = hipStreamSynchronize(st);
+        return e == hipSuccess ? TCPCSUM_OK : hip_fail(e);
+    }
     // segments per chunk: (cnt-1)*stride + len <= scratch (at least one segment)
     uint64_t per = 1;
     if (stride == 0) per = n;
     else if (c->scratch > len) per = (c->scratch - len) / stride + 1;
     if (per > n) per = n;
     const uint64_t chunk_bytes = (per - 1) * stride + len;
-    int rc = ctx_ensure(c, (size_t)chunk_bytes + 16, (size_t)per);
+    rc = ctx_ensure(c, (size_t)chunk_bytes + 16, (size_t)per);
     if (rc) return rc;
-    const tcpcsum::Tuning tu = tuning();
     uint64_t k = 0;
     for (uint64_t s0 = 0; s0 < n; s0 += per, ++k) {
         const int slot = (int)(k & 1);
@@ -342,7 +404,7 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t st
         // keep the device-side start alignment mod 16 equal to the host's so the
         // kernel shape matches what the same batch gets on device memory
         const size_t mis = (uintptr_t)src & 15u;
-        hipError_t e = hipMemcpyAsync(c->d_buf[slot] + mis, src, bytes, hipMemcpyHostToDevice, st);
+        e = hipMemcpyAsync(c->d_buf[slot] + mis, src, bytes, hipMemcpyHostToDevice, st);
         if (e == hipSuccess && h_sum_start)
             e = hipMemcpyAsync(c->d_ss[slot], h_sum_start + s0, cnt * sizeof(uint32_t), hipMemcpyHostToDevice, st);
         if (e != hipSuccess) return hip_fail(e);
@@ -359,12 +421,16 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t st
         }
     }
     for (int i = 0; i < 2; ++i) {
-        hipError_t e = hipStreamSynchronize(c->st[i]);
+        e = hipStreamSynchronize(c->st[i]);
         if (e != hipSuccess) return hip_fail(e);
     }
     return TCPCSUM_OK;
 }
 
+// Pinned packet pool: the kernel reads each packet's bytes over PCIe and (FILL)
+// stores the check field in place in host memory — no staging, no host-side
+// patching. Pageable pool: the region is copied H2D, checksummed, and the
+// results are stored at TCP+16 on the host.
 int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t* c, void* h_pkts, size_t region_bytes, const uint64_t* h_pkt_off,
                             uint64_t n, uint32_t cap, int mode, uint16_t* h_out, uint8_t* h_status) {
     if (!c) return TCPCSUM_EINVAL;
@@ -372,48 +438,55 @@ int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t* c, void* h_pkts, size_t region_bytes,
     if (!h_pkts || !h_pkt_off || !region_bytes || (mode != TCPCSUM_IPV4_FILL && mode != TCPCSUM_IPV4_VERIFY))
         return TCPCSUM_EINVAL;
     if (cap > 65535u) cap = 65535u;
-    // every packet (up to cap bytes, clipped to the region) must lie inside the region
+    // every packet header must lie inside the region; packets whose tot_len
+    // runs past its end are SKIPPED by the kernel (limit = region_bytes)
     for (uint64_t i = 0; i < n; ++i)
         if (h_pkt_off[i] + 20u > region_bytes) return TCPCSUM_EINVAL;
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard g(c->device);
     hipStream_t st = c->st[0];
-    const size_t mis = (uintptr_t)h_pkts & 15u;
-    const size_t need = region_bytes + mis + 65536u;   // slack: a packet's cap may run past the region end
+    int rc = ensure_pkt_scratch(c, n, st);
+    if (rc) return rc;
     hipError_t e = hipSuccess;
+    if (uint8_t* zp = (uint8_t*)pinned_dev_ptr(h_pkts)) {
+        const uint64_t* zoff = (const uint64_t*)pinned_dev_ptr(h_pkt_off);
+        if (!zoff) {
+            e = hipMemcpyAsync(c->d_off, h_pkt_off, n * sizeof(uint64_t), hipMemcpyHostToDevice, st);
+            if (e != hipSuccess) return hip_fail(e);
+            zoff = c->d_off;
+        }
+        uint16_t* zout = h_out ? (uint16_t*)pinned_dev_ptr(h_out) : nullptr;
+        uint8_t* zst = h_status ? (uint8_t*)pinned_dev_ptr(h_status) : nullptr;
+        tcpcsum::launch_ipv4(zp, zoff, n, cap, (uint64_t)region_bytes, mode, zout ? zout : c->d_wout,
+                             zst ? zst : c->d_wstat, st, tuning());
+        rc = check_launch();
+        if (rc) return rc;
+        if (h_out && !zout) e = hipMemcpyAsync(h_out, c->d_wout, n * sizeof(uint16_t), hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess && h_status && !zst) e = hipMemcpyAsync(h_status, c->d_wstat, n, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        return e == hipSuccess ? TCPCSUM_OK : hip_fail(e);
+    }
+    const size_t mis = (uintptr_t)h_pkts & 15u;
+    const size_t need = region_bytes + mis + 16u;
     if (need > c->d_region_bytes) {
-        hipStreamSynchronize(st);
-        if (c->d_region) hipFree(c->d_region);
+        (void)hipStreamSynchronize(st);
+        if (c->d_region) (void)hipFree(c->d_region);
         c->d_region = nullptr;
         c->d_region_bytes = 0;
         e = hipMalloc(&c->d_region, need);
         if (e != hipSuccess) { g_last_hip_error.store((int)e); return TCPCSUM_ENOMEM; }
         c->d_region_bytes = need;
     }
-    if (n > c->d_pkt_cap) {
-        hipStreamSynchronize(st);
-        if (c->d_off) hipFree(c->d_off);
-        if (c->d_wout) hipFree(c->d_wout);
-        if (c->d_wstat) hipFree(c->d_wstat);
-        c->d_off = nullptr; c->d_wout = nullptr; c->d_wstat = nullptr; c->d_pkt_cap = 0;
-        e = hipMalloc(&c->d_off, n * sizeof(uint64_t));
-        if (e == hipSuccess) e = hipMalloc(&c->d_wout, n * sizeof(uint16_t));
-        if (e == hipSuccess) e = hipMalloc(&c->d_wstat, n);
-        if (e != hipSuccess) { g_last_hip_error.store((int)e); return TCPCSUM_ENOMEM; }
-        c->d_pkt_cap = n;
-    }
-    // zero the slack so a malformed tot_len past the region reads zeros, not stale bytes
-    e = hipMemsetAsync(c->d_region + mis + region_bytes, 0, 65536u, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(c->d_region + mis, h_pkts, region_bytes, hipMemcpyHostToDevice, st);
+    e = hipMemcpyAsync(c->d_region + mis, h_pkts, region_bytes, hipMemcpyHostToDevice, st);
     if (e == hipSuccess) e = hipMemcpyAsync(c->d_off, h_pkt_off, n * sizeof(uint64_t), hipMemcpyHostToDevice, st);
     if (e != hipSuccess) return hip_fail(e);
-    // packets whose tot_len runs past the region end are SKIPPED by the kernel
-    tcpcsum::launch_ipv4(c->d_region + mis, c->d_off, n, cap, (uint64_t)region_bytes, mode, c->d_wout, c->d_wstat, st, tuning());
-    int rc = check_launch();
+    tcpcsum::launch_ipv4(c->d_region + mis, c->d_off, n, cap, (uint64_t)region_bytes, mode, c->d_wout, c->d_wstat,
+                         st, tuning());
+    rc = check_launch();
     if (rc) return rc;
     uint16_t* out = h_out;
     uint8_t* stat = h_status;
-    // FILL needs out+status on the host to patch checks in place
+    // FILL needs out+status on the host to store the checks in place
     uint16_t* tmp_out = nullptr;
     uint8_t* tmp_stat = nullptr;
     if (mode == TCPCSUM_IPV4_FILL) {

@@ -1,0 +1,91 @@
+#!/usr/bin/env python3
+"""End-to-end (host-memory) rates of the checksum path: PCIe-inclusive.
+
+The reference's packets start and end in host memory (raw-socket buffers).
+This measures the library's host entry points on MI355X:
+  * tcpcsum_batch_uniform_host over 1M x 1500 B in pageable memory
+    (pipelined H2D -> kernel -> D2H) and in pinned memory (zero-copy: the
+    kernel reads host memory over PCIe);
+  * tcpcsum_ipv4_batch_host FILL on one releaseSend-sized batch (1024 packets
+    of 1500 B, loop.c:27-94) in the reference's pool layout (32 KiB slots) and
+    packed, pageable vs pinned — per-batch latency.
+GPU path only; CPU rates come from bench.py's cpu_baseline.
+
+  python tools/e2e.py  -> one JSON line per measurement
+"""
+import json
+import os
+import statistics
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def best_of(fn, reps):
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return min(ts), statistics.median(ts)
+
+
+def main():
+    import numpy as np
+    import torch
+    import tcp_amd
+    from tests.packets import build_batch
+
+    rng = np.random.default_rng(1)
+    n, L = 1 << 20, 1500
+    nbytes = n * L
+    ctx = tcp_amd.HostContext(0)
+    pageable = np.empty(nbytes, np.uint8)
+    pageable[:] = rng.integers(0, 256, nbytes, dtype=np.uint8)
+    pinned = tcp_amd.pinned_empty(nbytes)
+    pinned[:] = pageable
+    ss = rng.integers(0, 393211, n, dtype=np.uint32)
+
+    for name, buf in (("pageable", pageable), ("pinned_zero_copy", pinned)):
+        ctx.batch_uniform(buf, L, L, n, ss)   # warm
+        tmin, tmed = best_of(lambda: ctx.batch_uniform(buf, L, L, n, ss), 5)
+        print(json.dumps({"measure": "uniform_host_1Mx1500", "memory": name, "best_s": round(tmin, 5),
+                          "GiB/s_best": round(nbytes / tmin / 2**30, 2),
+                          "GiB/s_median": round(nbytes / tmed / 2**30, 2)}), flush=True)
+
+    # raw PCIe reference: one pinned H2D copy of the same bytes
+    dst = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    src = torch.from_numpy(pinned)
+    dst.copy_(src, non_blocking=True)
+    torch.cuda.synchronize()
+
+    def h2d():
+        dst.copy_(src, non_blocking=True)
+        torch.cuda.synchronize()
+    tmin, _ = best_of(h2d, 5)
+    print(json.dumps({"measure": "raw_h2d_pinned_copy", "GiB/s_best": round(nbytes / tmin / 2**30, 2)}), flush=True)
+    del dst
+
+    # one releaseSend batch: 1024 packets, 1456-B payload -> 1500-B IP packets
+    for layout, slot in (("pool_32KiB_slots", 32768), ("packed_1500B", 1500)):
+        region, off, _ = build_batch(rng, 1024, slot=32768, max_payload=1456)
+        pkts = [region[o:o + 1500].copy() for o in off]
+        reg = np.zeros(1024 * slot, np.uint8)
+        offs = np.arange(1024, dtype=np.uint64) * np.uint64(slot)
+        for i, p in enumerate(pkts):
+            reg[i * slot:i * slot + p.size] = p
+        pin = tcp_amd.pinned_empty(reg.size)
+        pin[:] = reg
+        for name, r in (("pageable", reg), ("pinned_zero_copy", pin)):
+            ctx.ipv4_batch(r, offs, 32768, tcp_amd.IPV4_FILL)
+            tmin, tmed = best_of(lambda: ctx.ipv4_batch(r, offs, 32768, tcp_amd.IPV4_FILL), 50)
+            print(json.dumps({"measure": "ipv4_fill_host_1024x1500", "layout": layout, "memory": name,
+                              "us_best": round(tmin * 1e6, 1), "us_median": round(tmed * 1e6, 1),
+                              "region_bytes": int(r.size),
+                              "GiB/s_packet_bytes_median": round(1024 * 1500 / tmed / 2**30, 2)}), flush=True)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
