@@ -136,6 +136,7 @@ def main(argv=None) -> int:
     ap.add_argument("--max-blocks", type=int, default=0)
     ap.add_argument("--unroll", type=int, default=0)
     ap.add_argument("--shape", type=int, default=-1)
+    ap.add_argument("--flags", type=int, default=0, help="TCPCSUM_TUNE_* bits")
     args = ap.parse_args(argv)
 
     import numpy as np
@@ -157,7 +158,7 @@ def main(argv=None) -> int:
     rc, arch = tcp_amd.device_check()
     if rc != 0:
         raise SystemExit(f"bench.py: no usable gfx950 device ({rc}, '{arch}')")
-    tcp_amd.set_tuning(args.max_blocks, args.unroll, args.shape)
+    tcp_amd.set_tuning(args.max_blocks, args.unroll, args.shape, args.flags)
 
     per_gpu, L, desc = CONFIGS[args.config]
     total = per_gpu * world
@@ -219,7 +220,7 @@ def main(argv=None) -> int:
     probe = None
     if args.probe:
         pout = torch.zeros(tcp_amd.api.PROBE_SLOTS, dtype=torch.int64, device=device)
-        tcp_amd.set_tuning(0, 0, -1)
+        tcp_amd.set_tuning(0, 0, -1, 0)
         nb = (batch_bytes // 16) * 16
         for _ in range(3):
             tcp_amd.stream_probe(bufs[0], nb, pout)

@@ -174,9 +174,13 @@ int tcpcsum_plan_uniform(uint64_t base, uint64_t stride, uint32_t len, uint64_t 
 
 /* Launch-shape override for tuning (tools/sweep.py). 0 / -1 = built-in
  * per-shape defaults. unroll in {0,1,2,4,8}; shape in {-1, 0..9} (a forced
- * shape that cannot cover the segments is ignored). Affects batch calls
- * issued afterwards from any thread. */
-int tcpcsum_set_tuning(int max_blocks, int unroll, int shape);
+ * shape that cannot cover the segments is ignored); flags: TCPCSUM_TUNE_*
+ * bits (0 = defaults). Affects batch calls issued afterwards from any thread. */
+#define TCPCSUM_TUNE_PIPE_ON 1   /* software-pipelined tiles */
+#define TCPCSUM_TUNE_PIPE_OFF 2
+#define TCPCSUM_TUNE_NT_ON 4     /* non-temporal loads */
+#define TCPCSUM_TUNE_NT_OFF 8
+int tcpcsum_set_tuning(int max_blocks, int unroll, int shape, int flags);
 
 #ifdef __cplusplus
 }

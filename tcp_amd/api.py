@@ -83,7 +83,7 @@ SIGNATURES = {
     "tcpcsum_synth_fill_dev": (ctypes.c_int, [vp, u64, u64, vp]),
     "tcpcsum_synth_pseudo_dev": (ctypes.c_int, [vp, u64, u64, u32, vp]),
     "tcpcsum_stream_probe_dev": (ctypes.c_int, [vp, u64, vp, ctypes.POINTER(ctypes.c_int), vp]),
-    "tcpcsum_set_tuning": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "tcpcsum_set_tuning": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "tcpcsum_plan_uniform": (ctypes.c_int, [u64, u64, u32, u64, ctypes.POINTER(ctypes.c_int),
                                             ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                                             ctypes.POINTER(ctypes.c_int)]),
@@ -142,10 +142,11 @@ def device_check() -> tuple[int, str]:
 
 
 PROBE_SLOTS = 8192
+TUNE_PIPE_ON, TUNE_PIPE_OFF, TUNE_NT_ON, TUNE_NT_OFF = 1, 2, 4, 8
 
 
-def set_tuning(max_blocks: int = 0, unroll: int = 0, shape: int = -1) -> None:
-    _check(lib().tcpcsum_set_tuning(int(max_blocks), int(unroll), int(shape)), "tcpcsum_set_tuning")
+def set_tuning(max_blocks: int = 0, unroll: int = 0, shape: int = -1, flags: int = 0) -> None:
+    _check(lib().tcpcsum_set_tuning(int(max_blocks), int(unroll), int(shape), int(flags)), "tcpcsum_set_tuning")
 
 
 def plan_uniform(base_addr: int, stride: int, length: int, n: int) -> tuple[int, int, int, int]:

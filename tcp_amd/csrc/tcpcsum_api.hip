@@ -23,6 +23,7 @@ std::atomic<int> g_last_hip_error{0};
 std::atomic<int> g_max_blocks{0};
 std::atomic<int> g_unroll{0};
 std::atomic<int> g_shape{-1};
+std::atomic<int> g_flags{0};
 
 constexpr int kMaxDevices = 64;
 std::atomic<int> g_dev_ok[kMaxDevices];   // 0 unknown, 1 gfx950, -1 unusable
@@ -37,6 +38,7 @@ tcpcsum::Tuning tuning() {
     t.max_blocks = g_max_blocks.load(std::memory_order_relaxed);
     t.unroll = g_unroll.load(std::memory_order_relaxed);
     t.shape = g_shape.load(std::memory_order_relaxed);
+    t.flags = g_flags.load(std::memory_order_relaxed);
     return t;
 }
 
@@ -103,13 +105,14 @@ int tcpcsum_device_check(char* arch, size_t arch_len) {
     return require_device(arch, arch_len);
 }
 
-int tcpcsum_set_tuning(int max_blocks, int unroll, int shape) {
+int tcpcsum_set_tuning(int max_blocks, int unroll, int shape, int flags) {
     if (max_blocks < 0 || !(unroll == 0 || unroll == 1 || unroll == 2 || unroll == 4 || unroll == 8) ||
-        shape < -1 || shape > 9)
+        shape < -1 || shape > 9 || (flags & ~15) || (flags & 3) == 3 || (flags & 12) == 12)
         return TCPCSUM_EINVAL;
     g_max_blocks.store(max_blocks);
     g_unroll.store(unroll);
     g_shape.store(shape);
+    g_flags.store(flags);
     return TCPCSUM_OK;
 }
 

@@ -19,6 +19,7 @@ struct Tuning {
     int max_blocks = 0;   // 0 = per-shape default
     int unroll = 0;       // 0 = per-shape default; else 1, 2, 4 or 8
     int shape = -1;       // -1 = auto; else a forced lane-group shape (0..9)
+    int flags = 0;        // TCPCSUM_TUNE_* bits
 };
 
 struct UniformPlan {
@@ -26,6 +27,8 @@ struct UniformPlan {
     int shape;       // 0..8 segment-group shapes, 9 = one wave per long segment
     int unroll;      // segments in flight per lane group (shape 9: 8*unroll chunks per lane per round)
     int max_blocks;  // resident grid (workgroups of 256 threads)
+    bool pipe;       // software-pipelined tiles
+    bool nt;         // non-temporal loads
 };
 UniformPlan plan_uniform(uintptr_t base, uint64_t stride, uint32_t len, uint64_t n, const Tuning& tu);
 

@@ -130,24 +130,27 @@ __device__ __forceinline__ uint64_t combine(uint64_t start, uint64_t W, uint64_t
 // ---------------------------------------------------------------- uniform
 // Segment i at base + i*stride, all of length len; n segments.
 // G lanes per segment, C chunk loads per lane per segment (G*C >= chunks a
-// segment can touch), U segments per group in flight per iteration.
+// segment can touch), U segments per group in flight per tile.
 // A wave tile = (64/G)*U consecutive segments; load instruction (u, k) of the
 // wave reads chunk k*G+gl of segments tile+u*(64/G)+q — consecutive segments
 // across groups, i.e. one contiguous run of memory.
-template <int G, int C, int U, int MODE>
-__global__ __launch_bounds__(256) void k_uniform(const uint8_t* __restrict__ base, uint64_t stride,
-                                                 uint32_t len, const uint32_t* __restrict__ ss,
-                                                 uint32_t ss_scalar, uint16_t* __restrict__ out,
-                                                 uint64_t n) {
-    constexpr int GPW = 64 / G;
-    constexpr int SPT = GPW * U;
-    const int lane = threadIdx.x & 63;
-    const int q = lane / G, gl = lane % G;
-    const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
-    const uint64_t ntiles = (n + SPT - 1) / SPT;
-    for (uint64_t t = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6); t < ntiles; t += nwaves) {
-        u32x4 v[U][C];
-        uint32_t st[U], mm[U];
+template <bool NT>
+__device__ __forceinline__ u32x4 ldq(const uint8_t* p) {
+    if constexpr (NT) return ld16(p);
+    else return *reinterpret_cast<const u32x4*>(p);
+}
+
+template <int G, int C, int U, int MODE, bool NT>
+struct UniformTile {
+    static constexpr int GPW = 64 / G;
+    static constexpr int SPT = GPW * U;
+    u32x4 v[U][C];
+    uint32_t st[U], mm[U];
+
+    // issue every load of tile t (chunks, and the start values for lane 0 of each group)
+    __device__ __forceinline__ void load(uint64_t t, const uint8_t* __restrict__ base, uint64_t stride,
+                                         uint32_t len, const uint32_t* __restrict__ ss, uint32_t ss_scalar,
+                                         uint64_t n, int q, int gl) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint64_t seg = t * SPT + (uint64_t)(u * GPW + q);
@@ -161,9 +164,15 @@ __global__ __launch_bounds__(256) void k_uniform(const uint8_t* __restrict__ bas
 #pragma unroll
             for (int k = 0; k < C; ++k) {
                 const uint32_t idx = (uint32_t)(k * G + gl);
-                v[u][k] = (live && idx < nch) ? ld16(a0 + (uint64_t)idx * 16u) : u32x4{0u, 0u, 0u, 0u};
+                v[u][k] = (live && idx < nch) ? ldq<NT>(a0 + (uint64_t)idx * 16u) : u32x4{0u, 0u, 0u, 0u};
             }
         }
+    }
+
+    // sum, reduce over each group, fold, store
+    __device__ __forceinline__ void finish(uint64_t t, const uint8_t* __restrict__ base, uint64_t stride,
+                                           uint32_t len, uint16_t* __restrict__ out, uint64_t n, int q,
+                                           int gl) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint64_t seg = t * SPT + (uint64_t)(u * GPW + q);
@@ -183,49 +192,119 @@ __global__ __launch_bounds__(256) void k_uniform(const uint8_t* __restrict__ bas
             if (gl == 0 && seg < n) out[seg] = fold_ref(combine(st[u], w, o, odd));
         }
     }
+};
+
+// PIPE: software-pipelined over the wave's tiles — the loads of tile t+nwaves
+// are in flight while tile t is summed and stored (two register tiles).
+template <int G, int C, int U, int MODE, bool PIPE, bool NT>
+__global__ __launch_bounds__(256) void k_uniform(const uint8_t* __restrict__ base, uint64_t stride,
+                                                 uint32_t len, const uint32_t* __restrict__ ss,
+                                                 uint32_t ss_scalar, uint16_t* __restrict__ out,
+                                                 uint64_t n) {
+    using Tile = UniformTile<G, C, U, MODE, NT>;
+    const int lane = threadIdx.x & 63;
+    const int q = lane / G, gl = lane % G;
+    const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
+    const uint64_t ntiles = (n + Tile::SPT - 1) / Tile::SPT;
+    uint64_t t = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
+    if constexpr (!PIPE) {
+        Tile a;
+        for (; t < ntiles; t += nwaves) {
+            a.load(t, base, stride, len, ss, ss_scalar, n, q, gl);
+            a.finish(t, base, stride, len, out, n, q, gl);
+        }
+    } else {
+        Tile a, b;
+        if (t < ntiles) a.load(t, base, stride, len, ss, ss_scalar, n, q, gl);
+        while (t < ntiles) {
+            const uint64_t t2 = t + nwaves;
+            if (t2 < ntiles) b.load(t2, base, stride, len, ss, ss_scalar, n, q, gl);
+            a.finish(t, base, stride, len, out, n, q, gl);
+            if (t2 >= ntiles) break;
+            const uint64_t t3 = t2 + nwaves;
+            if (t3 < ntiles) a.load(t3, base, stride, len, ss, ss_scalar, n, q, gl);
+            b.finish(t2, base, stride, len, out, n, q, gl);
+            t = t3;
+        }
+    }
 }
 
 // Long segments (more than 512 chunks): one wave per segment, C chunk loads
 // per lane per round (C KiB per wave-round), u32 lane partials flushed to u64
-// every round so any length <= INT32_MAX is exact.
-template <int C, int MODE>
+// every round so any length <= INT32_MAX is exact. The wave's work is the flat
+// sequence of (segment, round) items; with PIPE the loads of item j+1 are in
+// flight while item j is summed, across segment boundaries too.
+template <int C, int MODE, bool PIPE, bool NT>
 __global__ __launch_bounds__(256) void k_uniform_long(const uint8_t* __restrict__ base, uint64_t stride,
-                                                      uint32_t len, const uint32_t* __restrict__ ss,
-                                                      uint32_t ss_scalar, uint16_t* __restrict__ out,
-                                                      uint64_t n) {
+                                                      uint32_t len, uint32_t rounds,
+                                                      const uint32_t* __restrict__ ss, uint32_t ss_scalar,
+                                                      uint16_t* __restrict__ out, uint64_t n) {
     const int lane = threadIdx.x & 63;
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
-    for (uint64_t seg = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6); seg < n; seg += nwaves) {
-        const uint8_t* p = base + seg * stride;
+    uint64_t seg = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
+    if (seg >= n) return;
+    uint32_t r = 0;
+    uint64_t W = 0, O = 0;
+    u32x4 va[C], vb[C];
+    auto load = [&](u32x4 (&v)[C], uint64_t sg, uint32_t rr) {
+        const uint8_t* p = base + sg * stride;
         const uint32_t m = (uint32_t)((uintptr_t)p & 15u);
         const uint8_t* a0 = p - m;
         const uint32_t nch = (uint32_t)(((uint64_t)m + len + 15u) >> 4);
-        const bool odd = (MODE == M1) && ((uintptr_t)p & 1u);
-        const uint32_t st = ss ? ss[seg] : ss_scalar;
-        uint64_t W = 0, O = 0;
-        for (uint32_t r = 0; r < nch; r += 64u * C) {
-            u32x4 v[C];
 #pragma unroll
-            for (int k = 0; k < C; ++k) {
-                const uint32_t idx = r + (uint32_t)(k * 64 + lane);
-                v[k] = idx < nch ? ld16(a0 + (uint64_t)idx * 16u) : u32x4{0u, 0u, 0u, 0u};
-            }
-            uint32_t w = 0, o = 0;
-#pragma unroll
-            for (int k = 0; k < C; ++k) {
-                const uint32_t idx = r + (uint32_t)(k * 64 + lane);
-                const uint32_t rel = idx * 16u - m;
-                if constexpr (MODE == M1)
-                    chunk_wo_bytes(v[k], (int64_t)idx * 16 - (int64_t)m, (int64_t)len, odd, w, o);
-                else
-                    w += chunk_w<MODE>(v[k], rel, len);
-            }
-            W += w;
-            O += o;
+        for (int k = 0; k < C; ++k) {
+            const uint32_t idx = rr * (64u * C) + (uint32_t)(k * 64 + lane);
+            v[k] = idx < nch ? ldq<NT>(a0 + (uint64_t)idx * 16u) : u32x4{0u, 0u, 0u, 0u};
         }
-        W = group_sum64<64>(W);
-        if constexpr (MODE == M1) O = group_sum64<64>(O);
-        if (lane == 0) out[seg] = fold_ref(combine(st, W, O, odd));
+    };
+    // sum item (sg, rr); on its last round reduce, fold and store
+    auto consume = [&](const u32x4 (&v)[C], uint64_t sg, uint32_t rr) {
+        const uint8_t* p = base + sg * stride;
+        const uint32_t m = (uint32_t)((uintptr_t)p & 15u);
+        const bool odd = (MODE == M1) && ((uintptr_t)p & 1u);
+        uint32_t w = 0, o = 0;
+#pragma unroll
+        for (int k = 0; k < C; ++k) {
+            const uint32_t idx = rr * (64u * C) + (uint32_t)(k * 64 + lane);
+            if constexpr (MODE == M1)
+                chunk_wo_bytes(v[k], (int64_t)idx * 16 - (int64_t)m, (int64_t)len, odd, w, o);
+            else
+                w += chunk_w<MODE>(v[k], idx * 16u - m, len);
+        }
+        W += w;
+        O += o;
+        if (rr + 1 == rounds) {
+            const uint64_t Wt = group_sum64<64>(W);
+            const uint64_t Ot = (MODE == M1) ? group_sum64<64>(O) : 0;
+            if (lane == 0) out[sg] = fold_ref(combine(ss ? ss[sg] : ss_scalar, Wt, Ot, odd));
+            W = 0;
+            O = 0;
+        }
+    };
+    auto next = [&](uint64_t& sg, uint32_t& rr) {
+        if (++rr == rounds) { rr = 0; sg += nwaves; }
+    };
+    if constexpr (!PIPE) {
+        for (; seg < n; next(seg, r)) {
+            load(va, seg, r);
+            consume(va, seg, r);
+        }
+    } else {
+        uint64_t s1 = seg;
+        uint32_t r1 = r;
+        load(va, seg, r);
+        while (true) {
+            next(s1, r1);
+            if (s1 < n) load(vb, s1, r1);
+            consume(va, seg, r);
+            if (s1 >= n) break;
+            seg = s1; r = r1;
+            next(s1, r1);
+            if (s1 < n) load(va, s1, r1);
+            consume(vb, seg, r);
+            if (s1 >= n) break;
+            seg = s1; r = r1;
+        }
     }
 }
 
@@ -422,22 +501,38 @@ inline unsigned grid_for(uint64_t waves_needed, int max_blocks) {
     return (unsigned)blocks;
 }
 
-template <int G, int C, int U, int MODE>
+template <int G, int C, int U, int MODE, bool PIPE, bool NT>
 void launch_uniform_t(const uint8_t* base, uint64_t stride, uint32_t len, const uint32_t* ss,
                       uint32_t ss0, uint16_t* out, uint64_t n, hipStream_t s, int max_blocks) {
-    // keep at most 32 chunk registers-quads in flight per lane (VGPR budget)
-    constexpr int UE = (C * U > 32) ? (32 / C) : U;
+    // VGPR budget: at most 32 chunk quads per lane (16 per buffer when pipelined)
+    constexpr int LIM = PIPE ? 16 : 32;
+    constexpr int UE = (C * U > LIM) ? (LIM / C > 0 ? LIM / C : 1) : U;
     constexpr int SPT = (64 / G) * UE;
     const uint64_t ntiles = (n + SPT - 1) / SPT;
-    hipLaunchKernelGGL((k_uniform<G, C, UE, MODE>), dim3(grid_for(ntiles, max_blocks)), dim3(256), 0, s,
-                       base, stride, len, ss, ss0, out, n);
+    hipLaunchKernelGGL((k_uniform<G, C, UE, MODE, PIPE, NT>), dim3(grid_for(ntiles, max_blocks)), dim3(256), 0,
+                       s, base, stride, len, ss, ss0, out, n);
 }
 
-template <int MODE>
+template <int C, int MODE, bool PIPE, bool NT>
+void launch_long_t(const uint8_t* base, uint64_t stride, uint32_t len, const uint32_t* ss, uint32_t ss0,
+                   uint16_t* out, uint64_t n, hipStream_t s, int max_blocks) {
+    // rounds per segment: enough for the worst start alignment in the batch
+    uint64_t nch = 0;
+    for (uint64_t i = 0; i < 16 && i < n; ++i) {
+        const uint64_t c = ((((uintptr_t)base + i * stride) & 15u) + len + 15u) >> 4;
+        if (c > nch) nch = c;
+    }
+    const uint32_t rounds = (uint32_t)((nch + 64u * C - 1) / (64u * C));
+    if (rounds == 0) return;
+    hipLaunchKernelGGL((k_uniform_long<C, MODE, PIPE, NT>), dim3(grid_for(n, max_blocks)), dim3(256), 0, s, base,
+                       stride, len, rounds, ss, ss0, out, n);
+}
+
+template <int MODE, bool PIPE, bool NT>
 void launch_uniform_mode(int shape, int unroll, const uint8_t* base, uint64_t stride, uint32_t len,
                          const uint32_t* ss, uint32_t ss0, uint16_t* out, uint64_t n, hipStream_t s,
                          int max_blocks) {
-#define TC_U(G, C, U) launch_uniform_t<G, C, U, MODE>(base, stride, len, ss, ss0, out, n, s, max_blocks)
+#define TC_U(G, C, U) launch_uniform_t<G, C, U, MODE, PIPE, NT>(base, stride, len, ss, ss0, out, n, s, max_blocks)
 #define TC_U4(G, C)                          \
     do {                                     \
         if (unroll == 1) TC_U(G, C, 1);      \
@@ -445,6 +540,7 @@ void launch_uniform_mode(int shape, int unroll, const uint8_t* base, uint64_t st
         else if (unroll == 4) TC_U(G, C, 4); \
         else TC_U(G, C, 8);                  \
     } while (0)
+#define TC_L(C) launch_long_t<C, MODE, PIPE, NT>(base, stride, len, ss, ss0, out, n, s, max_blocks)
     switch (shape) {
         case 0: TC_U4(4, 1); break;    // <= 4 chunks   (64 B)
         case 1: TC_U4(8, 1); break;    // <= 8
@@ -455,16 +551,12 @@ void launch_uniform_mode(int shape, int unroll, const uint8_t* base, uint64_t st
         case 6: TC_U4(64, 2); break;   // <= 128
         case 7: TC_U4(64, 4); break;   // <= 256
         case 8: TC_U4(64, 8); break;   // <= 512
-        default: {                     // one wave per segment, 8*unroll chunks per lane per round
-            const unsigned g = grid_for(n, max_blocks);
-            if (unroll <= 1)
-                hipLaunchKernelGGL((k_uniform_long<8, MODE>), dim3(g), dim3(256), 0, s, base, stride, len, ss, ss0, out, n);
-            else if (unroll == 2)
-                hipLaunchKernelGGL((k_uniform_long<16, MODE>), dim3(g), dim3(256), 0, s, base, stride, len, ss, ss0, out, n);
-            else
-                hipLaunchKernelGGL((k_uniform_long<32, MODE>), dim3(g), dim3(256), 0, s, base, stride, len, ss, ss0, out, n);
-        }
+        default:                       // one wave per segment, 8*unroll chunks per lane per round
+            if (unroll <= 1) TC_L(8);
+            else if (unroll == 2 || PIPE) TC_L(16);
+            else TC_L(32);
     }
+#undef TC_L
 #undef TC_U4
 #undef TC_U
 }
@@ -479,6 +571,8 @@ namespace tcpcsum {
 static const uint32_t kShapeChunks[9] = {4, 8, 16, 32, 64, 96, 128, 256, 512};
 static const int kShapeUnroll[10] = {4, 8, 8, 8, 8, 8, 8, 8, 4, 2};
 static const int kShapeBlocks[10] = {4096, 512, 4096, 4096, 4096, 512, 4096, 1024, 2048, 256};
+static const bool kShapePipe[10] = {false, false, false, false, false, false, false, false, false, false};
+static const bool kShapeNt[10] = {true, true, true, true, true, true, true, true, true, true};
 
 UniformPlan plan_uniform(uintptr_t b, uint64_t stride, uint32_t len, uint64_t n, const Tuning& tu) {
     UniformPlan p;
@@ -498,15 +592,29 @@ UniformPlan plan_uniform(uintptr_t b, uint64_t stride, uint32_t len, uint64_t n,
     if (tu.shape >= 0 && tu.shape <= 9 && (tu.shape == 9 || nch <= kShapeChunks[tu.shape])) p.shape = tu.shape;
     p.unroll = tu.unroll ? tu.unroll : kShapeUnroll[p.shape];
     p.max_blocks = tu.max_blocks > 0 ? tu.max_blocks : kShapeBlocks[p.shape];
+    p.pipe = tu.flags & TCPCSUM_TUNE_PIPE_ON ? true : tu.flags & TCPCSUM_TUNE_PIPE_OFF ? false : kShapePipe[p.shape];
+    p.nt = tu.flags & TCPCSUM_TUNE_NT_ON ? true : tu.flags & TCPCSUM_TUNE_NT_OFF ? false : kShapeNt[p.shape];
     return p;
+}
+
+template <bool PIPE, bool NT>
+static void launch_uniform_pn(const UniformPlan& p, const uint8_t* base, uint64_t stride, uint32_t len,
+                              const uint32_t* ss, uint32_t ss0, uint16_t* out, uint64_t n, hipStream_t s) {
+    if (p.mode == M16)
+        launch_uniform_mode<M16, PIPE, NT>(p.shape, p.unroll, base, stride, len, ss, ss0, out, n, s, p.max_blocks);
+    else if (p.mode == M4)
+        launch_uniform_mode<M4, PIPE, NT>(p.shape, p.unroll, base, stride, len, ss, ss0, out, n, s, p.max_blocks);
+    else
+        launch_uniform_mode<M1, PIPE, NT>(p.shape, p.unroll, base, stride, len, ss, ss0, out, n, s, p.max_blocks);
 }
 
 void launch_uniform(const uint8_t* base, uint64_t stride, uint32_t len, const uint32_t* ss, uint32_t ss0,
                     uint16_t* out, uint64_t n, hipStream_t s, const Tuning& tu) {
     const UniformPlan p = plan_uniform((uintptr_t)base, stride, len, n, tu);
-    if (p.mode == M16) launch_uniform_mode<M16>(p.shape, p.unroll, base, stride, len, ss, ss0, out, n, s, p.max_blocks);
-    else if (p.mode == M4) launch_uniform_mode<M4>(p.shape, p.unroll, base, stride, len, ss, ss0, out, n, s, p.max_blocks);
-    else launch_uniform_mode<M1>(p.shape, p.unroll, base, stride, len, ss, ss0, out, n, s, p.max_blocks);
+    if (p.pipe && p.nt) launch_uniform_pn<true, true>(p, base, stride, len, ss, ss0, out, n, s);
+    else if (p.pipe) launch_uniform_pn<true, false>(p, base, stride, len, ss, ss0, out, n, s);
+    else if (p.nt) launch_uniform_pn<false, true>(p, base, stride, len, ss, ss0, out, n, s);
+    else launch_uniform_pn<false, false>(p, base, stride, len, ss, ss0, out, n, s);
 }
 
 template <int G, int C>

@@ -90,10 +90,12 @@ def test_argument_errors_need_no_device():
     assert L.tcpcsum_ipv4_batch_dev(1 << 20, 1 << 20, 5, 1500, 7, None, None, None) == api.EINVAL  # bad mode
     ng = ctypes.c_int()
     assert L.tcpcsum_stream_probe_dev(1 << 20, 17, 1 << 20, ctypes.byref(ng), None) == api.EINVAL
-    assert L.tcpcsum_set_tuning(-1, 0, -1) == api.EINVAL
-    assert L.tcpcsum_set_tuning(0, 3, -1) == api.EINVAL
-    assert L.tcpcsum_set_tuning(0, 0, 10) == api.EINVAL
-    assert L.tcpcsum_set_tuning(0, 0, -1) == api.OK
+    assert L.tcpcsum_set_tuning(-1, 0, -1, 0) == api.EINVAL
+    assert L.tcpcsum_set_tuning(0, 3, -1, 0) == api.EINVAL
+    assert L.tcpcsum_set_tuning(0, 0, 10, 0) == api.EINVAL
+    assert L.tcpcsum_set_tuning(0, 0, -1, 3) == api.EINVAL      # PIPE_ON | PIPE_OFF
+    assert L.tcpcsum_set_tuning(0, 0, -1, 16) == api.EINVAL
+    assert L.tcpcsum_set_tuning(0, 0, -1, 0) == api.OK
     assert L.tcpcsum_batch_uniform_host(None, None, 0, 0, None, 0, None, 0) == api.EINVAL
     assert L.tcpcsum_strerror(api.EHIP) == b"HIP runtime error"
 
@@ -128,14 +130,14 @@ def test_plan_uniform(base, stride, length, n, expect):
 
 def test_plan_respects_overrides():
     try:
-        api.set_tuning(100, 1, -1)
+        api.set_tuning(100, 1, -1, 0)
         assert api.plan_uniform(0, 1500, 1500, 1000)[2:] == (1, 100)
         api.set_tuning(0, 0, 6)                       # G=64 x C=2 covers 95 chunks: honoured
         assert api.plan_uniform(0, 1500, 1500, 1000)[1] == 6
         api.set_tuning(0, 0, 0)                       # 4 chunks cannot cover 1500 B: ignored
         assert api.plan_uniform(0, 1500, 1500, 1000)[1] == 5
     finally:
-        api.set_tuning(0, 0, -1)
+        api.set_tuning(0, 0, -1, 0)
 
 
 def test_c_program_links_the_abi():

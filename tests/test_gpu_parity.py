@@ -84,15 +84,15 @@ def test_uniform_all_unrolls_and_grids(dev):
     d = to_dev(host, dev)
     try:
         for unroll in (1, 2, 4, 8):
-            for max_blocks in (1, 7, 0):
-                tcp_amd.set_tuning(max_blocks, unroll)
+            for max_blocks, flags in ((1, 1), (7, 0), (0, 1), (0, 2 | 8)):
+                tcp_amd.set_tuning(max_blocks, unroll, -1, flags)
                 for length in (64, 60, 1500, 1501, 2000, 8192, 20000):
                     n = (3 << 20) // (length + 1) - 1
                     got = u16(tcp_amd.batch_uniform(d, length, length, n, 99))
                     want = oracle.batch_uniform(host, length, length, n, 99)
-                    assert np.array_equal(got, want), (unroll, max_blocks, length)
+                    assert np.array_equal(got, want), (unroll, max_blocks, flags, length)
     finally:
-        tcp_amd.set_tuning(0, 0, -1)
+        tcp_amd.set_tuning(0, 0, -1, 0)
 
 
 def test_forced_shapes(dev):
@@ -102,15 +102,15 @@ def test_forced_shapes(dev):
     d = to_dev(host, dev)
     try:
         for shape in range(10):
-            for unroll in (1, 8):
-                tcp_amd.set_tuning(0, unroll, shape)
+            for unroll, flags in ((1, 0), (8, 0), (2, 1 | 8), (8, 1 | 4), (4, 2 | 8)):
+                tcp_amd.set_tuning(0, unroll, shape, flags)
                 for length, off in ((1500, 0), (1499, 1), (64, 4), (3000, 2)):
                     n = (1 << 21) // (length + 8) - 1
                     got = u16(tcp_amd.batch_uniform(d, length + 1, length, n, 3, offset=off))
                     want = oracle.batch_uniform(host, length + 1, length, n, 3, offset=off)
-                    assert np.array_equal(got, want), (shape, unroll, length, off)
+                    assert np.array_equal(got, want), (shape, unroll, flags, length, off)
     finally:
-        tcp_amd.set_tuning(0, 0, -1)
+        tcp_amd.set_tuning(0, 0, -1, 0)
 
 
 def test_two_fold_semantics_above_4g(dev):
@@ -259,11 +259,11 @@ def test_stream_probe_sums(dev):
     parts = torch.zeros(tcp_amd.api.PROBE_SLOTS, dtype=torch.int64, device=dev)
     want = int((host & 0xFFFF).astype(np.uint64).sum() + (host >> 16).astype(np.uint64).sum())
     for blocks, unroll in ((0, 0), (7, 1), (3000, 4)):
-        tcp_amd.set_tuning(blocks, unroll, -1)
+        tcp_amd.set_tuning(blocks, unroll, -1, 0)
         try:
             k = tcp_amd.stream_probe(d, host.nbytes, parts)
         finally:
-            tcp_amd.set_tuning(0, 0, -1)
+            tcp_amd.set_tuning(0, 0, -1, 0)
         assert int(parts[:k].sum().item()) == want
 
 

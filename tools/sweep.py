@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--blocks", default="256,512,1024,2048,4096,8192,0")
     ap.add_argument("--unrolls", default="1,2,4")
     ap.add_argument("--shapes", default="-1")
+    ap.add_argument("--flags", default="0", help="TCPCSUM_TUNE_* bits: 1 pipe on, 2 pipe off, 4 nt on, 8 nt off")
     ap.add_argument("--probe", action="store_true")
     args = ap.parse_args()
     import torch
@@ -50,10 +51,11 @@ def main():
         sss.append(s)
     out = torch.empty(per, dtype=torch.int16, device=dev)
     variants = []
-    for sh in [int(x) for x in args.shapes.split(",")]:
-        for b in [int(x) for x in args.blocks.split(",")]:
-            for u in [int(x) for x in args.unrolls.split(",")]:
-                variants.append((b, u, sh))
+    for fl in [int(x) for x in args.flags.split(",")]:
+        for sh in [int(x) for x in args.shapes.split(",")]:
+            for b in [int(x) for x in args.blocks.split(",")]:
+                for u in [int(x) for x in args.unrolls.split(",")]:
+                    variants.append((b, u, sh, fl))
     times = {v: [] for v in variants}
     ptimes = []
     st = torch.cuda.current_stream()
@@ -71,7 +73,7 @@ def main():
             times[v].append(e0.elapsed_time(e1) / args.steps)
         if args.probe:
             po = torch.zeros(tcp_amd.api.PROBE_SLOTS, dtype=torch.int64, device=dev)
-            tcp_amd.set_tuning(0, 0, -1)
+            tcp_amd.set_tuning(0, 0, -1, 0)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(st)
             for i in range(args.steps):
@@ -79,11 +81,11 @@ def main():
             e1.record(st)
             torch.cuda.synchronize()
             ptimes.append(e0.elapsed_time(e1) / args.steps)
-    tcp_amd.set_tuning(0, 0, -1)
+    tcp_amd.set_tuning(0, 0, -1, 0)
     res = []
     for v in variants:
         med, mn = statistics.median(times[v]), min(times[v])
-        res.append({"max_blocks": v[0], "unroll": v[1], "shape": v[2], "med_ms": round(med, 5), "min_ms": round(mn, 5),
+        res.append({"max_blocks": v[0], "unroll": v[1], "shape": v[2], "flags": v[3], "med_ms": round(med, 5), "min_ms": round(mn, 5),
                     "GB/s_med": round(nbytes / med / 1e6, 1), "GB/s_best": round(nbytes / mn / 1e6, 1)})
         print(json.dumps({"config": args.config, **res[-1]}), flush=True)
     if ptimes:
