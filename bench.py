@@ -137,6 +137,7 @@ def main(argv=None) -> int:
     ap.add_argument("--unroll", type=int, default=0)
     ap.add_argument("--shape", type=int, default=-1)
     ap.add_argument("--flags", type=int, default=0, help="TCPCSUM_TUNE_* bits")
+    ap.add_argument("--rotate", type=int, default=0, help="distinct batches to rotate (0 = auto)")
     args = ap.parse_args(argv)
 
     import numpy as np
@@ -167,6 +168,8 @@ def main(argv=None) -> int:
     # Batches under ~1 GiB would be served from the 256 MiB Infinity Cache on
     # repeat launches; rotate enough distinct batches that every launch reads HBM.
     rot = max(1, math.ceil((1 << 30) / batch_bytes)) if batch_bytes < (1 << 30) else 1
+    if args.rotate:
+        rot = args.rotate
     stream = torch.cuda.current_stream()
     bufs, sss = [], []
     for r in range(rot):

@@ -180,6 +180,7 @@ int tcpcsum_plan_uniform(uint64_t base, uint64_t stride, uint32_t len, uint64_t 
 #define TCPCSUM_TUNE_PIPE_OFF 2
 #define TCPCSUM_TUNE_NT_ON 4     /* non-temporal loads */
 #define TCPCSUM_TUNE_NT_OFF 8
+#define TCPCSUM_TUNE_BLOCKED 16  /* contiguous tile runs per wave (non-pipelined lane-group kernels) */
 int tcpcsum_set_tuning(int max_blocks, int unroll, int shape, int flags);
 
 #ifdef __cplusplus

@@ -29,6 +29,7 @@ struct UniformPlan {
     int max_blocks;  // resident grid (workgroups of 256 threads)
     bool pipe;       // software-pipelined tiles
     bool nt;         // non-temporal loads
+    int blocked;     // contiguous tile runs per wave instead of a grid stride
 };
 UniformPlan plan_uniform(uintptr_t base, uint64_t stride, uint32_t len, uint64_t n, const Tuning& tu);
 

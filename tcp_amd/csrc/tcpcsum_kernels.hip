@@ -200,15 +200,25 @@ template <int G, int C, int U, int MODE, bool PIPE, bool NT>
 __global__ __launch_bounds__(256) void k_uniform(const uint8_t* __restrict__ base, uint64_t stride,
                                                  uint32_t len, const uint32_t* __restrict__ ss,
                                                  uint32_t ss_scalar, uint16_t* __restrict__ out,
-                                                 uint64_t n) {
+                                                 uint64_t n, int blocked) {
     using Tile = UniformTile<G, C, U, MODE, NT>;
     const int lane = threadIdx.x & 63;
     const int q = lane / G, gl = lane % G;
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
     const uint64_t ntiles = (n + Tile::SPT - 1) / Tile::SPT;
-    uint64_t t = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
+    const uint64_t wave = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
+    uint64_t t = wave;
     if constexpr (!PIPE) {
         Tile a;
+        if (blocked) {   // each wave a contiguous run of tiles instead of a grid stride
+            const uint64_t per = (ntiles + nwaves - 1) / nwaves;
+            const uint64_t t1 = (wave + 1) * per < ntiles ? (wave + 1) * per : ntiles;
+            for (t = wave * per; t < t1; ++t) {
+                a.load(t, base, stride, len, ss, ss_scalar, n, q, gl);
+                a.finish(t, base, stride, len, out, n, q, gl);
+            }
+            return;
+        }
         for (; t < ntiles; t += nwaves) {
             a.load(t, base, stride, len, ss, ss_scalar, n, q, gl);
             a.finish(t, base, stride, len, out, n, q, gl);
@@ -503,14 +513,14 @@ inline unsigned grid_for(uint64_t waves_needed, int max_blocks) {
 
 template <int G, int C, int U, int MODE, bool PIPE, bool NT>
 void launch_uniform_t(const uint8_t* base, uint64_t stride, uint32_t len, const uint32_t* ss,
-                      uint32_t ss0, uint16_t* out, uint64_t n, hipStream_t s, int max_blocks) {
+                      uint32_t ss0, uint16_t* out, uint64_t n, hipStream_t s, int max_blocks, int blocked) {
     // VGPR budget: at most 32 chunk quads per lane (16 per buffer when pipelined)
     constexpr int LIM = PIPE ? 16 : 32;
     constexpr int UE = (C * U > LIM) ? (LIM / C > 0 ? LIM / C : 1) : U;
     constexpr int SPT = (64 / G) * UE;
     const uint64_t ntiles = (n + SPT - 1) / SPT;
     hipLaunchKernelGGL((k_uniform<G, C, UE, MODE, PIPE, NT>), dim3(grid_for(ntiles, max_blocks)), dim3(256), 0,
-                       s, base, stride, len, ss, ss0, out, n);
+                       s, base, stride, len, ss, ss0, out, n, blocked);
 }
 
 template <int C, int MODE, bool PIPE, bool NT>
@@ -531,8 +541,9 @@ void launch_long_t(const uint8_t* base, uint64_t stride, uint32_t len, const uin
 template <int MODE, bool PIPE, bool NT>
 void launch_uniform_mode(int shape, int unroll, const uint8_t* base, uint64_t stride, uint32_t len,
                          const uint32_t* ss, uint32_t ss0, uint16_t* out, uint64_t n, hipStream_t s,
-                         int max_blocks) {
-#define TC_U(G, C, U) launch_uniform_t<G, C, U, MODE, PIPE, NT>(base, stride, len, ss, ss0, out, n, s, max_blocks)
+                         int max_blocks, int blocked) {
+#define TC_U(G, C, U) \
+    launch_uniform_t<G, C, U, MODE, PIPE, NT>(base, stride, len, ss, ss0, out, n, s, max_blocks, blocked)
 #define TC_U4(G, C)                          \
     do {                                     \
         if (unroll == 1) TC_U(G, C, 1);      \
@@ -594,6 +605,7 @@ UniformPlan plan_uniform(uintptr_t b, uint64_t stride, uint32_t len, uint64_t n,
     p.max_blocks = tu.max_blocks > 0 ? tu.max_blocks : kShapeBlocks[p.shape];
     p.pipe = tu.flags & TCPCSUM_TUNE_PIPE_ON ? true : tu.flags & TCPCSUM_TUNE_PIPE_OFF ? false : kShapePipe[p.shape];
     p.nt = tu.flags & TCPCSUM_TUNE_NT_ON ? true : tu.flags & TCPCSUM_TUNE_NT_OFF ? false : kShapeNt[p.shape];
+    p.blocked = (tu.flags & TCPCSUM_TUNE_BLOCKED) ? 1 : 0;
     return p;
 }
 
@@ -601,11 +613,14 @@ template <bool PIPE, bool NT>
 static void launch_uniform_pn(const UniformPlan& p, const uint8_t* base, uint64_t stride, uint32_t len,
                               const uint32_t* ss, uint32_t ss0, uint16_t* out, uint64_t n, hipStream_t s) {
     if (p.mode == M16)
-        launch_uniform_mode<M16, PIPE, NT>(p.shape, p.unroll, base, stride, len, ss, ss0, out, n, s, p.max_blocks);
+        launch_uniform_mode<M16, PIPE, NT>(p.shape, p.unroll, base, stride, len, ss, ss0, out, n, s, p.max_blocks,
+                                           p.blocked);
     else if (p.mode == M4)
-        launch_uniform_mode<M4, PIPE, NT>(p.shape, p.unroll, base, stride, len, ss, ss0, out, n, s, p.max_blocks);
+        launch_uniform_mode<M4, PIPE, NT>(p.shape, p.unroll, base, stride, len, ss, ss0, out, n, s, p.max_blocks,
+                                          p.blocked);
     else
-        launch_uniform_mode<M1, PIPE, NT>(p.shape, p.unroll, base, stride, len, ss, ss0, out, n, s, p.max_blocks);
+        launch_uniform_mode<M1, PIPE, NT>(p.shape, p.unroll, base, stride, len, ss, ss0, out, n, s, p.max_blocks,
+                                          p.blocked);
 }
 
 void launch_uniform(const uint8_t* base, uint64_t stride, uint32_t len, const uint32_t* ss, uint32_t ss0,

@@ -102,7 +102,7 @@ def test_forced_shapes(dev):
     d = to_dev(host, dev)
     try:
         for shape in range(10):
-            for unroll, flags in ((1, 0), (8, 0), (2, 1 | 8), (8, 1 | 4), (4, 2 | 8)):
+            for unroll, flags in ((1, 0), (8, 0), (2, 1 | 8), (8, 1 | 4), (4, 2 | 8), (8, 16), (1, 16 | 8)):
                 tcp_amd.set_tuning(0, unroll, shape, flags)
                 for length, off in ((1500, 0), (1499, 1), (64, 4), (3000, 2)):
                     n = (1 << 21) // (length + 8) - 1
