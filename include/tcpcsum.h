@@ -56,10 +56,15 @@ typedef struct tcpcsum_desc {
 /* Wire-batch modes (tcpcsum_ipv4_batch_dev). */
 #define TCPCSUM_IPV4_FILL 0   /* tx: checksum with check=0, store it at TCP+16 */
 #define TCPCSUM_IPV4_VERIFY 1 /* rx: checksum incl. check; 0 means the segment verifies */
+/* OR-able: also the IPv4 header checksum over ihl*4 bytes (the reference's
+ * commented-out context.c:179; the kernel fills it for IPPROTO_RAW sockets).
+ * FILL stores it at IP+10; VERIFY reports TCPCSUM_PKT_IPHDR_BAD. */
+#define TCPCSUM_IPV4_IPHDR 2
 
 /* Wire-batch per-packet status. */
 #define TCPCSUM_PKT_OK 0
-#define TCPCSUM_PKT_SKIPPED 1 /* not IPv4/TCP, ihl < 5, or tot_len outside [ihl*4+20, cap] */
+#define TCPCSUM_PKT_SKIPPED 1    /* not IPv4/TCP, ihl < 5, or tot_len outside [ihl*4+20, cap] */
+#define TCPCSUM_PKT_IPHDR_BAD 2  /* VERIFY|IPHDR: the IPv4 header checksum does not verify */
 
 /* ---------------------------------------------------------------- library */
 int tcpcsum_abi_version(void);

@@ -153,7 +153,8 @@ void oracle_batch_desc(const uint8_t *base, const uint64_t *off, const uint32_t 
 
 /* ---- wire framing: context.c:169-209 (build) / loop.c:44-47 (flush) --------
  * struct iphdr on little-endian: byte0 = version<<4 | ihl, tot_len @2 (BE),
- * protocol @9, saddr @12, daddr @16. TCP header at ihl*4; check at TCP+16. */
+ * protocol @9, saddr @12, daddr @16. TCP header at ihl*4; check at TCP+16.
+ * mode bit0: verify; bit1: IPv4 header checksum too (status 2 = bad). */
 void oracle_ipv4_batch(uint8_t *base, const uint64_t *off, uint64_t n, uint32_t cap,
                        int mode, uint16_t *out, uint8_t *status) {
     for (uint64_t k = 0; k < n; ++k) {
@@ -172,7 +173,9 @@ void oracle_ipv4_batch(uint8_t *base, const uint64_t *off, uint64_t n, uint32_t 
         uint8_t *tcp = ip + ihl * 4u;
         unsigned tcp_len = tot - ihl * 4u;
         unsigned long ps = oracle_pseudo(sa, da, htons((uint16_t) tcp_len));
-        if (mode == 0) {
+        int verify = mode & 1, iphdr = mode & 2;
+        uint8_t st = 0;
+        if (!verify) {
             tcp[16] = 0;
             tcp[17] = 0;
             uint16_t c = oracle_csum_continue(ps, (const char *) tcp, (int) tcp_len);
@@ -181,7 +184,17 @@ void oracle_ipv4_batch(uint8_t *base, const uint64_t *off, uint64_t n, uint32_t 
         } else {
             if (out) out[k] = oracle_csum_continue(ps, (const char *) tcp, (int) tcp_len);
         }
-        if (status) status[k] = 0;
+        if (iphdr) { /* context.c:179 (commented out in the reference), over ihl*4 bytes */
+            if (!verify) {
+                ip[10] = 0;
+                ip[11] = 0;
+                uint16_t c = oracle_csum_continue(0, (const char *) ip, (int) (ihl * 4u));
+                memcpy(ip + 10, &c, 2);
+            } else if (oracle_csum_continue(0, (const char *) ip, (int) (ihl * 4u)) != 0) {
+                st = 2;
+            }
+        }
+        if (status) status[k] = st;
     }
 }
 

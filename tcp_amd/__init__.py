@@ -17,7 +17,9 @@ from __future__ import annotations
 from .api import (  # noqa: F401
     DESC_DTYPE,
     IPV4_FILL,
+    IPV4_IPHDR,
     IPV4_VERIFY,
+    PKT_IPHDR_BAD,
     PKT_OK,
     PKT_SKIPPED,
     TcpCsumError,
@@ -38,7 +40,7 @@ from .api import (  # noqa: F401
 )
 
 __all__ = [
-    "DESC_DTYPE", "IPV4_FILL", "IPV4_VERIFY", "PKT_OK", "PKT_SKIPPED", "TcpCsumError",
+    "DESC_DTYPE", "IPV4_FILL", "IPV4_IPHDR", "PKT_IPHDR_BAD", "IPV4_VERIFY", "PKT_OK", "PKT_SKIPPED", "TcpCsumError",
     "HostContext", "batch_desc", "batch_uniform", "csum_continue", "device_check",
     "getPseudoHeaderSum", "ipv4_batch", "lib", "lib_path", "pinned_empty", "set_tuning", "stream_probe",
     "synth_fill", "synth_pseudo",

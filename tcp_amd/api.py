@@ -30,8 +30,10 @@ EHIP = -3
 ENOMEM = -4
 IPV4_FILL = 0
 IPV4_VERIFY = 1
+IPV4_IPHDR = 2
 PKT_OK = 0
 PKT_SKIPPED = 1
+PKT_IPHDR_BAD = 2
 
 # tcpcsum_desc_t {u64 offset; u32 len; u32 sum_start}
 DESC_DTYPE = np.dtype([("offset", "<u8"), ("len", "<u4"), ("sum_start", "<u4")])

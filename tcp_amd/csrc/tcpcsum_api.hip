@@ -152,11 +152,12 @@ int tcpcsum_batch_desc_dev(const void* d_base, const tcpcsum_desc_t* d_desc, uin
 int tcpcsum_ipv4_batch_dev(void* d_pkts, const uint64_t* d_pkt_off, uint64_t n, uint32_t cap, int mode,
                            uint16_t* d_out, uint8_t* d_status, void* stream) {
     if (n == 0) return TCPCSUM_OK;
-    if (!d_pkts || !d_pkt_off || (mode != TCPCSUM_IPV4_FILL && mode != TCPCSUM_IPV4_VERIFY)) return TCPCSUM_EINVAL;
+    if (!d_pkts || !d_pkt_off || (mode & ~3)) return TCPCSUM_EINVAL;
     if (cap > 65535u) cap = 65535u;   // tot_len is a u16
     int rc = require_device(nullptr, 0);
     if (rc) return rc;
-    tcpcsum::launch_ipv4((uint8_t*)d_pkts, d_pkt_off, n, cap, UINT64_MAX, mode, d_out, d_status, (hipStream_t)stream,
+    tcpcsum::launch_ipv4((uint8_t*)d_pkts, d_pkt_off, n, cap, UINT64_MAX, mode, d_out, d_status, nullptr,
+                         (hipStream_t)stream,
                          tuning());
     return check_launch();
 }
@@ -206,6 +207,7 @@ struct tcpcsum_ctx {
     uint64_t* d_off = nullptr;
     uint16_t* d_wout = nullptr;
     uint8_t* d_wstat = nullptr;
+    uint16_t* d_wip = nullptr;
     size_t d_pkt_cap = 0;
     std::mutex mu;
 };
@@ -297,6 +299,7 @@ void tcpcsum_ctx_destroy(tcpcsum_ctx_t* c) {
     if (c->d_off) hipFree(c->d_off);
     if (c->d_wout) hipFree(c->d_wout);
     if (c->d_wstat) hipFree(c->d_wstat);
+    if (c->d_wip) hipFree(c->d_wip);
     for (int i = 0; i < 2; ++i)
         if (c->st[i]) hipStreamDestroy(c->st[i]);
     delete c;
@@ -340,10 +343,12 @@ int ensure_pkt_scratch(tcpcsum_ctx* c, uint64_t n, hipStream_t st) {
     if (c->d_off) (void)hipFree(c->d_off);
     if (c->d_wout) (void)hipFree(c->d_wout);
     if (c->d_wstat) (void)hipFree(c->d_wstat);
-    c->d_off = nullptr; c->d_wout = nullptr; c->d_wstat = nullptr; c->d_pkt_cap = 0;
+    if (c->d_wip) (void)hipFree(c->d_wip);
+    c->d_off = nullptr; c->d_wout = nullptr; c->d_wstat = nullptr; c->d_wip = nullptr; c->d_pkt_cap = 0;
     hipError_t e = hipMalloc(&c->d_off, n * sizeof(uint64_t));
     if (e == hipSuccess) e = hipMalloc(&c->d_wout, n * sizeof(uint16_t));
     if (e == hipSuccess) e = hipMalloc(&c->d_wstat, n);
+    if (e == hipSuccess) e = hipMalloc(&c->d_wip, n * sizeof(uint16_t));
     if (e != hipSuccess) { g_last_hip_error.store((int)e); return TCPCSUM_ENOMEM; }
     c->d_pkt_cap = n;
     return TCPCSUM_OK;
@@ -438,8 +443,7 @@ int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t* c, void* h_pkts, size_t region_bytes,
                             uint64_t n, uint32_t cap, int mode, uint16_t* h_out, uint8_t* h_status) {
     if (!c) return TCPCSUM_EINVAL;
     if (n == 0) return TCPCSUM_OK;
-    if (!h_pkts || !h_pkt_off || !region_bytes || (mode != TCPCSUM_IPV4_FILL && mode != TCPCSUM_IPV4_VERIFY))
-        return TCPCSUM_EINVAL;
+    if (!h_pkts || !h_pkt_off || !region_bytes || (mode & ~3)) return TCPCSUM_EINVAL;
     if (cap > 65535u) cap = 65535u;
     // every packet header must lie inside the region; packets whose tot_len
     // runs past its end are SKIPPED by the kernel (limit = region_bytes)
@@ -461,7 +465,7 @@ int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t* c, void* h_pkts, size_t region_bytes,
         uint16_t* zout = h_out ? (uint16_t*)pinned_dev_ptr(h_out) : nullptr;
         uint8_t* zst = h_status ? (uint8_t*)pinned_dev_ptr(h_status) : nullptr;
         tcpcsum::launch_ipv4(zp, zoff, n, cap, (uint64_t)region_bytes, mode, zout ? zout : c->d_wout,
-                             zst ? zst : c->d_wstat, st, tuning());
+                             zst ? zst : c->d_wstat, nullptr, st, tuning());
         rc = check_launch();
         if (rc) return rc;
         if (h_out && !zout) e = hipMemcpyAsync(h_out, c->d_wout, n * sizeof(uint16_t), hipMemcpyDeviceToHost, st);
@@ -484,7 +488,7 @@ int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t* c, void* h_pkts, size_t region_bytes,
     if (e == hipSuccess) e = hipMemcpyAsync(c->d_off, h_pkt_off, n * sizeof(uint64_t), hipMemcpyHostToDevice, st);
     if (e != hipSuccess) return hip_fail(e);
     tcpcsum::launch_ipv4(c->d_region + mis, c->d_off, n, cap, (uint64_t)region_bytes, mode, c->d_wout, c->d_wstat,
-                         st, tuning());
+                         c->d_wip, st, tuning());
     rc = check_launch();
     if (rc) return rc;
     uint16_t* out = h_out;
@@ -492,7 +496,8 @@ int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t* c, void* h_pkts, size_t region_bytes,
     // FILL needs out+status on the host to store the checks in place
     uint16_t* tmp_out = nullptr;
     uint8_t* tmp_stat = nullptr;
-    if (mode == TCPCSUM_IPV4_FILL) {
+    const bool fill = (mode & TCPCSUM_IPV4_VERIFY) == 0;
+    if (fill) {
         if (!out) out = tmp_out = new (std::nothrow) uint16_t[n];
         if (!stat) stat = tmp_stat = new (std::nothrow) uint8_t[n];
         if (!out || !stat) { delete[] tmp_out; delete[] tmp_stat; return TCPCSUM_ENOMEM; }
@@ -501,14 +506,25 @@ int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t* c, void* h_pkts, size_t region_bytes,
     if (e == hipSuccess && stat) e = hipMemcpyAsync(stat, c->d_wstat, n, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) { delete[] tmp_out; delete[] tmp_stat; return hip_fail(e); }
-    if (mode == TCPCSUM_IPV4_FILL) {
-        // store each result at TCP+16 (native u16, as context.c:208) — no arithmetic here
+    if (fill) {
+        // store each result at TCP+16 (native u16, as context.c:208), and the IP
+        // header checksum the kernel stored in the device copy — no arithmetic here
         uint8_t* base = (uint8_t*)h_pkts;
         for (uint64_t i = 0; i < n; ++i) {
             if (stat[i] != TCPCSUM_PKT_OK) continue;
             uint8_t* ip = base + h_pkt_off[i];
             uint8_t* tcp = ip + (ip[0] & 15u) * 4u;
             memcpy(tcp + 16, &out[i], 2);
+        }
+        if (mode & TCPCSUM_IPV4_IPHDR) {
+            uint16_t* ipc = new (std::nothrow) uint16_t[n];
+            if (!ipc) { delete[] tmp_out; delete[] tmp_stat; return TCPCSUM_ENOMEM; }
+            e = hipMemcpyAsync(ipc, c->d_wip, n * sizeof(uint16_t), hipMemcpyDeviceToHost, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+            if (e != hipSuccess) { delete[] ipc; delete[] tmp_out; delete[] tmp_stat; return hip_fail(e); }
+            for (uint64_t i = 0; i < n; ++i)
+                if (stat[i] == TCPCSUM_PKT_OK) memcpy(base + h_pkt_off[i] + 10, &ipc[i], 2);
+            delete[] ipc;
         }
     }
     delete[] tmp_out;

@@ -382,7 +382,8 @@ __global__ __launch_bounds__(256) void k_desc(const uint8_t* __restrict__ base,
 template <int G, int C>
 __global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const uint64_t* __restrict__ off,
                                               uint64_t n, uint32_t cap, uint64_t limit, int mode,
-                                              uint16_t* __restrict__ out, uint8_t* __restrict__ status) {
+                                              uint16_t* __restrict__ out, uint8_t* __restrict__ status,
+                                              uint16_t* __restrict__ ipout) {
     constexpr int GPW = 64 / G;
     const int lane = threadIdx.x & 63;
     const int q = lane / G, gl = lane % G;
@@ -413,18 +414,38 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const 
         // context.c:104-119 closed form: six native u16 words of the pseudo header.
         const uint64_t ps = (sa & 0xffffu) + (sa >> 16) + (da & 0xffffu) + (da >> 16) + 0x0600u + len_be;
         const uint32_t check_word = (uint32_t)tcp[16] | ((uint32_t)tcp[17] << 8);
+        const bool verify = (mode & TCPCSUM_IPV4_VERIFY) != 0;
         uint64_t S = group_segment_sum<G, C>(tcp, tcp_len, gl) + ps;
         // FILL: the reference sums with check == 0 (context.c:182); TCP+16 is an
         // even relative offset, so its native word contributes exactly check_word.
-        if (mode == TCPCSUM_IPV4_FILL) S -= check_word;
+        if (!verify) S -= check_word;
         const uint16_t c = fold_ref(S);
+        uint32_t st = TCPCSUM_PKT_OK;
+        if (mode & TCPCSUM_IPV4_IPHDR) {
+            // IPv4 header checksum = csum_continue(0, ip, ihl*4) with check (IP+10)
+            // as zero — the reference's commented-out context.c:179, over ihl*4 bytes.
+            uint32_t acc = 0;
+            for (uint32_t w = (uint32_t)gl; w < ihl * 2u; w += G)
+                acc += (!verify && w == 5u) ? 0u : ((uint32_t)ip[2 * w] | ((uint32_t)ip[2 * w + 1] << 8));
+            acc = group_sum32<G>(acc);
+            const uint16_t ic = fold_ref(acc);
+            if (ipout && gl == 0) ipout[i] = ic;
+            if (!verify) {
+                if (gl == 0) {
+                    ip[10] = (uint8_t)(ic & 0xffu);
+                    ip[11] = (uint8_t)(ic >> 8);
+                }
+            } else if (ic != 0) {
+                st = TCPCSUM_PKT_IPHDR_BAD;
+            }
+        }
         if (gl == 0) {
-            if (mode == TCPCSUM_IPV4_FILL) {   // native u16 store, as context.c:208
+            if (!verify) {   // native u16 store, as context.c:208
                 tcp[16] = (uint8_t)(c & 0xffu);
                 tcp[17] = (uint8_t)(c >> 8);
             }
             if (out) out[i] = c;
-            if (status) status[i] = TCPCSUM_PKT_OK;
+            if (status) status[i] = (uint8_t)st;
         }
     }
 }
@@ -653,18 +674,18 @@ void launch_desc(const uint8_t* base, const tcpcsum_desc_t* d, uint64_t n, uint3
 }
 
 void launch_ipv4(uint8_t* pkts, const uint64_t* off, uint64_t n, uint32_t cap, uint64_t limit, int mode,
-                 uint16_t* out, uint8_t* status, hipStream_t s, const Tuning& tu) {
+                 uint16_t* out, uint8_t* status, uint16_t* ipout, hipStream_t s, const Tuning& tu) {
     const int max_blocks = tu.max_blocks > 0 ? tu.max_blocks : kDefaultMaxBlocks;
     const uint64_t nch = ((uint64_t)cap + 30u) >> 4;
     if (nch <= 8) {
         hipLaunchKernelGGL((k_ipv4<8, 1>), dim3(grid_for((n + 7) / 8, max_blocks)), dim3(256), 0, s, pkts, off,
-                           n, cap, limit, mode, out, status);
+                           n, cap, limit, mode, out, status, ipout);
     } else if (nch <= 96) {
         hipLaunchKernelGGL((k_ipv4<32, 3>), dim3(grid_for((n + 1) / 2, max_blocks)), dim3(256), 0, s, pkts, off,
-                           n, cap, limit, mode, out, status);
+                           n, cap, limit, mode, out, status, ipout);
     } else {
         hipLaunchKernelGGL((k_ipv4<64, 8>), dim3(grid_for(n, max_blocks)), dim3(256), 0, s, pkts, off, n, cap,
-                           limit, mode, out, status);
+                           limit, mode, out, status, ipout);
     }
 }
 

@@ -54,6 +54,8 @@ def test_header_constants_match_python():
     assert int(consts["TCPCSUM_IPV4_FILL"]) == api.IPV4_FILL
     assert int(consts["TCPCSUM_IPV4_VERIFY"]) == api.IPV4_VERIFY
     assert int(consts["TCPCSUM_PKT_SKIPPED"]) == api.PKT_SKIPPED
+    assert int(consts["TCPCSUM_PKT_IPHDR_BAD"]) == api.PKT_IPHDR_BAD
+    assert int(consts["TCPCSUM_IPV4_IPHDR"]) == api.IPV4_IPHDR
     assert int(consts["TCPCSUM_ABI_VERSION"]) == tcp_amd.lib().tcpcsum_abi_version()
     assert api.DESC_DTYPE.itemsize == 16
 
@@ -88,6 +90,7 @@ def test_argument_errors_need_no_device():
     assert L.tcpcsum_batch_uniform_dev(1 << 20, 0, 2**31, None, 0, 1 << 20, 5, None) == api.EINVAL
     assert L.tcpcsum_batch_desc_dev(1 << 20, (1 << 20) + 8, 5, 64, 1 << 20, None) == api.EINVAL   # unaligned desc
     assert L.tcpcsum_ipv4_batch_dev(1 << 20, 1 << 20, 5, 1500, 7, None, None, None) == api.EINVAL  # bad mode
+    assert L.tcpcsum_ipv4_batch_dev(1 << 20, 1 << 20, 5, 1500, 4, None, None, None) == api.EINVAL
     ng = ctypes.c_int()
     assert L.tcpcsum_stream_probe_dev(1 << 20, 17, 1 << 20, ctypes.byref(ng), None) == api.EINVAL
     assert L.tcpcsum_set_tuning(-1, 0, -1, 0) == api.EINVAL

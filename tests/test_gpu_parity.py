@@ -325,3 +325,41 @@ def test_host_context_zero_copy_pinned(dev):
         assert np.array_equal(pin, ref)          # checks stored in place in host memory by the kernel
         out, st = ctx.ipv4_batch(pin, off, 32768, tcp_amd.IPV4_VERIFY)
         assert np.all(out[st == 0] == 0)
+
+
+@pytest.mark.parametrize("memory", ["device", "pageable", "pinned"])
+def test_ipv4_iphdr_mode(dev, memory):
+    import tcp_amd
+    from tests.packets import build_batch
+    rng = np.random.default_rng(77)
+    region, off, _ = build_batch(rng, 300, malformed=True, odd_offsets=True)
+    ref = region.copy()
+    mode = tcp_amd.IPV4_FILL | tcp_amd.IPV4_IPHDR
+    want_out, want_st = oracle.ipv4_batch(ref, off, 32768, mode)
+    if memory == "device":
+        dreg = to_dev(region, dev)
+        doff = to_dev(off.view(np.int64), dev)
+        out = torch.empty(off.size, dtype=torch.int16, device=dev)
+        st = torch.empty(off.size, dtype=torch.uint8, device=dev)
+        tcp_amd.ipv4_batch(dreg, doff, off.size, 32768, mode, out, st)
+        got_out, got_st, got_reg = u16(out), st.cpu().numpy(), dreg.cpu().numpy()
+    else:
+        buf = region if memory == "pageable" else tcp_amd.pinned_empty(region.size)
+        buf[:] = region
+        with tcp_amd.HostContext(0) as ctx:
+            got_out, got_st = ctx.ipv4_batch(buf, off, 32768, mode)
+        got_reg = np.array(buf)
+    assert np.array_equal(got_st, want_st) and np.array_equal(got_out, want_out)
+    assert np.array_equal(got_reg, ref)
+    # verify with IP header check: OK everywhere it was filled; a corrupted TTL is flagged
+    bad = ref.copy()
+    okidx = np.flatnonzero(want_st == 0)
+    bad[int(off[okidx[0]]) + 8] ^= 0x40
+    want_v, want_vs = oracle.ipv4_batch(bad.copy(), off, 32768, tcp_amd.IPV4_VERIFY | tcp_amd.IPV4_IPHDR)
+    dbad = to_dev(bad, dev)
+    out = torch.empty(off.size, dtype=torch.int16, device=dev)
+    st = torch.empty(off.size, dtype=torch.uint8, device=dev)
+    tcp_amd.ipv4_batch(dbad, to_dev(off.view(np.int64), dev), off.size, 32768,
+                       tcp_amd.IPV4_VERIFY | tcp_amd.IPV4_IPHDR, out, st)
+    assert np.array_equal(st.cpu().numpy(), want_vs) and np.array_equal(u16(out), want_v)
+    assert want_vs[okidx[0]] == tcp_amd.PKT_IPHDR_BAD

@@ -116,3 +116,30 @@ def test_cpu_bench_harness_runs():
     assert gibs > 0 and passes >= 3
     # the harness checksums the Appendix B stream: its digest equals synth_batch's
     assert dg == oracle.digest(oracle.synth_batch(0, 4096, 1500))[0]
+
+
+def test_oracle_ipv4_iphdr_fill_then_verify():
+    """FILL|IPHDR writes an IPv4 header checksum that verifies; a flipped header byte is caught."""
+    import struct
+    from tests.packets import build_batch
+    region, off, _ = build_batch(np.random.default_rng(4), 40, malformed=True)
+    out, st = oracle.ipv4_batch(region, off, 32768, 0 | 2)
+    ok = st == 0
+    for o, good in zip(off, ok):
+        if good:
+            ihl = region[o] & 15
+            hdr = region[o:o + 4 * ihl].tobytes()
+            assert pyspec.csum_continue(0, hdr, len(hdr)) == 0
+            # RFC 1071 form: complemented 16-bit big-endian sum of the header words is zero too
+            words = struct.unpack("!%dH" % (2 * ihl), hdr)
+            s = sum(words)
+            while s >> 16:
+                s = (s & 0xFFFF) + (s >> 16)
+            assert s == 0xFFFF
+    _, st2 = oracle.ipv4_batch(region, off, 32768, 1 | 2)
+    assert np.array_equal(st2, st)
+    bad = region.copy()
+    first = int(off[np.flatnonzero(ok)[0]])
+    bad[first + 8] ^= 1                                  # TTL
+    _, st3 = oracle.ipv4_batch(bad, off, 32768, 1 | 2)
+    assert st3[np.flatnonzero(ok)[0]] == 2
