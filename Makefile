@@ -15,7 +15,9 @@ HIP_SRCS := tcp_amd/csrc/tcpcsum_kernels.hip tcp_amd/csrc/tcpcsum_api.hip
 HDRS := include/tcpcsum.h tcp_amd/csrc/tcpcsum_internal.h
 OBJDIR := build/obj
 
-all: $(LIB) oracle tests/c/abi_smoke
+PRELOAD := tcp_amd/libtcpcsum_preload.so
+
+all: $(LIB) $(PRELOAD) oracle tests/c/abi_smoke tests/c/mmsg_loop
 
 $(OBJDIR)/%.o: tcp_amd/csrc/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
@@ -28,6 +30,10 @@ $(OBJDIR)/scalar_dropin.o: tcp_amd/csrc/scalar_dropin.c include/tcpcsum.h
 $(LIB): $(OBJDIR)/tcpcsum_kernels.o $(OBJDIR)/tcpcsum_api.o $(OBJDIR)/scalar_dropin.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@.tmp $^ -Wl,-soname,libtcpcsum.so
 	mv $@.tmp $@
+
+# LD_PRELOAD seam library (sendmmsg / recvmmsg interposer) over the C ABI
+$(PRELOAD): tcp_amd/csrc/preload_mmsg.c include/tcpcsum.h $(LIB)
+	$(CC) -O2 -fPIC -shared -Wall -Wextra -Iinclude -o $@ $< -Ltcp_amd -ltcpcsum -ldl -lpthread -Wl,-rpath,'$$ORIGIN'
 
 oracle: oracle/build/liboracle.so oracle/build/liboracle_O0.so
 
@@ -42,7 +48,10 @@ oracle/build/liboracle_O0.so: oracle/csum_oracle.c oracle/oracle.h oracle/cpu_be
 tests/c/abi_smoke: tests/c/abi_smoke.c include/tcpcsum.h $(LIB)
 	$(CC) -O2 -Wall -Wextra -Iinclude -o $@ $< -Ltcp_amd -ltcpcsum -Wl,-rpath,'$$ORIGIN/../../tcp_amd'
 
+tests/c/mmsg_loop: tests/c/mmsg_loop.c include/tcpcsum.h $(LIB)
+	$(CC) -O2 -Wall -Wextra -Iinclude -o $@ $< -Ltcp_amd -ltcpcsum -Wl,-rpath,'$$ORIGIN/../../tcp_amd'
+
 clean:
-	rm -rf build oracle/build $(LIB) tests/c/abi_smoke
+	rm -rf build oracle/build $(LIB) $(PRELOAD) tests/c/abi_smoke tests/c/mmsg_loop
 
 .PHONY: all oracle clean

@@ -1,0 +1,125 @@
+/*
+ * mmsg_loop.c — drives the sendmmsg/recvmmsg seam the way the reference's loop
+ * does (loop.c:27-94 releaseSend, loop.c:22-25 fetchPackageBatch), over UDP
+ * loopback so no root is needed. Run under LD_PRELOAD=libtcpcsum_preload.so.
+ *
+ *   mmsg_loop <npkts> <out-file> [cpu-checks]
+ *
+ * Builds npkts IPv4/TCP packets in separate 32 KiB malloc'd buffers (as
+ * loop.c:180-183 allocates them) with the reference's framing
+ * (context.c:169-206): check = 0, or — with "cpu-checks" — the check the
+ * reference's CPU path would store (tcpcsum_continue == csum_continue,
+ * context.c:208). Sends them with sendmmsg in batches of <= 1024 and
+ * receives them with recvmmsg. Writes to <out-file>: for every packet
+ * u32 length + the bytes as built, then u32 length + the bytes as received.
+ * Exit 0 on success; 3 if sendmmsg failed (errno printed); 4 if recvmmsg
+ * failed; 5 if a packet went missing.
+ */
+#define _GNU_SOURCE
+#include <arpa/inet.h>
+#include <errno.h>
+#include <netinet/in.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include "tcpcsum.h"
+
+static uint64_t rng = 0x9E3779B97F4A7C15ull;
+static uint32_t next32(void) {
+    rng ^= rng << 13; rng ^= rng >> 7; rng ^= rng << 17;
+    return (uint32_t) (rng >> 16);
+}
+
+static size_t build(uint8_t *b, int i, int cpu_checks) {
+    size_t payload = (size_t) (next32() % 1457);            /* 0 .. 1456 (1500-B MTU) */
+    size_t tot = 20 + 24 + payload;
+    memset(b, 0, 44);
+    b[0] = 0x45;                                              /* version 4, ihl 5 */
+    b[2] = (uint8_t) (tot >> 8); b[3] = (uint8_t) tot;        /* tot_len (BE) */
+    b[4] = 0xd4; b[5] = 0x31;                                 /* id */
+    b[8] = 255; b[9] = 6;                                     /* ttl, IPPROTO_TCP */
+    uint32_t sa = htonl(0x7F000001u), da = htonl(0x0A000000u | (uint32_t) i);
+    memcpy(b + 12, &sa, 4); memcpy(b + 16, &da, 4);
+    uint8_t *t = b + 20;
+    t[0] = 4000 >> 8; t[1] = 4000 & 255; t[2] = 45001 >> 8; t[3] = 45001 & 255;
+    uint32_t seq = htonl(next32()), ack = htonl(next32());
+    memcpy(t + 4, &seq, 4); memcpy(t + 8, &ack, 4);
+    t[12] = 6 << 4; t[13] = 0x18;                             /* doff 6, PSH|ACK */
+    t[14] = 8192 >> 8; t[15] = 0;                             /* window */
+    t[20] = 3; t[21] = 3; t[22] = 5; t[23] = 0;               /* window scale option */
+    for (size_t k = 0; k < payload; ++k) t[24 + k] = (uint8_t) next32();
+    if (cpu_checks) {
+        uint16_t c = tcpcsum_continue(tcpcsum_pseudo(sa, da, htons((uint16_t) (24 + payload))),
+                                      (const char *) t, (int) (24 + payload));
+        memcpy(t + 16, &c, 2);
+    }
+    return tot;
+}
+
+int main(int argc, char **argv) {
+    if (argc < 3) { fprintf(stderr, "usage: %s npkts out [cpu-checks]\n", argv[0]); return 2; }
+    int n = atoi(argv[1]);
+    int cpu_checks = argc > 3 && !strcmp(argv[3], "cpu-checks");
+    FILE *f = fopen(argv[2], "wb");
+    if (!f || n <= 0) return 2;
+    int rx = socket(AF_INET, SOCK_DGRAM, 0), tx = socket(AF_INET, SOCK_DGRAM, 0);
+    struct sockaddr_in a = {0};
+    a.sin_family = AF_INET; a.sin_addr.s_addr = htonl(0x7F000001u); a.sin_port = 0;
+    if (bind(rx, (struct sockaddr *) &a, sizeof a)) { perror("bind"); return 2; }
+    socklen_t al = sizeof a;
+    getsockname(rx, (struct sockaddr *) &a, &al);
+    uint8_t **out = calloc((size_t) n, sizeof *out), **in = calloc((size_t) n, sizeof *in);
+    size_t *olen = calloc((size_t) n, sizeof *olen), *ilen = calloc((size_t) n, sizeof *ilen);
+    uint8_t **orig = calloc((size_t) n, sizeof *orig);
+    for (int i = 0; i < n; ++i) {
+        out[i] = malloc(32768); in[i] = malloc(32768);
+        olen[i] = build(out[i], i, cpu_checks);
+        orig[i] = malloc(olen[i]);
+        memcpy(orig[i], out[i], olen[i]);
+    }
+    enum { B = 64 };   /* stay below the default socket receive buffer per burst */
+    struct mmsghdr mv[B];
+    struct iovec iv[B];
+    for (int s0 = 0; s0 < n; s0 += B) {
+        int cnt = n - s0 < B ? n - s0 : B;
+        memset(mv, 0, sizeof mv);
+        for (int k = 0; k < cnt; ++k) {
+            iv[k].iov_base = out[s0 + k]; iv[k].iov_len = olen[s0 + k];
+            mv[k].msg_hdr.msg_iov = &iv[k]; mv[k].msg_hdr.msg_iovlen = 1;
+            mv[k].msg_hdr.msg_name = &a; mv[k].msg_hdr.msg_namelen = sizeof a;
+        }
+        int sent = 0;
+        while (sent < cnt) {
+            int r = sendmmsg(tx, mv + sent, (unsigned) (cnt - sent), 0);
+            if (r < 0) { fprintf(stderr, "sendmmsg: %s\n", strerror(errno)); return 3; }
+            sent += r;
+        }
+        int got = 0;
+        while (got < cnt) {
+            memset(mv, 0, sizeof mv);
+            for (int k = 0; k < cnt - got; ++k) {
+                iv[k].iov_base = in[s0 + got + k]; iv[k].iov_len = 32768;
+                mv[k].msg_hdr.msg_iov = &iv[k]; mv[k].msg_hdr.msg_iovlen = 1;
+            }
+            struct timespec to = {5, 0};
+            int r = recvmmsg(rx, mv, (unsigned) (cnt - got), MSG_WAITFORONE, &to);
+            if (r < 0) { fprintf(stderr, "recvmmsg: %s\n", strerror(errno)); return 4; }
+            if (r == 0) return 5;
+            for (int k = 0; k < r; ++k) ilen[s0 + got + k] = mv[k].msg_len;
+            got += r;
+        }
+    }
+    for (int i = 0; i < n; ++i) {
+        uint32_t l = (uint32_t) olen[i];
+        fwrite(&l, 4, 1, f); fwrite(orig[i], 1, l, f);
+        l = (uint32_t) ilen[i];
+        fwrite(&l, 4, 1, f); fwrite(in[i], 1, l, f);
+    }
+    fclose(f);
+    printf("ok %d\n", n);
+    return 0;
+}

@@ -1,0 +1,108 @@
+"""The zero-edit seam: libtcpcsum_preload.so interposing sendmmsg / recvmmsg.
+
+tests/c/mmsg_loop builds packets with the reference's framing in separate
+32 KiB buffers and pushes them through sendmmsg/recvmmsg over UDP loopback
+(no root needed). With TCPCSUM_PRELOAD_TX=fill every received packet must equal
+the oracle's FILL of the packet as built (check computed per context.c:208).
+"""
+import os
+import re
+import struct
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(REPO, "tests", "c", "mmsg_loop")
+PRELOAD = os.path.join(REPO, "tcp_amd", "libtcpcsum_preload.so")
+
+
+def _ensure_built():
+    if not (os.path.exists(EXE) and os.path.exists(PRELOAD)):
+        subprocess.run(["make", "-C", REPO, "tests/c/mmsg_loop", "tcp_amd/libtcpcsum_preload.so"], check=True)
+
+
+def run_loop(tmp_path, n, env_extra, cpu_checks=False):
+    _ensure_built()
+    out = tmp_path / "mm.bin"
+    env = dict(os.environ)
+    env.update({"LD_PRELOAD": PRELOAD, "TCPCSUM_PRELOAD_ANY_SOCKET": "1", "TCPCSUM_PRELOAD_STATS": "1"})
+    env.update(env_extra)
+    args = [EXE, str(n), str(out)] + (["cpu-checks"] if cpu_checks else [])
+    r = subprocess.run(args, env=env, capture_output=True, text=True, timeout=120)
+    pkts = []
+    if r.returncode == 0:
+        data = out.read_bytes()
+        pos = 0
+        while pos < len(data):
+            (lo,) = struct.unpack_from("<I", data, pos)
+            built = data[pos + 4:pos + 4 + lo]
+            pos += 4 + lo
+            (li,) = struct.unpack_from("<I", data, pos)
+            got = data[pos + 4:pos + 4 + li]
+            pos += 4 + li
+            pkts.append((built, got))
+    stats = {}
+    m = re.search(r"tcpcsum_preload: (.*)", r.stderr)
+    if m:
+        for side, body in zip(("tx", "rx"), m.group(1).split("|")[:2]):
+            for k, v in re.findall(r"(\w+)=(\d+)", body):
+                stats[f"{side}_{k}"] = int(v)
+    return r, pkts, stats
+
+
+def oracle_fill(pkt: bytes, mode=0) -> bytes:
+    region = np.frombuffer(pkt + b"\0" * 16, np.uint8).copy()
+    oracle.ipv4_batch(region, np.array([0], np.uint64), 65535, mode)
+    return region[:len(pkt)].tobytes()
+
+
+def test_passthrough_when_off(tmp_path):
+    r, pkts, stats = run_loop(tmp_path, 150, {"TCPCSUM_PRELOAD_TX": "off"})
+    assert r.returncode == 0, r.stderr
+    assert len(pkts) == 150 and all(b == g for b, g in pkts)
+    assert stats["tx_packets"] == 0
+
+
+def test_fails_loudly_without_gpu(tmp_path):
+    import tcp_amd
+    if tcp_amd.device_check()[0] == 0:
+        pytest.skip("a GPU is present")
+    r, _, stats = run_loop(tmp_path, 10, {"TCPCSUM_PRELOAD_TX": "fill"})
+    assert r.returncode == 3 and "No such device or address" in r.stderr
+    assert "refusing" in r.stderr
+
+
+@pytest.mark.gpu
+def test_tx_fill_on_gpu(tmp_path):
+    r, pkts, stats = run_loop(tmp_path, 3000, {"TCPCSUM_PRELOAD_TX": "fill", "TCPCSUM_PRELOAD_RX": "verify"})
+    assert r.returncode == 0, r.stderr
+    assert len(pkts) == 3000
+    for built, got in pkts:
+        assert got == oracle_fill(built)
+    assert stats["tx_filled"] == 3000 and stats["rx_verified"] == 3000 and stats["rx_verify_failed"] == 0
+
+
+@pytest.mark.gpu
+def test_tx_verify_live_parity_with_cpu_checks(tmp_path):
+    """Checks written by the reference's CPU path (tcpcsum_continue == csum_continue) verify on the GPU."""
+    r, pkts, stats = run_loop(tmp_path, 2000, {"TCPCSUM_PRELOAD_TX": "verify"}, cpu_checks=True)
+    assert r.returncode == 0, r.stderr
+    assert stats["tx_verified"] == 2000 and stats["tx_verify_failed"] == 0
+    assert all(b == g for b, g in pkts)            # verify mode never edits packets
+    # and without checks every packet fails verification
+    r, _, stats = run_loop(tmp_path, 500, {"TCPCSUM_PRELOAD_TX": "verify"})
+    assert stats["tx_verify_failed"] == 500
+
+
+@pytest.mark.gpu
+def test_tx_fill_with_ip_header(tmp_path):
+    r, pkts, stats = run_loop(tmp_path, 700, {"TCPCSUM_PRELOAD_TX": "fill", "TCPCSUM_PRELOAD_IPHDR": "1",
+                                              "TCPCSUM_PRELOAD_RX": "verify"})
+    assert r.returncode == 0, r.stderr
+    for built, got in pkts:
+        assert got == oracle_fill(built, 2)
+    assert stats["rx_verify_failed"] == 0
