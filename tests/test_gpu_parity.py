@@ -363,3 +363,13 @@ def test_ipv4_iphdr_mode(dev, memory):
                        tcp_amd.IPV4_VERIFY | tcp_amd.IPV4_IPHDR, out, st)
     assert np.array_equal(st.cpu().numpy(), want_vs) and np.array_equal(u16(out), want_v)
     assert want_vs[okidx[0]] == tcp_amd.PKT_IPHDR_BAD
+
+
+def test_c_client_on_gpu(dev):
+    """The plain-C ABI client (tests/c/abi_smoke.c) runs a host batch on the GPU."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "c", "abi_smoke")
+    r = subprocess.run([exe, "--gpu"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "mismatches: 0 /" in r.stdout
