@@ -117,6 +117,42 @@ int tcpcsum_batch_desc_dev(const void *d_base, const tcpcsum_desc_t *d_desc, uin
 int tcpcsum_ipv4_batch_dev(void *d_pkts, const uint64_t *d_pkt_off, uint64_t n, uint32_t cap,
                            int mode, uint16_t *d_out, uint8_t *d_status, void *stream);
 
+/* Segment assembly + checksum in one pass (device-side
+ * us_internal_socket_context_send_packet, context.c:150-213, minus its 10 %
+ * drop and printf trace). For each descriptor the kernel writes a complete
+ * IPv4/TCP packet at d_out_pkts + out_off, laid out exactly as context.c:169-206
+ * builds it (ihl 5, tot_len, id = (u16)htonl(54321), ttl 255, TCP, window-scale
+ * option 03 03 05 00, doff 6, window 8192), copies the payload (the memcpy at
+ * context.c:190) and stores the TCP check (context.c:208) — the payload is
+ * read once and written once. 48-byte descriptor: */
+#define TCPCSUM_TXF_ACK 1
+#define TCPCSUM_TXF_SYN 2
+#define TCPCSUM_TXF_FIN 4
+#define TCPCSUM_TXF_RST 8
+#define TCPCSUM_TXF_DATA 16   /* payload present: PSH set and len bytes copied (context.c:188-191) */
+typedef struct tcpcsum_txseg {
+    uint64_t payload_off;   /* payload at d_payload + payload_off */
+    uint64_t out_off;       /* packet (44 + len bytes) written at d_out_pkts + out_off */
+    uint32_t saddr_be;      /* networkSourceIp, as stored (context.c:177) */
+    uint32_t daddr_be;      /* networkDestIp (context.c:178) */
+    uint32_t seq;           /* hostSeq, host order (stored htonl, context.c:194) */
+    uint32_t ack;           /* hostAck, host order (context.c:193) */
+    uint16_t sport;         /* hostSourcePort, host order (context.c:195) */
+    uint16_t dport;         /* hostDestPort, host order (context.c:196) */
+    uint16_t len;           /* payload bytes, <= 65491; forced to 0 without TCPCSUM_TXF_DATA */
+    uint8_t flags;          /* TCPCSUM_TXF_* */
+    uint8_t reserved0;
+    uint64_t reserved1;
+} tcpcsum_txseg_t;
+
+/* mode: 0, or TCPCSUM_IPV4_IPHDR to also fill the IPv4 header checksum (the
+ * reference leaves it 0 for the kernel, context.c:179). max_len: an upper
+ * bound on the payload lengths (kernel shape only). d_check (nullable): the
+ * TCP checks, also stored in the packets. Segments with len > 65491 are not
+ * written (d_check = 0). Packets must not overlap; d_segs 16-B aligned. */
+int tcpcsum_tx_build_dev(const void *d_payload, const tcpcsum_txseg_t *d_segs, uint64_t n, uint32_t max_len,
+                         void *d_out_pkts, int mode, uint16_t *d_check, void *stream);
+
 /* ------------------------------------------------------ host-memory batches
  * The path as the reference sees it: segments start and end in host memory
  * (raw-socket buffers). A context owns one device, pinned staging and device

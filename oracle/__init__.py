@@ -37,6 +37,7 @@ _SIGS = {
     "oracle_synth_batch": (ctypes.c_int, [u64, u64, u32, vp, ctypes.c_int]),
     "oracle_batch_desc": (None, [vp, vp, vp, vp, u64, vp]),
     "oracle_ipv4_batch": (None, [vp, vp, u64, u32, ctypes.c_int, vp, vp]),
+    "oracle_tx_build": (None, [vp, vp, u64, vp, ctypes.c_int, vp]),
     "oracle_digest": (None, [vp, u64, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_uint16)]),
     "oracle_cpu_bench": (ctypes.c_double, [ctypes.c_int, u32, u64, ctypes.c_double, ctypes.POINTER(u64),
                                            ctypes.POINTER(ctypes.c_int)]),
@@ -134,3 +135,14 @@ def cpu_bench(threads: int, seg_len: int, nseg: int, min_seconds: float, opt: st
     p = ctypes.c_int()
     gibs = lib(opt).oracle_cpu_bench(threads, seg_len, nseg, min_seconds, ctypes.byref(d), ctypes.byref(p))
     return float(gibs), f"{d.value:016x}", int(p.value)
+
+
+def tx_build(payload: np.ndarray, segs: np.ndarray, out: np.ndarray, iphdr: bool = False) -> np.ndarray:
+    """context.c:150-213 for every record of segs (TXSEG layout); mutates out, returns the TCP checks."""
+    payload = np.ascontiguousarray(payload, np.uint8)
+    segs = np.ascontiguousarray(segs)
+    assert segs.dtype.itemsize == 48 and out.dtype == np.uint8 and out.flags.c_contiguous
+    checks = np.empty(segs.size, np.uint16)
+    lib().oracle_tx_build(payload.ctypes.data, segs.ctypes.data, segs.size, out.ctypes.data, int(iphdr),
+                          checks.ctypes.data)
+    return checks

@@ -19,6 +19,9 @@
 #include "oracle.h"
 
 #include <arpa/inet.h>
+#include <netinet/in.h>
+#include <netinet/ip.h>
+#include <netinet/tcp.h>
 #include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
@@ -195,6 +198,55 @@ void oracle_ipv4_batch(uint8_t *base, const uint64_t *off, uint64_t n, uint32_t 
             }
         }
         if (status) status[k] = st;
+    }
+}
+
+/* ---- context.c:150-213, us_internal_socket_context_send_packet -------------
+ * The same field assignments on the same system structs (struct iphdr, the
+ * reference's struct TcpHeader = struct tcphdr + options[4], Packets.h:46-50).
+ * Not restated: the 10 % drop (:153-156), getIpPacketBuffer (:167), printf. */
+void oracle_tx_build(const uint8_t *payload, const oracle_txseg_t *segs, uint64_t n, uint8_t *out, int iphdr,
+                     uint16_t *checks) {
+    for (uint64_t k = 0; k < n; ++k) {
+        const oracle_txseg_t *d = &segs[k];
+        const int data = (d->flags & 16) != 0;
+        const size_t length = data ? d->len : 0;
+        if (length > 65491) {
+            if (checks) checks[k] = 0;
+            continue;
+        }
+        struct iphdr *ip = (struct iphdr *) (out + d->out_off);
+        memset(ip, 0, sizeof(struct iphdr));                           /* :169 */
+        ip->ihl = 5;                                                   /* :171 */
+        ip->version = 4;
+        ip->tot_len = htons((uint16_t) (sizeof(struct iphdr) + 24 + length));
+        ip->id = (uint16_t) htonl(54321);                              /* :174, u32 -> u16 as stored */
+        ip->ttl = 255;
+        ip->protocol = IPPROTO_TCP;
+        ip->saddr = d->saddr_be;
+        ip->daddr = d->daddr_be;
+        uint8_t *tcp = (uint8_t *) ip + sizeof(struct iphdr);
+        struct tcphdr *th = (struct tcphdr *) tcp;
+        memset(tcp, 0, 24);                                            /* :182, sizeof(struct TcpHeader) */
+        th->ack = (d->flags & 1) != 0;                                 /* :184-187 */
+        th->syn = (d->flags & 2) != 0;
+        th->fin = (d->flags & 4) != 0;
+        th->rst = (d->flags & 8) != 0;
+        if (data) {                                                    /* :188-191 */
+            th->psh = 1;
+            memcpy(tcp + 24, payload + d->payload_off, length);
+        }
+        th->ack_seq = htonl(d->ack);                                   /* :193-196 */
+        th->seq = htonl(d->seq);
+        th->source = htons(d->sport);
+        th->dest = htons(d->dport);
+        tcp[20] = 3; tcp[21] = 3; tcp[22] = 5; tcp[23] = 0;            /* :199-202 */
+        th->doff = 6;                                                  /* :205 */
+        th->window = htons(8192);
+        th->check = oracle_csum_continue(oracle_pseudo(d->saddr_be, d->daddr_be, htons((uint16_t) (24 + length))),
+                                         (const char *) tcp, (int) (24 + length));   /* :208-209 */
+        if (iphdr) ip->check = oracle_csum_continue(0, (const char *) ip, sizeof(struct iphdr));   /* :179 */
+        if (checks) checks[k] = th->check;
     }
 }
 

@@ -50,6 +50,19 @@ void oracle_batch_desc(const uint8_t *base, const uint64_t *off, const uint32_t 
 void oracle_ipv4_batch(uint8_t *base, const uint64_t *off, uint64_t n, uint32_t cap,
                        int mode, uint16_t *out, uint8_t *status);
 
+/* context.c:150-213 segment builder (minus the drop and the trace) for a
+ * batch: layout-identical to tcpcsum_txseg_t (48 bytes). iphdr: also fill the
+ * IPv4 header checksum. checks (nullable) receives the TCP checks. */
+typedef struct oracle_txseg {
+    uint64_t payload_off, out_off;
+    uint32_t saddr_be, daddr_be, seq, ack;
+    uint16_t sport, dport, len;
+    uint8_t flags, reserved0;
+    uint64_t reserved1;
+} oracle_txseg_t;
+void oracle_tx_build(const uint8_t *payload, const oracle_txseg_t *segs, uint64_t n, uint8_t *out, int iphdr,
+                     uint16_t *checks);
+
 /* Digests of SURVEY.md Appendix B: fnv1a64 over out[] as LE u16 bytes. */
 void oracle_digest(const uint16_t *out, uint64_t n, uint64_t *fnv, uint64_t *sum,
                    uint16_t *xr);

@@ -37,11 +37,13 @@ from .api import (  # noqa: F401
     stream_probe,
     synth_fill,
     synth_pseudo,
+    tx_build,
+    TXSEG_DTYPE,
 )
 
 __all__ = [
     "DESC_DTYPE", "IPV4_FILL", "IPV4_IPHDR", "PKT_IPHDR_BAD", "IPV4_VERIFY", "PKT_OK", "PKT_SKIPPED", "TcpCsumError",
     "HostContext", "batch_desc", "batch_uniform", "csum_continue", "device_check",
     "getPseudoHeaderSum", "ipv4_batch", "lib", "lib_path", "pinned_empty", "set_tuning", "stream_probe",
-    "synth_fill", "synth_pseudo",
+    "synth_fill", "synth_pseudo", "tx_build", "TXSEG_DTYPE",
 ]

@@ -37,6 +37,11 @@ PKT_IPHDR_BAD = 2
 
 # tcpcsum_desc_t {u64 offset; u32 len; u32 sum_start}
 DESC_DTYPE = np.dtype([("offset", "<u8"), ("len", "<u4"), ("sum_start", "<u4")])
+# tcpcsum_txseg_t (48 bytes)
+TXSEG_DTYPE = np.dtype([("payload_off", "<u8"), ("out_off", "<u8"), ("saddr_be", "<u4"), ("daddr_be", "<u4"),
+                        ("seq", "<u4"), ("ack", "<u4"), ("sport", "<u2"), ("dport", "<u2"), ("len", "<u2"),
+                        ("flags", "u1"), ("reserved0", "u1"), ("reserved1", "<u8")])
+TXF_ACK, TXF_SYN, TXF_FIN, TXF_RST, TXF_DATA = 1, 2, 4, 8, 16
 
 _ERRNAMES = {EINVAL: "EINVAL", ENODEV: "ENODEV", EHIP: "EHIP", ENOMEM: "ENOMEM"}
 
@@ -82,6 +87,7 @@ SIGNATURES = {
     "tcpcsum_host_free": (None, [vp]),
     "tcpcsum_batch_uniform_host": (ctypes.c_int, [vp, vp, u64, u32, vp, u32, vp, u64]),
     "tcpcsum_ipv4_batch_host": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp, u64, u32, ctypes.c_int, vp, vp]),
+    "tcpcsum_tx_build_dev": (ctypes.c_int, [vp, vp, u64, u32, vp, ctypes.c_int, vp, vp]),
     "tcpcsum_synth_fill_dev": (ctypes.c_int, [vp, u64, u64, vp]),
     "tcpcsum_synth_pseudo_dev": (ctypes.c_int, [vp, u64, u64, u32, vp]),
     "tcpcsum_stream_probe_dev": (ctypes.c_int, [vp, u64, vp, ctypes.POINTER(ctypes.c_int), vp]),
@@ -215,6 +221,16 @@ def ipv4_batch(pkts, pkt_off, n: int, cap: int, mode: int, out=None, status=None
                                       _dev_ptr(out, "out"), _dev_ptr(status, "status"), _stream_handle(stream))
     _check(rc, "tcpcsum_ipv4_batch_dev")
     return out, status
+
+
+def tx_build(payload, segs, n: int, max_len: int, out_pkts, mode: int = 0, checks=None, stream=None):
+    """Assemble + checksum n IPv4/TCP packets on the GPU (device-side context.c:150-213).
+    ``segs``: device tensor holding n TXSEG_DTYPE records (16-B aligned)."""
+    rc = lib().tcpcsum_tx_build_dev(_dev_ptr(payload, "payload"), _dev_ptr(segs, "segs"), n, max_len,
+                                    _dev_ptr(out_pkts, "out_pkts"), mode, _dev_ptr(checks, "checks"),
+                                    _stream_handle(stream))
+    _check(rc, "tcpcsum_tx_build_dev")
+    return checks
 
 
 def synth_fill(dst, stream_off: int, nbytes: int, dst_offset: int = 0, stream=None) -> None:

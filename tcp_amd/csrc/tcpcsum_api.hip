@@ -17,6 +17,9 @@
 #include "tcpcsum.h"
 #include "tcpcsum_internal.h"
 
+static_assert(sizeof(tcpcsum_desc_t) == 16, "descriptor is read as one 16-B load");
+static_assert(sizeof(tcpcsum_txseg_t) == 48, "tx descriptor is read as three 16-B loads");
+
 namespace {
 
 std::atomic<int> g_last_hip_error{0};
@@ -159,6 +162,18 @@ int tcpcsum_ipv4_batch_dev(void* d_pkts, const uint64_t* d_pkt_off, uint64_t n, 
     tcpcsum::launch_ipv4((uint8_t*)d_pkts, d_pkt_off, n, cap, UINT64_MAX, mode, d_out, d_status, nullptr,
                          (hipStream_t)stream,
                          tuning());
+    return check_launch();
+}
+
+int tcpcsum_tx_build_dev(const void* d_payload, const tcpcsum_txseg_t* d_segs, uint64_t n, uint32_t max_len,
+                         void* d_out_pkts, int mode, uint16_t* d_check, void* stream) {
+    if (n == 0) return TCPCSUM_OK;
+    if (!d_segs || !d_out_pkts || (mode & ~TCPCSUM_IPV4_IPHDR) || (((uintptr_t)d_segs) & 15u))
+        return TCPCSUM_EINVAL;
+    int rc = require_device(nullptr, 0);
+    if (rc) return rc;
+    tcpcsum::launch_tx_build((const uint8_t*)d_payload, d_segs, n, max_len, (uint8_t*)d_out_pkts, mode, d_check,
+                             (hipStream_t)stream, tuning());
     return check_launch();
 }
 

@@ -40,6 +40,8 @@ void launch_desc(const uint8_t* base, const tcpcsum_desc_t* d, uint64_t n, uint3
 // ipout (nullable): per-packet IPv4 header checksum when mode has TCPCSUM_IPV4_IPHDR
 void launch_ipv4(uint8_t* pkts, const uint64_t* off, uint64_t n, uint32_t cap, uint64_t limit, int mode,
                  uint16_t* out, uint8_t* status, uint16_t* ipout, hipStream_t s, const Tuning& tu);
+void launch_tx_build(const uint8_t* payload, const tcpcsum_txseg_t* segs, uint64_t n, uint32_t max_len,
+                     uint8_t* outp, int mode, uint16_t* checks, hipStream_t s, const Tuning& tu);
 void launch_synth_fill(uint8_t* dst, uint64_t off, uint64_t nbytes, hipStream_t s);
 void launch_synth_pseudo(uint32_t* ss, uint64_t seg0, uint64_t n, uint32_t seg_len, hipStream_t s);
 // returns the grid size (= partials written)

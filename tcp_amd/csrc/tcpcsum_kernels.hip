@@ -450,6 +450,168 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const 
     }
 }
 
+// ---------------------------------------------------------------- tx build
+// Device-side context.c:150-213: write the IPv4/TCP packet of each descriptor
+// and checksum it in the same pass. Phase 1 (all lanes of the group): the
+// payload is copied in 16-byte destination chunks — each lane loads the (at
+// most two) aligned 16-B source chunks under its destination chunk and funnel-
+// shifts them into place (v_alignbyte), stores the chunk (one dwordx4 store,
+// byte stores only at the two ragged ends) and sums it from registers. Phase 2
+// (lanes 0..10): the 44 header bytes of context.c:169-206 as 11 dwords, the
+// TCP and optional IP checks folded in, stored after the group reduction.
+__device__ __forceinline__ uint32_t funnel(const uint32_t (&w)[8], int q, int k, uint32_t r) {
+    // bytes [4(q+k)+r, +4) of the 32-byte window w
+    const int i = q + k;
+    uint32_t lo, hi;
+    switch (i) {   // static register indices (no scratch)
+        case 0: lo = w[0]; hi = w[1]; break;
+        case 1: lo = w[1]; hi = w[2]; break;
+        case 2: lo = w[2]; hi = w[3]; break;
+        case 3: lo = w[3]; hi = w[4]; break;
+        case 4: lo = w[4]; hi = w[5]; break;
+        case 5: lo = w[5]; hi = w[6]; break;
+        default: lo = w[6]; hi = w[7]; break;
+    }
+    return __builtin_amdgcn_alignbyte(hi, lo, r);
+}
+
+__device__ __forceinline__ uint32_t sum_halves(uint32_t d) { return (d & 0xffffu) + (d >> 16); }
+
+template <int G, int C>
+__global__ __launch_bounds__(256) void k_tx_build(const uint8_t* __restrict__ payload,
+                                                  const tcpcsum_txseg_t* __restrict__ segs, uint64_t n,
+                                                  uint8_t* __restrict__ outp, int mode,
+                                                  uint16_t* __restrict__ checks) {
+    constexpr int GPW = 64 / G;
+    const int lane = threadIdx.x & 63;
+    const int q0 = lane / G, gl = lane % G;
+    const uint64_t ngroups = (uint64_t)gridDim.x * 4u * GPW;
+    for (uint64_t i = ((uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6)) * GPW + q0; i < n; i += ngroups) {
+        const u32x4* dp = reinterpret_cast<const u32x4*>(segs + i);
+        const u32x4 d0 = dp[0], d1 = dp[1], d2 = dp[2];
+        const uint64_t payload_off = (uint64_t)d0.x | ((uint64_t)d0.y << 32);
+        const uint64_t out_off = (uint64_t)d0.z | ((uint64_t)d0.w << 32);
+        const uint32_t sa = d1.x, da = d1.y, seq = d1.z, ack = d1.w;
+        const uint32_t sport = d2.x & 0xffffu, dport = d2.x >> 16;
+        const uint32_t flags = (d2.y >> 16) & 0xffu;
+        const bool data = (flags & TCPCSUM_TXF_DATA) != 0;
+        const uint32_t len = data ? (d2.y & 0xffffu) : 0u;
+        if (len > 65491u) {
+            if (gl == 0 && checks) checks[i] = 0;
+            continue;
+        }
+        uint8_t* ip = outp + out_off;
+        uint8_t* dst = ip + 44;
+        const uint8_t* src = payload + payload_off;
+        const bool odd = ((uintptr_t)ip & 1u) != 0;   // parity of the TCP start (ip + 20)
+
+        // ---- phase 1: payload copy + sum
+        const uint32_t dm = (uint32_t)((uintptr_t)dst & 15u);
+        uint8_t* dbase = dst - dm;
+        const uint32_t nch = (dm + len + 15u) >> 4;
+        const uintptr_t s0 = (uintptr_t)src - dm;               // source address under dest chunk 0
+        const uint32_t sh = (uint32_t)(s0 & 15u);
+        const int q = (int)(sh >> 2);
+        const uint32_t r = sh & 3u;
+        const uint8_t* sbase = (const uint8_t*)(s0 - sh);         // aligned source chunk under dest chunk 0
+        const uintptr_t src_lo = (uintptr_t)src, src_hi = (uintptr_t)src + len;
+        uint64_t W = 0, O = 0;
+        for (uint32_t rr = 0; rr < nch; rr += (uint32_t)(G * C)) {
+            uint32_t w[C][8];
+#pragma unroll
+            for (int k = 0; k < C; ++k) {
+                const uint32_t idx = rr + (uint32_t)(k * G + gl);
+                const uint8_t* a = sbase + (uint64_t)idx * 16u;
+                const uint8_t* b = a + 16;
+                const bool va = idx < nch && (uintptr_t)a < src_hi && (uintptr_t)a + 16 > src_lo;
+                const bool vb = idx < nch && sh != 0 && (uintptr_t)b < src_hi && (uintptr_t)b + 16 > src_lo;
+                const u32x4 A = va ? ld16(a) : u32x4{0u, 0u, 0u, 0u};
+                const u32x4 B = vb ? ld16(b) : u32x4{0u, 0u, 0u, 0u};
+                w[k][0] = A.x; w[k][1] = A.y; w[k][2] = A.z; w[k][3] = A.w;
+                w[k][4] = B.x; w[k][5] = B.y; w[k][6] = B.z; w[k][7] = B.w;
+            }
+            uint32_t wsum = 0, osum = 0;
+#pragma unroll
+            for (int k = 0; k < C; ++k) {
+                const uint32_t idx = rr + (uint32_t)(k * G + gl);
+                if (idx >= nch) continue;
+                u32x4 v;
+                v.x = funnel(w[k], q, 0, r);
+                v.y = funnel(w[k], q, 1, r);
+                v.z = funnel(w[k], q, 2, r);
+                v.w = funnel(w[k], q, 3, r);
+                const int64_t rel = (int64_t)idx * 16 - (int64_t)dm;   // dest chunk start - dst
+                uint8_t* dc = dbase + (uint64_t)idx * 16u;
+                if (rel >= 0 && rel + 16 <= (int64_t)len) {
+                    *reinterpret_cast<u32x4*>(dc) = v;
+                    wsum = sad16(v.x, wsum); wsum = sad16(v.y, wsum);
+                    wsum = sad16(v.z, wsum); wsum = sad16(v.w, wsum);
+                    if (odd) {
+                        osum = sad8(v.x & 0xff00ff00u, osum); osum = sad8(v.y & 0xff00ff00u, osum);
+                        osum = sad8(v.z & 0xff00ff00u, osum); osum = sad8(v.w & 0xff00ff00u, osum);
+                    }
+                } else {
+                    const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                    for (int b2 = 0; b2 < 16; ++b2) {
+                        const int64_t pos = rel + b2;
+                        if (pos >= 0 && pos < (int64_t)len) dc[b2] = (uint8_t)(vv[b2 >> 2] >> (8 * (b2 & 3)));
+                    }
+                    chunk_wo_bytes(v, rel, (int64_t)len, odd, wsum, osum);
+                }
+            }
+            W += wsum;
+            O += osum;
+        }
+        W = group_sum64<G>(W);
+        O = odd ? group_sum64<G>(O) : 0;
+        const uint64_t Spay = combine(0, W, O, odd);   // payload sum, relative to its even start (TCP+24)
+
+        // ---- phase 2: header (context.c:169-206), checks, stores
+        const uint32_t tot = 44u + len;
+        const uint32_t tcp_len = 24u + len;
+        const uint32_t len_be = ((tcp_len & 0xffu) << 8) | ((tcp_len >> 8) & 0xffu);
+        const uint32_t tflags = (flags & TCPCSUM_TXF_FIN ? 1u : 0u) | (flags & TCPCSUM_TXF_SYN ? 2u : 0u) |
+                                (flags & TCPCSUM_TXF_RST ? 4u : 0u) | (data ? 8u : 0u) |
+                                (flags & TCPCSUM_TXF_ACK ? 16u : 0u);
+        uint32_t hd[11];
+        hd[0] = 0x45u | ((tot >> 8) << 16) | ((tot & 0xffu) << 24);
+        hd[1] = 0u;                                          // id = (u16)htonl(54321) = 0, frag_off 0
+        hd[2] = 0xffu | (6u << 8);                           // ttl 255, IPPROTO_TCP, check 0
+        hd[3] = sa;
+        hd[4] = da;
+        hd[5] = (sport >> 8) | ((sport & 0xffu) << 8) | ((dport >> 8) << 16) | ((dport & 0xffu) << 24);
+        hd[6] = __builtin_bswap32(seq);
+        hd[7] = __builtin_bswap32(ack);
+        hd[8] = 0x60u | (tflags << 8) | (0x20u << 16);       // doff 6, flags, window 8192 (BE 20 00)
+        hd[9] = 0u;                                          // check (set below), urg_ptr 0
+        hd[10] = 0x00050303u;                                // options 03 03 05 00
+        uint64_t S = Spay + (sa & 0xffffu) + (sa >> 16) + (da & 0xffffu) + (da >> 16) + 0x0600u + len_be;
+#pragma unroll
+        for (int k = 5; k < 11; ++k) S += sum_halves(hd[k]);
+        const uint16_t c = fold_ref(S);
+        hd[9] = c;
+        if (mode & TCPCSUM_IPV4_IPHDR) {
+            uint32_t is = 0;
+#pragma unroll
+            for (int k = 0; k < 5; ++k) is += sum_halves(hd[k]);
+            hd[2] |= (uint32_t)fold_ref(is) << 16;
+        }
+        for (int j = gl; j < 11; j += G) {   // lane j stores header dword j
+            uint32_t v = hd[0];
+#pragma unroll
+            for (int k = 1; k < 11; ++k) v = j == k ? hd[k] : v;
+            uint8_t* hp = ip + 4 * j;
+            if ((((uintptr_t)ip) & 3u) == 0) {
+                *reinterpret_cast<uint32_t*>(hp) = v;
+            } else {
+                hp[0] = (uint8_t)v; hp[1] = (uint8_t)(v >> 8); hp[2] = (uint8_t)(v >> 16); hp[3] = (uint8_t)(v >> 24);
+            }
+        }
+        if (gl == 0 && checks) checks[i] = c;
+    }
+}
+
 // ---------------------------------------------------------------- synthetic
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -686,6 +848,22 @@ void launch_ipv4(uint8_t* pkts, const uint64_t* off, uint64_t n, uint32_t cap, u
     } else {
         hipLaunchKernelGGL((k_ipv4<64, 8>), dim3(grid_for(n, max_blocks)), dim3(256), 0, s, pkts, off, n, cap,
                            limit, mode, out, status, ipout);
+    }
+}
+
+void launch_tx_build(const uint8_t* payload, const tcpcsum_txseg_t* segs, uint64_t n, uint32_t max_len,
+                     uint8_t* outp, int mode, uint16_t* checks, hipStream_t s, const Tuning& tu) {
+    const int max_blocks = tu.max_blocks > 0 ? tu.max_blocks : kDefaultMaxBlocks;
+    const uint64_t nch = ((uint64_t)max_len + 30u) >> 4;
+    if (nch <= 8) {
+        hipLaunchKernelGGL((k_tx_build<8, 1>), dim3(grid_for((n + 7) / 8, max_blocks)), dim3(256), 0, s, payload,
+                           segs, n, outp, mode, checks);
+    } else if (nch <= 96) {
+        hipLaunchKernelGGL((k_tx_build<32, 3>), dim3(grid_for((n + 1) / 2, max_blocks)), dim3(256), 0, s,
+                           payload, segs, n, outp, mode, checks);
+    } else {
+        hipLaunchKernelGGL((k_tx_build<64, 4>), dim3(grid_for(n, max_blocks)), dim3(256), 0, s, payload, segs, n,
+                           outp, mode, checks);
     }
 }
 

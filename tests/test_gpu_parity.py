@@ -373,3 +373,35 @@ def test_c_client_on_gpu(dev):
     r = subprocess.run([exe, "--gpu"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "mismatches: 0 /" in r.stdout
+
+
+@pytest.mark.parametrize("layout", ["packed", "packed_odd", "slots", "jumbo"])
+def test_tx_build_vs_oracle(dev, layout):
+    """Device-side segment assembly + checksum == the oracle's context.c:150-213, byte for byte."""
+    import tcp_amd
+    from tests.test_oracle import make_txsegs
+    rng = np.random.default_rng({"packed": 1, "packed_odd": 2, "slots": 3, "jumbo": 4}[layout])
+    payload = rng.integers(0, 256, 1 << 20, dtype=np.uint8)
+    max_len = 9000 if layout == "jumbo" else 1456
+    n = 400 if layout == "jumbo" else 3000
+    segs, size = make_txsegs(rng, n, payload.size, max_len=max_len, odd=layout == "packed_odd",
+                             slot=32768 if layout == "slots" else None)
+    garbage = rng.integers(0, 256, size, dtype=np.uint8)     # bytes between packets must survive
+    for mode in (0, tcp_amd.IPV4_IPHDR):
+        want = garbage.copy()
+        want_c = oracle.tx_build(payload, segs, want, iphdr=bool(mode))
+        dout = to_dev(garbage, dev)
+        dseg = to_dev(segs.view(np.uint8), dev)
+        chk = torch.empty(n, dtype=torch.int16, device=dev)
+        tcp_amd.tx_build(to_dev(payload, dev), dseg, n, max_len, dout, mode, chk)
+        got = dout.cpu().numpy()
+        assert np.array_equal(u16(chk), want_c), layout
+        if not np.array_equal(got, want):
+            bad = np.flatnonzero(got != want)
+            raise AssertionError(f"{layout} mode={mode}: {bad.size} bytes differ, first at {bad[:8]}")
+    # a too-small shape hint is slower, never wrong
+    dout = to_dev(garbage, dev)
+    tcp_amd.tx_build(to_dev(payload, dev), to_dev(segs.view(np.uint8), dev), n, 16, dout, 0, None)
+    want = garbage.copy()
+    oracle.tx_build(payload, segs, want)
+    assert np.array_equal(dout.cpu().numpy(), want)

@@ -143,3 +143,60 @@ def test_oracle_ipv4_iphdr_fill_then_verify():
     bad[first + 8] ^= 1                                  # TTL
     _, st3 = oracle.ipv4_batch(bad, off, 32768, 1 | 2)
     assert st3[np.flatnonzero(ok)[0]] == 2
+
+
+def make_txsegs(rng, n, payload_size, max_len=1456, odd=False, slot=None):
+    """Random tx descriptors (TXSEG layout) with non-overlapping packets; returns (segs, out_size)."""
+    import tcp_amd
+    segs = np.zeros(n, tcp_amd.TXSEG_DTYPE)
+    lens = rng.integers(0, max_len + 1, n)
+    lens[:4] = [0, 1, max_len, 3][:min(4, n)]
+    pos = 0
+    for i in range(n):
+        L = int(lens[i])
+        segs[i]["payload_off"] = int(rng.integers(0, payload_size - L)) if payload_size > L else 0
+        if slot:
+            segs[i]["out_off"] = i * slot + (int(rng.integers(0, 8)) if odd else 0)
+        else:
+            pos += int(rng.integers(0, 9)) if odd else 0
+            segs[i]["out_off"] = pos
+            pos += 44 + L
+        segs[i]["saddr_be"] = int(rng.integers(0, 2**32))
+        segs[i]["daddr_be"] = int(rng.integers(0, 2**32))
+        segs[i]["seq"] = int(rng.integers(0, 2**32))
+        segs[i]["ack"] = int(rng.integers(0, 2**32))
+        segs[i]["sport"] = int(rng.integers(0, 2**16))
+        segs[i]["dport"] = int(rng.integers(0, 2**16))
+        segs[i]["len"] = L
+        segs[i]["flags"] = int(rng.integers(0, 32)) | (16 if i % 3 else 0)
+    out_size = (n * slot + 64) if slot else pos + 64
+    return segs, out_size
+
+
+def test_oracle_tx_build_layout_and_verify():
+    """The builder's packets carry the reference's header fields and verify to zero."""
+    import struct
+    rng = np.random.default_rng(6)
+    payload = rng.integers(0, 256, 1 << 16, dtype=np.uint8)
+    segs, size = make_txsegs(rng, 200, payload.size, odd=True)
+    out = np.zeros(size, np.uint8)
+    checks = oracle.tx_build(payload, segs, out, iphdr=True)
+    offs = segs["out_off"].astype(np.uint64)
+    v, st = oracle.ipv4_batch(out.copy(), offs, 65535, 1 | 2)
+    assert np.all(st == 0) and np.all(v == 0)
+    for s, c in zip(segs[:50], checks[:50]):
+        o = int(s["out_off"])
+        data = bool(s["flags"] & 16)
+        L = int(s["len"]) if data else 0
+        ip = out[o:o + 44 + L].tobytes()
+        ver_ihl, tos, tot, ident, frag, ttl, proto = struct.unpack("!BBHHHBB", ip[:10])
+        assert (ver_ihl, tos, tot, ident, frag, ttl, proto) == (0x45, 0, 44 + L, 0, 0, 255, 6)
+        sport, dport, seq, ack, offf, flg, win = struct.unpack("!HHIIBBH", ip[20:36])
+        assert (sport, dport, seq, ack) == (s["sport"], s["dport"], s["seq"], s["ack"])
+        assert offf == 0x60 and win == 8192 and ip[40:44] == bytes([3, 3, 5, 0])
+        f = int(s["flags"])
+        assert flg == ((f >> 2 & 1) | (f >> 1 & 1) << 1 | (f >> 3 & 1) << 2 | int(data) << 3 | (f & 1) << 4)
+        assert struct.unpack("<H", ip[36:38])[0] == c
+        if data:
+            po = int(s["payload_off"])
+            assert ip[44:] == payload[po:po + L].tobytes()
