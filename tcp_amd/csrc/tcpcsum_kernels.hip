@@ -508,25 +508,23 @@ __global__ __launch_bounds__(256) void k_tx_build(const uint8_t* __restrict__ pa
         // ---- phase 1: payload copy + sum
         const uint32_t dm = (uint32_t)((uintptr_t)dst & 15u);
         uint8_t* dbase = dst - dm;
-        const uint32_t nch = (dm + len + 15u) >> 4;
         const uintptr_t s0 = (uintptr_t)src - dm;               // source address under dest chunk 0
         const uint32_t sh = (uint32_t)(s0 & 15u);
         const int q = (int)(sh >> 2);
         const uint32_t r = sh & 3u;
         const uint8_t* sbase = (const uint8_t*)(s0 - sh);         // aligned source chunk under dest chunk 0
-        const uintptr_t src_lo = (uintptr_t)src, src_hi = (uintptr_t)src + len;
+        // destination chunks entirely inside the payload: [f0, f1)
+        const uint32_t f0 = dm ? 1u : 0u;
+        const uint32_t f1 = (dm + len) >> 4;
         uint64_t W = 0, O = 0;
-        for (uint32_t rr = 0; rr < nch; rr += (uint32_t)(G * C)) {
+        for (uint32_t rr = f0; rr < f1; rr += (uint32_t)(G * C)) {
             uint32_t w[C][8];
 #pragma unroll
-            for (int k = 0; k < C; ++k) {
+            for (int k = 0; k < C; ++k) {   // every source byte under a full chunk is payload
                 const uint32_t idx = rr + (uint32_t)(k * G + gl);
                 const uint8_t* a = sbase + (uint64_t)idx * 16u;
-                const uint8_t* b = a + 16;
-                const bool va = idx < nch && (uintptr_t)a < src_hi && (uintptr_t)a + 16 > src_lo;
-                const bool vb = idx < nch && sh != 0 && (uintptr_t)b < src_hi && (uintptr_t)b + 16 > src_lo;
-                const u32x4 A = va ? ld16(a) : u32x4{0u, 0u, 0u, 0u};
-                const u32x4 B = vb ? ld16(b) : u32x4{0u, 0u, 0u, 0u};
+                const u32x4 A = idx < f1 ? ld16(a) : u32x4{0u, 0u, 0u, 0u};
+                const u32x4 B = (idx < f1 && sh) ? ld16(a + 16) : u32x4{0u, 0u, 0u, 0u};
                 w[k][0] = A.x; w[k][1] = A.y; w[k][2] = A.z; w[k][3] = A.w;
                 w[k][4] = B.x; w[k][5] = B.y; w[k][6] = B.z; w[k][7] = B.w;
             }
@@ -534,34 +532,54 @@ __global__ __launch_bounds__(256) void k_tx_build(const uint8_t* __restrict__ pa
 #pragma unroll
             for (int k = 0; k < C; ++k) {
                 const uint32_t idx = rr + (uint32_t)(k * G + gl);
-                if (idx >= nch) continue;
+                if (idx >= f1) continue;
                 u32x4 v;
                 v.x = funnel(w[k], q, 0, r);
                 v.y = funnel(w[k], q, 1, r);
                 v.z = funnel(w[k], q, 2, r);
                 v.w = funnel(w[k], q, 3, r);
-                const int64_t rel = (int64_t)idx * 16 - (int64_t)dm;   // dest chunk start - dst
-                uint8_t* dc = dbase + (uint64_t)idx * 16u;
-                if (rel >= 0 && rel + 16 <= (int64_t)len) {
-                    *reinterpret_cast<u32x4*>(dc) = v;
-                    wsum = sad16(v.x, wsum); wsum = sad16(v.y, wsum);
-                    wsum = sad16(v.z, wsum); wsum = sad16(v.w, wsum);
-                    if (odd) {
-                        osum = sad8(v.x & 0xff00ff00u, osum); osum = sad8(v.y & 0xff00ff00u, osum);
-                        osum = sad8(v.z & 0xff00ff00u, osum); osum = sad8(v.w & 0xff00ff00u, osum);
-                    }
-                } else {
-                    const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                    for (int b2 = 0; b2 < 16; ++b2) {
-                        const int64_t pos = rel + b2;
-                        if (pos >= 0 && pos < (int64_t)len) dc[b2] = (uint8_t)(vv[b2 >> 2] >> (8 * (b2 & 3)));
-                    }
-                    chunk_wo_bytes(v, rel, (int64_t)len, odd, wsum, osum);
+                *reinterpret_cast<u32x4*>(dbase + (uint64_t)idx * 16u) = v;
+                wsum = sad16(v.x, wsum); wsum = sad16(v.y, wsum);
+                wsum = sad16(v.z, wsum); wsum = sad16(v.w, wsum);
+                if (odd) {
+                    osum = sad8(v.x & 0xff00ff00u, osum); osum = sad8(v.y & 0xff00ff00u, osum);
+                    osum = sad8(v.z & 0xff00ff00u, osum); osum = sad8(v.w & 0xff00ff00u, osum);
                 }
             }
             W += wsum;
             O += osum;
+        }
+        // the ragged ends: the head chunk (lane 0) and the tail chunk (lane 1), byte-masked
+        if (len && gl < 2) {
+            const bool head = dm != 0;
+            const bool tail = ((dm + len) & 15u) != 0 && f1 >= f0 && !(head && f1 == 0);
+            const bool mine = gl == 0 ? head : tail;
+            if (mine) {
+                const uint32_t idx = gl == 0 ? 0u : f1;
+                const uint8_t* a = sbase + (uint64_t)idx * 16u;
+                const uintptr_t src_lo = (uintptr_t)src, src_hi = (uintptr_t)src + len;
+                const bool va = (uintptr_t)a < src_hi && (uintptr_t)a + 16 > src_lo;
+                const bool vb = sh != 0 && (uintptr_t)a + 16 < src_hi && (uintptr_t)a + 32 > src_lo;
+                const u32x4 A = va ? ld16(a) : u32x4{0u, 0u, 0u, 0u};
+                const u32x4 B = vb ? ld16(a + 16) : u32x4{0u, 0u, 0u, 0u};
+                const uint32_t w[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
+                u32x4 v;
+                v.x = funnel(w, q, 0, r);
+                v.y = funnel(w, q, 1, r);
+                v.z = funnel(w, q, 2, r);
+                v.w = funnel(w, q, 3, r);
+                const int64_t rel = (int64_t)idx * 16 - (int64_t)dm;   // dest chunk start - dst
+                uint8_t* dc = dbase + (uint64_t)idx * 16u;
+                const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+                for (int b2 = 0; b2 < 16; ++b2) {
+                    const int64_t pos = rel + b2;
+                    if (pos >= 0 && pos < (int64_t)len) dc[b2] = (uint8_t)(vv[b2 >> 2] >> (8 * (b2 & 3)));
+                }
+                uint32_t wsum = 0, osum = 0;
+                chunk_wo_bytes(v, rel, (int64_t)len, odd, wsum, osum);
+                W += wsum;
+                O += osum;
+            }
         }
         W = group_sum64<G>(W);
         O = odd ? group_sum64<G>(O) : 0;
