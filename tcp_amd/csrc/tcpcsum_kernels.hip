@@ -459,20 +459,21 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const 
 // byte stores only at the two ragged ends) and sums it from registers. Phase 2
 // (lanes 0..10): the 44 header bytes of context.c:169-206 as 11 dwords, the
 // TCP and optional IP checks folded in, stored after the group reduction.
-__device__ __forceinline__ uint32_t funnel(const uint32_t (&w)[8], int q, int k, uint32_t r) {
-    // bytes [4(q+k)+r, +4) of the 32-byte window w
-    const int i = q + k;
-    uint32_t lo, hi;
-    switch (i) {   // static register indices (no scratch)
-        case 0: lo = w[0]; hi = w[1]; break;
-        case 1: lo = w[1]; hi = w[2]; break;
-        case 2: lo = w[2]; hi = w[3]; break;
-        case 3: lo = w[3]; hi = w[4]; break;
-        case 4: lo = w[4]; hi = w[5]; break;
-        case 5: lo = w[5]; hi = w[6]; break;
-        default: lo = w[6]; hi = w[7]; break;
-    }
-    return __builtin_amdgcn_alignbyte(hi, lo, r);
+// The 16 bytes at byte offset 4q+r of the 32-byte window A:B (q, r uniform
+// per packet): five selected dwords, four v_alignbyte. Register-only — a
+// dynamically indexed window array would be placed in scratch.
+__device__ __forceinline__ u32x4 funnel16(const u32x4 A, const u32x4 B, int q, uint32_t r) {
+    const uint32_t w0 = q == 0 ? A.x : q == 1 ? A.y : q == 2 ? A.z : A.w;
+    const uint32_t w1 = q == 0 ? A.y : q == 1 ? A.z : q == 2 ? A.w : B.x;
+    const uint32_t w2 = q == 0 ? A.z : q == 1 ? A.w : q == 2 ? B.x : B.y;
+    const uint32_t w3 = q == 0 ? A.w : q == 1 ? B.x : q == 2 ? B.y : B.z;
+    const uint32_t w4 = q == 0 ? B.x : q == 1 ? B.y : q == 2 ? B.z : B.w;
+    u32x4 v;
+    v.x = __builtin_amdgcn_alignbyte(w1, w0, r);
+    v.y = __builtin_amdgcn_alignbyte(w2, w1, r);
+    v.z = __builtin_amdgcn_alignbyte(w3, w2, r);
+    v.w = __builtin_amdgcn_alignbyte(w4, w3, r);
+    return v;
 }
 
 __device__ __forceinline__ uint32_t sum_halves(uint32_t d) { return (d & 0xffffu) + (d >> 16); }
@@ -512,32 +513,28 @@ __global__ __launch_bounds__(256) void k_tx_build(const uint8_t* __restrict__ pa
         const uint32_t sh = (uint32_t)(s0 & 15u);
         const int q = (int)(sh >> 2);
         const uint32_t r = sh & 3u;
-        const uint8_t* sbase = (const uint8_t*)(s0 - sh);         // aligned source chunk under dest chunk 0
+        // aligned source chunk under dest chunk 0 (derived from the kernel argument,
+        // not from an integer, so the compiler keeps global_ rather than flat_ loads)
+        const uint8_t* sbase = src - (int64_t)(dm + sh);
         // destination chunks entirely inside the payload: [f0, f1)
         const uint32_t f0 = dm ? 1u : 0u;
         const uint32_t f1 = (dm + len) >> 4;
         uint64_t W = 0, O = 0;
         for (uint32_t rr = f0; rr < f1; rr += (uint32_t)(G * C)) {
-            uint32_t w[C][8];
+            u32x4 A[C], B[C];
 #pragma unroll
             for (int k = 0; k < C; ++k) {   // every source byte under a full chunk is payload
                 const uint32_t idx = rr + (uint32_t)(k * G + gl);
                 const uint8_t* a = sbase + (uint64_t)idx * 16u;
-                const u32x4 A = idx < f1 ? ld16(a) : u32x4{0u, 0u, 0u, 0u};
-                const u32x4 B = (idx < f1 && sh) ? ld16(a + 16) : u32x4{0u, 0u, 0u, 0u};
-                w[k][0] = A.x; w[k][1] = A.y; w[k][2] = A.z; w[k][3] = A.w;
-                w[k][4] = B.x; w[k][5] = B.y; w[k][6] = B.z; w[k][7] = B.w;
+                A[k] = idx < f1 ? ld16(a) : u32x4{0u, 0u, 0u, 0u};
+                B[k] = (idx < f1 && sh) ? ld16(a + 16) : u32x4{0u, 0u, 0u, 0u};
             }
             uint32_t wsum = 0, osum = 0;
 #pragma unroll
             for (int k = 0; k < C; ++k) {
                 const uint32_t idx = rr + (uint32_t)(k * G + gl);
                 if (idx >= f1) continue;
-                u32x4 v;
-                v.x = funnel(w[k], q, 0, r);
-                v.y = funnel(w[k], q, 1, r);
-                v.z = funnel(w[k], q, 2, r);
-                v.w = funnel(w[k], q, 3, r);
+                const u32x4 v = funnel16(A[k], B[k], q, r);
                 *reinterpret_cast<u32x4*>(dbase + (uint64_t)idx * 16u) = v;
                 wsum = sad16(v.x, wsum); wsum = sad16(v.y, wsum);
                 wsum = sad16(v.z, wsum); wsum = sad16(v.w, wsum);
@@ -562,18 +559,14 @@ __global__ __launch_bounds__(256) void k_tx_build(const uint8_t* __restrict__ pa
                 const bool vb = sh != 0 && (uintptr_t)a + 16 < src_hi && (uintptr_t)a + 32 > src_lo;
                 const u32x4 A = va ? ld16(a) : u32x4{0u, 0u, 0u, 0u};
                 const u32x4 B = vb ? ld16(a + 16) : u32x4{0u, 0u, 0u, 0u};
-                const uint32_t w[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
-                u32x4 v;
-                v.x = funnel(w, q, 0, r);
-                v.y = funnel(w, q, 1, r);
-                v.z = funnel(w, q, 2, r);
-                v.w = funnel(w, q, 3, r);
+                const u32x4 v = funnel16(A, B, q, r);
                 const int64_t rel = (int64_t)idx * 16 - (int64_t)dm;   // dest chunk start - dst
                 uint8_t* dc = dbase + (uint64_t)idx * 16u;
-                const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
                 for (int b2 = 0; b2 < 16; ++b2) {
+                    const uint32_t word = b2 < 4 ? v.x : b2 < 8 ? v.y : b2 < 12 ? v.z : v.w;
                     const int64_t pos = rel + b2;
-                    if (pos >= 0 && pos < (int64_t)len) dc[b2] = (uint8_t)(vv[b2 >> 2] >> (8 * (b2 & 3)));
+                    if (pos >= 0 && pos < (int64_t)len) dc[b2] = (uint8_t)(word >> (8 * (b2 & 3)));
                 }
                 uint32_t wsum = 0, osum = 0;
                 chunk_wo_bytes(v, rel, (int64_t)len, odd, wsum, osum);
