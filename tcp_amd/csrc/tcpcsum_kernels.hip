@@ -478,148 +478,219 @@ __device__ __forceinline__ u32x4 funnel16(const u32x4 A, const u32x4 B, int q, u
 
 __device__ __forceinline__ uint32_t sum_halves(uint32_t d) { return (d & 0xffffu) + (d >> 16); }
 
-template <int G, int C>
+// One packet of a tile, as decoded from its descriptor.
+struct TxPkt {
+    const uint8_t* src;     // payload
+    const uint8_t* sbase;   // aligned source chunk under destination chunk 0
+    uint8_t* ip;            // packet start
+    uint8_t* dbase;         // aligned destination chunk holding the first payload byte
+    uint32_t sa, da, seq, ack, ports, flags, len;
+    uint32_t dm, sh, f0, f1;
+    bool live, odd;
+};
+
+__device__ __forceinline__ void tx_decode(TxPkt& p, const tcpcsum_txseg_t* segs, uint64_t i, uint64_t n,
+                                          const uint8_t* payload, uint8_t* outp) {
+    p.live = i < n;
+    u32x4 d0 = {0u, 0u, 0u, 0u}, d1 = d0, d2 = d0;
+    if (p.live) {
+        const u32x4* dp = reinterpret_cast<const u32x4*>(segs + i);
+        d0 = dp[0]; d1 = dp[1]; d2 = dp[2];
+    }
+    const uint64_t payload_off = (uint64_t)d0.x | ((uint64_t)d0.y << 32);
+    const uint64_t out_off = (uint64_t)d0.z | ((uint64_t)d0.w << 32);
+    p.sa = d1.x; p.da = d1.y; p.seq = d1.z; p.ack = d1.w;
+    p.ports = d2.x;
+    p.flags = (d2.y >> 16) & 0xffu;
+    p.len = (p.flags & TCPCSUM_TXF_DATA) ? (d2.y & 0xffffu) : 0u;
+    if (p.len > 65491u) p.live = false;   // not written (d_check = 0)
+    p.ip = outp + out_off;
+    p.src = payload + payload_off;
+    uint8_t* dst = p.ip + 44;
+    p.odd = ((uintptr_t)p.ip & 1u) != 0;   // parity of the TCP start (ip + 20)
+    p.dm = (uint32_t)((uintptr_t)dst & 15u);
+    p.dbase = dst - p.dm;
+    p.sh = (uint32_t)(((uintptr_t)p.src - p.dm) & 15u);
+    // derived from the argument pointer (not an integer): keeps global_ loads
+    p.sbase = p.src - (int64_t)(p.dm + p.sh);
+    // destination chunks entirely inside the payload: [f0, f1)
+    p.f0 = p.dm ? 1u : 0u;
+    p.f1 = (p.dm + p.len) >> 4;
+    if (!p.live) { p.len = 0; p.f0 = 0; p.f1 = 0; }
+}
+
+// chunk e of the packet's ragged ends for lane gl: 0 = head (lane 0), 1 = tail (lane 1); -1 none
+__device__ __forceinline__ int tx_edge_chunk(const TxPkt& p, int gl) {
+    if (!p.len || gl > 1) return -1;
+    const bool head = p.dm != 0;
+    const bool tail = ((p.dm + p.len) & 15u) != 0 && p.f1 >= p.f0 && !(head && p.f1 == 0);
+    if (gl == 0) return head ? 0 : -1;
+    return tail ? (int)p.f1 : -1;
+}
+
+__device__ __forceinline__ void tx_edge_load(const TxPkt& p, int e, u32x4& A, u32x4& B) {
+    A = u32x4{0u, 0u, 0u, 0u};
+    B = A;
+    if (e < 0) return;
+    const uint8_t* a = p.sbase + (uint64_t)e * 16u;
+    const uintptr_t lo = (uintptr_t)p.src, hi = (uintptr_t)p.src + p.len;
+    if ((uintptr_t)a < hi && (uintptr_t)a + 16 > lo) A = ld16(a);
+    if (p.sh != 0 && (uintptr_t)a + 16 < hi && (uintptr_t)a + 32 > lo) B = ld16(a + 16);
+}
+
+// Phase 1 for a full chunk already loaded: shift into place, store, sum.
+__device__ __forceinline__ void tx_full_chunk(const TxPkt& p, uint32_t idx, const u32x4 A, const u32x4 B,
+                                              uint32_t& wsum, uint32_t& osum) {
+    const u32x4 v = funnel16(A, B, (int)(p.sh >> 2), p.sh & 3u);
+    *reinterpret_cast<u32x4*>(p.dbase + (uint64_t)idx * 16u) = v;
+    wsum = sad16(v.x, wsum); wsum = sad16(v.y, wsum);
+    wsum = sad16(v.z, wsum); wsum = sad16(v.w, wsum);
+    if (p.odd) {
+        osum = sad8(v.x & 0xff00ff00u, osum); osum = sad8(v.y & 0xff00ff00u, osum);
+        osum = sad8(v.z & 0xff00ff00u, osum); osum = sad8(v.w & 0xff00ff00u, osum);
+    }
+}
+
+// Ragged end: byte-masked store and sum of chunk e.
+__device__ __forceinline__ void tx_edge_chunk_store(const TxPkt& p, int e, const u32x4 A, const u32x4 B,
+                                                    uint32_t& wsum, uint32_t& osum) {
+    const u32x4 v = funnel16(A, B, (int)(p.sh >> 2), p.sh & 3u);
+    const int64_t rel = (int64_t)e * 16 - (int64_t)p.dm;   // dest chunk start - first payload byte
+    uint8_t* dc = p.dbase + (uint64_t)e * 16u;
+#pragma unroll
+    for (int b2 = 0; b2 < 16; ++b2) {
+        const uint32_t word = b2 < 4 ? v.x : b2 < 8 ? v.y : b2 < 12 ? v.z : v.w;
+        const int64_t pos = rel + b2;
+        if (pos >= 0 && pos < (int64_t)p.len) dc[b2] = (uint8_t)(word >> (8 * (b2 & 3)));
+    }
+    chunk_wo_bytes(v, rel, (int64_t)p.len, p.odd, wsum, osum);
+}
+
+// Phase 2: header (context.c:169-206) with the checks folded in; lanes store it.
+template <int G>
+__device__ __forceinline__ void tx_header(const TxPkt& p, uint64_t Spay, int mode, int gl, uint16_t* checks,
+                                          uint64_t i) {
+    const uint32_t tot = 44u + p.len;
+    const uint32_t tcp_len = 24u + p.len;
+    const uint32_t len_be = ((tcp_len & 0xffu) << 8) | ((tcp_len >> 8) & 0xffu);
+    const uint32_t fl = p.flags;
+    const uint32_t tflags = (fl & TCPCSUM_TXF_FIN ? 1u : 0u) | (fl & TCPCSUM_TXF_SYN ? 2u : 0u) |
+                            (fl & TCPCSUM_TXF_RST ? 4u : 0u) | (fl & TCPCSUM_TXF_DATA ? 8u : 0u) |
+                            (fl & TCPCSUM_TXF_ACK ? 16u : 0u);
+    const uint32_t sport = p.ports & 0xffffu, dport = p.ports >> 16;
+    uint32_t hd[11];
+    hd[0] = 0x45u | ((tot >> 8) << 16) | ((tot & 0xffu) << 24);
+    hd[1] = 0u;                                          // id = (u16)htonl(54321) = 0, frag_off 0
+    hd[2] = 0xffu | (6u << 8);                           // ttl 255, IPPROTO_TCP, check 0
+    hd[3] = p.sa;
+    hd[4] = p.da;
+    hd[5] = (sport >> 8) | ((sport & 0xffu) << 8) | ((dport >> 8) << 16) | ((dport & 0xffu) << 24);
+    hd[6] = __builtin_bswap32(p.seq);
+    hd[7] = __builtin_bswap32(p.ack);
+    hd[8] = 0x60u | (tflags << 8) | (0x20u << 16);       // doff 6, flags, window 8192 (BE 20 00)
+    hd[9] = 0u;                                          // check (below), urg_ptr 0
+    hd[10] = 0x00050303u;                                // options 03 03 05 00
+    uint64_t S = Spay + (p.sa & 0xffffu) + (p.sa >> 16) + (p.da & 0xffffu) + (p.da >> 16) + 0x0600u + len_be;
+#pragma unroll
+    for (int k = 5; k < 11; ++k) S += sum_halves(hd[k]);
+    const uint16_t c = fold_ref(S);
+    hd[9] = c;
+    if (mode & TCPCSUM_IPV4_IPHDR) {
+        uint32_t is = 0;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) is += sum_halves(hd[k]);
+        hd[2] |= (uint32_t)fold_ref(is) << 16;
+    }
+    for (int j = gl; j < 11; j += G) {   // lane j stores header dword j
+        uint32_t v = hd[0];
+#pragma unroll
+        for (int k = 1; k < 11; ++k) v = j == k ? hd[k] : v;
+        uint8_t* hp = p.ip + 4 * j;
+        if ((((uintptr_t)p.ip) & 3u) == 0) {
+            *reinterpret_cast<uint32_t*>(hp) = v;
+        } else {
+            hp[0] = (uint8_t)v; hp[1] = (uint8_t)(v >> 8); hp[2] = (uint8_t)(v >> 16); hp[3] = (uint8_t)(v >> 24);
+        }
+    }
+    if (gl == 0 && checks) checks[i] = c;
+}
+
+// Tile of (64/G)*U packets per wave: U packets per lane group in flight. All
+// descriptor loads, then all payload loads (bulk chunks and both ragged ends)
+// of the tile are issued before any is consumed. Payloads with more full
+// chunks than G*C take extra (un-overlapped) rounds.
+template <int G, int C, int U>
 __global__ __launch_bounds__(256) void k_tx_build(const uint8_t* __restrict__ payload,
                                                   const tcpcsum_txseg_t* __restrict__ segs, uint64_t n,
                                                   uint8_t* __restrict__ outp, int mode,
                                                   uint16_t* __restrict__ checks) {
     constexpr int GPW = 64 / G;
+    constexpr int SPT = GPW * U;
     const int lane = threadIdx.x & 63;
     const int q0 = lane / G, gl = lane % G;
-    const uint64_t ngroups = (uint64_t)gridDim.x * 4u * GPW;
-    for (uint64_t i = ((uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6)) * GPW + q0; i < n; i += ngroups) {
-        const u32x4* dp = reinterpret_cast<const u32x4*>(segs + i);
-        const u32x4 d0 = dp[0], d1 = dp[1], d2 = dp[2];
-        const uint64_t payload_off = (uint64_t)d0.x | ((uint64_t)d0.y << 32);
-        const uint64_t out_off = (uint64_t)d0.z | ((uint64_t)d0.w << 32);
-        const uint32_t sa = d1.x, da = d1.y, seq = d1.z, ack = d1.w;
-        const uint32_t sport = d2.x & 0xffffu, dport = d2.x >> 16;
-        const uint32_t flags = (d2.y >> 16) & 0xffu;
-        const bool data = (flags & TCPCSUM_TXF_DATA) != 0;
-        const uint32_t len = data ? (d2.y & 0xffffu) : 0u;
-        if (len > 65491u) {
-            if (gl == 0 && checks) checks[i] = 0;
-            continue;
-        }
-        uint8_t* ip = outp + out_off;
-        uint8_t* dst = ip + 44;
-        const uint8_t* src = payload + payload_off;
-        const bool odd = ((uintptr_t)ip & 1u) != 0;   // parity of the TCP start (ip + 20)
-
-        // ---- phase 1: payload copy + sum
-        const uint32_t dm = (uint32_t)((uintptr_t)dst & 15u);
-        uint8_t* dbase = dst - dm;
-        const uintptr_t s0 = (uintptr_t)src - dm;               // source address under dest chunk 0
-        const uint32_t sh = (uint32_t)(s0 & 15u);
-        const int q = (int)(sh >> 2);
-        const uint32_t r = sh & 3u;
-        // aligned source chunk under dest chunk 0 (derived from the kernel argument,
-        // not from an integer, so the compiler keeps global_ rather than flat_ loads)
-        const uint8_t* sbase = src - (int64_t)(dm + sh);
-        // destination chunks entirely inside the payload: [f0, f1)
-        const uint32_t f0 = dm ? 1u : 0u;
-        const uint32_t f1 = (dm + len) >> 4;
-        uint64_t W = 0, O = 0;
-        for (uint32_t rr = f0; rr < f1; rr += (uint32_t)(G * C)) {
-            u32x4 A[C], B[C];
+    const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
+    const uint64_t ntiles = (n + SPT - 1) / SPT;
+    for (uint64_t t = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6); t < ntiles; t += nwaves) {
+        TxPkt p[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) tx_decode(p[u], segs, t * SPT + (uint64_t)(u * GPW + q0), n, payload, outp);
+        u32x4 A[U][C], B[U][C], EA[U], EB[U];
+        int e[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
 #pragma unroll
             for (int k = 0; k < C; ++k) {   // every source byte under a full chunk is payload
-                const uint32_t idx = rr + (uint32_t)(k * G + gl);
-                const uint8_t* a = sbase + (uint64_t)idx * 16u;
-                A[k] = idx < f1 ? ld16(a) : u32x4{0u, 0u, 0u, 0u};
-                B[k] = (idx < f1 && sh) ? ld16(a + 16) : u32x4{0u, 0u, 0u, 0u};
+                const uint32_t idx = p[u].f0 + (uint32_t)(k * G + gl);
+                const uint8_t* a = p[u].sbase + (uint64_t)idx * 16u;
+                A[u][k] = idx < p[u].f1 ? ld16(a) : u32x4{0u, 0u, 0u, 0u};
+                B[u][k] = (idx < p[u].f1 && p[u].sh) ? ld16(a + 16) : u32x4{0u, 0u, 0u, 0u};
             }
+            e[u] = tx_edge_chunk(p[u], gl);
+            tx_edge_load(p[u], e[u], EA[u], EB[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
             uint32_t wsum = 0, osum = 0;
 #pragma unroll
             for (int k = 0; k < C; ++k) {
-                const uint32_t idx = rr + (uint32_t)(k * G + gl);
-                if (idx >= f1) continue;
-                const u32x4 v = funnel16(A[k], B[k], q, r);
-                *reinterpret_cast<u32x4*>(dbase + (uint64_t)idx * 16u) = v;
-                wsum = sad16(v.x, wsum); wsum = sad16(v.y, wsum);
-                wsum = sad16(v.z, wsum); wsum = sad16(v.w, wsum);
-                if (odd) {
-                    osum = sad8(v.x & 0xff00ff00u, osum); osum = sad8(v.y & 0xff00ff00u, osum);
-                    osum = sad8(v.z & 0xff00ff00u, osum); osum = sad8(v.w & 0xff00ff00u, osum);
+                const uint32_t idx = p[u].f0 + (uint32_t)(k * G + gl);
+                if (idx < p[u].f1) tx_full_chunk(p[u], idx, A[u][k], B[u][k], wsum, osum);
+            }
+            uint64_t W = wsum, O = osum;
+            // long payloads: further rounds of G*C full chunks
+            for (uint32_t rr = p[u].f0 + (uint32_t)(G * C); rr < p[u].f1; rr += (uint32_t)(G * C)) {
+                u32x4 a2[C], b2[C];
+#pragma unroll
+                for (int k = 0; k < C; ++k) {
+                    const uint32_t idx = rr + (uint32_t)(k * G + gl);
+                    const uint8_t* a = p[u].sbase + (uint64_t)idx * 16u;
+                    a2[k] = idx < p[u].f1 ? ld16(a) : u32x4{0u, 0u, 0u, 0u};
+                    b2[k] = (idx < p[u].f1 && p[u].sh) ? ld16(a + 16) : u32x4{0u, 0u, 0u, 0u};
                 }
-            }
-            W += wsum;
-            O += osum;
-        }
-        // the ragged ends: the head chunk (lane 0) and the tail chunk (lane 1), byte-masked
-        if (len && gl < 2) {
-            const bool head = dm != 0;
-            const bool tail = ((dm + len) & 15u) != 0 && f1 >= f0 && !(head && f1 == 0);
-            const bool mine = gl == 0 ? head : tail;
-            if (mine) {
-                const uint32_t idx = gl == 0 ? 0u : f1;
-                const uint8_t* a = sbase + (uint64_t)idx * 16u;
-                const uintptr_t src_lo = (uintptr_t)src, src_hi = (uintptr_t)src + len;
-                const bool va = (uintptr_t)a < src_hi && (uintptr_t)a + 16 > src_lo;
-                const bool vb = sh != 0 && (uintptr_t)a + 16 < src_hi && (uintptr_t)a + 32 > src_lo;
-                const u32x4 A = va ? ld16(a) : u32x4{0u, 0u, 0u, 0u};
-                const u32x4 B = vb ? ld16(a + 16) : u32x4{0u, 0u, 0u, 0u};
-                const u32x4 v = funnel16(A, B, q, r);
-                const int64_t rel = (int64_t)idx * 16 - (int64_t)dm;   // dest chunk start - dst
-                uint8_t* dc = dbase + (uint64_t)idx * 16u;
+                uint32_t ws = 0, os = 0;
 #pragma unroll
-                for (int b2 = 0; b2 < 16; ++b2) {
-                    const uint32_t word = b2 < 4 ? v.x : b2 < 8 ? v.y : b2 < 12 ? v.z : v.w;
-                    const int64_t pos = rel + b2;
-                    if (pos >= 0 && pos < (int64_t)len) dc[b2] = (uint8_t)(word >> (8 * (b2 & 3)));
+                for (int k = 0; k < C; ++k) {
+                    const uint32_t idx = rr + (uint32_t)(k * G + gl);
+                    if (idx < p[u].f1) tx_full_chunk(p[u], idx, a2[k], b2[k], ws, os);
                 }
-                uint32_t wsum = 0, osum = 0;
-                chunk_wo_bytes(v, rel, (int64_t)len, odd, wsum, osum);
-                W += wsum;
-                O += osum;
+                W += ws;
+                O += os;
+            }
+            if (e[u] >= 0) {
+                uint32_t ws = 0, os = 0;
+                tx_edge_chunk_store(p[u], e[u], EA[u], EB[u], ws, os);
+                W += ws;
+                O += os;
+            }
+            W = group_sum64<G>(W);
+            O = p[u].odd ? group_sum64<G>(O) : 0;
+            const uint64_t i = t * SPT + (uint64_t)(u * GPW + q0);
+            if (p[u].live) {
+                tx_header<G>(p[u], combine(0, W, O, p[u].odd), mode, gl, checks, i);
+            } else if (i < n && gl == 0 && checks) {
+                checks[i] = 0;
             }
         }
-        W = group_sum64<G>(W);
-        O = odd ? group_sum64<G>(O) : 0;
-        const uint64_t Spay = combine(0, W, O, odd);   // payload sum, relative to its even start (TCP+24)
-
-        // ---- phase 2: header (context.c:169-206), checks, stores
-        const uint32_t tot = 44u + len;
-        const uint32_t tcp_len = 24u + len;
-        const uint32_t len_be = ((tcp_len & 0xffu) << 8) | ((tcp_len >> 8) & 0xffu);
-        const uint32_t tflags = (flags & TCPCSUM_TXF_FIN ? 1u : 0u) | (flags & TCPCSUM_TXF_SYN ? 2u : 0u) |
-                                (flags & TCPCSUM_TXF_RST ? 4u : 0u) | (data ? 8u : 0u) |
-                                (flags & TCPCSUM_TXF_ACK ? 16u : 0u);
-        uint32_t hd[11];
-        hd[0] = 0x45u | ((tot >> 8) << 16) | ((tot & 0xffu) << 24);
-        hd[1] = 0u;                                          // id = (u16)htonl(54321) = 0, frag_off 0
-        hd[2] = 0xffu | (6u << 8);                           // ttl 255, IPPROTO_TCP, check 0
-        hd[3] = sa;
-        hd[4] = da;
-        hd[5] = (sport >> 8) | ((sport & 0xffu) << 8) | ((dport >> 8) << 16) | ((dport & 0xffu) << 24);
-        hd[6] = __builtin_bswap32(seq);
-        hd[7] = __builtin_bswap32(ack);
-        hd[8] = 0x60u | (tflags << 8) | (0x20u << 16);       // doff 6, flags, window 8192 (BE 20 00)
-        hd[9] = 0u;                                          // check (set below), urg_ptr 0
-        hd[10] = 0x00050303u;                                // options 03 03 05 00
-        uint64_t S = Spay + (sa & 0xffffu) + (sa >> 16) + (da & 0xffffu) + (da >> 16) + 0x0600u + len_be;
-#pragma unroll
-        for (int k = 5; k < 11; ++k) S += sum_halves(hd[k]);
-        const uint16_t c = fold_ref(S);
-        hd[9] = c;
-        if (mode & TCPCSUM_IPV4_IPHDR) {
-            uint32_t is = 0;
-#pragma unroll
-            for (int k = 0; k < 5; ++k) is += sum_halves(hd[k]);
-            hd[2] |= (uint32_t)fold_ref(is) << 16;
-        }
-        for (int j = gl; j < 11; j += G) {   // lane j stores header dword j
-            uint32_t v = hd[0];
-#pragma unroll
-            for (int k = 1; k < 11; ++k) v = j == k ? hd[k] : v;
-            uint8_t* hp = ip + 4 * j;
-            if ((((uintptr_t)ip) & 3u) == 0) {
-                *reinterpret_cast<uint32_t*>(hp) = v;
-            } else {
-                hp[0] = (uint8_t)v; hp[1] = (uint8_t)(v >> 8); hp[2] = (uint8_t)(v >> 16); hp[3] = (uint8_t)(v >> 24);
-            }
-        }
-        if (gl == 0 && checks) checks[i] = c;
     }
 }
 
@@ -862,20 +933,29 @@ void launch_ipv4(uint8_t* pkts, const uint64_t* off, uint64_t n, uint32_t cap, u
     }
 }
 
+template <int G, int C, int U>
+static void launch_tx_t(const uint8_t* payload, const tcpcsum_txseg_t* segs, uint64_t n, uint8_t* outp, int mode,
+                        uint16_t* checks, hipStream_t s, int max_blocks) {
+    constexpr int SPT = (64 / G) * U;
+    hipLaunchKernelGGL((k_tx_build<G, C, U>), dim3(grid_for((n + SPT - 1) / SPT, max_blocks)), dim3(256), 0, s,
+                       payload, segs, n, outp, mode, checks);
+}
+
 void launch_tx_build(const uint8_t* payload, const tcpcsum_txseg_t* segs, uint64_t n, uint32_t max_len,
                      uint8_t* outp, int mode, uint16_t* checks, hipStream_t s, const Tuning& tu) {
-    const int max_blocks = tu.max_blocks > 0 ? tu.max_blocks : kDefaultMaxBlocks;
-    const uint64_t nch = ((uint64_t)max_len + 30u) >> 4;
-    if (nch <= 8) {
-        hipLaunchKernelGGL((k_tx_build<8, 1>), dim3(grid_for((n + 7) / 8, max_blocks)), dim3(256), 0, s, payload,
-                           segs, n, outp, mode, checks);
-    } else if (nch <= 96) {
-        hipLaunchKernelGGL((k_tx_build<32, 3>), dim3(grid_for((n + 1) / 2, max_blocks)), dim3(256), 0, s,
-                           payload, segs, n, outp, mode, checks);
-    } else {
-        hipLaunchKernelGGL((k_tx_build<64, 4>), dim3(grid_for(n, max_blocks)), dim3(256), 0, s, payload, segs, n,
-                           outp, mode, checks);
-    }
+    const int max_blocks = tu.max_blocks > 0 ? tu.max_blocks : 1024;
+    const int unroll = tu.unroll ? tu.unroll : 2;
+    const uint64_t nfull = ((uint64_t)max_len + 15u) >> 4;   // full chunks a payload can have
+#define TX_U(G, C)                                                                         \
+    do {                                                                                   \
+        if (unroll <= 1) launch_tx_t<G, C, 1>(payload, segs, n, outp, mode, checks, s, max_blocks); \
+        else if (unroll == 2) launch_tx_t<G, C, 2>(payload, segs, n, outp, mode, checks, s, max_blocks); \
+        else launch_tx_t<G, C, 4>(payload, segs, n, outp, mode, checks, s, max_blocks);    \
+    } while (0)
+    if (nfull <= 8) TX_U(8, 1);
+    else if (nfull <= 96) TX_U(32, 3);
+    else TX_U(64, 4);
+#undef TX_U
 }
 
 void launch_synth_fill(uint8_t* dst, uint64_t off, uint64_t nbytes, hipStream_t s) {
