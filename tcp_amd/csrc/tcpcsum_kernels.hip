@@ -943,8 +943,8 @@ static void launch_tx_t(const uint8_t* payload, const tcpcsum_txseg_t* segs, uin
 
 void launch_tx_build(const uint8_t* payload, const tcpcsum_txseg_t* segs, uint64_t n, uint32_t max_len,
                      uint8_t* outp, int mode, uint16_t* checks, hipStream_t s, const Tuning& tu) {
-    const int max_blocks = tu.max_blocks > 0 ? tu.max_blocks : 1024;
-    const int unroll = tu.unroll ? tu.unroll : 2;
+    const int max_blocks = tu.max_blocks > 0 ? tu.max_blocks : 4096;
+    const int unroll = tu.unroll ? tu.unroll : 1;
     const uint64_t nfull = ((uint64_t)max_len + 15u) >> 4;   // full chunks a payload can have
 #define TX_U(G, C)                                                                         \
     do {                                                                                   \
@@ -952,9 +952,15 @@ void launch_tx_build(const uint8_t* payload, const tcpcsum_txseg_t* segs, uint64
         else if (unroll == 2) launch_tx_t<G, C, 2>(payload, segs, n, outp, mode, checks, s, max_blocks); \
         else launch_tx_t<G, C, 4>(payload, segs, n, outp, mode, checks, s, max_blocks);    \
     } while (0)
-    if (nfull <= 8) TX_U(8, 1);
-    else if (nfull <= 96) TX_U(32, 3);
-    else TX_U(64, 4);
+    int shape = nfull <= 8 ? 0 : nfull <= 96 ? 2 : 4;
+    if (tu.shape >= 0 && tu.shape <= 4) shape = tu.shape;   // any shape is correct (extra rounds)
+    switch (shape) {
+        case 0: TX_U(8, 1); break;
+        case 1: TX_U(16, 2); break;
+        case 2: TX_U(32, 3); break;
+        case 3: TX_U(64, 2); break;
+        default: TX_U(64, 4);
+    }
 #undef TX_U
 }
 

@@ -399,9 +399,15 @@ def test_tx_build_vs_oracle(dev, layout):
         if not np.array_equal(got, want):
             bad = np.flatnonzero(got != want)
             raise AssertionError(f"{layout} mode={mode}: {bad.size} bytes differ, first at {bad[:8]}")
-    # a too-small shape hint is slower, never wrong
-    dout = to_dev(garbage, dev)
-    tcp_amd.tx_build(to_dev(payload, dev), to_dev(segs.view(np.uint8), dev), n, 16, dout, 0, None)
+    # a too-small shape hint, or any forced shape / unroll, is slower, never wrong
     want = garbage.copy()
     oracle.tx_build(payload, segs, want)
-    assert np.array_equal(dout.cpu().numpy(), want)
+    dpay, dseg = to_dev(payload, dev), to_dev(segs.view(np.uint8), dev)
+    try:
+        for shape, unroll, hint in ((-1, 0, 16), (0, 2, max_len), (1, 4, max_len), (3, 1, max_len), (4, 2, 64)):
+            tcp_amd.set_tuning(0, unroll, shape, 0)
+            dout = to_dev(garbage, dev)
+            tcp_amd.tx_build(dpay, dseg, n, hint, dout, 0, None)
+            assert np.array_equal(dout.cpu().numpy(), want), (shape, unroll, hint)
+    finally:
+        tcp_amd.set_tuning(0, 0, -1, 0)

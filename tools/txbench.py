@@ -53,11 +53,13 @@ def main():
         return e0.elapsed_time(e1) / steps * 1e-3
 
     if "--sweep" in sys.argv:
-        for mb in (256, 512, 1024, 2048, 4096):
-            for un in (1, 2, 4):
-                tcp_amd.set_tuning(mb, un, -1, 0)
+        for sh in (0, 1, 2, 3, 4):
+          for mb in (1024, 2048, 4096, 8192):
+            for un in (1, 2):
+                tcp_amd.set_tuning(mb, un, sh, 0)
                 tt = timeit(lambda: tcp_amd.tx_build(payload, dsegs, n, L, out, 0, chk), 20)
-                print(json.dumps({"sweep": "tx_build", "max_blocks": mb, "unroll": un, "ms": round(tt * 1e3, 4),
+                print(json.dumps({"sweep": "tx_build", "shape": sh, "max_blocks": mb, "unroll": un,
+                                  "ms": round(tt * 1e3, 4),
                                   "GB/s": round((n * L + n * (L + 44) + n * 48) / tt / 1e9, 1)}), flush=True)
         tcp_amd.set_tuning(0, 0, -1, 0)
     t = timeit(lambda: tcp_amd.tx_build(payload, dsegs, n, L, out, 0, chk))
