@@ -78,6 +78,13 @@ def main():
     t2 = timeit(unfused)
     print(json.dumps({"measure": "unfused_copy_plus_checksum", "ms": round(t2 * 1e3, 4),
                       "fused_speedup": round(t2 / t, 2)}), flush=True)
+    # practical ceiling for a read+write stream on this device: a contiguous copy
+    src_c = payload[: n * L]
+    dst_c = torch.empty_like(src_c)
+    t3 = timeit(lambda: dst_c.copy_(src_c))
+    print(json.dumps({"measure": "contiguous_copy_same_bytes", "ms": round(t3 * 1e3, 4),
+                      "GB/s_read+write": round(2 * n * L / t3 / 1e9, 1)}), flush=True)
+    del dst_c
     # correctness spot check on the device result: every packet verifies to zero
     offs = torch.from_numpy((np.arange(4096, dtype=np.uint64) * (L + 44)).view(np.int64)).to(dev)
     tcp_amd.tx_build(payload, dsegs, n, L, out, 0, chk)
