@@ -827,6 +827,8 @@ void launch_uniform_mode(int shape, int unroll, const uint8_t* base, uint64_t st
         case 6: TC_U4(64, 2); break;   // <= 128
         case 7: TC_U4(64, 4); break;   // <= 256
         case 8: TC_U4(64, 8); break;   // <= 512
+        case 10: TC_U4(1, 5); break;   // <= 5: one lane per segment, no cross-lane reduction
+        case 11: TC_U4(2, 4); break;   // <= 8: two lanes per segment
         default:                       // one wave per segment, 8*unroll chunks per lane per round
             if (unroll <= 1) TC_L(8);
             else if (unroll == 2 || PIPE) TC_L(16);
@@ -844,11 +846,13 @@ namespace tcpcsum {
 // Segment-group shapes: shape k covers up to kShapeChunks[k] 16-B chunks per
 // segment. Defaults per shape (measured on MI355X, tools/sweep.py; see
 // DESIGN.md): segments-in-flight per group and the resident grid.
-static const uint32_t kShapeChunks[9] = {4, 8, 16, 32, 64, 96, 128, 256, 512};
-static const int kShapeUnroll[10] = {4, 8, 8, 8, 8, 8, 8, 8, 4, 2};
-static const int kShapeBlocks[10] = {4096, 512, 4096, 4096, 4096, 512, 4096, 1024, 2048, 256};
-static const bool kShapePipe[10] = {false, false, false, false, false, false, false, false, false, false};
-static const bool kShapeNt[10] = {true, true, true, true, true, true, true, true, true, true};
+// Shapes 10/11 are the thin lane groups (1 or 2 lanes per segment) for tiny
+// segments; shape 9 (one wave per segment) has no chunk limit.
+static const uint32_t kShapeChunks[12] = {4, 8, 16, 32, 64, 96, 128, 256, 512, 0xffffffffu, 5, 8};
+static const int kShapeUnroll[12] = {4, 8, 8, 8, 8, 8, 8, 8, 4, 2, 2, 2};
+static const int kShapeBlocks[12] = {4096, 512, 4096, 4096, 4096, 512, 4096, 1024, 2048, 256, 2048, 2048};
+static const bool kShapePipe[12] = {false, false, false, false, false, false, false, false, false, false, false, false};
+static const bool kShapeNt[12] = {true, true, true, true, true, true, true, true, true, true, true, true};
 
 UniformPlan plan_uniform(uintptr_t b, uint64_t stride, uint32_t len, uint64_t n, const Tuning& tu) {
     UniformPlan p;
@@ -865,7 +869,7 @@ UniformPlan plan_uniform(uintptr_t b, uint64_t stride, uint32_t len, uint64_t n,
     for (int k = 0; k < 9; ++k)
         if (nch <= kShapeChunks[k]) { p.shape = k; break; }
     // a forced shape is honoured only if it covers the segment
-    if (tu.shape >= 0 && tu.shape <= 9 && (tu.shape == 9 || nch <= kShapeChunks[tu.shape])) p.shape = tu.shape;
+    if (tu.shape >= 0 && tu.shape <= 11 && nch <= kShapeChunks[tu.shape]) p.shape = tu.shape;
     p.unroll = tu.unroll ? tu.unroll : kShapeUnroll[p.shape];
     p.max_blocks = tu.max_blocks > 0 ? tu.max_blocks : kShapeBlocks[p.shape];
     p.pipe = tu.flags & TCPCSUM_TUNE_PIPE_ON ? true : tu.flags & TCPCSUM_TUNE_PIPE_OFF ? false : kShapePipe[p.shape];

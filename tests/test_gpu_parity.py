@@ -101,10 +101,10 @@ def test_forced_shapes(dev):
     host = rng.integers(0, 256, 1 << 21, dtype=np.uint8)
     d = to_dev(host, dev)
     try:
-        for shape in range(10):
+        for shape in range(12):
             for unroll, flags in ((1, 0), (8, 0), (2, 1 | 8), (8, 1 | 4), (4, 2 | 8), (8, 16), (1, 16 | 8)):
                 tcp_amd.set_tuning(0, unroll, shape, flags)
-                for length, off in ((1500, 0), (1499, 1), (64, 4), (3000, 2)):
+                for length, off in ((1500, 0), (1499, 1), (64, 4), (3000, 2), (64, 0), (60, 3), (100, 0)):
                     n = (1 << 21) // (length + 8) - 1
                     got = u16(tcp_amd.batch_uniform(d, length + 1, length, n, 3, offset=off))
                     want = oracle.batch_uniform(host, length + 1, length, n, 3, offset=off)
