@@ -108,19 +108,31 @@ def cpu_baseline(seg_len: int, seconds: float) -> dict:
     # the same batch as the GPU step when it fits in 1.5 GiB (1M x 1500 B: exactly it), so the
     # sample streams from host DRAM like the GPU's does from HBM
     nseg = max(1, min(1 << 20, (3 << 29) // seg_len))
-    threads = min(16, os.cpu_count() or 1)
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    threads = max(1, min(16, avail))
     res = {}
     for key, th, opt, secs in (("o2_all", threads, "O2", seconds * 0.4), ("o2_1", 1, "O2", seconds * 0.35),
                                ("o0_1", 1, "O0", seconds * 0.25)):
         gibs, _, passes = oracle.cpu_bench(th, seg_len, nseg, secs, opt)
         res[key] = (gibs, th, passes)
     gibs, th, _ = res["o2_all"]
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
     return {
         "value": round(gibs, 3), "unit": "GiB/s", "cores": th, "kind": "port",
         "sample": f"{nseg} x {seg_len}-byte segments (Appendix B stream, host DRAM), gcc -O2, "
                   f"{th} pthreads, best pass of >=3 over ~{seconds * 0.4:.0f}s",
         "single_core_O2": round(res["o2_1"][0], 3),
         "single_core_O0_makefile_flags": round(res["o0_1"][0], 3),
+        "host_cpu": model,
+        "threads_available": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count(),
     }
 
 
