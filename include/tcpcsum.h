@@ -65,6 +65,10 @@ typedef struct tcpcsum_desc {
 #define TCPCSUM_PKT_OK 0
 #define TCPCSUM_PKT_SKIPPED 1    /* not IPv4/TCP, ihl < 5, or tot_len outside [ihl*4+20, cap] */
 #define TCPCSUM_PKT_IPHDR_BAD 2  /* VERIFY|IPHDR: the IPv4 header checksum does not verify */
+/* VERIFY: the TCP check does not verify but holds the un-complemented folded
+ * pseudo-header sum — a CHECKSUM_PARTIAL segment whose checksum was left for
+ * NIC offload (Linux loopback does this). OR-ed with the above. */
+#define TCPCSUM_PKT_CSUM_PARTIAL 4
 
 /* ---------------------------------------------------------------- library */
 int tcpcsum_abi_version(void);

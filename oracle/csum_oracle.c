@@ -185,7 +185,13 @@ void oracle_ipv4_batch(uint8_t *base, const uint64_t *off, uint64_t n, uint32_t 
             memcpy(tcp + 16, &c, 2);
             if (out) out[k] = c;
         } else {
-            if (out) out[k] = oracle_csum_continue(ps, (const char *) tcp, (int) tcp_len);
+            uint16_t v = oracle_csum_continue(ps, (const char *) tcp, (int) tcp_len);
+            if (out) out[k] = v;
+            /* CHECKSUM_PARTIAL: check holds the un-complemented folded pseudo sum
+             * (new behaviour, no reference result: SURVEY.md §4.5) */
+            uint16_t cw;
+            memcpy(&cw, tcp + 16, 2);
+            if (v != 0 && cw == (uint16_t) ~oracle_csum_continue(ps, "", 0)) st |= 4;
         }
         if (iphdr) { /* context.c:179 (commented out in the reference), over ihl*4 bytes */
             if (!verify) {
@@ -194,7 +200,7 @@ void oracle_ipv4_batch(uint8_t *base, const uint64_t *off, uint64_t n, uint32_t 
                 uint16_t c = oracle_csum_continue(0, (const char *) ip, (int) (ihl * 4u));
                 memcpy(ip + 10, &c, 2);
             } else if (oracle_csum_continue(0, (const char *) ip, (int) (ihl * 4u)) != 0) {
-                st = 2;
+                st |= 2;
             }
         }
         if (status) status[k] = st;

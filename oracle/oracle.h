@@ -46,7 +46,8 @@ void oracle_batch_desc(const uint8_t *base, const uint64_t *off, const uint32_t 
 /* Wire batch: IPv4 packets at base + off[k]. mode 0 = fill (check treated as
  * 0, result written to check and out), mode 1 = verify (out = csum incl.
  * check; 0 == valid); | 2 = also the IPv4 header checksum (fill at IP+10 /
- * verify). status[k]: 0 ok, 1 not IPv4/TCP or malformed, 2 IP header bad. */
+ * verify). status[k]: 0 ok, 1 not IPv4/TCP or malformed, |2 IP header bad,
+ * |4 verify found a CHECKSUM_PARTIAL check (un-complemented pseudo sum). */
 void oracle_ipv4_batch(uint8_t *base, const uint64_t *off, uint64_t n, uint32_t cap,
                        int mode, uint16_t *out, uint8_t *status);
 

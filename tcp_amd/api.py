@@ -34,6 +34,7 @@ IPV4_IPHDR = 2
 PKT_OK = 0
 PKT_SKIPPED = 1
 PKT_IPHDR_BAD = 2
+PKT_CSUM_PARTIAL = 4
 
 # tcpcsum_desc_t {u64 offset; u32 len; u32 sum_start}
 DESC_DTYPE = np.dtype([("offset", "<u8"), ("len", "<u4"), ("sum_start", "<u4")])

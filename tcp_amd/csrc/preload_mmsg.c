@@ -48,7 +48,7 @@ enum { MODE_OFF = 0, MODE_FILL = 1, MODE_VERIFY = 2 };
 
 struct tcpcsum_preload_stats {
     unsigned long long tx_batches, tx_packets, tx_filled, tx_verified, tx_verify_failed, tx_skipped;
-    unsigned long long rx_batches, rx_packets, rx_verified, rx_verify_failed, rx_skipped;
+    unsigned long long rx_batches, rx_packets, rx_verified, rx_verify_failed, rx_skipped, rx_partial;
     unsigned long long errors;
 };
 
@@ -80,11 +80,11 @@ static void print_stats(void) {
     if (!g_stats) return;
     fprintf(stderr,
             "tcpcsum_preload: tx batches=%llu packets=%llu filled=%llu verified=%llu verify_failed=%llu "
-            "skipped=%llu | rx batches=%llu packets=%llu verified=%llu verify_failed=%llu skipped=%llu | "
-            "errors=%llu\n",
+            "skipped=%llu | rx batches=%llu packets=%llu verified=%llu verify_failed=%llu skipped=%llu "
+            "partial=%llu | errors=%llu\n",
             g_st.tx_batches, g_st.tx_packets, g_st.tx_filled, g_st.tx_verified, g_st.tx_verify_failed,
             g_st.tx_skipped, g_st.rx_batches, g_st.rx_packets, g_st.rx_verified, g_st.rx_verify_failed,
-            g_st.rx_skipped, g_st.errors);
+            g_st.rx_skipped, g_st.rx_partial, g_st.errors);
 }
 
 static void init_once(void) {
@@ -200,7 +200,7 @@ static int gpu_batch(struct mmsghdr *vec, unsigned int vlen, const unsigned int 
         const uint8_t *sp = g_stage + g_off[k];
         uint8_t *dp = (uint8_t *) vec[i].msg_hdr.msg_iov[0].iov_base;
         const unsigned int tot = ((unsigned) sp[2] << 8) | sp[3];
-        const int ok = g_status[k] != TCPCSUM_PKT_SKIPPED && tot <= lens[i];
+        const int ok = !(g_status[k] & TCPCSUM_PKT_SKIPPED) && tot <= lens[i];
         if (!ok) {
             if (is_tx) g_st.tx_skipped++; else g_st.rx_skipped++;
         } else if (fill) {
@@ -209,9 +209,12 @@ static int gpu_batch(struct mmsghdr *vec, unsigned int vlen, const unsigned int 
             if (g_iphdr) memcpy(dp + 10, sp + 10, 2);
             g_st.tx_filled++;
         } else {
-            const int bad = g_out[k] != 0 || g_status[k] == TCPCSUM_PKT_IPHDR_BAD;
+            /* CHECKSUM_PARTIAL segments (checksum left to offload, e.g. Linux
+             * loopback) are counted apart, not as corrupt */
+            const int partial = (g_status[k] & TCPCSUM_PKT_CSUM_PARTIAL) != 0;
+            const int bad = (g_out[k] != 0 && !partial) || (g_status[k] & TCPCSUM_PKT_IPHDR_BAD);
             if (is_tx) { g_st.tx_verified++; if (bad) g_st.tx_verify_failed++; }
-            else { g_st.rx_verified++; if (bad) g_st.rx_verify_failed++; }
+            else { g_st.rx_verified++; if (bad) g_st.rx_verify_failed++; if (partial) g_st.rx_partial++; }
         }
         ++k;
     }

@@ -421,6 +421,7 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const 
         if (!verify) S -= check_word;
         const uint16_t c = fold_ref(S);
         uint32_t st = TCPCSUM_PKT_OK;
+        if (verify && c != 0 && check_word == (uint32_t)(uint16_t)~fold_ref(ps)) st |= TCPCSUM_PKT_CSUM_PARTIAL;
         if (mode & TCPCSUM_IPV4_IPHDR) {
             // IPv4 header checksum = csum_continue(0, ip, ihl*4) with check (IP+10)
             // as zero — the reference's commented-out context.c:179, over ihl*4 bytes.
@@ -436,7 +437,7 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const 
                     ip[11] = (uint8_t)(ic >> 8);
                 }
             } else if (ic != 0) {
-                st = TCPCSUM_PKT_IPHDR_BAD;
+                st |= TCPCSUM_PKT_IPHDR_BAD;
             }
         }
         if (gl == 0) {

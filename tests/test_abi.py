@@ -55,6 +55,7 @@ def test_header_constants_match_python():
     assert int(consts["TCPCSUM_IPV4_VERIFY"]) == api.IPV4_VERIFY
     assert int(consts["TCPCSUM_PKT_SKIPPED"]) == api.PKT_SKIPPED
     assert int(consts["TCPCSUM_PKT_IPHDR_BAD"]) == api.PKT_IPHDR_BAD
+    assert int(consts["TCPCSUM_PKT_CSUM_PARTIAL"]) == api.PKT_CSUM_PARTIAL
     assert int(consts["TCPCSUM_IPV4_IPHDR"]) == api.IPV4_IPHDR
     assert int(consts["TCPCSUM_ABI_VERSION"]) == tcp_amd.lib().tcpcsum_abi_version()
     assert api.DESC_DTYPE.itemsize == 16

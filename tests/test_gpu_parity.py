@@ -411,3 +411,18 @@ def test_tx_build_vs_oracle(dev, layout):
             assert np.array_equal(dout.cpu().numpy(), want), (shape, unroll, hint)
     finally:
         tcp_amd.set_tuning(0, 0, -1, 0)
+
+
+def test_ipv4_verify_flags_checksum_partial(dev):
+    """New behaviour (no reference result — parity pinned to the oracle only): VERIFY marks
+    CHECKSUM_PARTIAL segments (check = un-complemented pseudo sum) instead of plain failures."""
+    import tcp_amd
+    from tests.test_oracle import partial_offload_batch
+    region, off = partial_offload_batch(seed=10, n=500)
+    want_out, want_st = oracle.ipv4_batch(region.copy(), off, 32768, tcp_amd.IPV4_VERIFY)
+    out = torch.empty(off.size, dtype=torch.int16, device=dev)
+    st = torch.empty(off.size, dtype=torch.uint8, device=dev)
+    tcp_amd.ipv4_batch(to_dev(region, dev), to_dev(off.view(np.int64), dev), off.size, 32768,
+                       tcp_amd.IPV4_VERIFY, out, st)
+    assert np.array_equal(u16(out), want_out) and np.array_equal(st.cpu().numpy(), want_st)
+    assert (want_st == tcp_amd.api.PKT_CSUM_PARTIAL).sum() > 300

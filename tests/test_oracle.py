@@ -200,3 +200,33 @@ def test_oracle_tx_build_layout_and_verify():
         if data:
             po = int(s["payload_off"])
             assert ip[44:] == payload[po:po + L].tobytes()
+
+
+def partial_offload_batch(seed=9, n=64):
+    """Packets whose TCP check holds the un-complemented folded pseudo-header sum, as Linux leaves
+    CHECKSUM_PARTIAL segments on loopback; every 3rd packet is fully checksummed."""
+    import socket
+    import struct
+    from tests.packets import build_batch
+    region, off, _ = build_batch(np.random.default_rng(seed), n)
+    oracle.ipv4_batch(region, off, 32768, 0)          # FILL: valid checks everywhere
+    for k, o in enumerate(off):
+        if k % 3 == 0:
+            continue
+        o = int(o)
+        tot = struct.unpack("!H", region[o + 2:o + 4].tobytes())[0]
+        sa, da = struct.unpack("<II", region[o + 12:o + 20].tobytes())
+        ps = oracle.pseudo(sa, da, socket.htons(tot - 20))
+        partial = (~oracle.csum_continue(ps, b"", 0)) & 0xFFFF
+        region[o + 36:o + 38] = np.frombuffer(struct.pack("<H", partial), np.uint8)
+    return region, off
+
+
+def test_oracle_flags_checksum_partial():
+    region, off = partial_offload_batch()
+    out, st = oracle.ipv4_batch(region, off, 32768, 1)
+    for k in range(off.size):
+        if k % 3 == 0:
+            assert out[k] == 0 and st[k] == 0
+        else:
+            assert out[k] != 0 and st[k] == 4

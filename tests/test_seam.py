@@ -84,6 +84,7 @@ def test_tx_fill_on_gpu(tmp_path):
     for built, got in pkts:
         assert got == oracle_fill(built)
     assert stats["tx_filled"] == 3000 and stats["rx_verified"] == 3000 and stats["rx_verify_failed"] == 0
+    assert stats["rx_partial"] == 0
 
 
 @pytest.mark.gpu
