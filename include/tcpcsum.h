@@ -213,13 +213,15 @@ int tcpcsum_stream_probe_dev(const void *d_src, uint64_t nbytes, uint64_t *d_par
  * for a uniform batch at device address base. mode: 0 = 16-B aligned, 1 =
  * 4-B aligned, 2 = byte-granular; shape: 0..8 = lane-group shapes covering
  * 4,8,16,32,64,96,128,256,512 chunks, 9 = one wave per long segment,
- * 10 / 11 = one / two lanes per segment (up to 5 / 8 chunks);
+ * 10 / 11 = one / two lanes per segment (up to 5 / 8 chunks), 12 = flat
+ * tiles (contiguous 1 KiB per load instruction; 1-32 KiB segments, 4-B
+ * aligned, stride >= len);
  * unroll: segments in flight per lane group; max_blocks: resident grid. */
 int tcpcsum_plan_uniform(uint64_t base, uint64_t stride, uint32_t len, uint64_t n, int *mode,
                          int *shape, int *unroll, int *max_blocks);
 
 /* Launch-shape override for tuning (tools/sweep.py). 0 / -1 = built-in
- * per-shape defaults. unroll in {0,1,2,4,8}; shape in {-1, 0..11} (a forced
+ * per-shape defaults. unroll in {0,1,2,4,8}; shape in {-1, 0..12} (a forced
  * shape that cannot cover the segments is ignored); flags: TCPCSUM_TUNE_*
  * bits (0 = defaults). Affects batch calls issued afterwards from any thread. */
 #define TCPCSUM_TUNE_PIPE_ON 1   /* software-pipelined tiles */

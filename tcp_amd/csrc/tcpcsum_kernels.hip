@@ -318,6 +318,72 @@ __global__ __launch_bounds__(256) void k_uniform_long(const uint8_t* __restrict_
     }
 }
 
+// Flat tiles (segments of >= 1 KiB, 4-byte aligned): a wave takes SPT
+// consecutive segments and reads their byte span as one contiguous stream —
+// lane l loads chunk c0 + 64k + l, so every load instruction is one contiguous
+// 1 KiB (the read probe's access shape). Instruction k covers at most two
+// segments (stride >= 1 KiB): the lanes split its dwords into the first /
+// second segment, two wave reductions give their sums, and lane j of the wave
+// accumulates the sum of the tile's segment j; at the end lane j folds and
+// stores segment j (coalesced start-value loads and result stores).
+__device__ __forceinline__ uint32_t wave_sum32(uint32_t x) {
+    x = group_sum32<16>(x);   // every lane holds its row's sum
+    return __builtin_amdgcn_readlane(x, 0) + __builtin_amdgcn_readlane(x, 16) + __builtin_amdgcn_readlane(x, 32) +
+           __builtin_amdgcn_readlane(x, 48);
+}
+
+template <int C>
+__global__ __launch_bounds__(256) void k_flat(const uint8_t* __restrict__ base, uint32_t stride, uint32_t len,
+                                              const uint32_t* __restrict__ ss, uint32_t ss_scalar,
+                                              uint16_t* __restrict__ out, uint64_t n, uint32_t spt) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
+    const uint64_t ntiles = (n + spt - 1) / spt;
+    const uint32_t bm = (uint32_t)((uintptr_t)base & 15u);
+    const uint8_t* b0 = base - bm;   // 16-B aligned
+    for (uint64_t t = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6); t < ntiles; t += nwaves) {
+        const uint64_t s_first = t * spt;
+        const uint32_t nseg = (uint32_t)((n - s_first) < spt ? (n - s_first) : spt);
+        const uint64_t tbase = s_first * (uint64_t)stride + bm;        // tile's first byte, from b0
+        const uint64_t tend = tbase + (uint64_t)(nseg - 1) * stride + len;
+        const uint64_t c0 = tbase >> 4, c1 = (tend + 15) >> 4;
+        // start value for the segment this lane will own
+        const uint32_t st = lane < (int)nseg ? (ss ? ss[s_first + lane] : ss_scalar) : 0u;
+        u32x4 v[C];
+#pragma unroll
+        for (int k = 0; k < C; ++k) {
+            const uint64_t ci = c0 + (uint64_t)(k * 64 + lane);
+            v[k] = ci < c1 ? ld16(b0 + ci * 16u) : u32x4{0u, 0u, 0u, 0u};
+        }
+        uint32_t acc = 0;
+        const int32_t x0 = (int32_t)((int64_t)(c0 * 16) - (int64_t)tbase);   // in (-16, 0]
+        int32_t ja = x0 < 0 ? -1 : 0;   // tile segment holding instruction k's first dword
+#pragma unroll
+        for (int k = 0; k < C; ++k) {
+            const int32_t xk = x0 + k * 1024;
+            if (xk >= (ja + 1) * (int32_t)stride) ++ja;   // wave-uniform; at most one step (stride >= 1 KiB)
+            const int32_t bnd = (ja + 1) * (int32_t)stride;
+            const int32_t x = xk + lane * 16;
+            const uint32_t d[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+            uint32_t a = 0, b = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int32_t xd = x + 4 * j;
+                const bool in_a = xd < bnd;
+                const int32_t js = in_a ? ja : ja + 1;
+                const int32_t r = xd - js * (int32_t)stride;
+                const bool valid = js >= 0 && js < (int32_t)nseg && r >= 0 && r < (int32_t)len;
+                const uint32_t w = valid ? d[j] : 0u;
+                if (in_a) a = sad16(w, a); else b = sad16(w, b);
+            }
+            const uint32_t sa = wave_sum32(a), sb = wave_sum32(b);
+            acc += lane == ja ? sa : 0u;
+            acc += lane == ja + 1 ? sb : 0u;
+        }
+        if (lane < (int)nseg) out[s_first + lane] = fold_ref((uint64_t)st + acc);
+    }
+}
+
 // ---------------------------------------------------------------- ragged
 // Exact sum of one segment [p, p+len) by the G lanes of a group, C chunk
 // loads per lane per round. Returns the group total S - start (i.e. with the
@@ -804,6 +870,23 @@ void launch_long_t(const uint8_t* base, uint64_t stride, uint32_t len, const uin
                        stride, len, rounds, ss, ss0, out, n);
 }
 
+// flat tiles: unroll selects C (8 * unroll chunks per lane, 8 KiB * unroll per wave tile)
+inline void launch_flat(const uint8_t* base, uint64_t stride, uint32_t len, const uint32_t* ss, uint32_t ss0,
+                        uint16_t* out, uint64_t n, hipStream_t s, int max_blocks, int unroll) {
+    int C = unroll <= 1 ? 8 : unroll == 2 ? 16 : unroll == 4 ? 24 : 32;
+    // a tile must hold at least one segment: (stride + 30) / 16 + 1 <= 64 * C
+    while (C < 32 && stride + 46u > (uint64_t)C * 1024u) C += 8;
+    uint64_t spt = ((uint64_t)C * 1024u - 46u) / stride;
+    if (spt > 64) spt = 64;
+    if (spt < 1) spt = 1;
+    const uint64_t ntiles = (n + spt - 1) / spt;
+    const unsigned g = grid_for(ntiles, max_blocks);
+    if (C == 8) hipLaunchKernelGGL(k_flat<8>, dim3(g), dim3(256), 0, s, base, (uint32_t)stride, len, ss, ss0, out, n, (uint32_t)spt);
+    else if (C == 16) hipLaunchKernelGGL(k_flat<16>, dim3(g), dim3(256), 0, s, base, (uint32_t)stride, len, ss, ss0, out, n, (uint32_t)spt);
+    else if (C == 24) hipLaunchKernelGGL(k_flat<24>, dim3(g), dim3(256), 0, s, base, (uint32_t)stride, len, ss, ss0, out, n, (uint32_t)spt);
+    else hipLaunchKernelGGL(k_flat<32>, dim3(g), dim3(256), 0, s, base, (uint32_t)stride, len, ss, ss0, out, n, (uint32_t)spt);
+}
+
 template <int MODE, bool PIPE, bool NT>
 void launch_uniform_mode(int shape, int unroll, const uint8_t* base, uint64_t stride, uint32_t len,
                          const uint32_t* ss, uint32_t ss0, uint16_t* out, uint64_t n, hipStream_t s,
@@ -828,6 +911,7 @@ void launch_uniform_mode(int shape, int unroll, const uint8_t* base, uint64_t st
         case 6: TC_U4(64, 2); break;   // <= 128
         case 7: TC_U4(64, 4); break;   // <= 256
         case 8: TC_U4(64, 8); break;   // <= 512
+        case 12: launch_flat(base, stride, len, ss, ss0, out, n, s, max_blocks, unroll); break;
         case 10: TC_U4(1, 5); break;   // <= 5: one lane per segment, no cross-lane reduction
         case 11: TC_U4(2, 4); break;   // <= 8: two lanes per segment
         default:                       // one wave per segment, 8*unroll chunks per lane per round
@@ -849,11 +933,19 @@ namespace tcpcsum {
 // DESIGN.md): segments-in-flight per group and the resident grid.
 // Shapes 10/11 are the thin lane groups (1 or 2 lanes per segment) for tiny
 // segments; shape 9 (one wave per segment) has no chunk limit.
-static const uint32_t kShapeChunks[12] = {4, 8, 16, 32, 64, 96, 128, 256, 512, 0xffffffffu, 5, 8};
-static const int kShapeUnroll[12] = {4, 8, 8, 8, 8, 8, 8, 8, 4, 2, 2, 2};
-static const int kShapeBlocks[12] = {4096, 512, 4096, 4096, 4096, 512, 4096, 1024, 2048, 256, 2048, 2048};
-static const bool kShapePipe[12] = {false, false, false, false, false, false, false, false, false, false, false, false};
-static const bool kShapeNt[12] = {true, true, true, true, true, true, true, true, true, true, true, true};
+// Shape 12 is the flat tile (segments of 1 KiB .. 32 KiB, 4-byte aligned, stride
+// >= len), only used when forced or when kFlatAuto says so.
+static const uint32_t kShapeChunks[13] = {4, 8, 16, 32, 64, 96, 128, 256, 512, 0xffffffffu, 5, 8, 2048};
+static const int kShapeUnroll[13] = {4, 8, 8, 8, 8, 8, 8, 8, 4, 2, 2, 2, 2};
+static const int kShapeBlocks[13] = {4096, 512, 4096, 4096, 4096, 512, 4096, 1024, 2048, 256, 2048, 2048, 512};
+static const bool kShapePipe[13] = {false, false, false, false, false, false, false, false, false, false, false, false,
+                                    false};
+static const bool kShapeNt[13] = {true, true, true, true, true, true, true, true, true, true, true, true, true};
+
+static bool flat_ok(uintptr_t b, uint64_t stride, uint32_t len, int mode) {
+    return mode != M1 && stride >= 1024 && stride >= len && stride + 46u <= 32u * 1024u && len >= 1024 &&
+           (b & 3u) == 0;
+}
 
 UniformPlan plan_uniform(uintptr_t b, uint64_t stride, uint32_t len, uint64_t n, const Tuning& tu) {
     UniformPlan p;
@@ -870,7 +962,11 @@ UniformPlan plan_uniform(uintptr_t b, uint64_t stride, uint32_t len, uint64_t n,
     for (int k = 0; k < 9; ++k)
         if (nch <= kShapeChunks[k]) { p.shape = k; break; }
     // a forced shape is honoured only if it covers the segment
-    if (tu.shape >= 0 && tu.shape <= 11 && nch <= kShapeChunks[tu.shape]) p.shape = tu.shape;
+    if (tu.shape == 12) {
+        if (flat_ok(b, stride, len, p.mode)) p.shape = 12;
+    } else if (tu.shape >= 0 && tu.shape <= 11 && nch <= kShapeChunks[tu.shape]) {
+        p.shape = tu.shape;
+    }
     p.unroll = tu.unroll ? tu.unroll : kShapeUnroll[p.shape];
     p.max_blocks = tu.max_blocks > 0 ? tu.max_blocks : kShapeBlocks[p.shape];
     p.pipe = tu.flags & TCPCSUM_TUNE_PIPE_ON ? true : tu.flags & TCPCSUM_TUNE_PIPE_OFF ? false : kShapePipe[p.shape];

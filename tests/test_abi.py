@@ -96,7 +96,7 @@ def test_argument_errors_need_no_device():
     assert L.tcpcsum_stream_probe_dev(1 << 20, 17, 1 << 20, ctypes.byref(ng), None) == api.EINVAL
     assert L.tcpcsum_set_tuning(-1, 0, -1, 0) == api.EINVAL
     assert L.tcpcsum_set_tuning(0, 3, -1, 0) == api.EINVAL
-    assert L.tcpcsum_set_tuning(0, 0, 12, 0) == api.EINVAL
+    assert L.tcpcsum_set_tuning(0, 0, 13, 0) == api.EINVAL
     assert L.tcpcsum_set_tuning(0, 0, -1, 3) == api.EINVAL      # PIPE_ON | PIPE_OFF
     assert L.tcpcsum_set_tuning(0, 0, -1, 32) == api.EINVAL
     assert L.tcpcsum_set_tuning(0, 0, -1, 0) == api.OK

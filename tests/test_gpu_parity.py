@@ -101,10 +101,11 @@ def test_forced_shapes(dev):
     host = rng.integers(0, 256, 1 << 21, dtype=np.uint8)
     d = to_dev(host, dev)
     try:
-        for shape in range(12):
+        for shape in range(13):
             for unroll, flags in ((1, 0), (8, 0), (2, 1 | 8), (8, 1 | 4), (4, 2 | 8), (8, 16), (1, 16 | 8)):
                 tcp_amd.set_tuning(0, unroll, shape, flags)
-                for length, off in ((1500, 0), (1499, 1), (64, 4), (3000, 2), (64, 0), (60, 3), (100, 0)):
+                for length, off in ((1500, 0), (1499, 1), (64, 4), (3000, 2), (64, 0), (60, 3), (100, 0),
+                                    (1500, 4), (2048, 0), (1024, 12), (9000, 8)):
                     n = (1 << 21) // (length + 8) - 1
                     got = u16(tcp_amd.batch_uniform(d, length + 1, length, n, 3, offset=off))
                     want = oracle.batch_uniform(host, length + 1, length, n, 3, offset=off)
@@ -426,3 +427,27 @@ def test_ipv4_verify_flags_checksum_partial(dev):
                        tcp_amd.IPV4_VERIFY, out, st)
     assert np.array_equal(u16(out), want_out) and np.array_equal(st.cpu().numpy(), want_st)
     assert (want_st == tcp_amd.api.PKT_CSUM_PARTIAL).sum() > 300
+
+
+@pytest.mark.parametrize("unroll", [1, 2, 4, 8])
+def test_flat_tiles_vs_oracle(dev, unroll):
+    """Shape 12 (flat tiles): packed and gapped layouts, aligned and 4-byte-misaligned bases."""
+    import tcp_amd
+    rng = np.random.default_rng(40 + unroll)
+    host = rng.integers(0, 256, 6 << 20, dtype=np.uint8)
+    d = to_dev(host, dev)
+    try:
+        tcp_amd.set_tuning(0, unroll, 12, 0)
+        for stride, length, off in ((1500, 1500, 0), (1500, 1500, 4), (1504, 1500, 12), (2048, 1024, 8),
+                                    (4096, 4096, 0), (9000, 8996, 4), (32000, 30000, 0), (1024, 1024, 4)):
+            n = (host.size - off - length) // stride
+            assert tcp_amd.api.plan_uniform(d.data_ptr() + off, stride, length, n)[1] == 12
+            ss = rng.integers(0, 393211, n, dtype=np.uint32)
+            got = u16(tcp_amd.batch_uniform(d, stride, length, n, to_dev(ss.view(np.int32), dev), offset=off))
+            want = oracle.batch_uniform(host, stride, length, n, ss, offset=off)
+            assert np.array_equal(got, want), (stride, length, off)
+            for n2 in (1, 2, 63, 65):   # partial tiles
+                got = u16(tcp_amd.batch_uniform(d, stride, length, n2, 7, offset=off))
+                assert np.array_equal(got, oracle.batch_uniform(host, stride, length, n2, 7, offset=off))
+    finally:
+        tcp_amd.set_tuning(0, 0, -1, 0)
