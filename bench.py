@@ -61,6 +61,8 @@ def max_over_ranks(x: float, dist, device) -> float:
     if dist is None:
         return x
     import torch
+    if dist.get_backend() == "gloo":
+        device = torch.device("cpu")
     t = torch.tensor([x], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
@@ -161,12 +163,21 @@ def main(argv=None) -> int:
         if world == 1 and args.gpus > 1:
             print("bench.py: --gpus > 1 needs torch.distributed.run with one process per GPU", file=sys.stderr)
             return 2
+    # Rehearsal knobs for a 1-GPU box (never needed on an N-GPU node):
+    # TCPCSUM_BENCH_SHARE_DEVICE=1 puts every rank on GPU 0, TCPCSUM_BENCH_BACKEND=gloo
+    # runs the barriers / max-reduce on the CPU (RCCL refuses two ranks on one GPU).
+    if os.environ.get("TCPCSUM_BENCH_SHARE_DEVICE") == "1":
+        local = 0
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     dist = None
     if world > 1:
         import torch.distributed as tdist
-        tdist.init_process_group("nccl", device_id=device)
+        backend = os.environ.get("TCPCSUM_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            tdist.init_process_group("nccl", device_id=device)
+        else:
+            tdist.init_process_group(backend)
         dist = tdist
     rc, arch = tcp_amd.device_check()
     if rc != 0:
