@@ -228,6 +228,11 @@ def main(argv=None) -> int:
     except Exception:
         check = None
 
+    if dist is not None:   # the check holds only if it holds on every rank
+        flag = 1.0 if check else (0.0 if check is False else -1.0)
+        fl = -max_over_ranks(-flag, dist, device)   # min over ranks
+        check = None if fl < 0 else bool(fl == 1.0)
+
     k = [0]
 
     def step():
