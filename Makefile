@@ -7,7 +7,11 @@ ROCM ?= /opt/rocm
 HIPCC ?= $(ROCM)/bin/hipcc
 CC ?= gcc
 ARCH ?= gfx950
-HIPFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Wno-unused-parameter -Wno-unused-value -Wno-unused-result
+# TUNING_VARIANTS=1 also compiles the pipelined / default-load kernel variants the
+# TCPCSUM_TUNE_PIPE_* / NT_* flags select (tuning experiments only)
+TUNING_VARIANTS ?= 0
+HIPFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Wno-unused-parameter -Wno-unused-value -Wno-unused-result \
+	-DTCPCSUM_TUNING_VARIANTS=$(TUNING_VARIANTS)
 CFLAGS_LIB ?= -O2 -fPIC -Wall -Wextra
 
 LIB := tcp_amd/libtcpcsum.so

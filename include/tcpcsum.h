@@ -224,6 +224,7 @@ int tcpcsum_plan_uniform(uint64_t base, uint64_t stride, uint32_t len, uint64_t 
  * per-shape defaults. unroll in {0,1,2,4,8}; shape in {-1, 0..12} (a forced
  * shape that cannot cover the segments is ignored); flags: TCPCSUM_TUNE_*
  * bits (0 = defaults). Affects batch calls issued afterwards from any thread. */
+/* PIPE_* and NT_* take effect only in a library built with TUNING_VARIANTS=1 */
 #define TCPCSUM_TUNE_PIPE_ON 1   /* software-pipelined tiles */
 #define TCPCSUM_TUNE_PIPE_OFF 2
 #define TCPCSUM_TUNE_NT_ON 4     /* non-temporal loads */

@@ -32,6 +32,10 @@
 #include "tcpcsum.h"
 #include "tcpcsum_internal.h"
 
+#ifndef TCPCSUM_TUNING_VARIANTS
+#define TCPCSUM_TUNING_VARIANTS 0
+#endif
+
 namespace tcpcsum {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -992,10 +996,16 @@ static void launch_uniform_pn(const UniformPlan& p, const uint8_t* base, uint64_
 void launch_uniform(const uint8_t* base, uint64_t stride, uint32_t len, const uint32_t* ss, uint32_t ss0,
                     uint16_t* out, uint64_t n, hipStream_t s, const Tuning& tu) {
     const UniformPlan p = plan_uniform((uintptr_t)base, stride, len, n, tu);
+#if TCPCSUM_TUNING_VARIANTS
+    // experiment build: software-pipelined tiles and default-policy loads
+    // (neither beat the shipped kernel on MI355X)
     if (p.pipe && p.nt) launch_uniform_pn<true, true>(p, base, stride, len, ss, ss0, out, n, s);
     else if (p.pipe) launch_uniform_pn<true, false>(p, base, stride, len, ss, ss0, out, n, s);
     else if (p.nt) launch_uniform_pn<false, true>(p, base, stride, len, ss, ss0, out, n, s);
     else launch_uniform_pn<false, false>(p, base, stride, len, ss, ss0, out, n, s);
+#else
+    launch_uniform_pn<false, true>(p, base, stride, len, ss, ss0, out, n, s);
+#endif
 }
 
 template <int G, int C>
