@@ -110,16 +110,19 @@ int tcpcsum_batch_desc_dev(const void *d_base, const tcpcsum_desc_t *d_desc, uin
 
 /* Wire layout (the loop's out-buffers, loop.c:107-116 / releaseSend
  * loop.c:27-94): packet i is a raw IPv4 packet at d_pkts + d_pkt_off[i], of
- * at most cap bytes. The pseudo header comes from the IP header (saddr @12,
+ * at most cap bytes, inside a device region of region_bytes bytes (the kernel
+ * reads at most min(cap, region_bytes - off) bytes of each packet, never
+ * outside the region). The pseudo header comes from the IP header (saddr @12,
  * daddr @16, tcp length = tot_len - ihl*4), the TCP segment starts at ihl*4.
  *   FILL:   the sum is taken with the check field (TCP+16) as zero, as
  *           context.c:182 leaves it; the result is stored at TCP+16 in place
  *           (and in d_out[i] when d_out != NULL).
  *   VERIFY: d_out[i] = csum over the segment including check (0 == valid).
- * d_status[i] (may be NULL) = TCPCSUM_PKT_OK or TCPCSUM_PKT_SKIPPED; skipped
- * packets are left untouched and d_out[i] = 0. */
-int tcpcsum_ipv4_batch_dev(void *d_pkts, const uint64_t *d_pkt_off, uint64_t n, uint32_t cap,
-                           int mode, uint16_t *d_out, uint8_t *d_status, void *stream);
+ * d_status[i] (may be NULL) = TCPCSUM_PKT_OK or TCPCSUM_PKT_SKIPPED (also when
+ * off + tot_len > region_bytes); skipped packets are left untouched and
+ * d_out[i] = 0. */
+int tcpcsum_ipv4_batch_dev(void *d_pkts, uint64_t region_bytes, const uint64_t *d_pkt_off, uint64_t n,
+                           uint32_t cap, int mode, uint16_t *d_out, uint8_t *d_status, void *stream);
 
 /* Segment assembly + checksum in one pass (device-side
  * us_internal_socket_context_send_packet, context.c:150-213, minus its 10 %

@@ -81,7 +81,7 @@ SIGNATURES = {
     "tcpcsum_continue": (ctypes.c_ushort, [ctypes.c_ulong, ctypes.c_char_p, ctypes.c_int]),
     "tcpcsum_batch_uniform_dev": (ctypes.c_int, [vp, u64, u32, vp, u32, vp, u64, vp]),
     "tcpcsum_batch_desc_dev": (ctypes.c_int, [vp, vp, u64, u32, vp, vp]),
-    "tcpcsum_ipv4_batch_dev": (ctypes.c_int, [vp, vp, u64, u32, ctypes.c_int, vp, vp, vp]),
+    "tcpcsum_ipv4_batch_dev": (ctypes.c_int, [vp, u64, vp, u64, u32, ctypes.c_int, vp, vp, vp]),
     "tcpcsum_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_size_t, ctypes.POINTER(vp)]),
     "tcpcsum_ctx_destroy": (None, [vp]),
     "tcpcsum_host_alloc": (vp, [ctypes.c_size_t]),
@@ -218,7 +218,9 @@ def batch_desc(data, desc, n: int, max_len: int, out=None, stream=None):
 
 
 def ipv4_batch(pkts, pkt_off, n: int, cap: int, mode: int, out=None, status=None, stream=None):
-    rc = lib().tcpcsum_ipv4_batch_dev(_dev_ptr(pkts, "pkts"), _dev_ptr(pkt_off, "pkt_off"), n, cap, mode,
+    """Wire batch over the device tensor ``pkts`` (its whole size is the region)."""
+    region = pkts.numel() * pkts.element_size()
+    rc = lib().tcpcsum_ipv4_batch_dev(_dev_ptr(pkts, "pkts"), region, _dev_ptr(pkt_off, "pkt_off"), n, cap, mode,
                                       _dev_ptr(out, "out"), _dev_ptr(status, "status"), _stream_handle(stream))
     _check(rc, "tcpcsum_ipv4_batch_dev")
     return out, status

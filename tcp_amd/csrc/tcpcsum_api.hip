@@ -152,14 +152,14 @@ int tcpcsum_batch_desc_dev(const void* d_base, const tcpcsum_desc_t* d_desc, uin
     return check_launch();
 }
 
-int tcpcsum_ipv4_batch_dev(void* d_pkts, const uint64_t* d_pkt_off, uint64_t n, uint32_t cap, int mode,
-                           uint16_t* d_out, uint8_t* d_status, void* stream) {
+int tcpcsum_ipv4_batch_dev(void* d_pkts, uint64_t region_bytes, const uint64_t* d_pkt_off, uint64_t n, uint32_t cap,
+                           int mode, uint16_t* d_out, uint8_t* d_status, void* stream) {
     if (n == 0) return TCPCSUM_OK;
-    if (!d_pkts || !d_pkt_off || (mode & ~3)) return TCPCSUM_EINVAL;
+    if (!d_pkts || !d_pkt_off || !region_bytes || (mode & ~3)) return TCPCSUM_EINVAL;
     if (cap > 65535u) cap = 65535u;   // tot_len is a u16
     int rc = require_device(nullptr, 0);
     if (rc) return rc;
-    tcpcsum::launch_ipv4((uint8_t*)d_pkts, d_pkt_off, n, cap, UINT64_MAX, mode, d_out, d_status, nullptr,
+    tcpcsum::launch_ipv4((uint8_t*)d_pkts, d_pkt_off, n, cap, region_bytes, mode, d_out, d_status, nullptr,
                          (hipStream_t)stream,
                          tuning());
     return check_launch();

@@ -447,76 +447,171 @@ __global__ __launch_bounds__(256) void k_desc(const uint8_t* __restrict__ base,
 }
 
 // ---------------------------------------------------------------- wire (IPv4)
-// Packet i at pkts + off[i]. Header fields are read by every lane of the
-// group (same addresses: one broadcast request per group). See tcpcsum.h.
-template <int G, int C>
+// Packet i at pkts + off[i] (see tcpcsum.h). Tiles of U packets per lane
+// group: the offsets of the tile are loaded first; then, for every packet at
+// once, the IP header fields (byte loads, every lane of the group the same
+// address: one broadcast request) AND the payload chunks — speculatively, the
+// aligned hull of [ip, ip + cap) up to the group's G*C chunks — so a packet
+// costs two dependent memory round trips, not three. The TCP range
+// [ihl*4, tot_len) and (IPHDR) the IP header range [0, ihl*4) are then summed
+// from registers with byte masks at their ends. Longer packets take extra
+// rounds. FILL subtracts the check word (what zeroing it does: TCP+16 is an
+// even offset) and stores the result in place.
+struct IpPkt {
+    uint8_t* ip;
+    uint64_t o;
+    uint32_t m;   // ip & 15
+    uint32_t b0, t2, t3, proto, ck0, ck1, ic0, ic1;
+    uint32_t sa, da;
+    bool live;     // a packet of the batch
+    bool hdr;      // its 20-byte IP header lies inside the region
+    bool ck5;      // ck0/ck1 loaded (the TCP check when ihl == 5)
+};
+
+template <int G, int C, int U>
 __global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const uint64_t* __restrict__ off,
                                               uint64_t n, uint32_t cap, uint64_t limit, int mode,
                                               uint16_t* __restrict__ out, uint8_t* __restrict__ status,
                                               uint16_t* __restrict__ ipout) {
     constexpr int GPW = 64 / G;
+    constexpr int SPT = GPW * U;
     const int lane = threadIdx.x & 63;
     const int q = lane / G, gl = lane % G;
-    const uint64_t ngroups = (uint64_t)gridDim.x * 4u * GPW;
-    for (uint64_t i = ((uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6)) * GPW + q; i < n; i += ngroups) {
-        const uint64_t o = off[i];
-        uint8_t* ip = pkts + o;
-        const uint32_t b0 = ip[0];
-        const uint32_t ver = b0 >> 4, ihl = b0 & 15u;
-        const uint32_t tot = ((uint32_t)ip[2] << 8) | ip[3];
-        const uint32_t proto = ip[9];
-        const bool ok = ver == 4u && proto == 6u && ihl >= 5u && tot >= ihl * 4u + 20u && tot <= cap &&
-                        o + tot <= limit;
-        if (!ok) {   // group-uniform
-            if (gl == 0) {
-                if (out) out[i] = 0;
-                if (status) status[i] = TCPCSUM_PKT_SKIPPED;
-            }
-            continue;
+    const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
+    const uint64_t ntiles = (n + SPT - 1) / SPT;
+    const bool verify = (mode & TCPCSUM_IPV4_VERIFY) != 0;
+    const bool iphdr = (mode & TCPCSUM_IPV4_IPHDR) != 0;
+    for (uint64_t t = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6); t < ntiles; t += nwaves) {
+        IpPkt p[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = t * SPT + (uint64_t)(u * GPW + q);
+            p[u].live = i < n;
+            p[u].o = p[u].live ? off[i] : 0;
         }
-        // saddr/daddr as stored (network order), read as native u32 (bytewise:
-        // the IP header start need not be 4-byte aligned).
-        const uint32_t sa = (uint32_t)ip[12] | ((uint32_t)ip[13] << 8) | ((uint32_t)ip[14] << 16) | ((uint32_t)ip[15] << 24);
-        const uint32_t da = (uint32_t)ip[16] | ((uint32_t)ip[17] << 8) | ((uint32_t)ip[18] << 16) | ((uint32_t)ip[19] << 24);
-        uint8_t* tcp = ip + ihl * 4u;
-        const uint32_t tcp_len = tot - ihl * 4u;
-        const uint32_t len_be = ((tcp_len & 0xffu) << 8) | ((tcp_len >> 8) & 0xffu);   // htons
-        // context.c:104-119 closed form: six native u16 words of the pseudo header.
-        const uint64_t ps = (sa & 0xffffu) + (sa >> 16) + (da & 0xffffu) + (da >> 16) + 0x0600u + len_be;
-        const uint32_t check_word = (uint32_t)tcp[16] | ((uint32_t)tcp[17] << 8);
-        const bool verify = (mode & TCPCSUM_IPV4_VERIFY) != 0;
-        uint64_t S = group_segment_sum<G, C>(tcp, tcp_len, gl) + ps;
-        // FILL: the reference sums with check == 0 (context.c:182); TCP+16 is an
-        // even relative offset, so its native word contributes exactly check_word.
-        if (!verify) S -= check_word;
-        const uint16_t c = fold_ref(S);
-        uint32_t st = TCPCSUM_PKT_OK;
-        if (verify && c != 0 && check_word == (uint32_t)(uint16_t)~fold_ref(ps)) st |= TCPCSUM_PKT_CSUM_PARTIAL;
-        if (mode & TCPCSUM_IPV4_IPHDR) {
-            // IPv4 header checksum = csum_continue(0, ip, ihl*4) with check (IP+10)
-            // as zero — the reference's commented-out context.c:179, over ihl*4 bytes.
-            uint32_t acc = 0;
-            for (uint32_t w = (uint32_t)gl; w < ihl * 2u; w += G)
-                acc += (!verify && w == 5u) ? 0u : ((uint32_t)ip[2 * w] | ((uint32_t)ip[2 * w + 1] << 8));
-            acc = group_sum32<G>(acc);
-            const uint16_t ic = fold_ref(acc);
-            if (ipout && gl == 0) ipout[i] = ic;
-            if (!verify) {
+        u32x4 v[U][C];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            uint8_t* ip = pkts + p[u].o;
+            p[u].ip = ip;
+            p[u].m = (uint32_t)((uintptr_t)ip & 15u);
+            p[u].hdr = p[u].live && p[u].o < limit && limit - p[u].o >= 20u;
+            p[u].ck5 = p[u].hdr && limit - p[u].o >= 38u;
+            const bool live = p[u].hdr;
+            p[u].b0 = live ? ip[0] : 0u;
+            p[u].t2 = live ? ip[2] : 0u;
+            p[u].t3 = live ? ip[3] : 0u;
+            p[u].proto = live ? ip[9] : 0u;
+            p[u].ic0 = (live && iphdr) ? ip[10] : 0u;
+            p[u].ic1 = (live && iphdr) ? ip[11] : 0u;
+            p[u].sa = live ? ((uint32_t)ip[12] | ((uint32_t)ip[13] << 8) | ((uint32_t)ip[14] << 16) | ((uint32_t)ip[15] << 24)) : 0u;
+            p[u].da = live ? ((uint32_t)ip[16] | ((uint32_t)ip[17] << 8) | ((uint32_t)ip[18] << 16) | ((uint32_t)ip[19] << 24)) : 0u;
+            p[u].ck0 = p[u].ck5 ? ip[36] : 0u;   // TCP check if ihl == 5 (reloaded below otherwise)
+            p[u].ck1 = p[u].ck5 ? ip[37] : 0u;
+            // speculative payload chunks: the aligned hull of [ip, ip + min(cap, limit - o))
+            const uint64_t room = live ? limit - p[u].o : 0u;
+            const uint32_t span = (uint32_t)(room < cap ? room : cap);
+            const uint32_t nch = (p[u].m + span + 15u) >> 4;
+            const uint8_t* a0 = ip - p[u].m;
+#pragma unroll
+            for (int k = 0; k < C; ++k) {
+                const uint32_t idx = (uint32_t)(k * G + gl);
+                v[u][k] = (live && idx < nch) ? ld16(a0 + (uint64_t)idx * 16u) : u32x4{0u, 0u, 0u, 0u};
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = t * SPT + (uint64_t)(u * GPW + q);
+            if (!p[u].live) continue;   // group-uniform
+            uint8_t* ip = p[u].ip;
+            const uint32_t ver = p[u].b0 >> 4, ihl = p[u].b0 & 15u;
+            const uint32_t tot = (p[u].t2 << 8) | p[u].t3;
+            const bool ok = p[u].hdr && ver == 4u && p[u].proto == 6u && ihl >= 5u && tot >= ihl * 4u + 20u && tot <= cap &&
+                            p[u].o + tot <= limit;
+            if (!ok) {   // group-uniform
                 if (gl == 0) {
-                    ip[10] = (uint8_t)(ic & 0xffu);
-                    ip[11] = (uint8_t)(ic >> 8);
+                    if (out) out[i] = 0;
+                    if (status) status[i] = TCPCSUM_PKT_SKIPPED;
                 }
-            } else if (ic != 0) {
-                st |= TCPCSUM_PKT_IPHDR_BAD;
+                continue;
             }
-        }
-        if (gl == 0) {
-            if (!verify) {   // native u16 store, as context.c:208
-                tcp[16] = (uint8_t)(c & 0xffu);
-                tcp[17] = (uint8_t)(c >> 8);
+            const uint32_t th = ihl * 4u;   // TCP start, packet-relative (even)
+            const bool odd = (p[u].m & 1u) != 0;
+            const uint32_t m = p[u].m;
+            uint32_t w = 0, o = 0, wi = 0, oi = 0;
+#pragma unroll
+            for (int k = 0; k < C; ++k) {
+                const int32_t pos = (int32_t)((uint32_t)(k * G + gl) * 16u) - (int32_t)m;   // chunk start, packet-relative
+                const u32x4 x = v[u][k];
+                if (pos >= (int32_t)th && pos + 16 <= (int32_t)tot) {
+                    w = sad16(x.x, w); w = sad16(x.y, w); w = sad16(x.z, w); w = sad16(x.w, w);
+                    if (odd) {
+                        o = sad8(x.x & 0xff00ff00u, o); o = sad8(x.y & 0xff00ff00u, o);
+                        o = sad8(x.z & 0xff00ff00u, o); o = sad8(x.w & 0xff00ff00u, o);
+                    }
+                } else if (pos + 16 > (int32_t)th && pos < (int32_t)tot) {
+                    chunk_wo_bytes(x, (int64_t)pos - th, (int64_t)(tot - th), odd, w, o);
+                }
+                if (iphdr && pos < (int32_t)th) chunk_wo_bytes(x, (int64_t)pos, (int64_t)th, odd, wi, oi);
             }
-            if (out) out[i] = c;
-            if (status) status[i] = (uint8_t)st;
+            uint64_t W = w, O = o;
+            // packets longer than the group's first G*C chunks
+            const uint32_t nch_tot = (m + tot + 15u) >> 4;
+            for (uint32_t r = (uint32_t)(G * C); r < nch_tot; r += (uint32_t)(G * C)) {
+                uint32_t w2 = 0, o2 = 0;
+#pragma unroll
+                for (int k = 0; k < C; ++k) {
+                    const uint32_t idx = r + (uint32_t)(k * G + gl);
+                    if (idx >= nch_tot) continue;
+                    const u32x4 x = ld16(ip - m + (uint64_t)idx * 16u);
+                    chunk_wo_bytes(x, (int64_t)idx * 16 - m - th, (int64_t)(tot - th), odd, w2, o2);
+                }
+                W += w2;
+                O += o2;
+            }
+            W = group_sum64<G>(W);
+            O = odd ? group_sum64<G>(O) : 0;
+            const uint32_t tcp_len = tot - th;
+            const uint32_t len_be = ((tcp_len & 0xffu) << 8) | ((tcp_len >> 8) & 0xffu);   // htons
+            const uint32_t sa = p[u].sa, da = p[u].da;
+            // context.c:104-119 closed form: six native u16 words of the pseudo header.
+            const uint64_t ps = (sa & 0xffffu) + (sa >> 16) + (da & 0xffffu) + (da >> 16) + 0x0600u + len_be;
+            uint8_t* tcp = ip + th;
+            const uint32_t check_word = (ihl == 5u && p[u].ck5) ? (p[u].ck0 | (p[u].ck1 << 8))
+                                                                : ((uint32_t)tcp[16] | ((uint32_t)tcp[17] << 8));
+            uint64_t S = combine(ps, W, O, odd);
+            // FILL: the reference sums with check == 0 (context.c:182); TCP+16 is an
+            // even relative offset, so its native word contributes exactly check_word.
+            if (!verify) S -= check_word;
+            const uint16_t c = fold_ref(S);
+            uint32_t st = TCPCSUM_PKT_OK;
+            if (verify && c != 0 && check_word == (uint32_t)(uint16_t)~fold_ref(ps)) st |= TCPCSUM_PKT_CSUM_PARTIAL;
+            if (iphdr) {
+                // IPv4 header checksum = csum_continue(0, ip, ihl*4) with check (IP+10)
+                // as zero — the reference's commented-out context.c:179, over ihl*4 bytes.
+                const uint64_t WI = group_sum64<G>((uint64_t)wi);
+                const uint64_t OI = odd ? group_sum64<G>((uint64_t)oi) : 0;
+                uint64_t IS = combine(0, WI, OI, odd);
+                if (!verify) IS -= p[u].ic0 | (p[u].ic1 << 8);
+                const uint16_t ic = fold_ref(IS);
+                if (ipout && gl == 0) ipout[i] = ic;
+                if (!verify) {
+                    if (gl == 0) {
+                        ip[10] = (uint8_t)(ic & 0xffu);
+                        ip[11] = (uint8_t)(ic >> 8);
+                    }
+                } else if (ic != 0) {
+                    st |= TCPCSUM_PKT_IPHDR_BAD;
+                }
+            }
+            if (gl == 0) {
+                if (!verify) {   // native u16 store, as context.c:208
+                    tcp[16] = (uint8_t)(c & 0xffu);
+                    tcp[17] = (uint8_t)(c >> 8);
+                }
+                if (out) out[i] = c;
+                if (status) status[i] = (uint8_t)st;
+            }
         }
     }
 }
@@ -1028,20 +1123,29 @@ void launch_desc(const uint8_t* base, const tcpcsum_desc_t* d, uint64_t n, uint3
     else launch_desc_t<64, 8>(base, d, n, out, s, max_blocks);
 }
 
+template <int G, int C, int U>
+static void launch_ipv4_t(uint8_t* pkts, const uint64_t* off, uint64_t n, uint32_t cap, uint64_t limit, int mode,
+                          uint16_t* out, uint8_t* status, uint16_t* ipout, hipStream_t s, int max_blocks) {
+    constexpr int SPT = (64 / G) * U;
+    hipLaunchKernelGGL((k_ipv4<G, C, U>), dim3(grid_for((n + SPT - 1) / SPT, max_blocks)), dim3(256), 0, s, pkts,
+                       off, n, cap, limit, mode, out, status, ipout);
+}
+
 void launch_ipv4(uint8_t* pkts, const uint64_t* off, uint64_t n, uint32_t cap, uint64_t limit, int mode,
                  uint16_t* out, uint8_t* status, uint16_t* ipout, hipStream_t s, const Tuning& tu) {
-    const int max_blocks = tu.max_blocks > 0 ? tu.max_blocks : kDefaultMaxBlocks;
+    const int max_blocks = tu.max_blocks > 0 ? tu.max_blocks : 2048;
+    const int unroll = tu.unroll ? tu.unroll : 2;
     const uint64_t nch = ((uint64_t)cap + 30u) >> 4;
-    if (nch <= 8) {
-        hipLaunchKernelGGL((k_ipv4<8, 1>), dim3(grid_for((n + 7) / 8, max_blocks)), dim3(256), 0, s, pkts, off,
-                           n, cap, limit, mode, out, status, ipout);
-    } else if (nch <= 96) {
-        hipLaunchKernelGGL((k_ipv4<32, 3>), dim3(grid_for((n + 1) / 2, max_blocks)), dim3(256), 0, s, pkts, off,
-                           n, cap, limit, mode, out, status, ipout);
-    } else {
-        hipLaunchKernelGGL((k_ipv4<64, 8>), dim3(grid_for(n, max_blocks)), dim3(256), 0, s, pkts, off, n, cap,
-                           limit, mode, out, status, ipout);
-    }
+#define IP_U(G, C)                                                                                          \
+    do {                                                                                                    \
+        if (unroll <= 1) launch_ipv4_t<G, C, 1>(pkts, off, n, cap, limit, mode, out, status, ipout, s, max_blocks); \
+        else if (unroll == 2) launch_ipv4_t<G, C, 2>(pkts, off, n, cap, limit, mode, out, status, ipout, s, max_blocks); \
+        else launch_ipv4_t<G, C, 4>(pkts, off, n, cap, limit, mode, out, status, ipout, s, max_blocks);       \
+    } while (0)
+    if (nch <= 8) IP_U(8, 1);
+    else if (nch <= 96) IP_U(32, 3);
+    else IP_U(64, 4);
+#undef IP_U
 }
 
 template <int G, int C, int U>

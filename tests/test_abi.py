@@ -90,8 +90,9 @@ def test_argument_errors_need_no_device():
     assert L.tcpcsum_batch_uniform_dev(None, 0, 10, None, 0, None, 5, None) == api.EINVAL
     assert L.tcpcsum_batch_uniform_dev(1 << 20, 0, 2**31, None, 0, 1 << 20, 5, None) == api.EINVAL
     assert L.tcpcsum_batch_desc_dev(1 << 20, (1 << 20) + 8, 5, 64, 1 << 20, None) == api.EINVAL   # unaligned desc
-    assert L.tcpcsum_ipv4_batch_dev(1 << 20, 1 << 20, 5, 1500, 7, None, None, None) == api.EINVAL  # bad mode
-    assert L.tcpcsum_ipv4_batch_dev(1 << 20, 1 << 20, 5, 1500, 4, None, None, None) == api.EINVAL
+    assert L.tcpcsum_ipv4_batch_dev(1 << 20, 1 << 20, 1 << 20, 5, 1500, 7, None, None, None) == api.EINVAL
+    assert L.tcpcsum_ipv4_batch_dev(1 << 20, 1 << 20, 1 << 20, 5, 1500, 4, None, None, None) == api.EINVAL
+    assert L.tcpcsum_ipv4_batch_dev(1 << 20, 0, 1 << 20, 5, 1500, 0, None, None, None) == api.EINVAL
     ng = ctypes.c_int()
     assert L.tcpcsum_stream_probe_dev(1 << 20, 17, 1 << 20, ctypes.byref(ng), None) == api.EINVAL
     assert L.tcpcsum_set_tuning(-1, 0, -1, 0) == api.EINVAL

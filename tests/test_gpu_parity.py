@@ -451,3 +451,33 @@ def test_flat_tiles_vs_oracle(dev, unroll):
                 assert np.array_equal(got, oracle.batch_uniform(host, stride, length, n2, 7, offset=off))
     finally:
         tcp_amd.set_tuning(0, 0, -1, 0)
+
+
+def test_ipv4_region_bounds(dev):
+    """Reads never leave the region: a packet whose tot_len runs past it is skipped, offsets at the
+    very end (no room for a header) are skipped, and the rest is still exact."""
+    import tcp_amd
+    from tests.packets import ip_packet
+    rng = np.random.default_rng(5)
+    pkts = [ip_packet(rng, int(rng.integers(0, 1456))) for _ in range(40)]
+    offs, pos = [], 0
+    for p in pkts:
+        offs.append(pos)
+        pos += len(p)
+    region = np.zeros(pos, np.uint8)
+    for o, p in zip(offs, pkts):
+        region[o:o + len(p)] = np.frombuffer(p, np.uint8)
+    cut = offs[-1] + len(pkts[-1]) - 5            # last packet truncated by the region end
+    region = region[:cut].copy()
+    off = np.array(offs + [cut - 10, cut - 1], np.uint64)
+    want_out, want_st = oracle.ipv4_batch(np.concatenate([region, np.zeros(64, np.uint8)]), off, 32768,
+                                          tcp_amd.IPV4_FILL)
+    # the oracle reads past the region for the cut packet; the device must skip it (region-bounded)
+    want_st[-3:] = tcp_amd.PKT_SKIPPED
+    want_out[-3:] = 0
+    dreg = to_dev(region, dev)
+    out = torch.empty(off.size, dtype=torch.int16, device=dev)
+    st = torch.empty(off.size, dtype=torch.uint8, device=dev)
+    tcp_amd.ipv4_batch(dreg, to_dev(off.view(np.int64), dev), off.size, 32768, tcp_amd.IPV4_FILL, out, st)
+    assert np.array_equal(st.cpu().numpy(), want_st)
+    assert np.array_equal(u16(out)[:-3], want_out[:-3])
