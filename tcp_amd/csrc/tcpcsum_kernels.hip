@@ -389,60 +389,81 @@ __global__ __launch_bounds__(256) void k_flat(const uint8_t* __restrict__ base, 
 }
 
 // ---------------------------------------------------------------- ragged
-// Exact sum of one segment [p, p+len) by the G lanes of a group, C chunk
-// loads per lane per round. Returns the group total S - start (i.e. with the
-// parity rule applied) in every lane of the group.
+// Sum of one round of C chunks already in registers (chunk r + k*G + gl).
 template <int G, int C>
-__device__ __forceinline__ uint64_t group_segment_sum(const uint8_t* p, uint32_t len, int gl) {
-    const uint32_t m = (uint32_t)((uintptr_t)p & 15u);
-    const uint8_t* a0 = p - m;
-    const uint32_t nch = (uint32_t)(((uint64_t)m + len + 15u) >> 4);
-    const bool a4 = (((uintptr_t)p | len) & 3u) == 0;
-    const bool odd = ((uintptr_t)p & 1u) != 0;
-    uint64_t W = 0, O = 0;
-    for (uint32_t r = 0; r < nch; r += (uint32_t)(G * C)) {
-        u32x4 v[C];
+__device__ __forceinline__ void round_sum(const u32x4 (&v)[C], uint32_t r, uint32_t m, uint32_t len, bool a4,
+                                          bool odd, int gl, uint32_t& w, uint32_t& o) {
+    if (a4) {
 #pragma unroll
-        for (int k = 0; k < C; ++k) {
-            const uint32_t idx = r + (uint32_t)(k * G + gl);
-            v[k] = idx < nch ? ld16(a0 + (uint64_t)idx * 16u) : u32x4{0u, 0u, 0u, 0u};
-        }
-        uint32_t w = 0, o = 0;
-        if (a4) {
+        for (int k = 0; k < C; ++k) w += chunk_w<M4>(v[k], (r + (uint32_t)(k * G + gl)) * 16u - m, len);
+    } else {
 #pragma unroll
-            for (int k = 0; k < C; ++k) {
-                const uint32_t idx = r + (uint32_t)(k * G + gl);
-                w += chunk_w<M4>(v[k], idx * 16u - m, len);
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < C; ++k) {
-                const uint32_t idx = r + (uint32_t)(k * G + gl);
-                chunk_wo_bytes(v[k], (int64_t)idx * 16 - (int64_t)m, (int64_t)len, odd, w, o);
-            }
-        }
-        W += w;
-        O += o;
+        for (int k = 0; k < C; ++k)
+            chunk_wo_bytes(v[k], (int64_t)(r + (uint32_t)(k * G + gl)) * 16 - (int64_t)m, (int64_t)len, odd, w, o);
     }
-    W = group_sum64<G>(W);
-    O = odd ? group_sum64<G>(O) : 0;
-    return combine(0, W, O, odd);
 }
 
-template <int G, int C>
+// Ragged descriptors in tiles of U segments per lane group: all descriptor
+// loads of the tile, then the first round of chunk loads of all U segments,
+// then the sums (longer segments take further rounds).
+template <int G, int C, int U>
 __global__ __launch_bounds__(256) void k_desc(const uint8_t* __restrict__ base,
                                               const tcpcsum_desc_t* __restrict__ desc, uint64_t n,
                                               uint16_t* __restrict__ out) {
     constexpr int GPW = 64 / G;
+    constexpr int SPT = GPW * U;
     const int lane = threadIdx.x & 63;
     const int q = lane / G, gl = lane % G;
-    const uint64_t ngroups = (uint64_t)gridDim.x * 4u * GPW;
-    for (uint64_t seg = ((uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6)) * GPW + q; seg < n;
-         seg += ngroups) {
-        const u32x4 d = *reinterpret_cast<const u32x4*>(desc + seg);   // one 16-B load
-        const uint64_t off = (uint64_t)d.x | ((uint64_t)d.y << 32);
-        const uint64_t S = group_segment_sum<G, C>(base + off, d.z, gl) + (uint64_t)d.w;
-        if (gl == 0) out[seg] = fold_ref(S);
+    const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
+    const uint64_t ntiles = (n + SPT - 1) / SPT;
+    for (uint64_t t = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6); t < ntiles; t += nwaves) {
+        u32x4 d[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t seg = t * SPT + (uint64_t)(u * GPW + q);
+            d[u] = seg < n ? *reinterpret_cast<const u32x4*>(desc + seg) : u32x4{0u, 0u, 0u, 0u};   // one 16-B load
+        }
+        u32x4 v[U][C];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint8_t* p = base + ((uint64_t)d[u].x | ((uint64_t)d[u].y << 32));
+            const uint32_t m = (uint32_t)((uintptr_t)p & 15u);
+            const uint32_t nch = (uint32_t)(((uint64_t)m + d[u].z + 15u) >> 4);   // 0 for dead slots (len 0)
+#pragma unroll
+            for (int k = 0; k < C; ++k) {
+                const uint32_t idx = (uint32_t)(k * G + gl);
+                v[u][k] = idx < nch ? ld16(p - m + (uint64_t)idx * 16u) : u32x4{0u, 0u, 0u, 0u};
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t seg = t * SPT + (uint64_t)(u * GPW + q);
+            if (seg >= n) continue;   // group-uniform
+            const uint8_t* p = base + ((uint64_t)d[u].x | ((uint64_t)d[u].y << 32));
+            const uint32_t len = d[u].z;
+            const uint32_t m = (uint32_t)((uintptr_t)p & 15u);
+            const uint32_t nch = (uint32_t)(((uint64_t)m + len + 15u) >> 4);
+            const bool a4 = (((uintptr_t)p | len) & 3u) == 0;
+            const bool odd = ((uintptr_t)p & 1u) != 0;
+            uint32_t w = 0, o = 0;
+            round_sum<G, C>(v[u], 0u, m, len, a4, odd, gl, w, o);
+            uint64_t W = w, O = o;
+            for (uint32_t r = (uint32_t)(G * C); r < nch; r += (uint32_t)(G * C)) {
+                u32x4 x[C];
+#pragma unroll
+                for (int k = 0; k < C; ++k) {
+                    const uint32_t idx = r + (uint32_t)(k * G + gl);
+                    x[k] = idx < nch ? ld16(p - m + (uint64_t)idx * 16u) : u32x4{0u, 0u, 0u, 0u};
+                }
+                uint32_t w2 = 0, o2 = 0;
+                round_sum<G, C>(x, r, m, len, a4, odd, gl, w2, o2);
+                W += w2;
+                O += o2;
+            }
+            W = group_sum64<G>(W);
+            O = odd ? group_sum64<G>(O) : 0;
+            if (gl == 0) out[seg] = fold_ref(combine((uint64_t)d[u].w, W, O, odd));
+        }
     }
 }
 
@@ -1103,24 +1124,33 @@ void launch_uniform(const uint8_t* base, uint64_t stride, uint32_t len, const ui
 #endif
 }
 
-template <int G, int C>
+template <int G, int C, int U>
 static void launch_desc_t(const uint8_t* base, const tcpcsum_desc_t* d, uint64_t n, uint16_t* out,
                           hipStream_t s, int max_blocks) {
-    const uint64_t waves = (n + (64 / G) - 1) / (64 / G);
-    hipLaunchKernelGGL((k_desc<G, C>), dim3(grid_for(waves, max_blocks)), dim3(256), 0, s, base, d, n, out);
+    constexpr int SPT = (64 / G) * U;
+    hipLaunchKernelGGL((k_desc<G, C, U>), dim3(grid_for((n + SPT - 1) / SPT, max_blocks)), dim3(256), 0, s, base, d,
+                       n, out);
 }
 
 void launch_desc(const uint8_t* base, const tcpcsum_desc_t* d, uint64_t n, uint32_t max_len, uint16_t* out,
                  hipStream_t s, const Tuning& tu) {
     const uint64_t nch = ((uint64_t)max_len + 30u) >> 4;   // worst-case start alignment
     const int max_blocks = tu.max_blocks > 0 ? tu.max_blocks : kDefaultMaxBlocks;
-    if (nch <= 4) launch_desc_t<4, 1>(base, d, n, out, s, max_blocks);
-    else if (nch <= 8) launch_desc_t<8, 1>(base, d, n, out, s, max_blocks);
-    else if (nch <= 16) launch_desc_t<16, 1>(base, d, n, out, s, max_blocks);
-    else if (nch <= 32) launch_desc_t<32, 1>(base, d, n, out, s, max_blocks);
-    else if (nch <= 96) launch_desc_t<32, 3>(base, d, n, out, s, max_blocks);
-    else if (nch <= 256) launch_desc_t<64, 4>(base, d, n, out, s, max_blocks);
-    else launch_desc_t<64, 8>(base, d, n, out, s, max_blocks);
+    const int unroll = tu.unroll ? tu.unroll : 2;
+#define DS_U(G, C)                                                                 \
+    do {                                                                           \
+        if (unroll <= 1) launch_desc_t<G, C, 1>(base, d, n, out, s, max_blocks);   \
+        else if (unroll == 2) launch_desc_t<G, C, 2>(base, d, n, out, s, max_blocks); \
+        else launch_desc_t<G, C, 4>(base, d, n, out, s, max_blocks);               \
+    } while (0)
+    if (nch <= 4) DS_U(4, 1);
+    else if (nch <= 8) DS_U(8, 1);
+    else if (nch <= 16) DS_U(16, 1);
+    else if (nch <= 32) DS_U(32, 1);
+    else if (nch <= 96) DS_U(32, 3);
+    else if (nch <= 256) DS_U(64, 4);
+    else DS_U(64, 8);
+#undef DS_U
 }
 
 template <int G, int C, int U>

@@ -52,9 +52,13 @@ def main():
             order = np.argsort(lens, kind="stable")
             d2 = desc[order]
             ddesc = torch.from_numpy(d2.view(np.uint8)).to(dev)
-        t = timeit(lambda: tcp_amd.batch_desc(data, ddesc, n, 1500, out))
-        print(json.dumps({"measure": "desc_imix_1M", "sorted_by_len": sorted_, "ms": round(t * 1e3, 4),
-                          "GB/s": round(int(lens.sum()) / t / 1e9, 1), "Mseg/s": round(n / t / 1e6, 1)}), flush=True)
+        for un in ((1, 2, 4) if "--sweep" in sys.argv else (0,)):
+            tcp_amd.set_tuning(0, un, -1, 0)
+            t = timeit(lambda: tcp_amd.batch_desc(data, ddesc, n, 1500, out))
+            print(json.dumps({"measure": "desc_imix_1M", "sorted_by_len": sorted_, "unroll": un,
+                              "ms": round(t * 1e3, 4), "GB/s": round(int(lens.sum()) / t / 1e9, 1),
+                              "Mseg/s": round(n / t / 1e6, 1)}), flush=True)
+        tcp_amd.set_tuning(0, 0, -1, 0)
 
     # wire: 1M packets of 1500 B (IP 20 + TCP 24 + 1456 payload) in 1536-B slots
     payload = torch.empty(n * 1456, dtype=torch.uint8, device=dev)
@@ -69,10 +73,14 @@ def main():
     offs = torch.from_numpy((np.arange(n, dtype=np.uint64) * 1536).view(np.int64)).to(dev)
     stat = torch.empty(n, dtype=torch.uint8, device=dev)
     for name, mode in (("FILL", tcp_amd.IPV4_FILL), ("VERIFY", tcp_amd.IPV4_VERIFY)):
-        t = timeit(lambda: tcp_amd.ipv4_batch(data, offs, n, 1536, mode, out, stat))
-        print(json.dumps({"measure": "ipv4_1Mx1500", "mode": name, "ms": round(t * 1e3, 4),
-                          "GB/s_tcp_bytes": round(n * 1480 / t / 1e9, 1), "Mpkt/s": round(n / t / 1e6, 1)}),
-              flush=True)
+        for mb, un in (((1024, 1), (1024, 2), (2048, 2), (4096, 2), (2048, 4), (8192, 1)) if "--sweep" in sys.argv
+                       else ((0, 0),)):
+            tcp_amd.set_tuning(mb, un, -1, 0)
+            t = timeit(lambda: tcp_amd.ipv4_batch(data, offs, n, 1536, mode, out, stat))
+            print(json.dumps({"measure": "ipv4_1Mx1500", "mode": name, "max_blocks": mb, "unroll": un,
+                              "ms": round(t * 1e3, 4), "GB/s_tcp_bytes": round(n * 1480 / t / 1e9, 1),
+                              "Mpkt/s": round(n / t / 1e6, 1)}), flush=True)
+        tcp_amd.set_tuning(0, 0, -1, 0)
     ok = bool((out == 0).all().item()) and bool((stat == 0).all().item())
     print(json.dumps({"measure": "ipv4_verify_all_zero", "ok": ok}))
 
