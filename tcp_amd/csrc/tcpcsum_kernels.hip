@@ -46,6 +46,14 @@ __device__ __forceinline__ u32x4 ld16(const uint8_t* p) {
     return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
 }
 
+// Zero-filled device memory: lanes with nothing to load read it instead of
+// predicating the load. A predicated load in a tile becomes a branch whose
+// join point drains vmcnt, which serialises the tile's loads; an address
+// select keeps every load unconditional and in flight together.
+__device__ __attribute__((aligned(64))) uint8_t g_zero[64];
+
+__device__ __forceinline__ const uint8_t* zsel(bool use, const uint8_t* p) { return use ? p : g_zero; }
+
 // context.c:140-144, on the exact sum.
 __device__ __forceinline__ uint16_t fold_ref(uint64_t S) {
     uint64_t s = (S >> 16) + (S & 0xffffu);
@@ -421,7 +429,8 @@ __global__ __launch_bounds__(256) void k_desc(const uint8_t* __restrict__ base,
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint64_t seg = t * SPT + (uint64_t)(u * GPW + q);
-            d[u] = seg < n ? *reinterpret_cast<const u32x4*>(desc + seg) : u32x4{0u, 0u, 0u, 0u};   // one 16-B load
+            // one 16-B load; slots past n read zeros (len 0)
+            d[u] = *reinterpret_cast<const u32x4*>(zsel(seg < n, reinterpret_cast<const uint8_t*>(desc + seg)));
         }
         u32x4 v[U][C];
 #pragma unroll
@@ -432,7 +441,7 @@ __global__ __launch_bounds__(256) void k_desc(const uint8_t* __restrict__ base,
 #pragma unroll
             for (int k = 0; k < C; ++k) {
                 const uint32_t idx = (uint32_t)(k * G + gl);
-                v[u][k] = idx < nch ? ld16(p - m + (uint64_t)idx * 16u) : u32x4{0u, 0u, 0u, 0u};
+                v[u][k] = ld16(zsel(idx < nch, p - m + (uint64_t)idx * 16u));
             }
         }
 #pragma unroll
@@ -508,7 +517,7 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const 
         for (int u = 0; u < U; ++u) {
             const uint64_t i = t * SPT + (uint64_t)(u * GPW + q);
             p[u].live = i < n;
-            p[u].o = p[u].live ? off[i] : 0;
+            p[u].o = *reinterpret_cast<const uint64_t*>(zsel(p[u].live, reinterpret_cast<const uint8_t*>(off + i)));
         }
         u32x4 v[U][C];
 #pragma unroll
@@ -519,16 +528,18 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const 
             p[u].hdr = p[u].live && p[u].o < limit && limit - p[u].o >= 20u;
             p[u].ck5 = p[u].hdr && limit - p[u].o >= 38u;
             const bool live = p[u].hdr;
-            p[u].b0 = live ? ip[0] : 0u;
-            p[u].t2 = live ? ip[2] : 0u;
-            p[u].t3 = live ? ip[3] : 0u;
-            p[u].proto = live ? ip[9] : 0u;
-            p[u].ic0 = (live && iphdr) ? ip[10] : 0u;
-            p[u].ic1 = (live && iphdr) ? ip[11] : 0u;
-            p[u].sa = live ? ((uint32_t)ip[12] | ((uint32_t)ip[13] << 8) | ((uint32_t)ip[14] << 16) | ((uint32_t)ip[15] << 24)) : 0u;
-            p[u].da = live ? ((uint32_t)ip[16] | ((uint32_t)ip[17] << 8) | ((uint32_t)ip[18] << 16) | ((uint32_t)ip[19] << 24)) : 0u;
-            p[u].ck0 = p[u].ck5 ? ip[36] : 0u;   // TCP check if ihl == 5 (reloaded below otherwise)
-            p[u].ck1 = p[u].ck5 ? ip[37] : 0u;
+            const uint8_t* h = zsel(live, ip);   // a dead slot reads zeros: ver 0, skipped
+            p[u].b0 = h[0];
+            p[u].t2 = h[2];
+            p[u].t3 = h[3];
+            p[u].proto = h[9];
+            p[u].ic0 = h[10];
+            p[u].ic1 = h[11];
+            p[u].sa = (uint32_t)h[12] | ((uint32_t)h[13] << 8) | ((uint32_t)h[14] << 16) | ((uint32_t)h[15] << 24);
+            p[u].da = (uint32_t)h[16] | ((uint32_t)h[17] << 8) | ((uint32_t)h[18] << 16) | ((uint32_t)h[19] << 24);
+            const uint8_t* hc = zsel(p[u].ck5, ip + 36) ;   // TCP check if ihl == 5 (reloaded below otherwise)
+            p[u].ck0 = hc[0];
+            p[u].ck1 = hc[1];
             // speculative payload chunks: the aligned hull of [ip, ip + min(cap, limit - o))
             const uint64_t room = live ? limit - p[u].o : 0u;
             const uint32_t span = (uint32_t)(room < cap ? room : cap);
@@ -537,7 +548,7 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const 
 #pragma unroll
             for (int k = 0; k < C; ++k) {
                 const uint32_t idx = (uint32_t)(k * G + gl);
-                v[u][k] = (live && idx < nch) ? ld16(a0 + (uint64_t)idx * 16u) : u32x4{0u, 0u, 0u, 0u};
+                v[u][k] = ld16(zsel(live && idx < nch, a0 + (uint64_t)idx * 16u));
             }
         }
 #pragma unroll
@@ -679,11 +690,9 @@ struct TxPkt {
 __device__ __forceinline__ void tx_decode(TxPkt& p, const tcpcsum_txseg_t* segs, uint64_t i, uint64_t n,
                                           const uint8_t* payload, uint8_t* outp) {
     p.live = i < n;
-    u32x4 d0 = {0u, 0u, 0u, 0u}, d1 = d0, d2 = d0;
-    if (p.live) {
-        const u32x4* dp = reinterpret_cast<const u32x4*>(segs + i);
-        d0 = dp[0]; d1 = dp[1]; d2 = dp[2];
-    }
+    // dead slots read zeros (g_zero is 64 bytes: covers the 48-byte record)
+    const u32x4* dp = reinterpret_cast<const u32x4*>(zsel(p.live, reinterpret_cast<const uint8_t*>(segs + i)));
+    const u32x4 d0 = dp[0], d1 = dp[1], d2 = dp[2];
     const uint64_t payload_off = (uint64_t)d0.x | ((uint64_t)d0.y << 32);
     const uint64_t out_off = (uint64_t)d0.z | ((uint64_t)d0.w << 32);
     p.sa = d1.x; p.da = d1.y; p.seq = d1.z; p.ack = d1.w;
@@ -722,7 +731,7 @@ __device__ __forceinline__ void tx_edge_load(const TxPkt& p, int e, u32x4& A, u3
     const uint8_t* a = p.sbase + (uint64_t)e * 16u;
     const uintptr_t lo = (uintptr_t)p.src, hi = (uintptr_t)p.src + p.len;
     if ((uintptr_t)a < hi && (uintptr_t)a + 16 > lo) A = ld16(a);
-    if (p.sh != 0 && (uintptr_t)a + 16 < hi && (uintptr_t)a + 32 > lo) B = ld16(a + 16);
+    if (p.sh != 0 && (uintptr_t)a + 16 < hi && (uintptr_t)a + 32 > lo) B = ld16(a + 16);   // rare: ragged ends only
 }
 
 // Phase 1 for a full chunk already loaded: shift into place, store, sum.
@@ -829,8 +838,8 @@ __global__ __launch_bounds__(256) void k_tx_build(const uint8_t* __restrict__ pa
             for (int k = 0; k < C; ++k) {   // every source byte under a full chunk is payload
                 const uint32_t idx = p[u].f0 + (uint32_t)(k * G + gl);
                 const uint8_t* a = p[u].sbase + (uint64_t)idx * 16u;
-                A[u][k] = idx < p[u].f1 ? ld16(a) : u32x4{0u, 0u, 0u, 0u};
-                B[u][k] = (idx < p[u].f1 && p[u].sh) ? ld16(a + 16) : u32x4{0u, 0u, 0u, 0u};
+                A[u][k] = ld16(zsel(idx < p[u].f1, a));
+                B[u][k] = ld16(zsel(idx < p[u].f1 && p[u].sh, a + 16));
             }
             e[u] = tx_edge_chunk(p[u], gl);
             tx_edge_load(p[u], e[u], EA[u], EB[u]);
