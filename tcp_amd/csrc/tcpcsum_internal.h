@@ -18,7 +18,7 @@ constexpr int kProbeSlots = TCPCSUM_PROBE_SLOTS;
 struct Tuning {
     int max_blocks = 0;   // 0 = per-shape default
     int unroll = 0;       // 0 = per-shape default; else 1, 2, 4 or 8
-    int shape = -1;       // -1 = auto; else a forced lane-group shape (0..9)
+    int shape = -1;       // -1 = auto; else a forced lane-group shape (per launcher)
     int flags = 0;        // TCPCSUM_TUNE_* bits
 };
 

@@ -424,14 +424,21 @@ __global__ __launch_bounds__(256) void k_desc(const uint8_t* __restrict__ base,
     const int q = lane / G, gl = lane % G;
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
     const uint64_t ntiles = (n + SPT - 1) / SPT;
-    for (uint64_t t = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6); t < ntiles; t += nwaves) {
-        u32x4 d[U];
+    uint64_t t = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
+    // one 16-B load per descriptor; slots past n read zeros (len 0)
+    auto load_desc = [&](uint64_t tile, u32x4 (&dst)[U]) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint64_t seg = t * SPT + (uint64_t)(u * GPW + q);
-            // one 16-B load; slots past n read zeros (len 0)
-            d[u] = *reinterpret_cast<const u32x4*>(zsel(seg < n, reinterpret_cast<const uint8_t*>(desc + seg)));
+            const uint64_t seg = tile * SPT + (uint64_t)(u * GPW + q);
+            dst[u] = *reinterpret_cast<const u32x4*>(zsel(seg < n, reinterpret_cast<const uint8_t*>(desc + seg)));
         }
+    };
+    u32x4 dn[U];
+    load_desc(t, dn);
+    for (; t < ntiles; t += nwaves) {
+        u32x4 d[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) d[u] = dn[u];
         u32x4 v[U][C];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -444,6 +451,8 @@ __global__ __launch_bounds__(256) void k_desc(const uint8_t* __restrict__ base,
                 v[u][k] = ld16(zsel(idx < nch, p - m + (uint64_t)idx * 16u));
             }
         }
+        // the next tile's descriptors, in flight while this tile is summed
+        load_desc(t + nwaves, dn);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint64_t seg = t * SPT + (uint64_t)(u * GPW + q);
@@ -478,31 +487,57 @@ __global__ __launch_bounds__(256) void k_desc(const uint8_t* __restrict__ base,
 
 // ---------------------------------------------------------------- wire (IPv4)
 // Packet i at pkts + off[i] (see tcpcsum.h). Tiles of U packets per lane
-// group: the offsets of the tile are loaded first; then, for every packet at
-// once, the IP header fields (byte loads, every lane of the group the same
-// address: one broadcast request) AND the payload chunks — speculatively, the
-// aligned hull of [ip, ip + cap) up to the group's G*C chunks — so a packet
-// costs two dependent memory round trips, not three. The TCP range
-// [ihl*4, tot_len) and (IPHDR) the IP header range [0, ihl*4) are then summed
-// from registers with byte masks at their ends. Longer packets take extra
-// rounds. FILL subtracts the check word (what zeroing it does: TCP+16 is an
-// even offset) and stores the result in place.
+// group; the offsets of the next tile are in flight while a tile is summed.
+// Each packet costs one memory round trip: the group loads the aligned hull of
+// [ip, ip + span) speculatively (up to its G*C chunks; span = cap, bounded by
+// the region and by the next packet's offset when that lies ahead — a hint:
+// a packet longer than its span takes fix-up loads), and the IP header
+// fields and the TCP check are then read out of the first G chunks — lane gl
+// holds chunk gl, so a field is a group-local ds_bpermute plus v_alignbyte,
+// not a global byte load (G >= 8 covers bytes [0, 113): any IHL and the check
+// at ihl*4 + 16). The TCP range [ihl*4, tot_len) and (IPHDR) the IP header
+// range [0, ihl*4) are summed from registers with byte masks at their ends.
+// Longer packets take extra rounds. FILL subtracts the check word (what
+// zeroing it does: TCP+16 is an even offset) and stores the result in place.
 struct IpPkt {
     uint8_t* ip;
     uint64_t o;
-    uint32_t m;   // ip & 15
-    uint32_t b0, t2, t3, proto, ck0, ck1, ic0, ic1;
-    uint32_t sa, da;
-    bool live;     // a packet of the batch
-    bool hdr;      // its 20-byte IP header lies inside the region
-    bool ck5;      // ck0/ck1 loaded (the TCP check when ihl == 5)
+    uint32_t m;      // ip & 15
+    uint32_t spec;   // chunks loaded speculatively
+    bool live;    // a packet of the batch
+    bool hdr;     // its 20-byte IP header lies inside the region
 };
+
+// A native u16 at p: one 2-byte store when p is even, two byte stores otherwise.
+__device__ __forceinline__ void store_u16(uint8_t* p, uint16_t v) {
+    if (((uintptr_t)p & 1u) == 0) {
+        *reinterpret_cast<uint16_t*>(p) = v;
+    } else {
+        p[0] = (uint8_t)(v & 0xffu);
+        p[1] = (uint8_t)(v >> 8);
+    }
+}
+
+// Dword D (counted from the aligned start of the packet's window) out of the
+// group's first-round chunks c0 (lane gbase + k holds chunk k).
+__device__ __forceinline__ uint32_t grp_dword(const u32x4 c0, int gbase, uint32_t D) {
+    const uint32_t j = D & 3u;
+    const uint32_t mine = j == 0 ? c0.x : j == 1 ? c0.y : j == 2 ? c0.z : c0.w;
+    return (uint32_t)__shfl((int)mine, gbase + (int)(D >> 2), 64);
+}
+
+// The 4 packet bytes at window offset a (little-endian dword).
+__device__ __forceinline__ uint32_t grp_bytes4(const u32x4 c0, int gbase, uint32_t a) {
+    const uint32_t lo = grp_dword(c0, gbase, a >> 2), hi = grp_dword(c0, gbase, (a >> 2) + 1u);
+    return __builtin_amdgcn_alignbyte(hi, lo, a & 3u);
+}
 
 template <int G, int C, int U>
 __global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const uint64_t* __restrict__ off,
                                               uint64_t n, uint32_t cap, uint64_t limit, int mode,
                                               uint16_t* __restrict__ out, uint8_t* __restrict__ status,
                                               uint16_t* __restrict__ ipout) {
+    static_assert(G >= 8, "the header and TCP check are read from the group's first 6 chunks");
     constexpr int GPW = 64 / G;
     constexpr int SPT = GPW * U;
     const int lane = threadIdx.x & 63;
@@ -511,13 +546,25 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const 
     const uint64_t ntiles = (n + SPT - 1) / SPT;
     const bool verify = (mode & TCPCSUM_IPV4_VERIFY) != 0;
     const bool iphdr = (mode & TCPCSUM_IPV4_IPHDR) != 0;
-    for (uint64_t t = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6); t < ntiles; t += nwaves) {
+    uint64_t t = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
+    // offsets of packet i and of packet i + 1 (0 past the end: no bound)
+    auto load_off = [&](uint64_t tile, uint64_t (&dst)[U], uint64_t (&nxt)[U]) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = tile * SPT + (uint64_t)(u * GPW + q);
+            dst[u] = *reinterpret_cast<const uint64_t*>(zsel(i < n, reinterpret_cast<const uint8_t*>(off + i)));
+            nxt[u] = *reinterpret_cast<const uint64_t*>(zsel(i + 1 < n, reinterpret_cast<const uint8_t*>(off + i + 1)));
+        }
+    };
+    uint64_t on[U], on1[U];
+    load_off(t, on, on1);
+    for (; t < ntiles; t += nwaves) {
         IpPkt p[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint64_t i = t * SPT + (uint64_t)(u * GPW + q);
             p[u].live = i < n;
-            p[u].o = *reinterpret_cast<const uint64_t*>(zsel(p[u].live, reinterpret_cast<const uint8_t*>(off + i)));
+            p[u].o = on[u];
         }
         u32x4 v[U][C];
 #pragma unroll
@@ -526,24 +573,16 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const 
             p[u].ip = ip;
             p[u].m = (uint32_t)((uintptr_t)ip & 15u);
             p[u].hdr = p[u].live && p[u].o < limit && limit - p[u].o >= 20u;
-            p[u].ck5 = p[u].hdr && limit - p[u].o >= 38u;
-            const bool live = p[u].hdr;
-            const uint8_t* h = zsel(live, ip);   // a dead slot reads zeros: ver 0, skipped
-            p[u].b0 = h[0];
-            p[u].t2 = h[2];
-            p[u].t3 = h[3];
-            p[u].proto = h[9];
-            p[u].ic0 = h[10];
-            p[u].ic1 = h[11];
-            p[u].sa = (uint32_t)h[12] | ((uint32_t)h[13] << 8) | ((uint32_t)h[14] << 16) | ((uint32_t)h[15] << 24);
-            p[u].da = (uint32_t)h[16] | ((uint32_t)h[17] << 8) | ((uint32_t)h[18] << 16) | ((uint32_t)h[19] << 24);
-            const uint8_t* hc = zsel(p[u].ck5, ip + 36) ;   // TCP check if ihl == 5 (reloaded below otherwise)
-            p[u].ck0 = hc[0];
-            p[u].ck1 = hc[1];
-            // speculative payload chunks: the aligned hull of [ip, ip + min(cap, limit - o))
+            const bool live = p[u].hdr;   // a dead slot reads zeros: ver 0, skipped
+            // speculative payload chunks: the aligned hull of [ip, ip + span); at
+            // least 80 bytes (any IP header and the TCP check) when the region has them
             const uint64_t room = live ? limit - p[u].o : 0u;
-            const uint32_t span = (uint32_t)(room < cap ? room : cap);
-            const uint32_t nch = (p[u].m + span + 15u) >> 4;
+            uint64_t span = room < cap ? room : cap;
+            const uint64_t gap = on1[u] > p[u].o ? on1[u] - p[u].o : ~0ull;
+            const uint64_t hint = gap > 80u ? gap : 80u;
+            span = span < hint ? span : hint;
+            const uint32_t nch = (p[u].m + (uint32_t)span + 15u) >> 4;
+            p[u].spec = nch;
             const uint8_t* a0 = ip - p[u].m;
 #pragma unroll
             for (int k = 0; k < C; ++k) {
@@ -551,14 +590,21 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const 
                 v[u][k] = ld16(zsel(live && idx < nch, a0 + (uint64_t)idx * 16u));
             }
         }
+        // the next tile's offsets, in flight while this tile is summed
+        load_off(t + nwaves, on, on1);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint64_t i = t * SPT + (uint64_t)(u * GPW + q);
             if (!p[u].live) continue;   // group-uniform
             uint8_t* ip = p[u].ip;
-            const uint32_t ver = p[u].b0 >> 4, ihl = p[u].b0 & 15u;
-            const uint32_t tot = (p[u].t2 << 8) | p[u].t3;
-            const bool ok = p[u].hdr && ver == 4u && p[u].proto == 6u && ihl >= 5u && tot >= ihl * 4u + 20u && tot <= cap &&
+            const int gbase = lane - gl;
+            const uint32_t m = p[u].m;
+            const uint32_t h0 = grp_bytes4(v[u][0], gbase, m);        // ver/ihl, tos, tot_len
+            const uint32_t h8 = grp_bytes4(v[u][0], gbase, m + 8u);   // ttl, protocol, check
+            const uint32_t ver = (h0 >> 4) & 15u, ihl = h0 & 15u;
+            const uint32_t tot = ((h0 >> 8) & 0xff00u) | (h0 >> 24);
+            const uint32_t proto = (h8 >> 8) & 0xffu;
+            const bool ok = p[u].hdr && ver == 4u && proto == 6u && ihl >= 5u && tot >= ihl * 4u + 20u && tot <= cap &&
                             p[u].o + tot <= limit;
             if (!ok) {   // group-uniform
                 if (gl == 0) {
@@ -568,8 +614,17 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const 
                 continue;
             }
             const uint32_t th = ihl * 4u;   // TCP start, packet-relative (even)
-            const bool odd = (p[u].m & 1u) != 0;
-            const uint32_t m = p[u].m;
+            const bool odd = (m & 1u) != 0;
+            const uint32_t sa = grp_bytes4(v[u][0], gbase, m + 12u), da = grp_bytes4(v[u][0], gbase, m + 16u);
+            const uint32_t check_word = grp_bytes4(v[u][0], gbase, m + th + 16u) & 0xffffu;
+            const uint32_t nch_tot = (m + tot + 15u) >> 4;
+            if (nch_tot > p[u].spec) {   // longer than its span hint (group-uniform, rare)
+#pragma unroll
+                for (int k = 0; k < C; ++k) {
+                    const uint32_t idx = (uint32_t)(k * G + gl);
+                    if (idx >= p[u].spec && idx < nch_tot) v[u][k] = ld16(ip - m + (uint64_t)idx * 16u);
+                }
+            }
             uint32_t w = 0, o = 0, wi = 0, oi = 0;
 #pragma unroll
             for (int k = 0; k < C; ++k) {
@@ -588,7 +643,6 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const 
             }
             uint64_t W = w, O = o;
             // packets longer than the group's first G*C chunks
-            const uint32_t nch_tot = (m + tot + 15u) >> 4;
             for (uint32_t r = (uint32_t)(G * C); r < nch_tot; r += (uint32_t)(G * C)) {
                 uint32_t w2 = 0, o2 = 0;
 #pragma unroll
@@ -605,12 +659,9 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const 
             O = odd ? group_sum64<G>(O) : 0;
             const uint32_t tcp_len = tot - th;
             const uint32_t len_be = ((tcp_len & 0xffu) << 8) | ((tcp_len >> 8) & 0xffu);   // htons
-            const uint32_t sa = p[u].sa, da = p[u].da;
             // context.c:104-119 closed form: six native u16 words of the pseudo header.
             const uint64_t ps = (sa & 0xffffu) + (sa >> 16) + (da & 0xffffu) + (da >> 16) + 0x0600u + len_be;
             uint8_t* tcp = ip + th;
-            const uint32_t check_word = (ihl == 5u && p[u].ck5) ? (p[u].ck0 | (p[u].ck1 << 8))
-                                                                : ((uint32_t)tcp[16] | ((uint32_t)tcp[17] << 8));
             uint64_t S = combine(ps, W, O, odd);
             // FILL: the reference sums with check == 0 (context.c:182); TCP+16 is an
             // even relative offset, so its native word contributes exactly check_word.
@@ -624,23 +675,17 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const 
                 const uint64_t WI = group_sum64<G>((uint64_t)wi);
                 const uint64_t OI = odd ? group_sum64<G>((uint64_t)oi) : 0;
                 uint64_t IS = combine(0, WI, OI, odd);
-                if (!verify) IS -= p[u].ic0 | (p[u].ic1 << 8);
+                if (!verify) IS -= h8 >> 16;
                 const uint16_t ic = fold_ref(IS);
                 if (ipout && gl == 0) ipout[i] = ic;
                 if (!verify) {
-                    if (gl == 0) {
-                        ip[10] = (uint8_t)(ic & 0xffu);
-                        ip[11] = (uint8_t)(ic >> 8);
-                    }
+                    if (gl == 0) store_u16(ip + 10, ic);
                 } else if (ic != 0) {
                     st |= TCPCSUM_PKT_IPHDR_BAD;
                 }
             }
             if (gl == 0) {
-                if (!verify) {   // native u16 store, as context.c:208
-                    tcp[16] = (uint8_t)(c & 0xffu);
-                    tcp[17] = (uint8_t)(c >> 8);
-                }
+                if (!verify) store_u16(tcp + 16, c);   // native u16 store, as context.c:208
                 if (out) out[i] = c;
                 if (status) status[i] = (uint8_t)st;
             }
@@ -687,12 +732,21 @@ struct TxPkt {
     bool live, odd;
 };
 
-__device__ __forceinline__ void tx_decode(TxPkt& p, const tcpcsum_txseg_t* segs, uint64_t i, uint64_t n,
-                                          const uint8_t* payload, uint8_t* outp) {
-    p.live = i < n;
-    // dead slots read zeros (g_zero is 64 bytes: covers the 48-byte record)
-    const u32x4* dp = reinterpret_cast<const u32x4*>(zsel(p.live, reinterpret_cast<const uint8_t*>(segs + i)));
-    const u32x4 d0 = dp[0], d1 = dp[1], d2 = dp[2];
+// the 48-byte record of segment i as three 16-byte loads; dead slots read
+// zeros (g_zero is 64 bytes: covers the record)
+struct TxRec {
+    u32x4 d0, d1, d2;
+};
+
+__device__ __forceinline__ TxRec tx_load(const tcpcsum_txseg_t* segs, uint64_t i, uint64_t n) {
+    const u32x4* dp = reinterpret_cast<const u32x4*>(zsel(i < n, reinterpret_cast<const uint8_t*>(segs + i)));
+    return TxRec{dp[0], dp[1], dp[2]};
+}
+
+__device__ __forceinline__ void tx_decode(TxPkt& p, const TxRec& r, bool live, const uint8_t* payload,
+                                          uint8_t* outp) {
+    p.live = live;
+    const u32x4 d0 = r.d0, d1 = r.d1, d2 = r.d2;
     const uint64_t payload_off = (uint64_t)d0.x | ((uint64_t)d0.y << 32);
     const uint64_t out_off = (uint64_t)d0.z | ((uint64_t)d0.w << 32);
     p.sa = d1.x; p.da = d1.y; p.seq = d1.z; p.ack = d1.w;
@@ -826,10 +880,17 @@ __global__ __launch_bounds__(256) void k_tx_build(const uint8_t* __restrict__ pa
     const int q0 = lane / G, gl = lane % G;
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
     const uint64_t ntiles = (n + SPT - 1) / SPT;
-    for (uint64_t t = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6); t < ntiles; t += nwaves) {
+    uint64_t t = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
+    TxRec rn[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) rn[u] = tx_load(segs, t * SPT + (uint64_t)(u * GPW + q0), n);
+    for (; t < ntiles; t += nwaves) {
         TxPkt p[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) tx_decode(p[u], segs, t * SPT + (uint64_t)(u * GPW + q0), n, payload, outp);
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = t * SPT + (uint64_t)(u * GPW + q0);
+            tx_decode(p[u], rn[u], i < n, payload, outp);
+        }
         u32x4 A[U][C], B[U][C], EA[U], EB[U];
         int e[U];
 #pragma unroll
@@ -844,6 +905,9 @@ __global__ __launch_bounds__(256) void k_tx_build(const uint8_t* __restrict__ pa
             e[u] = tx_edge_chunk(p[u], gl);
             tx_edge_load(p[u], e[u], EA[u], EB[u]);
         }
+        // the next tile's records, in flight while this tile is built
+#pragma unroll
+        for (int u = 0; u < U; ++u) rn[u] = tx_load(segs, (t + nwaves) * SPT + (uint64_t)(u * GPW + q0), n);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             uint32_t wsum = 0, osum = 0;
@@ -1152,13 +1216,19 @@ void launch_desc(const uint8_t* base, const tcpcsum_desc_t* d, uint64_t n, uint3
         else if (unroll == 2) launch_desc_t<G, C, 2>(base, d, n, out, s, max_blocks); \
         else launch_desc_t<G, C, 4>(base, d, n, out, s, max_blocks);               \
     } while (0)
-    if (nch <= 4) DS_U(4, 1);
-    else if (nch <= 8) DS_U(8, 1);
-    else if (nch <= 16) DS_U(16, 1);
-    else if (nch <= 32) DS_U(32, 1);
-    else if (nch <= 96) DS_U(32, 3);
-    else if (nch <= 256) DS_U(64, 4);
-    else DS_U(64, 8);
+    // lane-group shape: by max_len, or forced (tuning shape 0..6, in this order)
+    int sh = tu.shape;
+    if (sh < 0 || sh > 6)
+        sh = nch <= 4 ? 0 : nch <= 8 ? 1 : nch <= 16 ? 2 : nch <= 32 ? 3 : nch <= 96 ? 4 : nch <= 256 ? 5 : 6;
+    switch (sh) {
+        case 0: DS_U(4, 1); break;
+        case 1: DS_U(8, 1); break;
+        case 2: DS_U(16, 1); break;
+        case 3: DS_U(32, 1); break;
+        case 4: DS_U(32, 3); break;
+        case 5: DS_U(64, 4); break;
+        default: DS_U(64, 8); break;
+    }
 #undef DS_U
 }
 
@@ -1172,18 +1242,31 @@ static void launch_ipv4_t(uint8_t* pkts, const uint64_t* off, uint64_t n, uint32
 
 void launch_ipv4(uint8_t* pkts, const uint64_t* off, uint64_t n, uint32_t cap, uint64_t limit, int mode,
                  uint16_t* out, uint8_t* status, uint16_t* ipout, hipStream_t s, const Tuning& tu) {
-    const int max_blocks = tu.max_blocks > 0 ? tu.max_blocks : 2048;
-    const int unroll = tu.unroll ? tu.unroll : 2;
-    const uint64_t nch = ((uint64_t)cap + 30u) >> 4;
+    const int max_blocks = tu.max_blocks > 0 ? tu.max_blocks : 8192;
+    const int unroll = tu.unroll ? tu.unroll : 1;
+    // shape by the cap and by the mean packet footprint limit / n (packed small
+    // packets: one chunk per lane; MTU slots: one round of 96 chunks per packet)
+    const uint64_t nch = ((uint64_t)cap + 15u) >> 4;   // an odd start takes one extra round
+    const uint64_t mean = n ? limit / n : 0;
 #define IP_U(G, C)                                                                                          \
     do {                                                                                                    \
         if (unroll <= 1) launch_ipv4_t<G, C, 1>(pkts, off, n, cap, limit, mode, out, status, ipout, s, max_blocks); \
         else if (unroll == 2) launch_ipv4_t<G, C, 2>(pkts, off, n, cap, limit, mode, out, status, ipout, s, max_blocks); \
         else launch_ipv4_t<G, C, 4>(pkts, off, n, cap, limit, mode, out, status, ipout, s, max_blocks);       \
     } while (0)
-    if (nch <= 8) IP_U(8, 1);
-    else if (nch <= 96) IP_U(32, 3);
-    else IP_U(64, 4);
+    // forced: 0 (8,1), 1 (32,3), 2 (64,4), 3 (16,2), 4 (16,6), 5 (8,12), 6 (8,2), 7 (8,4)
+    int sh = tu.shape;
+    if (sh < 0 || sh > 7) sh = (nch <= 8 || mean <= 112u) ? 0 : nch <= 96 ? 5 : 1;
+    switch (sh) {
+        case 0: IP_U(8, 1); break;
+        case 1: IP_U(32, 3); break;
+        case 2: IP_U(64, 4); break;
+        case 3: IP_U(16, 2); break;
+        case 4: IP_U(16, 6); break;
+        case 5: IP_U(8, 12); break;
+        case 6: IP_U(8, 2); break;
+        default: IP_U(8, 4); break;
+    }
 #undef IP_U
 }
 

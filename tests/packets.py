@@ -48,6 +48,8 @@ def build_batch(rng, n, slot=32768, malformed=False, odd_offsets=False, max_payl
             p = ip_packet(rng, pl, proto=17)
         elif kind == 7:
             p = ip_packet(rng, pl, ihl=4)
+        elif kind == 8:
+            p = ip_packet(rng, pl, ihl=15)          # valid, longest IP options (check at byte 76)
         elif kind == 9:
             p = ip_packet(rng, pl, ihl=7)           # valid, with IP options
         elif kind == 10:

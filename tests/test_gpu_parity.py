@@ -481,3 +481,88 @@ def test_ipv4_region_bounds(dev):
     tcp_amd.ipv4_batch(dreg, to_dev(off.view(np.int64), dev), off.size, 32768, tcp_amd.IPV4_FILL, out, st)
     assert np.array_equal(st.cpu().numpy(), want_st)
     assert np.array_equal(u16(out)[:-3], want_out[:-3])
+
+
+@pytest.mark.parametrize("shape", range(8))
+def test_ipv4_forced_shapes(dev, shape):
+    """Every wire lane-group shape (tcpcsum.h: wire 0..7) and tile depth is exact, incl. IHL 5..15,
+    odd offsets and malformed packets; the header fields come from the group's chunk registers."""
+    import tcp_amd
+    from tests.packets import build_batch
+    rng = np.random.default_rng(900 + shape)
+    region, off, _ = build_batch(rng, 700, malformed=True, odd_offsets=True)
+    for mode in (tcp_amd.IPV4_FILL | tcp_amd.IPV4_IPHDR, tcp_amd.IPV4_VERIFY):
+        ref = region.copy()
+        want_out, want_st = oracle.ipv4_batch(ref, off, 32768, mode)
+        for un in (1, 2, 4):
+            for mb in (0, 3):
+                tcp_amd.set_tuning(mb, un, shape, 0)
+                try:
+                    dreg = to_dev(region, dev)
+                    out = torch.empty(off.size, dtype=torch.int16, device=dev)
+                    st = torch.empty(off.size, dtype=torch.uint8, device=dev)
+                    tcp_amd.ipv4_batch(dreg, to_dev(off.view(np.int64), dev), off.size, 32768, mode, out, st)
+                finally:
+                    tcp_amd.set_tuning(0, 0, -1, 0)
+                assert np.array_equal(st.cpu().numpy(), want_st), (mode, un, mb)
+                assert np.array_equal(u16(out), want_out), (mode, un, mb)
+                assert np.array_equal(dreg.cpu().numpy(), ref), (mode, un, mb)
+        region = ref   # VERIFY runs over the filled packets
+
+
+@pytest.mark.parametrize("shape", range(7))
+def test_desc_forced_shapes(dev, shape):
+    """Every ragged lane-group shape (tcpcsum.h: ragged 0..6) and tile depth is exact on lengths
+    0..9000 at arbitrary offsets."""
+    import tcp_amd
+    rng = np.random.default_rng(700 + shape)
+    size = 2 << 20
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    n = 2500
+    lens = rng.choice(np.array([0, 1, 2, 3, 15, 16, 17, 64, 576, 1500, 9000], np.uint32), n)
+    off = np.array([rng.integers(0, size - l) for l in lens], np.uint64)
+    ss = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    want = oracle.batch_desc(host, off, lens, ss)
+    d = to_dev(host, dev)
+    dd = to_dev(_desc(off, lens, ss), dev)
+    for un in (1, 2, 4):
+        for mb in (0, 5):
+            tcp_amd.set_tuning(mb, un, shape, 0)
+            try:
+                got = u16(tcp_amd.batch_desc(d, dd, n, 9000))
+            finally:
+                tcp_amd.set_tuning(0, 0, -1, 0)
+            assert np.array_equal(got, want), (un, mb)
+
+
+@pytest.mark.parametrize("shape", [-1, 1, 3])
+def test_ipv4_span_hint_mispredicted(dev, shape):
+    """The next packet's offset only bounds the speculative span: shuffled offsets (gaps unrelated
+    to lengths, negative gaps) and extra offsets inside packets (gap < tot_len: fix-up loads) are
+    still exact."""
+    import tcp_amd
+    from tests.packets import build_batch
+    rng = np.random.default_rng(1234)
+    region, off, _ = build_batch(rng, 600, malformed=True, odd_offsets=True)
+    perm = rng.permutation(off.size)
+    inside = off[rng.integers(0, off.size, 200)] + rng.integers(1, 90, 200).astype(np.uint64)
+    cases = {"shuffled": (off[perm], (tcp_amd.IPV4_FILL, tcp_amd.IPV4_VERIFY)),
+             "interleaved": (np.insert(off, rng.integers(0, off.size, 200), inside), (tcp_amd.IPV4_VERIFY,))}
+    for name, (offs, modes) in cases.items():
+        offs = np.ascontiguousarray(offs, np.uint64)
+        reg = region.copy()
+        for mode in modes:
+            ref = reg.copy()
+            want_out, want_st = oracle.ipv4_batch(ref, offs, 32768, mode)
+            tcp_amd.set_tuning(0, 0, shape, 0)
+            try:
+                dreg = to_dev(reg, dev)
+                out = torch.empty(offs.size, dtype=torch.int16, device=dev)
+                st = torch.empty(offs.size, dtype=torch.uint8, device=dev)
+                tcp_amd.ipv4_batch(dreg, to_dev(offs.view(np.int64), dev), offs.size, 32768, mode, out, st)
+            finally:
+                tcp_amd.set_tuning(0, 0, -1, 0)
+            assert np.array_equal(st.cpu().numpy(), want_st), name
+            assert np.array_equal(u16(out), want_out), name
+            assert np.array_equal(dreg.cpu().numpy(), ref), name
+            reg = ref

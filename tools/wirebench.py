@@ -52,10 +52,13 @@ def main():
             order = np.argsort(lens, kind="stable")
             d2 = desc[order]
             ddesc = torch.from_numpy(d2.view(np.uint8)).to(dev)
-        for un in ((1, 2, 4) if "--sweep" in sys.argv else (0,)):
-            tcp_amd.set_tuning(0, un, -1, 0)
+        grid = ([(mb, un, sh) for sh in (-1, 2, 3) for mb in (2048, 8192) for un in (1, 2)]
+                if "--sweep" in sys.argv else [(0, 0, -1)])
+        for mb, un, sh in grid:
+            tcp_amd.set_tuning(mb, un, sh, 0)
             t = timeit(lambda: tcp_amd.batch_desc(data, ddesc, n, 1500, out))
-            print(json.dumps({"measure": "desc_imix_1M", "sorted_by_len": sorted_, "unroll": un,
+            print(json.dumps({"measure": "desc_imix_1M", "sorted_by_len": sorted_, "max_blocks": mb,
+                              "unroll": un, "shape": sh,
                               "ms": round(t * 1e3, 4), "GB/s": round(int(lens.sum()) / t / 1e9, 1),
                               "Mseg/s": round(n / t / 1e6, 1)}), flush=True)
         tcp_amd.set_tuning(0, 0, -1, 0)
@@ -73,16 +76,93 @@ def main():
     offs = torch.from_numpy((np.arange(n, dtype=np.uint64) * 1536).view(np.int64)).to(dev)
     stat = torch.empty(n, dtype=torch.uint8, device=dev)
     for name, mode in (("FILL", tcp_amd.IPV4_FILL), ("VERIFY", tcp_amd.IPV4_VERIFY)):
-        for mb, un in (((1024, 1), (1024, 2), (2048, 2), (4096, 2), (2048, 4), (8192, 1)) if "--sweep" in sys.argv
-                       else ((0, 0),)):
-            tcp_amd.set_tuning(mb, un, -1, 0)
+        grid = ([(mb, un, sh) for sh in (-1, 3, 4) for mb in (2048, 8192) for un in (1, 2)]
+                if "--sweep" in sys.argv else [(0, 0, -1)])
+        for mb, un, sh in grid:
+            tcp_amd.set_tuning(mb, un, sh, 0)
             t = timeit(lambda: tcp_amd.ipv4_batch(data, offs, n, 1536, mode, out, stat))
-            print(json.dumps({"measure": "ipv4_1Mx1500", "mode": name, "max_blocks": mb, "unroll": un,
+            print(json.dumps({"measure": "ipv4_1Mx1500", "mode": name, "max_blocks": mb, "unroll": un, "shape": sh,
                               "ms": round(t * 1e3, 4), "GB/s_tcp_bytes": round(n * 1480 / t / 1e9, 1),
                               "Mpkt/s": round(n / t / 1e6, 1)}), flush=True)
         tcp_amd.set_tuning(0, 0, -1, 0)
     ok = bool((out == 0).all().item()) and bool((stat == 0).all().item())
     print(json.dumps({"measure": "ipv4_verify_all_zero", "ok": ok}))
+
+    # packed small packets (64-B TCP segments back to back, cap 1536): the next
+    # offset bounds each packet's speculative span
+    np_ = 1 << 22
+    plen = 84   # IP 20 + TCP 24 + 40 payload
+    segs = np.zeros(np_, tcp_amd.TXSEG_DTYPE)
+    segs["payload_off"] = 0
+    segs["out_off"] = np.arange(np_, dtype=np.uint64) * plen
+    segs["saddr_be"], segs["daddr_be"] = 0x0100007F, np.arange(np_, dtype=np.uint32)
+    segs["sport"], segs["dport"], segs["len"], segs["flags"] = 4000, 45001, 40, 1 | 16
+    small = torch.empty(np_ * plen, dtype=torch.uint8, device=dev)
+    tcp_amd.tx_build(payload, torch.from_numpy(segs.view(np.uint8)).to(dev), np_, 40, small, 0, None)
+    soffs = torch.from_numpy((np.arange(np_, dtype=np.uint64) * plen).view(np.int64)).to(dev)
+    sout = torch.empty(np_, dtype=torch.int16, device=dev)
+    sst = torch.empty(np_, dtype=torch.uint8, device=dev)
+    for sh in ((-1, 0, 6, 7, 5) if "--sweep" in sys.argv else (-1,)):
+        tcp_amd.set_tuning(0, 0, sh, 0)
+        t = timeit(lambda: tcp_amd.ipv4_batch(small, soffs, np_, 1536, tcp_amd.IPV4_VERIFY, sout, sst))
+        ok = bool((sout == 0).all().item()) and bool((sst == 0).all().item())
+        print(json.dumps({"measure": "ipv4_4Mx84_packed_verify", "shape": sh, "ms": round(t * 1e3, 4),
+                          "GB/s_packet_bytes": round(np_ * plen / t / 1e9, 1), "Mpkt/s": round(np_ / t / 1e6, 1),
+                          "ok": ok}), flush=True)
+    tcp_amd.set_tuning(0, 0, -1, 0)
+    del small
+
+    # packed IMIX (7:4:1 of 64, 576, 1500-byte TCP segments), back to back
+    ni = 1 << 20
+    tl = rng.choice(np.array([64, 576, 1500], np.uint32), ni, p=[7 / 12, 4 / 12, 1 / 12])
+    plens = (tl + 20).astype(np.uint64)            # IP 20 + TCP (24-byte header + payload)
+    ioff = np.concatenate([[0], np.cumsum(plens)[:-1]]).astype(np.uint64)
+    segs = np.zeros(ni, tcp_amd.TXSEG_DTYPE)
+    segs["payload_off"] = 0
+    segs["out_off"] = ioff
+    segs["saddr_be"], segs["daddr_be"] = 0x0100007F, np.arange(ni, dtype=np.uint32)
+    segs["sport"], segs["dport"], segs["len"], segs["flags"] = 4000, 45001, tl - 24, 1 | 16
+    ireg = torch.empty(int(plens.sum()), dtype=torch.uint8, device=dev)
+    tcp_amd.tx_build(payload, torch.from_numpy(segs.view(np.uint8)).to(dev), ni, 1500, ireg, 0, None)
+    ioffs = torch.from_numpy(ioff.view(np.int64)).to(dev)
+    iout = torch.empty(ni, dtype=torch.int16, device=dev)
+    ist = torch.empty(ni, dtype=torch.uint8, device=dev)
+    for sh in ((-1, 0, 6, 7, 5, 4) if "--sweep" in sys.argv else (-1,)):
+        for un in ((1, 2) if "--sweep" in sys.argv else (0,)):
+            tcp_amd.set_tuning(0, un, sh, 0)
+            t = timeit(lambda: tcp_amd.ipv4_batch(ireg, ioffs, ni, 1536, tcp_amd.IPV4_VERIFY, iout, ist))
+            ok = bool((iout == 0).all().item()) and bool((ist == 0).all().item())
+            print(json.dumps({"measure": "ipv4_1M_imix_packed_verify", "shape": sh, "unroll": un,
+                              "ms": round(t * 1e3, 4), "GB/s_tcp_bytes": round(int(tl.sum()) / t / 1e9, 1),
+                              "Mpkt/s": round(ni / t / 1e6, 1), "ok": ok}), flush=True)
+    tcp_amd.set_tuning(0, 0, -1, 0)
+    del ireg
+
+    # jumbo: 128K packets of 9000 B in 9216-B slots
+    nj, jl, js = 1 << 17, 8956, 9216
+    jpay = torch.empty(nj * jl, dtype=torch.uint8, device=dev)
+    tcp_amd.synth_fill(jpay, 7, nj * jl)
+    segs = np.zeros(nj, tcp_amd.TXSEG_DTYPE)
+    segs["payload_off"] = np.arange(nj, dtype=np.uint64) * jl
+    segs["out_off"] = np.arange(nj, dtype=np.uint64) * js
+    segs["saddr_be"], segs["daddr_be"] = 0x0100007F, np.arange(nj, dtype=np.uint32)
+    segs["sport"], segs["dport"], segs["len"], segs["flags"] = 4000, 45001, jl, 1 | 16
+    jreg = torch.empty(nj * js, dtype=torch.uint8, device=dev)
+    tcp_amd.tx_build(jpay, torch.from_numpy(segs.view(np.uint8)).to(dev), nj, jl, jreg, 0, None)
+    del jpay
+    joffs = torch.from_numpy((np.arange(nj, dtype=np.uint64) * js).view(np.int64)).to(dev)
+    jout = torch.empty(nj, dtype=torch.int16, device=dev)
+    jst = torch.empty(nj, dtype=torch.uint8, device=dev)
+    grid = ([(mb, un, sh) for sh in (-1, 1, 2, 4, 5) for mb in (2048, 8192) for un in (1, 2)]
+            if "--sweep" in sys.argv else [(0, 0, -1)])
+    for mb, un, sh in grid:
+        tcp_amd.set_tuning(mb, un, sh, 0)
+        t = timeit(lambda: tcp_amd.ipv4_batch(jreg, joffs, nj, js, tcp_amd.IPV4_VERIFY, jout, jst))
+        print(json.dumps({"measure": "ipv4_128Kx9000_verify", "max_blocks": mb, "unroll": un, "shape": sh,
+                          "ms": round(t * 1e3, 4), "GB/s_tcp_bytes": round(nj * 8980 / t / 1e9, 1)}), flush=True)
+    tcp_amd.set_tuning(0, 0, -1, 0)
+    ok = bool((jout == 0).all().item()) and bool((jst == 0).all().item())
+    print(json.dumps({"measure": "ipv4_jumbo_verify_all_zero", "ok": ok}))
 
 
 if __name__ == "__main__":
