@@ -22,6 +22,8 @@ from .api import (  # noqa: F401
     PKT_IPHDR_BAD,
     PKT_OK,
     PKT_SKIPPED,
+    TUNE_WIRE_CACHED,
+    TUNE_WIN16,
     TcpCsumError,
     HostContext,
     batch_desc,

@@ -152,6 +152,7 @@ def device_check() -> tuple[int, str]:
 
 PROBE_SLOTS = 8192
 TUNE_PIPE_ON, TUNE_PIPE_OFF, TUNE_NT_ON, TUNE_NT_OFF = 1, 2, 4, 8
+TUNE_WIRE_CACHED, TUNE_WIN16 = 32, 64   # wire kernel variants (tcpcsum.h)
 
 
 def set_tuning(max_blocks: int = 0, unroll: int = 0, shape: int = -1, flags: int = 0) -> None:

@@ -526,52 +526,87 @@ __device__ __forceinline__ uint32_t grp_dword(const u32x4 c0, int gbase, uint32_
     return (uint32_t)__shfl((int)mine, gbase + (int)(D >> 2), 64);
 }
 
-// The 4 packet bytes at window offset a (little-endian dword).
-__device__ __forceinline__ uint32_t grp_bytes4(const u32x4 c0, int gbase, uint32_t a) {
-    const uint32_t lo = grp_dword(c0, gbase, a >> 2), hi = grp_dword(c0, gbase, (a >> 2) + 1u);
+// Dword D out of the group's first two rounds of chunks (lane gbase + k holds
+// chunk k in c0 and chunk G + k in c1): windows of 2*G chunks for G = 8.
+template <int G>
+__device__ __forceinline__ uint32_t grp_dword2(const u32x4 c0, const u32x4 c1, int gbase, uint32_t D) {
+    const uint32_t j = D >> 2;
+    const bool hi = j >= (uint32_t)G;
+    const u32x4 c = hi ? c1 : c0;
+    const uint32_t q = D & 3u;
+    const uint32_t mine = q == 0 ? c.x : q == 1 ? c.y : q == 2 ? c.z : c.w;
+    return (uint32_t)__shfl((int)mine, gbase + (int)(hi ? j - (uint32_t)G : j), 64);
+}
+
+// The 4 packet bytes at window offset a (little-endian dword), out of the
+// group's first round (C == 1 or G >= 16) or first two rounds of chunks.
+template <int G, int C>
+__device__ __forceinline__ uint32_t grp_bytes4(const u32x4 (&v)[C], int gbase, uint32_t a) {
+    uint32_t lo, hi;
+    if constexpr (C == 1 || G >= 16) {
+        lo = grp_dword(v[0], gbase, a >> 2);
+        hi = grp_dword(v[0], gbase, (a >> 2) + 1u);
+    } else {
+        lo = grp_dword2<G>(v[0], v[1], gbase, a >> 2);
+        hi = grp_dword2<G>(v[0], v[1], gbase, (a >> 2) + 1u);
+    }
     return __builtin_amdgcn_alignbyte(hi, lo, a & 3u);
 }
 
-template <int G, int C, int U>
+// One packet's results, committed by the group's lane 0.
+struct IpDone {
+    uint8_t* ip;
+    uint64_t i;
+    uint32_t th;
+    uint16_t c, ic;
+    uint8_t st;
+    bool w;     // a packet of the batch: out / status are written
+    bool fill;  // checks are stored in place
+};
+
+template <int G, int C, int U, bool NT>
 __global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const uint64_t* __restrict__ off,
                                               uint64_t n, uint32_t cap, uint64_t limit, int mode,
                                               uint16_t* __restrict__ out, uint8_t* __restrict__ status,
-                                              uint16_t* __restrict__ ipout) {
-    static_assert(G >= 8, "the header and TCP check are read from the group's first 6 chunks");
+                                              uint16_t* __restrict__ ipout, uint32_t amask) {
+    // amask: window alignment - 1. Lane gl of a group loads window chunks k*G+gl,
+    // so with 128-B windows every group load instruction covers whole 128-B
+    // lines however the packet is aligned. Header fields lie in window bytes
+    // [0, amask + 81): 16-B windows need G >= 8, 128-B windows G >= 16 or C >= 2.
+    static_assert(G >= 8, "the header and TCP check are read from the group's first chunks");
+    if constexpr (C == 1 && G < 16) amask = 15u;
     constexpr int GPW = 64 / G;
     constexpr int SPT = GPW * U;
     const int lane = threadIdx.x & 63;
     const int q = lane / G, gl = lane % G;
+    const int gbase = lane - gl;
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
     const uint64_t ntiles = (n + SPT - 1) / SPT;
     const bool verify = (mode & TCPCSUM_IPV4_VERIFY) != 0;
     const bool iphdr = (mode & TCPCSUM_IPV4_IPHDR) != 0;
     uint64_t t = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
     // offsets of packet i and of packet i + 1 (0 past the end: no bound)
-    auto load_off = [&](uint64_t tile, uint64_t (&dst)[U], uint64_t (&nxt)[U]) {
+    uint64_t on[U], on1[U];
+    auto load_off = [&](uint64_t tile) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint64_t i = tile * SPT + (uint64_t)(u * GPW + q);
-            dst[u] = *reinterpret_cast<const uint64_t*>(zsel(i < n, reinterpret_cast<const uint8_t*>(off + i)));
-            nxt[u] = *reinterpret_cast<const uint64_t*>(zsel(i + 1 < n, reinterpret_cast<const uint8_t*>(off + i + 1)));
+            on[u] = *reinterpret_cast<const uint64_t*>(zsel(i < n, reinterpret_cast<const uint8_t*>(off + i)));
+            on1[u] = *reinterpret_cast<const uint64_t*>(zsel(i + 1 < n, reinterpret_cast<const uint8_t*>(off + i + 1)));
         }
     };
-    uint64_t on[U], on1[U];
-    load_off(t, on, on1);
-    for (; t < ntiles; t += nwaves) {
-        IpPkt p[U];
+    IpPkt p[U];
+    u32x4 v[U][C];
+    // the tile's speculative packet loads (offsets already in on / on1)
+    auto issue = [&](uint64_t tile) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint64_t i = t * SPT + (uint64_t)(u * GPW + q);
+            const uint64_t i = tile * SPT + (uint64_t)(u * GPW + q);
             p[u].live = i < n;
             p[u].o = on[u];
-        }
-        u32x4 v[U][C];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
             uint8_t* ip = pkts + p[u].o;
             p[u].ip = ip;
-            p[u].m = (uint32_t)((uintptr_t)ip & 15u);
+            p[u].m = (uint32_t)((uintptr_t)ip & amask);
             p[u].hdr = p[u].live && p[u].o < limit && limit - p[u].o >= 20u;
             const bool live = p[u].hdr;   // a dead slot reads zeros: ver 0, skipped
             // speculative payload chunks: the aligned hull of [ip, ip + span); at
@@ -587,109 +622,120 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const 
 #pragma unroll
             for (int k = 0; k < C; ++k) {
                 const uint32_t idx = (uint32_t)(k * G + gl);
-                v[u][k] = ld16(zsel(live && idx < nch, a0 + (uint64_t)idx * 16u));
+                // chunks wholly before the packet (128-B windows) are not read
+                v[u][k] = ldq<NT>(zsel(live && idx < nch && idx * 16u + 16u > p[u].m, a0 + (uint64_t)idx * 16u));
             }
         }
-        // the next tile's offsets, in flight while this tile is summed
-        load_off(t + nwaves, on, on1);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint64_t i = t * SPT + (uint64_t)(u * GPW + q);
-            if (!p[u].live) continue;   // group-uniform
-            uint8_t* ip = p[u].ip;
-            const int gbase = lane - gl;
-            const uint32_t m = p[u].m;
-            const uint32_t h0 = grp_bytes4(v[u][0], gbase, m);        // ver/ihl, tos, tot_len
-            const uint32_t h8 = grp_bytes4(v[u][0], gbase, m + 8u);   // ttl, protocol, check
-            const uint32_t ver = (h0 >> 4) & 15u, ihl = h0 & 15u;
-            const uint32_t tot = ((h0 >> 8) & 0xff00u) | (h0 >> 24);
-            const uint32_t proto = (h8 >> 8) & 0xffu;
-            const bool ok = p[u].hdr && ver == 4u && proto == 6u && ihl >= 5u && tot >= ihl * 4u + 20u && tot <= cap &&
-                            p[u].o + tot <= limit;
-            if (!ok) {   // group-uniform
-                if (gl == 0) {
-                    if (out) out[i] = 0;
-                    if (status) status[i] = TCPCSUM_PKT_SKIPPED;
-                }
-                continue;
-            }
-            const uint32_t th = ihl * 4u;   // TCP start, packet-relative (even)
-            const bool odd = (m & 1u) != 0;
-            const uint32_t sa = grp_bytes4(v[u][0], gbase, m + 12u), da = grp_bytes4(v[u][0], gbase, m + 16u);
-            const uint32_t check_word = grp_bytes4(v[u][0], gbase, m + th + 16u) & 0xffffu;
-            const uint32_t nch_tot = (m + tot + 15u) >> 4;
-            if (nch_tot > p[u].spec) {   // longer than its span hint (group-uniform, rare)
-#pragma unroll
-                for (int k = 0; k < C; ++k) {
-                    const uint32_t idx = (uint32_t)(k * G + gl);
-                    if (idx >= p[u].spec && idx < nch_tot) v[u][k] = ld16(ip - m + (uint64_t)idx * 16u);
-                }
-            }
-            uint32_t w = 0, o = 0, wi = 0, oi = 0;
+    };
+    auto process = [&](int u, uint64_t i) -> IpDone {
+        IpDone d;
+        d.w = false;
+        d.fill = false;
+        d.i = i;
+        d.ip = p[u].ip;
+        d.th = 0;
+        d.c = 0;
+        d.ic = 0;
+        d.st = TCPCSUM_PKT_SKIPPED;
+        if (!p[u].live) return d;   // group-uniform
+        d.w = true;
+        uint8_t* ip = p[u].ip;
+        const uint32_t m = p[u].m;
+        const uint32_t h0 = grp_bytes4<G, C>(v[u], gbase, m);        // ver/ihl, tos, tot_len
+        const uint32_t h8 = grp_bytes4<G, C>(v[u], gbase, m + 8u);   // ttl, protocol, check
+        const uint32_t ver = (h0 >> 4) & 15u, ihl = h0 & 15u;
+        const uint32_t tot = ((h0 >> 8) & 0xff00u) | (h0 >> 24);
+        const uint32_t proto = (h8 >> 8) & 0xffu;
+        const bool ok = p[u].hdr && ver == 4u && proto == 6u && ihl >= 5u && tot >= ihl * 4u + 20u && tot <= cap &&
+                        p[u].o + tot <= limit;
+        if (!ok) return d;   // group-uniform: skipped, out = 0
+        const uint32_t th = ihl * 4u;   // TCP start, packet-relative (even)
+        const bool odd = (m & 1u) != 0;
+        const uint32_t sa = grp_bytes4<G, C>(v[u], gbase, m + 12u), da = grp_bytes4<G, C>(v[u], gbase, m + 16u);
+        const uint32_t check_word = grp_bytes4<G, C>(v[u], gbase, m + th + 16u) & 0xffffu;
+        const uint32_t nch_tot = (m + tot + 15u) >> 4;
+        if (nch_tot > p[u].spec) {   // longer than its span hint (group-uniform, rare)
 #pragma unroll
             for (int k = 0; k < C; ++k) {
-                const int32_t pos = (int32_t)((uint32_t)(k * G + gl) * 16u) - (int32_t)m;   // chunk start, packet-relative
-                const u32x4 x = v[u][k];
-                if (pos >= (int32_t)th && pos + 16 <= (int32_t)tot) {
-                    w = sad16(x.x, w); w = sad16(x.y, w); w = sad16(x.z, w); w = sad16(x.w, w);
-                    if (odd) {
-                        o = sad8(x.x & 0xff00ff00u, o); o = sad8(x.y & 0xff00ff00u, o);
-                        o = sad8(x.z & 0xff00ff00u, o); o = sad8(x.w & 0xff00ff00u, o);
-                    }
-                } else if (pos + 16 > (int32_t)th && pos < (int32_t)tot) {
-                    chunk_wo_bytes(x, (int64_t)pos - th, (int64_t)(tot - th), odd, w, o);
-                }
-                if (iphdr && pos < (int32_t)th) chunk_wo_bytes(x, (int64_t)pos, (int64_t)th, odd, wi, oi);
-            }
-            uint64_t W = w, O = o;
-            // packets longer than the group's first G*C chunks
-            for (uint32_t r = (uint32_t)(G * C); r < nch_tot; r += (uint32_t)(G * C)) {
-                uint32_t w2 = 0, o2 = 0;
-#pragma unroll
-                for (int k = 0; k < C; ++k) {
-                    const uint32_t idx = r + (uint32_t)(k * G + gl);
-                    if (idx >= nch_tot) continue;
-                    const u32x4 x = ld16(ip - m + (uint64_t)idx * 16u);
-                    chunk_wo_bytes(x, (int64_t)idx * 16 - m - th, (int64_t)(tot - th), odd, w2, o2);
-                }
-                W += w2;
-                O += o2;
-            }
-            W = group_sum64<G>(W);
-            O = odd ? group_sum64<G>(O) : 0;
-            const uint32_t tcp_len = tot - th;
-            const uint32_t len_be = ((tcp_len & 0xffu) << 8) | ((tcp_len >> 8) & 0xffu);   // htons
-            // context.c:104-119 closed form: six native u16 words of the pseudo header.
-            const uint64_t ps = (sa & 0xffffu) + (sa >> 16) + (da & 0xffffu) + (da >> 16) + 0x0600u + len_be;
-            uint8_t* tcp = ip + th;
-            uint64_t S = combine(ps, W, O, odd);
-            // FILL: the reference sums with check == 0 (context.c:182); TCP+16 is an
-            // even relative offset, so its native word contributes exactly check_word.
-            if (!verify) S -= check_word;
-            const uint16_t c = fold_ref(S);
-            uint32_t st = TCPCSUM_PKT_OK;
-            if (verify && c != 0 && check_word == (uint32_t)(uint16_t)~fold_ref(ps)) st |= TCPCSUM_PKT_CSUM_PARTIAL;
-            if (iphdr) {
-                // IPv4 header checksum = csum_continue(0, ip, ihl*4) with check (IP+10)
-                // as zero — the reference's commented-out context.c:179, over ihl*4 bytes.
-                const uint64_t WI = group_sum64<G>((uint64_t)wi);
-                const uint64_t OI = odd ? group_sum64<G>((uint64_t)oi) : 0;
-                uint64_t IS = combine(0, WI, OI, odd);
-                if (!verify) IS -= h8 >> 16;
-                const uint16_t ic = fold_ref(IS);
-                if (ipout && gl == 0) ipout[i] = ic;
-                if (!verify) {
-                    if (gl == 0) store_u16(ip + 10, ic);
-                } else if (ic != 0) {
-                    st |= TCPCSUM_PKT_IPHDR_BAD;
-                }
-            }
-            if (gl == 0) {
-                if (!verify) store_u16(tcp + 16, c);   // native u16 store, as context.c:208
-                if (out) out[i] = c;
-                if (status) status[i] = (uint8_t)st;
+                const uint32_t idx = (uint32_t)(k * G + gl);
+                if (idx >= p[u].spec && idx < nch_tot) v[u][k] = ldq<NT>(ip - m + (uint64_t)idx * 16u);
             }
         }
+        uint32_t w = 0, o = 0, wi = 0, oi = 0;
+#pragma unroll
+        for (int k = 0; k < C; ++k) {
+            const int32_t pos = (int32_t)((uint32_t)(k * G + gl) * 16u) - (int32_t)m;   // chunk start, packet-relative
+            const u32x4 x = v[u][k];
+            if (pos >= (int32_t)th && pos + 16 <= (int32_t)tot) {
+                w = sad16(x.x, w); w = sad16(x.y, w); w = sad16(x.z, w); w = sad16(x.w, w);
+                if (odd) {
+                    o = sad8(x.x & 0xff00ff00u, o); o = sad8(x.y & 0xff00ff00u, o);
+                    o = sad8(x.z & 0xff00ff00u, o); o = sad8(x.w & 0xff00ff00u, o);
+                }
+            } else if (pos + 16 > (int32_t)th && pos < (int32_t)tot) {
+                chunk_wo_bytes(x, (int64_t)pos - th, (int64_t)(tot - th), odd, w, o);
+            }
+            if (iphdr && pos < (int32_t)th) chunk_wo_bytes(x, (int64_t)pos, (int64_t)th, odd, wi, oi);
+        }
+        uint64_t W = w, O = o;
+        // packets longer than the group's first G*C chunks
+        for (uint32_t r = (uint32_t)(G * C); r < nch_tot; r += (uint32_t)(G * C)) {
+            uint32_t w2 = 0, o2 = 0;
+#pragma unroll
+            for (int k = 0; k < C; ++k) {
+                const uint32_t idx = r + (uint32_t)(k * G + gl);
+                if (idx >= nch_tot) continue;
+                const u32x4 x = ldq<NT>(ip - m + (uint64_t)idx * 16u);
+                chunk_wo_bytes(x, (int64_t)idx * 16 - m - th, (int64_t)(tot - th), odd, w2, o2);
+            }
+            W += w2;
+            O += o2;
+        }
+        W = group_sum64<G>(W);
+        O = odd ? group_sum64<G>(O) : 0;
+        const uint32_t tcp_len = tot - th;
+        const uint32_t len_be = ((tcp_len & 0xffu) << 8) | ((tcp_len >> 8) & 0xffu);   // htons
+        // context.c:104-119 closed form: six native u16 words of the pseudo header.
+        const uint64_t ps = (sa & 0xffffu) + (sa >> 16) + (da & 0xffffu) + (da >> 16) + 0x0600u + len_be;
+        uint64_t S = combine(ps, W, O, odd);
+        // FILL: the reference sums with check == 0 (context.c:182); TCP+16 is an
+        // even relative offset, so its native word contributes exactly check_word.
+        if (!verify) S -= check_word;
+        d.c = fold_ref(S);
+        d.th = th;
+        d.fill = !verify;
+        uint32_t st = TCPCSUM_PKT_OK;
+        if (verify && d.c != 0 && check_word == (uint32_t)(uint16_t)~fold_ref(ps)) st |= TCPCSUM_PKT_CSUM_PARTIAL;
+        if (iphdr) {
+            // IPv4 header checksum = csum_continue(0, ip, ihl*4) with check (IP+10)
+            // as zero — the reference's commented-out context.c:179, over ihl*4 bytes.
+            const uint64_t WI = group_sum64<G>((uint64_t)wi);
+            const uint64_t OI = odd ? group_sum64<G>((uint64_t)oi) : 0;
+            uint64_t IS = combine(0, WI, OI, odd);
+            if (!verify) IS -= h8 >> 16;
+            d.ic = fold_ref(IS);
+            if (verify && d.ic != 0) st |= TCPCSUM_PKT_IPHDR_BAD;
+        }
+        d.st = (uint8_t)st;
+        return d;
+    };
+    auto commit = [&](const IpDone& d) {
+        if (!d.w || gl != 0) return;
+        if (d.fill) {
+            store_u16(d.ip + d.th + 16, d.c);   // native u16 store, as context.c:208
+            if (iphdr) store_u16(d.ip + 10, d.ic);
+        }
+        if (iphdr && ipout && d.st != TCPCSUM_PKT_SKIPPED) ipout[d.i] = d.ic;
+        if (out) out[d.i] = d.c;
+        if (status) status[d.i] = d.st;
+    };
+    load_off(t);
+    for (; t < ntiles; t += nwaves) {
+        issue(t);
+        // the next tile's offsets, in flight while this tile is summed
+        load_off(t + nwaves);
+#pragma unroll
+        for (int u = 0; u < U; ++u) commit(process(u, t * SPT + (uint64_t)(u * GPW + q)));
     }
 }
 
@@ -1234,25 +1280,36 @@ void launch_desc(const uint8_t* base, const tcpcsum_desc_t* d, uint64_t n, uint3
 
 template <int G, int C, int U>
 static void launch_ipv4_t(uint8_t* pkts, const uint64_t* off, uint64_t n, uint32_t cap, uint64_t limit, int mode,
-                          uint16_t* out, uint8_t* status, uint16_t* ipout, hipStream_t s, int max_blocks) {
+                          uint16_t* out, uint8_t* status, uint16_t* ipout, hipStream_t s, int max_blocks, bool nt,
+                          uint32_t amask) {
     constexpr int SPT = (64 / G) * U;
-    hipLaunchKernelGGL((k_ipv4<G, C, U>), dim3(grid_for((n + SPT - 1) / SPT, max_blocks)), dim3(256), 0, s, pkts,
-                       off, n, cap, limit, mode, out, status, ipout);
+    const dim3 grid(grid_for((n + SPT - 1) / SPT, max_blocks));
+    if (nt)
+        hipLaunchKernelGGL((k_ipv4<G, C, U, true>), grid, dim3(256), 0, s, pkts, off, n, cap, limit, mode, out,
+                           status, ipout, amask);
+    else
+        hipLaunchKernelGGL((k_ipv4<G, C, U, false>), grid, dim3(256), 0, s, pkts, off, n, cap, limit, mode, out,
+                           status, ipout, amask);
 }
 
 void launch_ipv4(uint8_t* pkts, const uint64_t* off, uint64_t n, uint32_t cap, uint64_t limit, int mode,
                  uint16_t* out, uint8_t* status, uint16_t* ipout, hipStream_t s, const Tuning& tu) {
     const int max_blocks = tu.max_blocks > 0 ? tu.max_blocks : 8192;
     const int unroll = tu.unroll ? tu.unroll : 1;
+    const bool nt = (tu.flags & TCPCSUM_TUNE_WIRE_CACHED) == 0;
+    const uint32_t amask = (tu.flags & TCPCSUM_TUNE_WIN16) ? 15u : 127u;
     // shape by the cap and by the mean packet footprint limit / n (packed small
     // packets: one chunk per lane; MTU slots: one round of 96 chunks per packet)
     const uint64_t nch = ((uint64_t)cap + 15u) >> 4;   // an odd start takes one extra round
     const uint64_t mean = n ? limit / n : 0;
-#define IP_U(G, C)                                                                                          \
-    do {                                                                                                    \
-        if (unroll <= 1) launch_ipv4_t<G, C, 1>(pkts, off, n, cap, limit, mode, out, status, ipout, s, max_blocks); \
-        else if (unroll == 2) launch_ipv4_t<G, C, 2>(pkts, off, n, cap, limit, mode, out, status, ipout, s, max_blocks); \
-        else launch_ipv4_t<G, C, 4>(pkts, off, n, cap, limit, mode, out, status, ipout, s, max_blocks);       \
+#define IP_U(G, C)                                                                                                 \
+    do {                                                                                                           \
+        if (unroll <= 1)                                                                                           \
+            launch_ipv4_t<G, C, 1>(pkts, off, n, cap, limit, mode, out, status, ipout, s, max_blocks, nt, amask); \
+        else if (unroll == 2)                                                                                      \
+            launch_ipv4_t<G, C, 2>(pkts, off, n, cap, limit, mode, out, status, ipout, s, max_blocks, nt, amask); \
+        else                                                                                                       \
+            launch_ipv4_t<G, C, 4>(pkts, off, n, cap, limit, mode, out, status, ipout, s, max_blocks, nt, amask); \
     } while (0)
     // forced: 0 (8,1), 1 (32,3), 2 (64,4), 3 (16,2), 4 (16,6), 5 (8,12), 6 (8,2), 7 (8,4)
     int sh = tu.shape;

@@ -495,8 +495,8 @@ def test_ipv4_forced_shapes(dev, shape):
         ref = region.copy()
         want_out, want_st = oracle.ipv4_batch(ref, off, 32768, mode)
         for un in (1, 2, 4):
-            for mb in (0, 3):
-                tcp_amd.set_tuning(mb, un, shape, 0)
+            for mb, fl in ((0, 0), (3, 0), (0, tcp_amd.TUNE_WIN16), (3, tcp_amd.TUNE_WIN16 | tcp_amd.TUNE_WIRE_CACHED)):
+                tcp_amd.set_tuning(mb, un, shape, fl)
                 try:
                     dreg = to_dev(region, dev)
                     out = torch.empty(off.size, dtype=torch.int16, device=dev)
@@ -504,9 +504,9 @@ def test_ipv4_forced_shapes(dev, shape):
                     tcp_amd.ipv4_batch(dreg, to_dev(off.view(np.int64), dev), off.size, 32768, mode, out, st)
                 finally:
                     tcp_amd.set_tuning(0, 0, -1, 0)
-                assert np.array_equal(st.cpu().numpy(), want_st), (mode, un, mb)
-                assert np.array_equal(u16(out), want_out), (mode, un, mb)
-                assert np.array_equal(dreg.cpu().numpy(), ref), (mode, un, mb)
+                assert np.array_equal(st.cpu().numpy(), want_st), (mode, un, mb, fl)
+                assert np.array_equal(u16(out), want_out), (mode, un, mb, fl)
+                assert np.array_equal(dreg.cpu().numpy(), ref), (mode, un, mb, fl)
         region = ref   # VERIFY runs over the filled packets
 
 
@@ -566,3 +566,42 @@ def test_ipv4_span_hint_mispredicted(dev, shape):
             assert np.array_equal(u16(out), want_out), name
             assert np.array_equal(dreg.cpu().numpy(), ref), name
             reg = ref
+
+
+@pytest.mark.parametrize("flags", [0, 32, 64, 96])
+@pytest.mark.parametrize("layout", ["odd", "slot64", "slot16", "packed"])
+def test_ipv4_window_and_store_variants(dev, flags, layout):
+    """Wire kernel variants (128-B or 16-B packet windows; non-temporal or default-policy loads)
+    are exact and FILL rewrites nothing but the checks, in every layout: odd packed
+    offsets, 64-B aligned slots, 16-B (not 64-B) aligned slots, packed tiny packets."""
+    import tcp_amd
+    from tests.packets import build_batch, ip_packet
+    rng = np.random.default_rng(4242 + flags)
+    if layout == "odd":
+        region, off, _ = build_batch(rng, 600, malformed=True, odd_offsets=True)
+    elif layout in ("slot64", "slot16"):
+        region, off, _ = build_batch(rng, 400, slot=1536, malformed=True)
+        if layout == "slot16":
+            region = np.concatenate([np.zeros(16, np.uint8), region])
+            off = off + np.uint64(16)
+    else:
+        pkts = [ip_packet(rng, int(rng.integers(0, 40))) for _ in range(900)]
+        off = np.cumsum([0] + [len(p) for p in pkts[:-1]]).astype(np.uint64)
+        region = np.zeros(int(off[-1]) + len(pkts[-1]), np.uint8)
+        for o, p in zip(off, pkts):
+            region[int(o):int(o) + len(p)] = np.frombuffer(p, np.uint8)
+    for mode in (tcp_amd.IPV4_FILL, tcp_amd.IPV4_FILL | tcp_amd.IPV4_IPHDR):
+        ref = region.copy()
+        want_out, want_st = oracle.ipv4_batch(ref, off, 1536 if layout != "odd" else 32768, mode)
+        tcp_amd.set_tuning(0, 0, -1, flags)
+        try:
+            dreg = to_dev(region, dev)
+            out = torch.empty(off.size, dtype=torch.int16, device=dev)
+            st = torch.empty(off.size, dtype=torch.uint8, device=dev)
+            tcp_amd.ipv4_batch(dreg, to_dev(off.view(np.int64), dev), off.size,
+                               1536 if layout != "odd" else 32768, mode, out, st)
+        finally:
+            tcp_amd.set_tuning(0, 0, -1, 0)
+        assert np.array_equal(st.cpu().numpy(), want_st), mode
+        assert np.array_equal(u16(out), want_out), mode
+        assert np.array_equal(dreg.cpu().numpy(), ref), mode
