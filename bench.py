@@ -138,6 +138,83 @@ def cpu_baseline(seg_len: int, seconds: float) -> dict:
     }
 
 
+def run_config(config: str, steps: int, warmup: int, rank: int, world: int, dist, device, rotate: int = 0):
+    """Generate this rank's shard of `config` in HBM, check rotation 0 against the reference's
+    digest, then time `steps` launches (after `warmup`) between barriers.
+    Returns (result dict, rank's buffers for the probe)."""
+    import numpy as np
+    import torch
+    import tcp_amd
+
+    per_gpu, L, desc = CONFIGS[config]
+    total = per_gpu * world
+    s0, cnt = shard_range(total, world, rank)
+    batch_bytes = cnt * L
+    # Small batches would be served from the 256 MiB Infinity Cache on repeat
+    # launches; rotate distinct batches so consecutive reads of the same bytes
+    # are >= 2 GiB apart (measured effect at 1.5 GB: < 1 %, DESIGN.md §5).
+    rot = max(1, math.ceil((2 << 30) / batch_bytes))
+    if rotate:
+        rot = rotate
+    stream = torch.cuda.current_stream()
+    bufs, sss = [], []
+    for r in range(rot):
+        data = torch.empty(batch_bytes, dtype=torch.uint8, device=device)
+        ss = torch.empty(cnt, dtype=torch.int32, device=device)
+        # rotation r holds the same segment indices with the stream bytes of a later block
+        tcp_amd.synth_fill(data, (s0 + r * total) * L, batch_bytes)
+        tcp_amd.synth_pseudo(ss, s0, cnt, L)
+        bufs.append(data)
+        sss.append(ss)
+    out = torch.empty(cnt, dtype=torch.int16, device=device)
+    torch.cuda.synchronize()
+
+    # Sanity (not a parity test — tests/ does that): rotation 0 of each shard is
+    # exactly the Appendix B batch whose digest the reference produced.
+    tcp_amd.batch_uniform(bufs[0], L, L, cnt, sss[0], out=out)
+    torch.cuda.synchronize()
+    res = out.cpu().numpy().view(np.uint16)
+    check = None
+    try:
+        gold = json.load(open(os.path.join(REPO, "tests", "golden", "reference_vectors.json")))["digests"]
+        key = {("1500", 1): "1Mx1500", ("64", 1): "1Mx64", ("64k", 1): "256Kx64KiB"}.get((config, world))
+        if config == "1500" and world == 8:
+            key = f"8Mx1500_shard{rank}"
+        elif config == "1500" and world > 1 and per_gpu == 1 << 20:
+            key = f"8Mx1500_shard{rank}" if rank < 8 else None
+        if key:
+            g = gold[key]
+            check = bool(int(res.astype(np.uint64).sum()) == g["sum"]
+                         and f"{int(np.bitwise_xor.reduce(res)):04x}" == g["xor"]
+                         and [f"{v:04x}" for v in res[:4]] == g["first4"] and f"{res[-1]:04x}" == g["last"])
+    except Exception:
+        check = None
+
+    if dist is not None:   # the check holds only if it holds on every rank
+        flag = 1.0 if check else (0.0 if check is False else -1.0)
+        fl = -max_over_ranks(-flag, dist, device)   # min over ranks
+        check = None if fl < 0 else bool(fl == 1.0)
+
+    k = [0]
+
+    def step():
+        r = k[0] % rot
+        k[0] += 1
+        tcp_amd.batch_uniform(bufs[r], L, L, cnt, sss[r], out=out)
+
+    # HIP events on the launch stream bracket the kernels of the timed region
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    wall = timed_region(step, steps, warmup, dist, torch.cuda.synchronize,
+                        on_start=lambda: ev0.record(stream), on_end=lambda: ev1.record(stream))
+    kernel_ms = ev0.elapsed_time(ev1) / steps
+    wall_max = max_over_ranks(wall, dist, device)
+    kernel_ms_max = max_over_ranks(kernel_ms, dist, device)
+    r = {"config": config, "desc": desc, "L": L, "cnt": cnt, "rot": rot, "batch_bytes": batch_bytes,
+         "check": check, "wall_max": wall_max, "kernel_ms": kernel_ms, "kernel_ms_max": kernel_ms_max}
+    return r, bufs, rot
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -146,6 +223,8 @@ def main(argv=None) -> int:
     ap.add_argument("--config", choices=sorted(CONFIGS), default="1500")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-other-configs", action="store_true",
+                    help="skip the other BASELINE configs (64 B, 64 KiB) reported beside the headline at N=1")
     ap.add_argument("--probe", action="store_true", help="also time the read-only stream probe")
     ap.add_argument("--max-blocks", type=int, default=0)
     ap.add_argument("--unroll", type=int, default=0)
@@ -184,70 +263,10 @@ def main(argv=None) -> int:
         raise SystemExit(f"bench.py: no usable gfx950 device ({rc}, '{arch}')")
     tcp_amd.set_tuning(args.max_blocks, args.unroll, args.shape, args.flags)
 
-    per_gpu, L, desc = CONFIGS[args.config]
-    total = per_gpu * world
-    s0, cnt = shard_range(total, world, rank)
-    batch_bytes = cnt * L
-    # Small batches would be served from the 256 MiB Infinity Cache on repeat
-    # launches; rotate distinct batches so consecutive reads of the same bytes
-    # are >= 2 GiB apart (measured effect at 1.5 GB: < 1 %).
-    rot = max(1, math.ceil((2 << 30) / batch_bytes))
-    if args.rotate:
-        rot = args.rotate
+    r, bufs, rot = run_config(args.config, args.steps, args.warmup, rank, world, dist, device, args.rotate)
+    L, cnt, batch_bytes, desc, check = r["L"], r["cnt"], r["batch_bytes"], r["desc"], r["check"]
+    wall_max, kernel_ms, kernel_ms_max = r["wall_max"], r["kernel_ms"], r["kernel_ms_max"]
     stream = torch.cuda.current_stream()
-    bufs, sss = [], []
-    for r in range(rot):
-        data = torch.empty(batch_bytes, dtype=torch.uint8, device=device)
-        ss = torch.empty(cnt, dtype=torch.int32, device=device)
-        # rotation r holds the same segment indices with the stream bytes of a later block
-        tcp_amd.synth_fill(data, (s0 + r * total) * L, batch_bytes)
-        tcp_amd.synth_pseudo(ss, s0, cnt, L)
-        bufs.append(data)
-        sss.append(ss)
-    out = torch.empty(cnt, dtype=torch.int16, device=device)
-    torch.cuda.synchronize()
-
-    # Sanity (not a parity test — tests/ does that): rotation 0 of each shard is
-    # exactly the Appendix B batch whose digest the reference produced.
-    tcp_amd.batch_uniform(bufs[0], L, L, cnt, sss[0], out=out)
-    torch.cuda.synchronize()
-    res = out.cpu().numpy().view(np.uint16)
-    check = None
-    try:
-        gold = json.load(open(os.path.join(REPO, "tests", "golden", "reference_vectors.json")))["digests"]
-        key = {("1500", 1): "1Mx1500", ("64", 1): "1Mx64", ("64k", 1): "256Kx64KiB"}.get((args.config, world))
-        if args.config == "1500" and world == 8:
-            key = f"8Mx1500_shard{rank}"
-        elif args.config == "1500" and world > 1 and per_gpu == 1 << 20:
-            key = f"8Mx1500_shard{rank}" if rank < 8 else None
-        if key:
-            g = gold[key]
-            check = bool(int(res.astype(np.uint64).sum()) == g["sum"]
-                         and f"{int(np.bitwise_xor.reduce(res)):04x}" == g["xor"]
-                         and [f"{v:04x}" for v in res[:4]] == g["first4"] and f"{res[-1]:04x}" == g["last"])
-    except Exception:
-        check = None
-
-    if dist is not None:   # the check holds only if it holds on every rank
-        flag = 1.0 if check else (0.0 if check is False else -1.0)
-        fl = -max_over_ranks(-flag, dist, device)   # min over ranks
-        check = None if fl < 0 else bool(fl == 1.0)
-
-    k = [0]
-
-    def step():
-        r = k[0] % rot
-        k[0] += 1
-        tcp_amd.batch_uniform(bufs[r], L, L, cnt, sss[r], out=out)
-
-    # HIP events on the launch stream bracket the kernels of the timed region
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    wall = timed_region(step, args.steps, args.warmup, dist, torch.cuda.synchronize,
-                        on_start=lambda: ev0.record(stream), on_end=lambda: ev1.record(stream))
-    kernel_ms = ev0.elapsed_time(ev1) / args.steps
-    wall_max = max_over_ranks(wall, dist, device)
-    kernel_ms_max = max_over_ranks(kernel_ms, dist, device)
 
     probe = None
     if args.probe:
@@ -266,6 +285,24 @@ def main(argv=None) -> int:
         pms = pe0.elapsed_time(pe1) / args.steps
         probe = {"kernel": "k_probe (read-only 16-B stream, same access shape)", "avg_ms": round(pms, 5),
                  "GB/s": round(nb / (pms * 1e-3) / 1e9, 1)}
+
+    # the other single-GPU BASELINE configs (parity configs, reported beside the
+    # headline: kernel rate vs the HBM roofline, digest check), N=1 only
+    extra = {}
+    if world == 1 and not args.no_other_configs:
+        tcp_amd.set_tuning(0, 0, -1, 0)   # built-in launch shapes for the other configs
+        for cfg in sorted(CONFIGS):
+            if cfg == args.config:
+                continue
+            steps = max(10, min(args.steps, 200 if CONFIGS[cfg][1] < 4096 else 40))
+            e, ebufs, _ = run_config(cfg, steps, min(args.warmup, 5), rank, world, dist, device)
+            del ebufs
+            gbs = e["batch_bytes"] / (e["kernel_ms"] * 1e-3) / 1e9
+            extra[cfg] = {"workload": e["desc"], "GiB/s": round(e["batch_bytes"] * steps / e["wall_max"] / (1 << 30), 2),
+                          "kernel_avg_ms": round(e["kernel_ms"], 5), "achieved_GB/s": round(gbs, 1),
+                          "roofline_frac": round(gbs / HBM_PEAK_GBS, 4), "steps": steps,
+                          "rotating_batches": e["rot"], "digest_check": e["check"]}
+            torch.cuda.empty_cache()
 
     if rank == 0:
         total_bytes = batch_bytes * world * args.steps
@@ -298,6 +335,8 @@ def main(argv=None) -> int:
         }
         if probe:
             line["stream_probe"] = probe
+        if extra:
+            line["other_configs"] = extra
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(L, args.cpu_seconds)
         print(json.dumps(line), flush=True)
