@@ -226,8 +226,10 @@ int tcpcsum_plan_uniform(uint64_t base, uint64_t stride, uint32_t len, uint64_t 
 /* Launch-shape override for tuning (tools/sweep.py). 0 / -1 = built-in
  * per-shape defaults. unroll in {0,1,2,4,8}; shape in {-1, 0..12}, read per
  * launcher: uniform 0..12 (a forced shape that cannot cover the segments is
- * ignored), ragged 0..6 = (G,C) (4,1) (8,1) (16,1) (32,1) (32,3) (64,4) (64,8),
- * wire 0..7 = (8,1) (32,3) (64,4) (16,2) (16,6) (8,12) (8,2) (8,4), builder 0..4; flags: TCPCSUM_TUNE_*
+ * ignored), ragged 0..6 = (G,C) (4,1) (8,1) (16,1) (32,1) (32,3) (64,4) (64,8)
+ * and 7..8 = balanced chunk space (4 / 8 loads per lane in flight),
+ * wire 0..7 = (8,1) (32,3) (64,4) (16,2) (16,6) (8,12) (8,2) (8,4) and 8..9 =
+ * balanced (4 / 8 loads per lane), builder 0..4; flags: TCPCSUM_TUNE_*
  * bits (0 = defaults). Affects batch calls issued afterwards from any thread. */
 /* PIPE_* and NT_* take effect only in a library built with TUNING_VARIANTS=1 */
 #define TCPCSUM_TUNE_PIPE_ON 1   /* software-pipelined tiles */

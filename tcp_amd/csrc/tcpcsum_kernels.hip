@@ -485,6 +485,198 @@ __global__ __launch_bounds__(256) void k_desc(const uint8_t* __restrict__ base,
     }
 }
 
+// ---------------------------------------------------------------- balanced
+// Mixed-length batches. A lane group per segment wastes lanes and loads when
+// lengths vary (a 64-B segment in a 96-chunk group). Here a wave takes 64
+// segments (one per lane), lays their aligned hulls end to end in a "chunk
+// space" by a wave prefix sum, and sweeps that space 64 chunks per load
+// instruction: lane l of sub-round k loads chunk R + 64k + l whatever segment
+// it belongs to, so every instruction does 64 useful 16-B loads. Each lane
+// finds its segment from the segments that start inside its 64-chunk window
+// (a short scalar loop over a ballot), masks its chunk to the segment's byte
+// range, and the per-segment sums come from a wave inclusive scan of the chunk
+// sums: the lane holding a segment's last chunk in the window adds
+// X[end] - X[run start - 1] to the segment's LDS accumulator.
+
+// Inclusive prefix sum over the 64 lanes: DPP row shifts, then row carries.
+__device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);   // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);   // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);   // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);   // row_shr:8
+    const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)x, 15);
+    const uint32_t r1 = (uint32_t)__builtin_amdgcn_readlane((int)x, 31);
+    const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)x, 47);
+    const int row = (threadIdx.x & 63) >> 4;
+    return x + (row >= 1 ? r0 : 0u) + (row >= 2 ? r1 : 0u) + (row >= 3 ? r2 : 0u);
+}
+
+__device__ __forceinline__ uint32_t bperm(uint32_t x, uint32_t src_lane) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src_lane << 2), (int)x);
+}
+
+constexpr uint32_t kNoHole = 0x40000000u;   // a hole offset past any segment (int32-safe)
+
+// Bytes [lo, hi) of a 16-byte chunk as two 64-bit byte masks.
+__device__ __forceinline__ void range_mask(int32_t lo, int32_t hi, uint64_t& m0, uint64_t& m1) {
+    lo = lo < 0 ? 0 : (lo > 16 ? 16 : lo);
+    hi = hi < 0 ? 0 : (hi > 16 ? 16 : hi);
+    const int32_t lo0 = lo < 8 ? lo : 8, hi0 = hi < 8 ? hi : 8;
+    const int32_t lo1 = lo > 8 ? lo - 8 : 0, hi1 = hi > 8 ? hi - 8 : 0;
+    m0 = bytemask64(hi0) & ~bytemask64(lo0);
+    m1 = bytemask64(hi1) & ~bytemask64(lo1);
+}
+
+// The chunk's bytes at segment-relative offsets [0, len) except the two-byte
+// hole [hole, hole + 2) (the zeroed check of a FILL; hole >= len: none);
+// rel = segment-relative offset of the chunk's first byte. W: aligned-word sum,
+// O: odd-address byte sum (only when want_odd).
+__device__ __forceinline__ void chunk_masked(u32x4 v, int32_t rel, int32_t len, int32_t hole, bool want_odd,
+                                             uint32_t& W, uint32_t& O) {
+    uint64_t m0, m1;
+    range_mask(-rel, len - rel, m0, m1);
+    if (hole != (int32_t)kNoHole) {   // kernel-uniform
+        uint64_t h0, h1;
+        range_mask(hole - rel, hole + 2 - rel, h0, h1);
+        m0 &= ~h0;
+        m1 &= ~h1;
+    }
+    const uint32_t d0 = v.x & (uint32_t)m0, d1 = v.y & (uint32_t)(m0 >> 32);
+    const uint32_t d2 = v.z & (uint32_t)m1, d3 = v.w & (uint32_t)(m1 >> 32);
+    W = sad16(d0, W); W = sad16(d1, W); W = sad16(d2, W); W = sad16(d3, W);
+    if (want_odd) {
+        O = sad8(d0 & 0xff00ff00u, O); O = sad8(d1 & 0xff00ff00u, O);
+        O = sad8(d2 & 0xff00ff00u, O); O = sad8(d3 & 0xff00ff00u, O);
+    }
+}
+
+// Per-lane segment [a, a + len) (len <= 1 MiB: the chunk space stays < 2^32),
+// hole (the same segment-relative offset for every segment, kNoHole: none) as
+// above. On return accW[lane] / accO[lane] hold the lane's segment sums W and O
+// (O only when want_odd, wave-uniform). acc: the wave's 2 x 64 u64 LDS slots.
+template <int C>
+__device__ __forceinline__ void lb_sums(const uint8_t* a, uint32_t len, uint32_t hole, bool want_odd,
+                                        uint64_t* accW, uint64_t* accO) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t m = (uint32_t)((uintptr_t)a & 15u);
+    const uint32_t nj = len ? (m + len + 15u) >> 4 : 0u;   // chunks of the aligned hull
+    const uint32_t lm = len | (m << 27);                     // len < 2^27
+    const uint32_t incl = wave_scan_incl(nj);
+    const uint32_t P = incl - nj;                           // first chunk in the chunk space
+    const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    const uint64_t a0 = (uint64_t)(uintptr_t)a - m;
+    const uint32_t a_lo = (uint32_t)a0, a_hi = (uint32_t)(a0 >> 32);
+    accW[lane] = 0;
+    if (want_odd) accO[lane] = 0;
+    uint32_t carry = 0;   // segment owning the next window's first chunk
+    for (uint32_t R = 0; R < T; R += 64u * C) {
+        uint32_t own[C], pc[C], po[C];
+        u32x4 v[C];
+#pragma unroll
+        for (int k = 0; k < C; ++k) {
+            const uint32_t W0 = R + 64u * k;
+            const uint32_t g = W0 + lane;
+            // segments starting inside [W0, W0 + 64), in lane (= start) order
+            uint64_t M = __ballot(nj != 0 && P - W0 < 64u && P >= W0);
+            uint32_t o = carry;
+            while (M) {
+                const int j = __builtin_ctzll(M);
+                M &= M - 1;
+                const uint32_t st = (uint32_t)__builtin_amdgcn_readlane((int)P, j) - W0;
+                o = lane >= st ? (uint32_t)j : o;
+            }
+            carry = (uint32_t)__builtin_amdgcn_readlane((int)o, 63);
+            own[k] = o;
+            po[k] = bperm(P, o);
+            pc[k] = g - po[k];   // chunk index inside the owner's hull
+            const uint64_t base = (uint64_t)bperm(a_lo, o) | ((uint64_t)bperm(a_hi, o) << 32);
+            v[k] = ld16(zsel(g < T, reinterpret_cast<const uint8_t*>(base + (uint64_t)pc[k] * 16u)));
+        }
+#pragma unroll
+        for (int k = 0; k < C; ++k) {
+            const uint32_t W0 = R + 64u * k;
+            const uint32_t g = W0 + lane;
+            const uint32_t o = own[k];
+            const uint32_t lmo = bperm(lm, o);
+            const uint32_t lo = lmo & ((1u << 27) - 1u), mo = lmo >> 27;
+            const uint32_t no = (mo + lo + 15u) >> 4;
+            uint32_t w = 0, od = 0;
+            if (g < T) chunk_masked(v[k], (int32_t)(pc[k] * 16u) - (int32_t)mo, (int32_t)lo, (int32_t)hole, want_odd, w, od);
+            const bool end = g < T && (pc[k] + 1u == no || lane == 63u || g + 1u == T);
+            const uint32_t sr = po[k] > W0 ? po[k] - W0 : 0u;   // the run's first lane in this window
+            const uint32_t X = wave_scan_incl(w);
+            const uint32_t Xp = bperm(X, sr ? sr - 1u : 0u);
+            if (end) atomicAdd(reinterpret_cast<unsigned long long*>(accW + o), (unsigned long long)(X - (sr ? Xp : 0u)));
+            if (want_odd) {
+                const uint32_t Y = wave_scan_incl(od);
+                const uint32_t Yp = bperm(Y, sr ? sr - 1u : 0u);
+                if (end) atomicAdd(reinterpret_cast<unsigned long long*>(accO + o), (unsigned long long)(Y - (sr ? Yp : 0u)));
+            }
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+// One segment summed by the whole wave (wave-uniform a, len): 64 chunks per
+// load instruction, u32 lane partials flushed to u64 every 8 rounds. For the
+// rare segments too long for the balanced chunk space.
+__device__ __forceinline__ void wave_seg_sums(const uint8_t* a, uint32_t len, bool want_odd, uint64_t& W,
+                                              uint64_t& O) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t m = (uint32_t)((uintptr_t)a & 15u);
+    const uint8_t* a0 = a - m;
+    const uint64_t nch = ((uint64_t)m + len + 15u) >> 4;
+    uint64_t w64 = 0, o64 = 0;
+    for (uint64_t r = 0; r < nch; r += 512) {
+        uint32_t w = 0, o = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint64_t idx = r + 64u * k + lane;
+            const u32x4 v = ld16(zsel(idx < nch, a0 + idx * 16u));
+            if (idx < nch) chunk_wo_bytes(v, (int64_t)idx * 16 - m, (int64_t)len, want_odd, w, o);
+        }
+        w64 += w;
+        o64 += o;
+    }
+    W = group_sum64<64>(w64);
+    O = want_odd ? group_sum64<64>(o64) : 0;
+}
+
+// Ragged descriptors, balanced: 64 descriptors per wave tile. Segments longer
+// than 1 MiB (chunk space kept < 2^32) are summed one at a time by the wave.
+template <int C>
+__global__ __launch_bounds__(256) void k_desc_lb(const uint8_t* __restrict__ base,
+                                                 const tcpcsum_desc_t* __restrict__ desc, uint64_t n,
+                                                 uint16_t* __restrict__ out) {
+    __shared__ uint64_t acc[4][2][64];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
+    const uint64_t ntiles = (n + 63) / 64;
+    for (uint64_t t = (uint64_t)blockIdx.x * 4u + wv; t < ntiles; t += nwaves) {
+        const uint64_t seg = t * 64 + lane;
+        const u32x4 d = *reinterpret_cast<const u32x4*>(zsel(seg < n, reinterpret_cast<const uint8_t*>(desc + seg)));
+        const uint8_t* p = base + ((uint64_t)d.x | ((uint64_t)d.y << 32));
+        const uint32_t len = d.z;   // 0 past n
+        const bool odd = ((uintptr_t)p & 1u) != 0;
+        const bool any_odd = __ballot(len != 0 && odd) != 0;
+        const bool big = len > (1u << 20);
+        uint64_t bw = 0, bo = 0;
+        for (uint64_t M = __ballot(big); M; M &= M - 1) {   // wave-uniform, rare
+            const int j = __builtin_ctzll(M);
+            const uint64_t pj = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uintptr_t)p, j) |
+                                ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uintptr_t)p >> 32), j) << 32);
+            const uint32_t lj = (uint32_t)__builtin_amdgcn_readlane((int)len, j);
+            uint64_t W, O;
+            wave_seg_sums(reinterpret_cast<const uint8_t*>(pj), lj, any_odd, W, O);
+            if (lane == j) { bw = W; bo = O; }
+        }
+        lb_sums<C>(p, big ? 0u : len, kNoHole, any_odd, acc[wv][0], acc[wv][1]);
+        const uint64_t W = big ? bw : acc[wv][0][lane];
+        const uint64_t O = !any_odd ? 0 : big ? bo : acc[wv][1][lane];
+        if (seg < n) out[seg] = fold_ref(combine((uint64_t)d.w, W, O, odd));
+    }
+}
+
 // ---------------------------------------------------------------- wire (IPv4)
 // Packet i at pkts + off[i] (see tcpcsum.h). Tiles of U packets per lane
 // group; the offsets of the next tile are in flight while a tile is summed.
@@ -736,6 +928,92 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const 
         load_off(t + nwaves);
 #pragma unroll
         for (int u = 0; u < U; ++u) commit(process(u, t * SPT + (uint64_t)(u * GPW + q)));
+    }
+}
+
+// Wire batches, balanced (mixed packet sizes, packed small packets): 64 packets
+// per wave tile. Each lane reads its packet's IP header with aligned dword loads
+// (fields funnel-shifted out of them: no dynamic register indexing), validates
+// it exactly like k_ipv4, and the TCP ranges [ip + ihl*4, ip + tot_len) are
+// summed by lb_sums — FILL then subtracts the check word (what zeroing it
+// does). The IPv4 header checksum (IPHDR) is summed per lane from the
+// header dwords: relative dwords, so its u16 halves are the reference's words.
+template <int C>
+__global__ __launch_bounds__(256) void k_ipv4_lb(uint8_t* __restrict__ pkts, const uint64_t* __restrict__ off,
+                                                 uint64_t n, uint32_t cap, uint64_t limit, int mode,
+                                                 uint16_t* __restrict__ out, uint8_t* __restrict__ status,
+                                                 uint16_t* __restrict__ ipout) {
+    __shared__ uint64_t acc[4][2][64];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
+    const uint64_t ntiles = (n + 63) / 64;
+    const bool verify = (mode & TCPCSUM_IPV4_VERIFY) != 0;
+    const bool iphdr = (mode & TCPCSUM_IPV4_IPHDR) != 0;
+    for (uint64_t t = (uint64_t)blockIdx.x * 4u + wv; t < ntiles; t += nwaves) {
+        const uint64_t i = t * 64 + lane;
+        const bool live = i < n;
+        const uint64_t o = *reinterpret_cast<const uint64_t*>(zsel(live, reinterpret_cast<const uint8_t*>(off + i)));
+        const bool hdr = live && o < limit && limit - o >= 20u;
+        uint8_t* ip = pkts + o;
+        const uint32_t sh = (uint32_t)((uintptr_t)ip & 3u);
+        const uint8_t* d0 = ip - sh;
+        // the dwords under header bytes [0, 20): D[5] only when ip is not 4-B aligned
+        // (an aligned dword holding a needed byte never crosses a page)
+        uint32_t D[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+            D[k] = *reinterpret_cast<const uint32_t*>(zsel(hdr && (k < 5 || sh != 0), d0 + 4 * k));
+        auto rel4 = [&](int k) { return __builtin_amdgcn_alignbyte(D[k + 1], D[k], sh); };   // bytes [4k, 4k+4)
+        const uint32_t h0 = rel4(0), h8 = rel4(2), sa = rel4(3), da = rel4(4);
+        const uint32_t ver = (h0 >> 4) & 15u, ihl = h0 & 15u;
+        const uint32_t tot = ((h0 >> 8) & 0xff00u) | (h0 >> 24);
+        const uint32_t proto = (h8 >> 8) & 0xffu;
+        const bool ok = hdr && ver == 4u && proto == 6u && ihl >= 5u && tot >= ihl * 4u + 20u && tot <= cap &&
+                        o + tot <= limit;
+        const uint32_t th = ihl * 4u;
+        const uint32_t len = ok ? tot - th : 0u;
+        uint8_t* tcp = ip + th;
+        const bool odd = ((uintptr_t)ip & 1u) != 0;   // th is even
+        const bool any_odd = __ballot(ok && odd) != 0;
+        lb_sums<C>(tcp, len, kNoHole, any_odd, acc[wv][0], acc[wv][1]);
+        if (!live) continue;
+        if (!ok) {
+            if (out) out[i] = 0;
+            if (status) status[i] = TCPCSUM_PKT_SKIPPED;
+            continue;
+        }
+        const uint32_t len_be = ((len & 0xffu) << 8) | ((len >> 8) & 0xffu);   // htons
+        // context.c:104-119 closed form
+        const uint64_t ps = (sa & 0xffffu) + (sa >> 16) + (da & 0xffffu) + (da >> 16) + 0x0600u + len_be;
+        uint64_t S = combine(ps, acc[wv][0][lane], any_odd ? acc[wv][1][lane] : 0, odd);
+        // FILL sums with the check as zero (context.c:182): TCP+16 is an even offset,
+        // so its native word (L2-hot: just summed) contributes exactly its value
+        if (!verify) S -= (uint32_t)tcp[16] | ((uint32_t)tcp[17] << 8);
+        const uint16_t c = fold_ref(S);
+        uint32_t st = TCPCSUM_PKT_OK;
+        if (verify && c != 0) {   // rare: was the check left as the bare pseudo-header sum?
+            const uint32_t cw = (uint32_t)tcp[16] | ((uint32_t)tcp[17] << 8);
+            if (cw == (uint32_t)(uint16_t)~fold_ref(ps)) st |= TCPCSUM_PKT_CSUM_PARTIAL;
+        }
+        if (iphdr) {
+            // csum_continue(0, ip, ihl*4) with check (IP+10) as zero: the reference's
+            // commented-out context.c:179
+            uint32_t w = 0;
+#pragma unroll
+            for (int k = 0; k < 5; ++k) w = sad16(rel4(k), w);
+            for (uint32_t k = 5; k < ihl; ++k) {   // IP options
+                const uint32_t lo = *reinterpret_cast<const uint32_t*>(d0 + 4 * k);
+                const uint32_t hi = sh ? *reinterpret_cast<const uint32_t*>(d0 + 4 * k + 4) : 0u;
+                w = sad16(__builtin_amdgcn_alignbyte(hi, lo, sh), w);
+            }
+            const uint16_t ic = fold_ref((uint64_t)w - (verify ? 0u : (h8 >> 16)));
+            if (ipout) ipout[i] = ic;
+            if (!verify) store_u16(ip + 10, ic);
+            else if (ic != 0) st |= TCPCSUM_PKT_IPHDR_BAD;
+        }
+        if (!verify) store_u16(tcp + 16, c);   // native u16 store, as context.c:208
+        if (out) out[i] = c;
+        if (status) status[i] = (uint8_t)st;
     }
 }
 
@@ -1262,10 +1540,22 @@ void launch_desc(const uint8_t* base, const tcpcsum_desc_t* d, uint64_t n, uint3
         else if (unroll == 2) launch_desc_t<G, C, 2>(base, d, n, out, s, max_blocks); \
         else launch_desc_t<G, C, 4>(base, d, n, out, s, max_blocks);               \
     } while (0)
-    // lane-group shape: by max_len, or forced (tuning shape 0..6, in this order)
+    // lane-group shape: by max_len, or forced (tuning shape 0..6, in this order;
+    // 7 / 8: balanced chunk space with 4 / 8 loads per lane in flight)
     int sh = tu.shape;
-    if (sh < 0 || sh > 6)
+    if (sh > 8) sh = -1;
+    // auto: a large ragged batch takes the balanced kernel (a ragged batch has mixed
+    // lengths by nature; uniform lengths belong to tcpcsum_batch_uniform_dev); small
+    // batches and very long segments the lane groups by max_len
+    if (sh < 0 && n >= 65536u && max_len <= 65536u) sh = 7;
+    if (sh < 0)
         sh = nch <= 4 ? 0 : nch <= 8 ? 1 : nch <= 16 ? 2 : nch <= 32 ? 3 : nch <= 96 ? 4 : nch <= 256 ? 5 : 6;
+    if (sh == 7 || sh == 8) {
+        const dim3 grid(grid_for((n + 63) / 64, max_blocks));
+        if (sh == 7) hipLaunchKernelGGL(k_desc_lb<4>, grid, dim3(256), 0, s, base, d, n, out);
+        else hipLaunchKernelGGL(k_desc_lb<8>, grid, dim3(256), 0, s, base, d, n, out);
+        return;
+    }
     switch (sh) {
         case 0: DS_U(4, 1); break;
         case 1: DS_U(8, 1); break;
@@ -1311,9 +1601,24 @@ void launch_ipv4(uint8_t* pkts, const uint64_t* off, uint64_t n, uint32_t cap, u
         else                                                                                                       \
             launch_ipv4_t<G, C, 4>(pkts, off, n, cap, limit, mode, out, status, ipout, s, max_blocks, nt, amask); \
     } while (0)
-    // forced: 0 (8,1), 1 (32,3), 2 (64,4), 3 (16,2), 4 (16,6), 5 (8,12), 6 (8,2), 7 (8,4)
+    // forced: 0 (8,1), 1 (32,3), 2 (64,4), 3 (16,2), 4 (16,6), 5 (8,12), 6 (8,2), 7 (8,4),
+    // 8 / 9: balanced chunk space (k_ipv4_lb) with 4 / 8 loads per lane in flight
     int sh = tu.shape;
-    if (sh < 0 || sh > 7) sh = (nch <= 8 || mean <= 112u) ? 0 : nch <= 96 ? 5 : 1;
+    // auto: large batches of small or mixed packets (mean footprint <= 1 KiB,
+    // e.g. packed IMIX) take the balanced kernel; MTU slots, jumbo packets and
+    // small batches (a releaseSend batch of <= 1024 packets: latency, not
+    // throughput — a balanced wave walks 64 packets in turn) the lane-group
+    // kernels, one speculative round trip per packet
+    if (sh < 0 || sh > 9)
+        sh = (n >= 65536u && mean <= 1024u) ? 8 : (nch <= 8 || mean <= 112u) ? 0 : nch <= 96 ? 5 : 1;
+    if (sh == 8 || sh == 9) {
+        const dim3 grid(grid_for((n + 63) / 64, max_blocks));
+        if (sh == 8)
+            hipLaunchKernelGGL(k_ipv4_lb<4>, grid, dim3(256), 0, s, pkts, off, n, cap, limit, mode, out, status, ipout);
+        else
+            hipLaunchKernelGGL(k_ipv4_lb<8>, grid, dim3(256), 0, s, pkts, off, n, cap, limit, mode, out, status, ipout);
+        return;
+    }
     switch (sh) {
         case 0: IP_U(8, 1); break;
         case 1: IP_U(32, 3); break;

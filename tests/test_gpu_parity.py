@@ -483,7 +483,7 @@ def test_ipv4_region_bounds(dev):
     assert np.array_equal(u16(out)[:-3], want_out[:-3])
 
 
-@pytest.mark.parametrize("shape", range(8))
+@pytest.mark.parametrize("shape", range(10))
 def test_ipv4_forced_shapes(dev, shape):
     """Every wire lane-group shape (tcpcsum.h: wire 0..7) and tile depth is exact, incl. IHL 5..15,
     odd offsets and malformed packets; the header fields come from the group's chunk registers."""
@@ -510,10 +510,10 @@ def test_ipv4_forced_shapes(dev, shape):
         region = ref   # VERIFY runs over the filled packets
 
 
-@pytest.mark.parametrize("shape", range(7))
+@pytest.mark.parametrize("shape", range(9))
 def test_desc_forced_shapes(dev, shape):
-    """Every ragged lane-group shape (tcpcsum.h: ragged 0..6) and tile depth is exact on lengths
-    0..9000 at arbitrary offsets."""
+    """Every ragged lane-group shape (tcpcsum.h: ragged 0..6, balanced 7..8) and tile depth is exact
+    on lengths 0..9000 at arbitrary offsets."""
     import tcp_amd
     rng = np.random.default_rng(700 + shape)
     size = 2 << 20
@@ -535,7 +535,7 @@ def test_desc_forced_shapes(dev, shape):
             assert np.array_equal(got, want), (un, mb)
 
 
-@pytest.mark.parametrize("shape", [-1, 1, 3])
+@pytest.mark.parametrize("shape", [-1, 1, 3, 8, 9])
 def test_ipv4_span_hint_mispredicted(dev, shape):
     """The next packet's offset only bounds the speculative span: shuffled offsets (gaps unrelated
     to lengths, negative gaps) and extra offsets inside packets (gap < tot_len: fix-up loads) are
@@ -568,9 +568,9 @@ def test_ipv4_span_hint_mispredicted(dev, shape):
             reg = ref
 
 
-@pytest.mark.parametrize("flags", [0, 32, 64, 96])
+@pytest.mark.parametrize("shape,flags", [(-1, 0), (-1, 32), (-1, 64), (-1, 96), (8, 0), (9, 0)])
 @pytest.mark.parametrize("layout", ["odd", "slot64", "slot16", "packed"])
-def test_ipv4_window_and_store_variants(dev, flags, layout):
+def test_ipv4_window_and_store_variants(dev, shape, flags, layout):
     """Wire kernel variants (128-B or 16-B packet windows; non-temporal or default-policy loads)
     are exact and FILL rewrites nothing but the checks, in every layout: odd packed
     offsets, 64-B aligned slots, 16-B (not 64-B) aligned slots, packed tiny packets."""
@@ -590,10 +590,10 @@ def test_ipv4_window_and_store_variants(dev, flags, layout):
         region = np.zeros(int(off[-1]) + len(pkts[-1]), np.uint8)
         for o, p in zip(off, pkts):
             region[int(o):int(o) + len(p)] = np.frombuffer(p, np.uint8)
-    for mode in (tcp_amd.IPV4_FILL, tcp_amd.IPV4_FILL | tcp_amd.IPV4_IPHDR):
+    for mode in (tcp_amd.IPV4_FILL, tcp_amd.IPV4_FILL | tcp_amd.IPV4_IPHDR, tcp_amd.IPV4_VERIFY | tcp_amd.IPV4_IPHDR):
         ref = region.copy()
         want_out, want_st = oracle.ipv4_batch(ref, off, 1536 if layout != "odd" else 32768, mode)
-        tcp_amd.set_tuning(0, 0, -1, flags)
+        tcp_amd.set_tuning(0, 0, shape, flags)
         try:
             dreg = to_dev(region, dev)
             out = torch.empty(off.size, dtype=torch.int16, device=dev)
@@ -605,3 +605,27 @@ def test_ipv4_window_and_store_variants(dev, flags, layout):
         assert np.array_equal(st.cpu().numpy(), want_st), mode
         assert np.array_equal(u16(out), want_out), mode
         assert np.array_equal(dreg.cpu().numpy(), ref), mode
+        region = ref   # the VERIFY pass runs over filled packets
+
+
+@pytest.mark.parametrize("shape", [7, 8])
+def test_desc_balanced_long_segments(dev, shape):
+    """The balanced ragged kernel on tiles that mix tiny, 64 KiB and > 1 MiB segments (the latter
+    summed by the whole wave) at odd offsets, with byte values that push sums above 2^32."""
+    import tcp_amd
+    rng = np.random.default_rng(88 + shape)
+    size = 24 << 20
+    host = rng.integers(200, 256, size, dtype=np.uint8)
+    n = 300
+    lens = rng.choice(np.array([0, 1, 3, 64, 1500, 65536, 65537, 300000, (1 << 20) + 1, 3 << 20], np.uint32), n)
+    off = np.array([rng.integers(0, size - l) for l in lens], np.uint64)
+    ss = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    want = oracle.batch_desc(host, off, lens, ss)
+    d = to_dev(host, dev)
+    dd = to_dev(_desc(off, lens, ss), dev)
+    tcp_amd.set_tuning(0, 0, shape, 0)
+    try:
+        got = u16(tcp_amd.batch_desc(d, dd, n, int(lens.max())))
+    finally:
+        tcp_amd.set_tuning(0, 0, -1, 0)
+    assert np.array_equal(got, want)

@@ -53,7 +53,7 @@ def main():
             d2 = desc[order]
             ddesc = torch.from_numpy(d2.view(np.uint8)).to(dev)
         grid = ([(mb, un, sh) for sh in (-1, 2, 3) for mb in (2048, 8192) for un in (1, 2)]
-                if "--sweep" in sys.argv else [(0, 0, -1)])
+                if "--sweep" in sys.argv else [(0, 0, -1), (0, 0, 7), (0, 0, 8), (2048, 0, 8)])
         for mb, un, sh in grid:
             tcp_amd.set_tuning(mb, un, sh, 0)
             t = timeit(lambda: tcp_amd.batch_desc(data, ddesc, n, 1500, out))
@@ -61,6 +61,19 @@ def main():
                               "unroll": un, "shape": sh,
                               "ms": round(t * 1e3, 4), "GB/s": round(int(lens.sum()) / t / 1e9, 1),
                               "Mseg/s": round(n / t / 1e6, 1)}), flush=True)
+        tcp_amd.set_tuning(0, 0, -1, 0)
+
+    # uniform-length descriptors: where the lane-group kernels are at home
+    for L in (64, 1500):
+        desc = np.zeros(n, tcp_amd.DESC_DTYPE)
+        desc["offset"] = np.arange(n, dtype=np.uint64) * 1536 + rng.integers(0, 8, n).astype(np.uint64) * 4
+        desc["len"] = L
+        ddesc = torch.from_numpy(desc.view(np.uint8)).to(dev)
+        for sh in (-1, 7, 8):
+            tcp_amd.set_tuning(0, 0, sh, 0)
+            t = timeit(lambda: tcp_amd.batch_desc(data, ddesc, n, L, out))
+            print(json.dumps({"measure": f"desc_1Mx{L}", "shape": sh, "ms": round(t * 1e3, 4),
+                              "GB/s": round(n * L / t / 1e9, 1), "Mseg/s": round(n / t / 1e6, 1)}), flush=True)
         tcp_amd.set_tuning(0, 0, -1, 0)
 
     # wire: 1M packets of 1500 B (IP 20 + TCP 24 + 1456 payload) in 1536-B slots
@@ -77,7 +90,7 @@ def main():
     stat = torch.empty(n, dtype=torch.uint8, device=dev)
     for name, mode in (("FILL", tcp_amd.IPV4_FILL), ("VERIFY", tcp_amd.IPV4_VERIFY)):
         grid = ([(mb, un, sh) for sh in (-1, 3, 4) for mb in (2048, 8192) for un in (1, 2)]
-                if "--sweep" in sys.argv else [(0, 0, -1)])
+                if "--sweep" in sys.argv else [(0, 0, -1), (0, 0, 8), (0, 0, 9)])
         for mb, un, sh in grid:
             tcp_amd.set_tuning(mb, un, sh, 0)
             t = timeit(lambda: tcp_amd.ipv4_batch(data, offs, n, 1536, mode, out, stat))
@@ -87,6 +100,21 @@ def main():
         tcp_amd.set_tuning(0, 0, -1, 0)
     ok = bool((out == 0).all().item()) and bool((stat == 0).all().item())
     print(json.dumps({"measure": "ipv4_verify_all_zero", "ok": ok}))
+
+    # pure ACKs (44 B: IP 20 + TCP 24, no payload) in 1536-B slots
+    segs = np.zeros(n, tcp_amd.TXSEG_DTYPE)
+    segs["payload_off"] = 0
+    segs["out_off"] = np.arange(n, dtype=np.uint64) * 1536
+    segs["saddr_be"], segs["daddr_be"] = 0x0100007F, np.arange(n, dtype=np.uint32)
+    segs["sport"], segs["dport"], segs["len"], segs["flags"] = 4000, 45001, 0, 16
+    tcp_amd.tx_build(payload, torch.from_numpy(segs.view(np.uint8)).to(dev), n, 0, data, 0, None)
+    for sh in (-1, 0, 8, 9):
+        tcp_amd.set_tuning(0, 0, sh, 0)
+        t = timeit(lambda: tcp_amd.ipv4_batch(data, offs, n, 1536, tcp_amd.IPV4_VERIFY, out, stat))
+        ok = bool((out == 0).all().item()) and bool((stat == 0).all().item())
+        print(json.dumps({"measure": "ipv4_1Mx44_ack_in_1536_slots_verify", "shape": sh, "ms": round(t * 1e3, 4),
+                          "Mpkt/s": round(n / t / 1e6, 1), "ok": ok}), flush=True)
+    tcp_amd.set_tuning(0, 0, -1, 0)
 
     # packed small packets (64-B TCP segments back to back, cap 1536): the next
     # offset bounds each packet's speculative span
@@ -102,7 +130,7 @@ def main():
     soffs = torch.from_numpy((np.arange(np_, dtype=np.uint64) * plen).view(np.int64)).to(dev)
     sout = torch.empty(np_, dtype=torch.int16, device=dev)
     sst = torch.empty(np_, dtype=torch.uint8, device=dev)
-    for sh in ((-1, 0, 6, 7, 5) if "--sweep" in sys.argv else (-1,)):
+    for sh in ((-1, 0, 6, 7, 5, 8, 9) if "--sweep" in sys.argv else (-1, 8, 9)):
         tcp_amd.set_tuning(0, 0, sh, 0)
         t = timeit(lambda: tcp_amd.ipv4_batch(small, soffs, np_, 1536, tcp_amd.IPV4_VERIFY, sout, sst))
         ok = bool((sout == 0).all().item()) and bool((sst == 0).all().item())
@@ -127,7 +155,7 @@ def main():
     ioffs = torch.from_numpy(ioff.view(np.int64)).to(dev)
     iout = torch.empty(ni, dtype=torch.int16, device=dev)
     ist = torch.empty(ni, dtype=torch.uint8, device=dev)
-    for sh in ((-1, 0, 6, 7, 5, 4) if "--sweep" in sys.argv else (-1,)):
+    for sh in ((-1, 0, 6, 7, 5, 4, 8, 9) if "--sweep" in sys.argv else (-1, 8, 9)):
         for un in ((1, 2) if "--sweep" in sys.argv else (0,)):
             tcp_amd.set_tuning(0, un, sh, 0)
             t = timeit(lambda: tcp_amd.ipv4_batch(ireg, ioffs, ni, 1536, tcp_amd.IPV4_VERIFY, iout, ist))
@@ -154,7 +182,7 @@ def main():
     jout = torch.empty(nj, dtype=torch.int16, device=dev)
     jst = torch.empty(nj, dtype=torch.uint8, device=dev)
     grid = ([(mb, un, sh) for sh in (-1, 1, 2, 4, 5) for mb in (2048, 8192) for un in (1, 2)]
-            if "--sweep" in sys.argv else [(0, 0, -1)])
+            if "--sweep" in sys.argv else [(0, 0, -1), (0, 0, 9)])
     for mb, un, sh in grid:
         tcp_amd.set_tuning(mb, un, sh, 0)
         t = timeit(lambda: tcp_amd.ipv4_batch(jreg, joffs, nj, js, tcp_amd.IPV4_VERIFY, jout, jst))
