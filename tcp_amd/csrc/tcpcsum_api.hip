@@ -219,11 +219,19 @@ struct tcpcsum_ctx {
     // wire path
     uint8_t* d_region = nullptr;
     size_t d_region_bytes = 0;
-    uint64_t* d_off = nullptr;
-    uint16_t* d_wout = nullptr;
-    uint8_t* d_wstat = nullptr;
-    uint16_t* d_wip = nullptr;
-    size_t d_pkt_cap = 0;
+    // pinned staging of the per-packet arrays (offsets in; results, status and
+    // IPv4 header checks out), host views h_* and device views k_*: a pageable
+    // caller array costs a CPU memcpy and the kernel reads / writes the staging
+    // over PCIe, instead of a staged pageable hipMemcpy per array per batch
+    uint64_t* h_off = nullptr;
+    uint16_t* h_wout = nullptr;
+    uint8_t* h_wstat = nullptr;
+    uint16_t* h_wip = nullptr;
+    uint64_t* k_off = nullptr;
+    uint16_t* k_wout = nullptr;
+    uint8_t* k_wstat = nullptr;
+    uint16_t* k_wip = nullptr;
+    size_t pkt_cap = 0;
     std::mutex mu;
 };
 
@@ -311,10 +319,10 @@ void tcpcsum_ctx_destroy(tcpcsum_ctx_t* c) {
         if (c->st[i]) hipStreamSynchronize(c->st[i]);
     ctx_free_buffers(c);
     if (c->d_region) hipFree(c->d_region);
-    if (c->d_off) hipFree(c->d_off);
-    if (c->d_wout) hipFree(c->d_wout);
-    if (c->d_wstat) hipFree(c->d_wstat);
-    if (c->d_wip) hipFree(c->d_wip);
+    if (c->h_off) hipHostFree(c->h_off);
+    if (c->h_wout) hipHostFree(c->h_wout);
+    if (c->h_wstat) hipHostFree(c->h_wstat);
+    if (c->h_wip) hipHostFree(c->h_wip);
     for (int i = 0; i < 2; ++i)
         if (c->st[i]) hipStreamDestroy(c->st[i]);
     delete c;
@@ -352,20 +360,27 @@ void* pinned_dev_ptr(const void* p) {
     return nullptr;
 }
 
-int ensure_pkt_scratch(tcpcsum_ctx* c, uint64_t n, hipStream_t st) {
-    if (n <= c->d_pkt_cap) return TCPCSUM_OK;
+int ensure_pkt_staging(tcpcsum_ctx* c, uint64_t n, hipStream_t st) {
+    if (n <= c->pkt_cap) return TCPCSUM_OK;
     (void)hipStreamSynchronize(st);
-    if (c->d_off) (void)hipFree(c->d_off);
-    if (c->d_wout) (void)hipFree(c->d_wout);
-    if (c->d_wstat) (void)hipFree(c->d_wstat);
-    if (c->d_wip) (void)hipFree(c->d_wip);
-    c->d_off = nullptr; c->d_wout = nullptr; c->d_wstat = nullptr; c->d_wip = nullptr; c->d_pkt_cap = 0;
-    hipError_t e = hipMalloc(&c->d_off, n * sizeof(uint64_t));
-    if (e == hipSuccess) e = hipMalloc(&c->d_wout, n * sizeof(uint16_t));
-    if (e == hipSuccess) e = hipMalloc(&c->d_wstat, n);
-    if (e == hipSuccess) e = hipMalloc(&c->d_wip, n * sizeof(uint16_t));
+    if (c->h_off) (void)hipHostFree(c->h_off);
+    if (c->h_wout) (void)hipHostFree(c->h_wout);
+    if (c->h_wstat) (void)hipHostFree(c->h_wstat);
+    if (c->h_wip) (void)hipHostFree(c->h_wip);
+    c->h_off = nullptr; c->h_wout = nullptr; c->h_wstat = nullptr; c->h_wip = nullptr; c->pkt_cap = 0;
+    size_t cap = 1024;
+    while (cap < n) cap *= 2;
+    hipError_t e = hipHostMalloc((void**)&c->h_off, cap * sizeof(uint64_t), hipHostMallocDefault);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_wout, cap * sizeof(uint16_t), hipHostMallocDefault);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_wstat, cap, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_wip, cap * sizeof(uint16_t), hipHostMallocDefault);
     if (e != hipSuccess) { g_last_hip_error.store((int)e); return TCPCSUM_ENOMEM; }
-    c->d_pkt_cap = n;
+    c->k_off = (uint64_t*)pinned_dev_ptr(c->h_off);
+    c->k_wout = (uint16_t*)pinned_dev_ptr(c->h_wout);
+    c->k_wstat = (uint8_t*)pinned_dev_ptr(c->h_wstat);
+    c->k_wip = (uint16_t*)pinned_dev_ptr(c->h_wip);
+    if (!c->k_off || !c->k_wout || !c->k_wstat || !c->k_wip) return TCPCSUM_ENOMEM;
+    c->pkt_cap = cap;
     return TCPCSUM_OK;
 }
 
@@ -451,9 +466,12 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t st
 }
 
 // Pinned packet pool: the kernel reads each packet's bytes over PCIe and (FILL)
-// stores the check field in place in host memory — no staging, no host-side
-// patching. Pageable pool: the region is copied H2D, checksummed, and the
-// results are stored at TCP+16 on the host.
+// stores the check field in place in host memory — no staging of the packets.
+// Pageable pool: the region is copied H2D, checksummed, and the results are
+// stored at TCP+16 on the host. Either way the per-packet arrays (offsets in,
+// results and status out) go through the context's pinned staging when the
+// caller's are pageable: a CPU memcpy and zero-copy kernel access instead of a
+// pageable hipMemcpy (a staged, synchronous copy) per array per batch.
 int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t* c, void* h_pkts, size_t region_bytes, const uint64_t* h_pkt_off,
                             uint64_t n, uint32_t cap, int mode, uint16_t* h_out, uint8_t* h_status) {
     if (!c) return TCPCSUM_EINVAL;
@@ -467,83 +485,68 @@ int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t* c, void* h_pkts, size_t region_bytes,
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard g(c->device);
     hipStream_t st = c->st[0];
-    int rc = ensure_pkt_scratch(c, n, st);
+    int rc = ensure_pkt_staging(c, n, st);
     if (rc) return rc;
-    hipError_t e = hipSuccess;
+    const uint64_t* koff = (const uint64_t*)pinned_dev_ptr(h_pkt_off);
+    if (!koff) {
+        memcpy(c->h_off, h_pkt_off, n * sizeof(uint64_t));
+        koff = c->k_off;
+    }
+    uint16_t* zout = h_out ? (uint16_t*)pinned_dev_ptr(h_out) : nullptr;
+    uint8_t* zst = h_status ? (uint8_t*)pinned_dev_ptr(h_status) : nullptr;
+    uint16_t* kout = zout ? zout : c->k_wout;
+    uint8_t* kst = zst ? zst : c->k_wstat;
+    const bool fill = (mode & TCPCSUM_IPV4_VERIFY) == 0;
+    hipError_t e;
     if (uint8_t* zp = (uint8_t*)pinned_dev_ptr(h_pkts)) {
-        const uint64_t* zoff = (const uint64_t*)pinned_dev_ptr(h_pkt_off);
-        if (!zoff) {
-            e = hipMemcpyAsync(c->d_off, h_pkt_off, n * sizeof(uint64_t), hipMemcpyHostToDevice, st);
-            if (e != hipSuccess) return hip_fail(e);
-            zoff = c->d_off;
-        }
-        uint16_t* zout = h_out ? (uint16_t*)pinned_dev_ptr(h_out) : nullptr;
-        uint8_t* zst = h_status ? (uint8_t*)pinned_dev_ptr(h_status) : nullptr;
-        tcpcsum::launch_ipv4(zp, zoff, n, cap, (uint64_t)region_bytes, mode, zout ? zout : c->d_wout,
-                             zst ? zst : c->d_wstat, nullptr, st, tuning());
+        // zero-copy over PCIe: 16-lane groups, 512 B per round (more waves with
+        // reads in flight) beat the HBM-tuned MTU shape — 1024 x 1500-B FILL
+        // batch 49 vs 59 us on MI355X (tools/e2e.py --sweep)
+        tcpcsum::Tuning tu = tuning();
+        if (tu.shape < 0 && n < 65536u) tu.shape = 3;
+        tcpcsum::launch_ipv4(zp, koff, n, cap, (uint64_t)region_bytes, mode, kout, kst, nullptr, st, tu);
         rc = check_launch();
         if (rc) return rc;
-        if (h_out && !zout) e = hipMemcpyAsync(h_out, c->d_wout, n * sizeof(uint16_t), hipMemcpyDeviceToHost, st);
-        if (e == hipSuccess && h_status && !zst) e = hipMemcpyAsync(h_status, c->d_wstat, n, hipMemcpyDeviceToHost, st);
-        if (e == hipSuccess) e = hipStreamSynchronize(st);
-        return e == hipSuccess ? TCPCSUM_OK : hip_fail(e);
-    }
-    const size_t mis = (uintptr_t)h_pkts & 15u;
-    const size_t need = region_bytes + mis + 16u;
-    if (need > c->d_region_bytes) {
-        (void)hipStreamSynchronize(st);
-        if (c->d_region) (void)hipFree(c->d_region);
-        c->d_region = nullptr;
-        c->d_region_bytes = 0;
-        e = hipMalloc(&c->d_region, need);
-        if (e != hipSuccess) { g_last_hip_error.store((int)e); return TCPCSUM_ENOMEM; }
-        c->d_region_bytes = need;
-    }
-    e = hipMemcpyAsync(c->d_region + mis, h_pkts, region_bytes, hipMemcpyHostToDevice, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(c->d_off, h_pkt_off, n * sizeof(uint64_t), hipMemcpyHostToDevice, st);
-    if (e != hipSuccess) return hip_fail(e);
-    tcpcsum::launch_ipv4(c->d_region + mis, c->d_off, n, cap, (uint64_t)region_bytes, mode, c->d_wout, c->d_wstat,
-                         c->d_wip, st, tuning());
-    rc = check_launch();
-    if (rc) return rc;
-    uint16_t* out = h_out;
-    uint8_t* stat = h_status;
-    // FILL needs out+status on the host to store the checks in place
-    uint16_t* tmp_out = nullptr;
-    uint8_t* tmp_stat = nullptr;
-    const bool fill = (mode & TCPCSUM_IPV4_VERIFY) == 0;
-    if (fill) {
-        if (!out) out = tmp_out = new (std::nothrow) uint16_t[n];
-        if (!stat) stat = tmp_stat = new (std::nothrow) uint8_t[n];
-        if (!out || !stat) { delete[] tmp_out; delete[] tmp_stat; return TCPCSUM_ENOMEM; }
-    }
-    if (out) e = hipMemcpyAsync(out, c->d_wout, n * sizeof(uint16_t), hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess && stat) e = hipMemcpyAsync(stat, c->d_wstat, n, hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
-    if (e != hipSuccess) { delete[] tmp_out; delete[] tmp_stat; return hip_fail(e); }
-    if (fill) {
-        // store each result at TCP+16 (native u16, as context.c:208), and the IP
-        // header checksum the kernel stored in the device copy — no arithmetic here
-        uint8_t* base = (uint8_t*)h_pkts;
-        for (uint64_t i = 0; i < n; ++i) {
-            if (stat[i] != TCPCSUM_PKT_OK) continue;
-            uint8_t* ip = base + h_pkt_off[i];
-            uint8_t* tcp = ip + (ip[0] & 15u) * 4u;
-            memcpy(tcp + 16, &out[i], 2);
+        e = hipStreamSynchronize(st);
+        if (e != hipSuccess) return hip_fail(e);
+    } else {
+        const size_t mis = (uintptr_t)h_pkts & 15u;
+        const size_t need = region_bytes + mis + 16u;
+        if (need > c->d_region_bytes) {
+            (void)hipStreamSynchronize(st);
+            if (c->d_region) (void)hipFree(c->d_region);
+            c->d_region = nullptr;
+            c->d_region_bytes = 0;
+            e = hipMalloc(&c->d_region, need);
+            if (e != hipSuccess) { g_last_hip_error.store((int)e); return TCPCSUM_ENOMEM; }
+            c->d_region_bytes = need;
         }
-        if (mode & TCPCSUM_IPV4_IPHDR) {
-            uint16_t* ipc = new (std::nothrow) uint16_t[n];
-            if (!ipc) { delete[] tmp_out; delete[] tmp_stat; return TCPCSUM_ENOMEM; }
-            e = hipMemcpyAsync(ipc, c->d_wip, n * sizeof(uint16_t), hipMemcpyDeviceToHost, st);
-            if (e == hipSuccess) e = hipStreamSynchronize(st);
-            if (e != hipSuccess) { delete[] ipc; delete[] tmp_out; delete[] tmp_stat; return hip_fail(e); }
-            for (uint64_t i = 0; i < n; ++i)
-                if (stat[i] == TCPCSUM_PKT_OK) memcpy(base + h_pkt_off[i] + 10, &ipc[i], 2);
-            delete[] ipc;
+        e = hipMemcpyAsync(c->d_region + mis, h_pkts, region_bytes, hipMemcpyHostToDevice, st);
+        if (e != hipSuccess) return hip_fail(e);
+        const bool ipfill = fill && (mode & TCPCSUM_IPV4_IPHDR);
+        tcpcsum::launch_ipv4(c->d_region + mis, koff, n, cap, (uint64_t)region_bytes, mode, kout, kst,
+                             ipfill ? c->k_wip : nullptr, st, tuning());
+        rc = check_launch();
+        if (rc) return rc;
+        e = hipStreamSynchronize(st);
+        if (e != hipSuccess) return hip_fail(e);
+        if (fill) {
+            // store each result at TCP+16 (native u16, as context.c:208), and the IP
+            // header checksum the kernel computed — no arithmetic here
+            const uint16_t* o = zout ? h_out : c->h_wout;
+            const uint8_t* s = zst ? h_status : c->h_wstat;
+            uint8_t* base = (uint8_t*)h_pkts;
+            for (uint64_t i = 0; i < n; ++i) {
+                if (s[i] != TCPCSUM_PKT_OK) continue;
+                uint8_t* ip = base + h_pkt_off[i];
+                uint8_t* tcp = ip + (ip[0] & 15u) * 4u;
+                memcpy(tcp + 16, &o[i], 2);
+                if (ipfill) memcpy(ip + 10, &c->h_wip[i], 2);
+            }
         }
     }
-    delete[] tmp_out;
-    delete[] tmp_stat;
+    if (h_out && !zout) memcpy(h_out, c->h_wout, n * sizeof(uint16_t));
+    if (h_status && !zst) memcpy(h_status, c->h_wstat, n);
     return TCPCSUM_OK;
 }
 

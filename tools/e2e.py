@@ -8,7 +8,8 @@ This measures the library's host entry points on MI355X:
     kernel reads host memory over PCIe);
   * tcpcsum_ipv4_batch_host FILL on one releaseSend-sized batch (1024 packets
     of 1500 B, loop.c:27-94) in the reference's pool layout (32 KiB slots) and
-    packed, pageable vs pinned — per-batch latency.
+    packed, pageable vs pinned — per-batch latency (--sweep: per wire kernel
+    shape / window flag).
 GPU path only; CPU rates come from bench.py's cpu_baseline.
 
   python tools/e2e.py  -> one JSON line per measurement
@@ -35,7 +36,7 @@ def main():
     import numpy as np
     import torch
     import tcp_amd
-    from tests.packets import build_batch
+    from tests.packets import ip_packet
 
     rng = np.random.default_rng(1)
     n, L = 1 << 20, 1500
@@ -69,21 +70,29 @@ def main():
 
     # one releaseSend batch: 1024 packets, 1456-B payload -> 1500-B IP packets
     for layout, slot in (("pool_32KiB_slots", 32768), ("packed_1500B", 1500)):
-        region, off, _ = build_batch(rng, 1024, slot=32768, max_payload=1456)
-        pkts = [region[o:o + 1500].copy() for o in off]
+        # full-size packets: 20 B IP + 24 B TCP + 1456 B payload = 1500 B each
+        pkts = [np.frombuffer(ip_packet(rng, 1456), np.uint8) for _ in range(1024)]
+        assert all(p.size == 1500 for p in pkts)
         reg = np.zeros(1024 * slot, np.uint8)
         offs = np.arange(1024, dtype=np.uint64) * np.uint64(slot)
         for i, p in enumerate(pkts):
             reg[i * slot:i * slot + p.size] = p
         pin = tcp_amd.pinned_empty(reg.size)
         pin[:] = reg
+        variants = ([(sh, fl) for sh in (-1, 0, 1, 3, 5) for fl in (0, tcp_amd.TUNE_WIN16)]
+                    if "--sweep" in sys.argv else [(-1, 0)])
         for name, r in (("pageable", reg), ("pinned_zero_copy", pin)):
-            ctx.ipv4_batch(r, offs, 32768, tcp_amd.IPV4_FILL)
-            tmin, tmed = best_of(lambda: ctx.ipv4_batch(r, offs, 32768, tcp_amd.IPV4_FILL), 50)
-            print(json.dumps({"measure": "ipv4_fill_host_1024x1500", "layout": layout, "memory": name,
-                              "us_best": round(tmin * 1e6, 1), "us_median": round(tmed * 1e6, 1),
-                              "region_bytes": int(r.size),
-                              "GiB/s_packet_bytes_median": round(1024 * 1500 / tmed / 2**30, 2)}), flush=True)
+            for sh, fl in variants:
+                tcp_amd.set_tuning(0, 0, sh, fl)
+                ctx.ipv4_batch(r, offs, 32768, tcp_amd.IPV4_FILL)
+                tmin, tmed = best_of(lambda: ctx.ipv4_batch(r, offs, 32768, tcp_amd.IPV4_FILL), 50)
+                print(json.dumps({"measure": "ipv4_fill_host_1024x1500", "layout": layout, "memory": name,
+                                  "shape": sh, "flags": fl,
+                                  "us_best": round(tmin * 1e6, 1), "us_median": round(tmed * 1e6, 1),
+                                  "region_bytes": int(r.size),
+                                  "GiB/s_packet_bytes_median": round(1024 * 1500 / tmed / 2**30, 2)}),
+                      flush=True)
+            tcp_amd.set_tuning(0, 0, -1, 0)
     ctx.close()
 
 
