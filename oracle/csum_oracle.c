@@ -221,7 +221,19 @@ void oracle_tx_build(const uint8_t *payload, const oracle_txseg_t *segs, uint64_
             if (checks) checks[k] = 0;
             continue;
         }
-        struct iphdr *ip = (struct iphdr *) (out + d->out_off);
+        /* The reference casts its (aligned) out-buffer to the system structs; the
+         * packets here may sit at any offset, so the same assignments go to an
+         * aligned 44-byte image that is then copied into place (UBSan-clean). */
+        union {
+            struct {
+                struct iphdr ip;
+                struct tcphdr th;
+                uint8_t opts[4];
+            } s;
+            uint8_t b[44];
+        } h;
+        _Static_assert(sizeof(struct iphdr) == 20 && sizeof(struct tcphdr) == 20, "wire header sizes");
+        struct iphdr *ip = &h.s.ip;
         memset(ip, 0, sizeof(struct iphdr));                           /* :169 */
         ip->ihl = 5;                                                   /* :171 */
         ip->version = 4;
@@ -231,17 +243,14 @@ void oracle_tx_build(const uint8_t *payload, const oracle_txseg_t *segs, uint64_
         ip->protocol = IPPROTO_TCP;
         ip->saddr = d->saddr_be;
         ip->daddr = d->daddr_be;
-        uint8_t *tcp = (uint8_t *) ip + sizeof(struct iphdr);
-        struct tcphdr *th = (struct tcphdr *) tcp;
+        struct tcphdr *th = &h.s.th;
+        uint8_t *tcp = h.b + sizeof(struct iphdr);
         memset(tcp, 0, 24);                                            /* :182, sizeof(struct TcpHeader) */
         th->ack = (d->flags & 1) != 0;                                 /* :184-187 */
         th->syn = (d->flags & 2) != 0;
         th->fin = (d->flags & 4) != 0;
         th->rst = (d->flags & 8) != 0;
-        if (data) {                                                    /* :188-191 */
-            th->psh = 1;
-            memcpy(tcp + 24, payload + d->payload_off, length);
-        }
+        if (data) th->psh = 1;                                         /* :188-189 */
         th->ack_seq = htonl(d->ack);                                   /* :193-196 */
         th->seq = htonl(d->seq);
         th->source = htons(d->sport);
@@ -249,10 +258,18 @@ void oracle_tx_build(const uint8_t *payload, const oracle_txseg_t *segs, uint64_
         tcp[20] = 3; tcp[21] = 3; tcp[22] = 5; tcp[23] = 0;            /* :199-202 */
         th->doff = 6;                                                  /* :205 */
         th->window = htons(8192);
-        th->check = oracle_csum_continue(oracle_pseudo(d->saddr_be, d->daddr_be, htons((uint16_t) (24 + length))),
-                                         (const char *) tcp, (int) (24 + length));   /* :208-209 */
-        if (iphdr) ip->check = oracle_csum_continue(0, (const char *) ip, sizeof(struct iphdr));   /* :179 */
-        if (checks) checks[k] = th->check;
+        uint8_t *op = out + d->out_off;
+        memcpy(op, h.b, 44);
+        if (data) memcpy(op + 44, payload + d->payload_off, length);   /* :190 */
+        const uint16_t c = oracle_csum_continue(oracle_pseudo(d->saddr_be, d->daddr_be,
+                                                              htons((uint16_t) (24 + length))),
+                                                (const char *) op + 20, (int) (24 + length));   /* :208-209 */
+        memcpy(op + 20 + 16, &c, 2);
+        if (iphdr) {                                                   /* :179 */
+            const uint16_t ic = oracle_csum_continue(0, (const char *) op, sizeof(struct iphdr));
+            memcpy(op + 10, &ic, 2);
+        }
+        if (checks) checks[k] = c;
     }
 }
 

@@ -1,0 +1,36 @@
+"""CPU: the host-side C under AddressSanitizer + UndefinedBehaviorSanitizer.
+
+Builds tests/c/sanitize_host.c with the library's scalar drop-ins
+(tcp_amd/csrc/scalar_dropin.c) and the oracle's C restatement
+(oracle/csum_oracle.c) under -fsanitize=address,undefined and runs it: exact-size
+heap buffers make any out-of-bounds byte an error ("ASan/UBSan on
+the host C"). Host code only — GPU sanitizers are not available on this pool.
+"""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.skipif(shutil.which("gcc") is None, reason="gcc not available")
+def test_host_c_under_asan_ubsan(tmp_path):
+    exe = tmp_path / "sanitize_host"
+    cmd = ["gcc", "-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
+           "-fno-sanitize-recover=all", "-Wall", "-Wextra",
+           "-I", os.path.join(REPO, "include"), "-I", os.path.join(REPO, "oracle"),
+           os.path.join(REPO, "tests", "c", "sanitize_host.c"),
+           os.path.join(REPO, "tcp_amd", "csrc", "scalar_dropin.c"),
+           os.path.join(REPO, "oracle", "csum_oracle.c"),
+           "-lpthread", "-o", str(exe)]
+    b = subprocess.run(cmd, capture_output=True, text=True)
+    assert b.returncode == 0, b.stderr
+    env = dict(os.environ)
+    # the environment may preload a library ahead of the ASan runtime: tolerate the link order
+    env["ASAN_OPTIONS"] = "detect_leaks=1:abort_on_error=0:verify_asan_link_order=0"
+    env["UBSAN_OPTIONS"] = "print_stacktrace=1"
+    r = subprocess.run([str(exe)], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "sanitize_host: ok" in r.stdout
