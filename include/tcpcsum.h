@@ -239,6 +239,7 @@ int tcpcsum_plan_uniform(uint64_t base, uint64_t stride, uint32_t len, uint64_t 
 #define TCPCSUM_TUNE_BLOCKED 16  /* contiguous tile runs per wave (non-pipelined lane-group kernels) */
 #define TCPCSUM_TUNE_WIRE_CACHED 32  /* wire: default-policy (not non-temporal) packet loads */
 #define TCPCSUM_TUNE_WIN16 64    /* wire: 16-B (not 128-B) aligned packet windows */
+#define TCPCSUM_TUNE_TX_NT_STORE 128  /* builder: non-temporal payload stores */
 int tcpcsum_set_tuning(int max_blocks, int unroll, int shape, int flags);
 
 #ifdef __cplusplus

@@ -110,7 +110,7 @@ int tcpcsum_device_check(char* arch, size_t arch_len) {
 
 int tcpcsum_set_tuning(int max_blocks, int unroll, int shape, int flags) {
     if (max_blocks < 0 || !(unroll == 0 || unroll == 1 || unroll == 2 || unroll == 4 || unroll == 8) ||
-        shape < -1 || shape > 12 || (flags & ~127) || (flags & 3) == 3 || (flags & 12) == 12)
+        shape < -1 || shape > 12 || (flags & ~255) || (flags & 3) == 3 || (flags & 12) == 12)
         return TCPCSUM_EINVAL;
     g_max_blocks.store(max_blocks);
     g_unroll.store(unroll);

@@ -498,17 +498,17 @@ __global__ __launch_bounds__(256) void k_desc(const uint8_t* __restrict__ base,
 // sums: the lane holding a segment's last chunk in the window adds
 // X[end] - X[run start - 1] to the segment's LDS accumulator.
 
-// Inclusive prefix sum over the 64 lanes: DPP row shifts, then row carries.
+// Inclusive prefix sum over the 64 lanes, all DPP: row shifts 1/2/4/8 scan
+// each row of 16, row_bcast:15 adds row 0's (row 2's) total into row 1 (row 3),
+// row_bcast:31 adds lane 31's running total into rows 2 and 3 (GFX9 DPP).
 __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);   // row_shr:1
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);   // row_shr:2
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);   // row_shr:4
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);   // row_shr:8
-    const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)x, 15);
-    const uint32_t r1 = (uint32_t)__builtin_amdgcn_readlane((int)x, 31);
-    const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)x, 47);
-    const int row = (threadIdx.x & 63) >> 4;
-    return x + (row >= 1 ? r0 : 0u) + (row >= 2 ? r1 : 0u) + (row >= 3 ? r2 : 0u);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);   // row_bcast:15 -> rows 1, 3
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);   // row_bcast:31 -> rows 2, 3
+    return x;
 }
 
 __device__ __forceinline__ uint32_t bperm(uint32_t x, uint32_t src_lane) {
@@ -1113,10 +1113,13 @@ __device__ __forceinline__ void tx_edge_load(const TxPkt& p, int e, u32x4& A, u3
 }
 
 // Phase 1 for a full chunk already loaded: shift into place, store, sum.
+template <bool NTS>
 __device__ __forceinline__ void tx_full_chunk(const TxPkt& p, uint32_t idx, const u32x4 A, const u32x4 B,
                                               uint32_t& wsum, uint32_t& osum) {
     const u32x4 v = funnel16(A, B, (int)(p.sh >> 2), p.sh & 3u);
-    *reinterpret_cast<u32x4*>(p.dbase + (uint64_t)idx * 16u) = v;
+    u32x4* d = reinterpret_cast<u32x4*>(p.dbase + (uint64_t)idx * 16u);
+    if constexpr (NTS) __builtin_nontemporal_store(v, d);
+    else *d = v;
     wsum = sad16(v.x, wsum); wsum = sad16(v.y, wsum);
     wsum = sad16(v.z, wsum); wsum = sad16(v.w, wsum);
     if (p.odd) {
@@ -1193,7 +1196,7 @@ __device__ __forceinline__ void tx_header(const TxPkt& p, uint64_t Spay, int mod
 // descriptor loads, then all payload loads (bulk chunks and both ragged ends)
 // of the tile are issued before any is consumed. Payloads with more full
 // chunks than G*C take extra (un-overlapped) rounds.
-template <int G, int C, int U>
+template <int G, int C, int U, bool NTS>
 __global__ __launch_bounds__(256) void k_tx_build(const uint8_t* __restrict__ payload,
                                                   const tcpcsum_txseg_t* __restrict__ segs, uint64_t n,
                                                   uint8_t* __restrict__ outp, int mode,
@@ -1238,7 +1241,7 @@ __global__ __launch_bounds__(256) void k_tx_build(const uint8_t* __restrict__ pa
 #pragma unroll
             for (int k = 0; k < C; ++k) {
                 const uint32_t idx = p[u].f0 + (uint32_t)(k * G + gl);
-                if (idx < p[u].f1) tx_full_chunk(p[u], idx, A[u][k], B[u][k], wsum, osum);
+                if (idx < p[u].f1) tx_full_chunk<NTS>(p[u], idx, A[u][k], B[u][k], wsum, osum);
             }
             uint64_t W = wsum, O = osum;
             // long payloads: further rounds of G*C full chunks
@@ -1255,7 +1258,7 @@ __global__ __launch_bounds__(256) void k_tx_build(const uint8_t* __restrict__ pa
 #pragma unroll
                 for (int k = 0; k < C; ++k) {
                     const uint32_t idx = rr + (uint32_t)(k * G + gl);
-                    if (idx < p[u].f1) tx_full_chunk(p[u], idx, a2[k], b2[k], ws, os);
+                    if (idx < p[u].f1) tx_full_chunk<NTS>(p[u], idx, a2[k], b2[k], ws, os);
                 }
                 W += ws;
                 O += os;
@@ -1634,10 +1637,13 @@ void launch_ipv4(uint8_t* pkts, const uint64_t* off, uint64_t n, uint32_t cap, u
 
 template <int G, int C, int U>
 static void launch_tx_t(const uint8_t* payload, const tcpcsum_txseg_t* segs, uint64_t n, uint8_t* outp, int mode,
-                        uint16_t* checks, hipStream_t s, int max_blocks) {
+                        uint16_t* checks, hipStream_t s, int max_blocks, bool nts) {
     constexpr int SPT = (64 / G) * U;
-    hipLaunchKernelGGL((k_tx_build<G, C, U>), dim3(grid_for((n + SPT - 1) / SPT, max_blocks)), dim3(256), 0, s,
-                       payload, segs, n, outp, mode, checks);
+    const dim3 grid(grid_for((n + SPT - 1) / SPT, max_blocks));
+    if (nts)
+        hipLaunchKernelGGL((k_tx_build<G, C, U, true>), grid, dim3(256), 0, s, payload, segs, n, outp, mode, checks);
+    else
+        hipLaunchKernelGGL((k_tx_build<G, C, U, false>), grid, dim3(256), 0, s, payload, segs, n, outp, mode, checks);
 }
 
 void launch_tx_build(const uint8_t* payload, const tcpcsum_txseg_t* segs, uint64_t n, uint32_t max_len,
@@ -1645,11 +1651,12 @@ void launch_tx_build(const uint8_t* payload, const tcpcsum_txseg_t* segs, uint64
     const int max_blocks = tu.max_blocks > 0 ? tu.max_blocks : 4096;
     const int unroll = tu.unroll ? tu.unroll : 1;
     const uint64_t nfull = ((uint64_t)max_len + 15u) >> 4;   // full chunks a payload can have
+    const bool nts = (tu.flags & TCPCSUM_TUNE_TX_NT_STORE) != 0;
 #define TX_U(G, C)                                                                         \
     do {                                                                                   \
-        if (unroll <= 1) launch_tx_t<G, C, 1>(payload, segs, n, outp, mode, checks, s, max_blocks); \
-        else if (unroll == 2) launch_tx_t<G, C, 2>(payload, segs, n, outp, mode, checks, s, max_blocks); \
-        else launch_tx_t<G, C, 4>(payload, segs, n, outp, mode, checks, s, max_blocks);    \
+        if (unroll <= 1) launch_tx_t<G, C, 1>(payload, segs, n, outp, mode, checks, s, max_blocks, nts); \
+        else if (unroll == 2) launch_tx_t<G, C, 2>(payload, segs, n, outp, mode, checks, s, max_blocks, nts); \
+        else launch_tx_t<G, C, 4>(payload, segs, n, outp, mode, checks, s, max_blocks, nts);    \
     } while (0)
     int shape = nfull <= 8 ? 0 : nfull <= 96 ? 2 : 4;
     if (tu.shape >= 0 && tu.shape <= 4) shape = tu.shape;   // any shape is correct (extra rounds)

@@ -100,7 +100,7 @@ def test_argument_errors_need_no_device():
     assert L.tcpcsum_set_tuning(0, 0, 13, 0) == api.EINVAL
     assert L.tcpcsum_set_tuning(0, 0, -1, 3) == api.EINVAL      # PIPE_ON | PIPE_OFF
     assert L.tcpcsum_set_tuning(0, 0, -1, 12) == api.EINVAL     # NT_ON | NT_OFF
-    assert L.tcpcsum_set_tuning(0, 0, -1, 128) == api.EINVAL
+    assert L.tcpcsum_set_tuning(0, 0, -1, 256) == api.EINVAL
     assert L.tcpcsum_set_tuning(0, 0, -1, 0) == api.OK
     assert L.tcpcsum_batch_uniform_host(None, None, 0, 0, None, 0, None, 0) == api.EINVAL
     assert L.tcpcsum_strerror(api.EHIP) == b"HIP runtime error"

@@ -405,11 +405,12 @@ def test_tx_build_vs_oracle(dev, layout):
     oracle.tx_build(payload, segs, want)
     dpay, dseg = to_dev(payload, dev), to_dev(segs.view(np.uint8), dev)
     try:
-        for shape, unroll, hint in ((-1, 0, 16), (0, 2, max_len), (1, 4, max_len), (3, 1, max_len), (4, 2, 64)):
-            tcp_amd.set_tuning(0, unroll, shape, 0)
+        for shape, unroll, hint, fl in ((-1, 0, 16, 0), (0, 2, max_len, 0), (1, 4, max_len, 0), (3, 1, max_len, 0),
+                                        (4, 2, 64, 0), (-1, 0, max_len, 128), (2, 2, max_len, 128)):
+            tcp_amd.set_tuning(0, unroll, shape, fl)   # 128: non-temporal payload stores
             dout = to_dev(garbage, dev)
             tcp_amd.tx_build(dpay, dseg, n, hint, dout, 0, None)
-            assert np.array_equal(dout.cpu().numpy(), want), (shape, unroll, hint)
+            assert np.array_equal(dout.cpu().numpy(), want), (shape, unroll, hint, fl)
     finally:
         tcp_amd.set_tuning(0, 0, -1, 0)
 

@@ -62,8 +62,20 @@ def main():
                                   "ms": round(tt * 1e3, 4),
                                   "GB/s": round((n * L + n * (L + 44) + n * 48) / tt / 1e9, 1)}), flush=True)
         tcp_amd.set_tuning(0, 0, -1, 0)
-    t = timeit(lambda: tcp_amd.tx_build(payload, dsegs, n, L, out, 0, chk))
+    # store policy: default vs non-temporal payload stores, interleaved rounds
     moved = n * L + n * (L + 44) + n * 48
+    pol = {0: [], 128: []}
+    for _ in range(5):
+        for fl in pol:
+            tcp_amd.set_tuning(0, 0, -1, fl)
+            pol[fl].append(timeit(lambda: tcp_amd.tx_build(payload, dsegs, n, L, out, 0, chk), 20))
+    tcp_amd.set_tuning(0, 0, -1, 0)
+    for fl, ts in pol.items():
+        ts.sort()
+        print(json.dumps({"measure": "tx_build_store_policy", "flags": fl, "nt_stores": fl == 128,
+                          "ms_median": round(ts[2] * 1e3, 4), "ms_min": round(ts[0] * 1e3, 4),
+                          "GB/s_read+write": round(moved / ts[2] / 1e9, 1)}), flush=True)
+    t = timeit(lambda: tcp_amd.tx_build(payload, dsegs, n, L, out, 0, chk))
     print(json.dumps({"measure": "tx_build_1Mx1456B", "kernel_ms": round(t * 1e3, 4),
                       "Mpkt/s": round(n / t / 1e6, 1), "GB/s_read+write": round(moved / t / 1e9, 1),
                       "frac_of_8TB/s": round(moved / t / 8e12, 4)}), flush=True)
