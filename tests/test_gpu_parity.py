@@ -630,3 +630,35 @@ def test_desc_balanced_long_segments(dev, shape):
     finally:
         tcp_amd.set_tuning(0, 0, -1, 0)
     assert np.array_equal(got, want)
+
+
+def test_host_context_staging_reuse_and_null_outputs(dev):
+    """One context across wire batches of growing / shrinking size (its pinned staging of offsets,
+    results and status is reallocated and reused), pageable and pinned regions, and the C ABI's
+    NULL h_out / h_status (FILL still patches the packets)."""
+    import ctypes
+    import tcp_amd
+    from tests.packets import build_batch
+    rng = np.random.default_rng(515)
+    with tcp_amd.HostContext(0) as ctx:
+        for n, pinned in ((100, False), (3000, True), (1500, False), (5000, False), (7, True)):
+            region, off, _ = build_batch(rng, n, slot=1536, malformed=True, max_payload=1400)
+            ref = region.copy()
+            want_out, want_st = oracle.ipv4_batch(ref, off, 1536, tcp_amd.IPV4_FILL)
+            buf = region
+            if pinned:
+                buf = tcp_amd.pinned_empty(region.size)
+                buf[:] = region
+            out, st = ctx.ipv4_batch(buf, off, 1536, tcp_amd.IPV4_FILL)
+            assert np.array_equal(st, want_st) and np.array_equal(out, want_out), (n, pinned)
+            assert np.array_equal(np.asarray(buf), ref), (n, pinned)
+        # NULL outputs through the raw ABI
+        region, off, _ = build_batch(rng, 800, slot=1536, malformed=True)
+        ref = region.copy()
+        oracle.ipv4_batch(ref, off, 1536, tcp_amd.IPV4_FILL | tcp_amd.IPV4_IPHDR)
+        off = np.ascontiguousarray(off, np.uint64)
+        rc = tcp_amd.lib().tcpcsum_ipv4_batch_host(ctx._h, region.ctypes.data, region.nbytes, off.ctypes.data,
+                                                   off.size, 1536, tcp_amd.IPV4_FILL | tcp_amd.IPV4_IPHDR,
+                                                   None, None)
+        assert rc == 0
+        assert np.array_equal(region, ref)
