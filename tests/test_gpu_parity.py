@@ -454,9 +454,11 @@ def test_flat_tiles_vs_oracle(dev, unroll):
         tcp_amd.set_tuning(0, 0, -1, 0)
 
 
-def test_ipv4_region_bounds(dev):
+@pytest.mark.parametrize("shape", [-1, 8, 9])
+def test_ipv4_region_bounds(dev, shape):
     """Reads never leave the region: a packet whose tot_len runs past it is skipped, offsets at the
-    very end (no room for a header) are skipped, and the rest is still exact."""
+    very end (no room for a header) are skipped, and the rest is still exact (lane-group and
+    balanced kernels)."""
     import tcp_amd
     from tests.packets import ip_packet
     rng = np.random.default_rng(5)
@@ -479,7 +481,11 @@ def test_ipv4_region_bounds(dev):
     dreg = to_dev(region, dev)
     out = torch.empty(off.size, dtype=torch.int16, device=dev)
     st = torch.empty(off.size, dtype=torch.uint8, device=dev)
-    tcp_amd.ipv4_batch(dreg, to_dev(off.view(np.int64), dev), off.size, 32768, tcp_amd.IPV4_FILL, out, st)
+    tcp_amd.set_tuning(0, 0, shape, 0)
+    try:
+        tcp_amd.ipv4_batch(dreg, to_dev(off.view(np.int64), dev), off.size, 32768, tcp_amd.IPV4_FILL, out, st)
+    finally:
+        tcp_amd.set_tuning(0, 0, -1, 0)
     assert np.array_equal(st.cpu().numpy(), want_st)
     assert np.array_equal(u16(out)[:-3], want_out[:-3])
 
@@ -662,3 +668,32 @@ def test_host_context_staging_reuse_and_null_outputs(dev):
                                                    None, None)
         assert rc == 0
         assert np.array_equal(region, ref)
+
+
+@pytest.mark.parametrize("shape", [7, 8])
+def test_desc_balanced_tile_edges(dev, shape):
+    """Balanced ragged kernel at tile edges: n = 1, 63, 64, 65, 129 segments; all-empty tiles; a
+    single segment spanning many windows; segments sharing bytes (overlapping descriptors)."""
+    import tcp_amd
+    rng = np.random.default_rng(shape)
+    size = 1 << 20
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    d = to_dev(host, dev)
+    cases = []
+    for n in (1, 63, 64, 65, 129):
+        lens = rng.integers(0, 3000, n).astype(np.uint32)
+        cases.append(lens)
+    cases.append(np.zeros(130, np.uint32))                       # nothing to sum
+    cases.append(np.array([0] * 10 + [200000] + [0] * 60, np.uint32))   # one long segment
+    for lens in cases:
+        n = lens.size
+        off = np.array([rng.integers(0, size - l) for l in lens], np.uint64)
+        if n > 3:
+            off[1] = off[0]                                      # identical / overlapping descriptors
+        ss = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+        tcp_amd.set_tuning(0, 0, shape, 0)
+        try:
+            got = u16(tcp_amd.batch_desc(d, to_dev(_desc(off, lens, ss), dev), n, int(max(lens.max(), 1))))
+        finally:
+            tcp_amd.set_tuning(0, 0, -1, 0)
+        assert np.array_equal(got, oracle.batch_desc(host, off, lens, ss)), n
