@@ -858,14 +858,20 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const 
         for (int k = 0; k < C; ++k) {
             const int32_t pos = (int32_t)((uint32_t)(k * G + gl) * 16u) - (int32_t)m;   // chunk start, packet-relative
             const u32x4 x = v[u][k];
-            if (pos >= (int32_t)th && pos + 16 <= (int32_t)tot) {
-                w = sad16(x.x, w); w = sad16(x.y, w); w = sad16(x.z, w); w = sad16(x.w, w);
-                if (odd) {
-                    o = sad8(x.x & 0xff00ff00u, o); o = sad8(x.y & 0xff00ff00u, o);
-                    o = sad8(x.z & 0xff00ff00u, o); o = sad8(x.w & 0xff00ff00u, o);
-                }
-            } else if (pos + 16 > (int32_t)th && pos < (int32_t)tot) {
-                chunk_wo_bytes(x, (int64_t)pos - th, (int64_t)(tot - th), odd, w, o);
+            // whole chunks of [th, tot): no masks (select the chunk's sum in or out)
+            const bool full = pos >= (int32_t)th && pos + 16 <= (int32_t)tot;
+            const uint32_t wk = sad16(x.w, sad16(x.z, sad16(x.y, sad16(x.x, 0u))));
+            w += full ? wk : 0u;
+            if (odd) {
+                const uint32_t ok8 = sad8(x.w & 0xff00ff00u, sad8(x.z & 0xff00ff00u,
+                                          sad8(x.y & 0xff00ff00u, sad8(x.x & 0xff00ff00u, 0u))));
+                o += full ? ok8 : 0u;
+            }
+            // the (at most two) edge chunks of a packet: masked, behind a wave-uniform
+            // branch — on MTU slots only one or two of the C rounds hold any
+            const bool part = !full && pos + 16 > (int32_t)th && pos < (int32_t)tot;
+            if (__builtin_amdgcn_ballot_w64(part) != 0) {
+                if (part) chunk_wo_bytes(x, (int64_t)pos - th, (int64_t)(tot - th), odd, w, o);
             }
             if (iphdr && pos < (int32_t)th) chunk_wo_bytes(x, (int64_t)pos, (int64_t)th, odd, wi, oi);
         }
