@@ -3,6 +3,7 @@
 #   oracle/build/liboracle.so  test infrastructure: C restatement, -O2 -g
 #   oracle/build/liboracle_O0.so  same at -O0 -g (the reference Makefile's flags)
 #   tests/c/abi_smoke          C program that links the ABI (C-callable proof)
+#   tools/mmsg_bench           sendmmsg-seam latency on the reference's buffer layout
 ROCM ?= /opt/rocm
 HIPCC ?= $(ROCM)/bin/hipcc
 CC ?= gcc
@@ -21,7 +22,7 @@ OBJDIR := build/obj
 
 PRELOAD := tcp_amd/libtcpcsum_preload.so
 
-all: $(LIB) $(PRELOAD) oracle tests/c/abi_smoke tests/c/mmsg_loop
+all: $(LIB) $(PRELOAD) oracle tests/c/abi_smoke tests/c/mmsg_loop tools/mmsg_bench
 
 $(OBJDIR)/%.o: tcp_amd/csrc/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
@@ -55,7 +56,10 @@ tests/c/abi_smoke: tests/c/abi_smoke.c include/tcpcsum.h $(LIB)
 tests/c/mmsg_loop: tests/c/mmsg_loop.c include/tcpcsum.h $(LIB)
 	$(CC) -O2 -Wall -Wextra -Iinclude -o $@ $< -Ltcp_amd -ltcpcsum -Wl,-rpath,'$$ORIGIN/../../tcp_amd'
 
+tools/mmsg_bench: tools/mmsg_bench.c include/tcpcsum.h $(LIB)
+	$(CC) -O2 -Wall -Wextra -Iinclude -o $@ $< -Ltcp_amd -ltcpcsum -Wl,-rpath,'$$ORIGIN/../tcp_amd'
+
 clean:
-	rm -rf build oracle/build $(LIB) $(PRELOAD) tests/c/abi_smoke tests/c/mmsg_loop
+	rm -rf build oracle/build $(LIB) $(PRELOAD) tests/c/abi_smoke tests/c/mmsg_loop tools/mmsg_bench
 
 .PHONY: all oracle clean

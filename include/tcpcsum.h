@@ -20,9 +20,12 @@
  *   - "stream" is a hipStream_t passed as void* (NULL = the default stream).
  *     Batch calls are asynchronous on that stream; the caller synchronises.
  *   - d_* pointers are device (or device-accessible) memory; h_* are host.
- *   - Return 0 on success or a negative TCPCSUM_E* code. No global state
- *     beyond what tcpcsum_ctx_* owns; no call keeps a pointer after it returns
- *     (async calls: until the stream reaches that point).
+ *   - Return 0 on success or a negative TCPCSUM_E* code. No mutable global
+ *     state: launch shapes come from an explicit per-call tcpcsum_tuning_t
+ *     (NULL = built-in defaults) or from the tcpcsum_ctx_t they run in; no
+ *     call keeps a pointer after it returns (async calls: until the stream
+ *     reaches that point), except the host-buffer registrations a context
+ *     holds (tcpcsum_ipv4_batch_ptrs_host).
  *   - The caller owns every buffer.
  *   - The batch API covers sum_start < 2^32 (getPseudoHeaderSum returns at
  *     most 6 * 0xFFFF) and segment lengths <= INT32_MAX (csum_continue's
@@ -44,7 +47,20 @@ extern "C" {
 #define TCPCSUM_EHIP (-3)     /* a HIP call failed (tcpcsum_last_hip_error) */
 #define TCPCSUM_ENOMEM (-4)   /* allocation failed */
 
-#define TCPCSUM_ABI_VERSION 1
+#define TCPCSUM_ABI_VERSION 2
+
+/* Launch-shape override, passed per call (NULL = the built-in shapes measured
+ * on MI355X). Fields: max_blocks (0 = per-shape default, else
+ * the resident grid), unroll in {0,1,2,4,8} (0 = default; segments in flight
+ * per lane group), shape in {-1, 0..12} (-1 = auto; meaning per entry point,
+ * see TCPCSUM_TUNE_* below), flags = TCPCSUM_TUNE_* bits (0 = defaults).
+ * Every entry point taking one returns TCPCSUM_EINVAL for an invalid value. */
+typedef struct tcpcsum_tuning {
+    int32_t max_blocks;
+    int32_t unroll;
+    int32_t shape;
+    int32_t flags;
+} tcpcsum_tuning_t;
 
 /* Ragged-batch descriptor: segment = d_base[offset .. offset+len). 16 bytes. */
 typedef struct tcpcsum_desc {
@@ -99,14 +115,14 @@ unsigned short tcpcsum_continue(unsigned long sum_start, const char *p, int nbyt
  * Replaces the per-packet call at context.c:208-209 for a whole batch. */
 int tcpcsum_batch_uniform_dev(const void *d_base, uint64_t stride, uint32_t len,
                               const uint32_t *d_sum_start, uint32_t sum_start,
-                              uint16_t *d_out, uint64_t n, void *stream);
+                              uint16_t *d_out, uint64_t n, void *stream, const tcpcsum_tuning_t *tune);
 
 /* Ragged layout: segment i = d_base[d_desc[i].offset .. +d_desc[i].len).
  * max_len: an upper bound on every d_desc[i].len (picks the kernel shape;
  * segments longer than max_len are still summed correctly, only slower).
  * d_out[i] = csum_continue(d_desc[i].sum_start, segment_i, d_desc[i].len). */
 int tcpcsum_batch_desc_dev(const void *d_base, const tcpcsum_desc_t *d_desc, uint64_t n,
-                           uint32_t max_len, uint16_t *d_out, void *stream);
+                           uint32_t max_len, uint16_t *d_out, void *stream, const tcpcsum_tuning_t *tune);
 
 /* Wire layout (the loop's out-buffers, loop.c:107-116 / releaseSend
  * loop.c:27-94): packet i is a raw IPv4 packet at d_pkts + d_pkt_off[i], of
@@ -122,7 +138,19 @@ int tcpcsum_batch_desc_dev(const void *d_base, const tcpcsum_desc_t *d_desc, uin
  * off + tot_len > region_bytes); skipped packets are left untouched and
  * d_out[i] = 0. */
 int tcpcsum_ipv4_batch_dev(void *d_pkts, uint64_t region_bytes, const uint64_t *d_pkt_off, uint64_t n,
-                           uint32_t cap, int mode, uint16_t *d_out, uint8_t *d_status, void *stream);
+                           uint32_t cap, int mode, uint16_t *d_out, uint8_t *d_status, void *stream,
+                           const tcpcsum_tuning_t *tune);
+
+/* Scatter-gather wire batch: packet i is a raw IPv4 packet at the
+ * device-accessible address d_pkt_ptrs[i] (HBM, or page-locked / registered
+ * host memory read over PCIe), with d_lens[i] readable bytes there (the
+ * iov_len / msg_len of its message; the kernel never reads past it, and a
+ * packet with tot_len > d_lens[i] or d_lens[i] < 20 is SKIPPED). cap, modes,
+ * results and status exactly as tcpcsum_ipv4_batch_dev. This is the
+ * loop's own layout — one separate out-buffer per packet (loop.c:180-183,
+ * iov_base per message at loop.c:53-54) — with no gather copy. */
+int tcpcsum_ipv4_batch_ptrs_dev(void *const *d_pkt_ptrs, const uint32_t *d_lens, uint64_t n, uint32_t cap, int mode,
+                                uint16_t *d_out, uint8_t *d_status, void *stream, const tcpcsum_tuning_t *tune);
 
 /* Segment assembly + checksum in one pass (device-side
  * us_internal_socket_context_send_packet, context.c:150-213, minus its 10 %
@@ -158,7 +186,8 @@ typedef struct tcpcsum_txseg {
  * TCP checks, also stored in the packets. Segments with len > 65491 are not
  * written (d_check = 0). Packets must not overlap; d_segs 16-B aligned. */
 int tcpcsum_tx_build_dev(const void *d_payload, const tcpcsum_txseg_t *d_segs, uint64_t n, uint32_t max_len,
-                         void *d_out_pkts, int mode, uint16_t *d_check, void *stream);
+                         void *d_out_pkts, int mode, uint16_t *d_check, void *stream,
+                         const tcpcsum_tuning_t *tune);
 
 /* ------------------------------------------------------ host-memory batches
  * The path as the reference sees it: segments start and end in host memory
@@ -169,6 +198,10 @@ typedef struct tcpcsum_ctx tcpcsum_ctx_t;
 /* scratch_bytes: device staging size per pipeline slot (0 = 64 MiB). */
 int tcpcsum_ctx_create(int device, size_t scratch_bytes, tcpcsum_ctx_t **out);
 void tcpcsum_ctx_destroy(tcpcsum_ctx_t *ctx);
+
+/* Launch shapes for this context's batches (NULL = built-in defaults). Only
+ * this context is affected; other contexts and the device calls are not. */
+int tcpcsum_ctx_set_tuning(tcpcsum_ctx_t *ctx, const tcpcsum_tuning_t *tune);
 
 /* Page-locked host memory for packet pools: copies from it are plain DMA
  * (pageable memory is staged by the runtime). NULL on failure. */
@@ -188,6 +221,29 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t *ctx, const void *h_base, uint64_t 
 int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t *ctx, void *h_pkts, size_t region_bytes,
                             const uint64_t *h_pkt_off, uint64_t n, uint32_t cap, int mode,
                             uint16_t *h_out, uint8_t *h_status);
+
+/* Wire batch over the caller's own per-packet buffers (the reference's
+ * layout: 1024 separately malloc'd 32 KiB out-buffers, loop.c:180-183, one
+ * iov_base per message, loop.c:53-54): packet i at h_pkts[i] with h_lens[i]
+ * readable bytes. Pageable buffers are page-locked with hipHostRegister on
+ * first use and stay registered with the context (cached; later batches over
+ * the same buffers cost no registration) until tcpcsum_ctx_unregister_host or
+ * tcpcsum_ctx_destroy: the caller must not release those pages to the OS
+ * (free() of a registered buffer) before then. The kernel reads the packets in
+ * host memory over PCIe and FILL stores each check in place — no CPU pass over
+ * packet bytes and no staging copy. Synchronous. */
+int tcpcsum_ipv4_batch_ptrs_host(tcpcsum_ctx_t *ctx, void *const *h_pkts, const uint32_t *h_lens, uint64_t n,
+                                 int mode, uint16_t *h_out, uint8_t *h_status);
+
+/* Page-lock [p, p+bytes) for this context ahead of time (what the first
+ * tcpcsum_ipv4_batch_ptrs_host over it would do), e.g. once per pool buffer at
+ * loop.c:180-183. */
+int tcpcsum_ctx_register_host(tcpcsum_ctx_t *ctx, void *p, size_t bytes);
+/* Drop every registration of this context that overlaps [p, p+bytes)
+ * (p = NULL: all of them). Call before freeing registered buffers. */
+int tcpcsum_ctx_unregister_host(tcpcsum_ctx_t *ctx, void *p, size_t bytes);
+/* Host memory this context has page-locked: ranges and bytes (either may be NULL). */
+int tcpcsum_ctx_registered(tcpcsum_ctx_t *ctx, uint64_t *ranges, uint64_t *bytes);
 
 /* ------------------------------------------------------ synthetic workload
  * Device-side generation of the SURVEY.md Appendix B batches, so benchmarks
@@ -210,7 +266,7 @@ int tcpcsum_synth_pseudo_dev(uint32_t *d_sum_start, uint64_t seg0, uint64_t n, u
  * u32 word of d_src. nbytes multiple of 16, d_src 16-B aligned. */
 #define TCPCSUM_PROBE_SLOTS 8192
 int tcpcsum_stream_probe_dev(const void *d_src, uint64_t nbytes, uint64_t *d_partials,
-                             int *n_partials, void *stream);
+                             int *n_partials, void *stream, const tcpcsum_tuning_t *tune);
 
 /* Host-side planning only (no device work): the kernel the library would use
  * for a uniform batch at device address base. mode: 0 = 16-B aligned, 1 =
@@ -220,17 +276,14 @@ int tcpcsum_stream_probe_dev(const void *d_src, uint64_t nbytes, uint64_t *d_par
  * tiles (contiguous 1 KiB per load instruction; 1-32 KiB segments, 4-B
  * aligned, stride >= len);
  * unroll: segments in flight per lane group; max_blocks: resident grid. */
-int tcpcsum_plan_uniform(uint64_t base, uint64_t stride, uint32_t len, uint64_t n, int *mode,
-                         int *shape, int *unroll, int *max_blocks);
+int tcpcsum_plan_uniform(uint64_t base, uint64_t stride, uint32_t len, uint64_t n,
+                         const tcpcsum_tuning_t *tune, int *mode, int *shape, int *unroll, int *max_blocks);
 
-/* Launch-shape override for tuning (tools/sweep.py). 0 / -1 = built-in
- * per-shape defaults. unroll in {0,1,2,4,8}; shape in {-1, 0..12}, read per
- * launcher: uniform 0..12 (a forced shape that cannot cover the segments is
+/* tcpcsum_tuning_t.shape, read per entry point: uniform 0..12 (a forced shape that cannot cover the segments is
  * ignored), ragged 0..6 = (G,C) (4,1) (8,1) (16,1) (32,1) (32,3) (64,4) (64,8)
  * and 7..8 = balanced chunk space (4 / 8 loads per lane in flight),
  * wire 0..7 = (8,1) (32,3) (64,4) (16,2) (16,6) (8,12) (8,2) (8,4) and 8..9 =
- * balanced (4 / 8 loads per lane), builder 0..4; flags: TCPCSUM_TUNE_*
- * bits (0 = defaults). Affects batch calls issued afterwards from any thread. */
+ * balanced (4 / 8 loads per lane), builder 0..4. tcpcsum_tuning_t.flags: */
 /* PIPE_* and NT_* take effect only in a library built with TUNING_VARIANTS=1 */
 #define TCPCSUM_TUNE_PIPE_ON 1   /* software-pipelined tiles */
 #define TCPCSUM_TUNE_PIPE_OFF 2
@@ -240,7 +293,8 @@ int tcpcsum_plan_uniform(uint64_t base, uint64_t stride, uint32_t len, uint64_t 
 #define TCPCSUM_TUNE_WIRE_CACHED 32  /* wire: default-policy (not non-temporal) packet loads */
 #define TCPCSUM_TUNE_WIN16 64    /* wire: 16-B (not 128-B) aligned packet windows */
 #define TCPCSUM_TUNE_TX_NT_STORE 128  /* builder: non-temporal payload stores */
-int tcpcsum_set_tuning(int max_blocks, int unroll, int shape, int flags);
+/* 0 if *tune is a valid tuning (NULL counts as valid), else TCPCSUM_EINVAL. */
+int tcpcsum_tuning_check(const tcpcsum_tuning_t *tune);
 
 #ifdef __cplusplus
 }

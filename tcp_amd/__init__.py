@@ -9,7 +9,7 @@ Reference path (``/root/reference``):
   * ``context.c:104-119`` getPseudoHeaderSum -> :func:`getPseudoHeaderSum`
   * ``context.c:121-145`` csum_continue      -> :func:`csum_continue` (scalar) and
     the batch entry points (:func:`batch_uniform`, :func:`batch_desc`,
-    :func:`ipv4_batch`) that replace the per-packet call at ``context.c:208-209``
+    :func:`ipv4_batch`, :func:`ipv4_batch_ptrs`) that replace the per-packet call at ``context.c:208-209``
     with one GPU launch per batch (the ``releaseSend`` seam, ``loop.c:27-94``).
 """
 from __future__ import annotations
@@ -32,10 +32,13 @@ from .api import (  # noqa: F401
     device_check,
     getPseudoHeaderSum,
     ipv4_batch,
+    ipv4_batch_ptrs,
     lib,
     lib_path,
     pinned_empty,
+    make_tuning,
     set_tuning,
+    Tuning,
     stream_probe,
     synth_fill,
     synth_pseudo,
@@ -46,6 +49,7 @@ from .api import (  # noqa: F401
 __all__ = [
     "DESC_DTYPE", "IPV4_FILL", "IPV4_IPHDR", "PKT_IPHDR_BAD", "IPV4_VERIFY", "PKT_OK", "PKT_SKIPPED", "TcpCsumError",
     "HostContext", "batch_desc", "batch_uniform", "csum_continue", "device_check",
-    "getPseudoHeaderSum", "ipv4_batch", "lib", "lib_path", "pinned_empty", "set_tuning", "stream_probe",
+    "getPseudoHeaderSum", "ipv4_batch", "ipv4_batch_ptrs", "lib", "lib_path", "make_tuning", "pinned_empty",
+    "set_tuning", "Tuning", "stream_probe",
     "synth_fill", "synth_pseudo", "tx_build", "TXSEG_DTYPE",
 ]

@@ -71,6 +71,15 @@ vp = ctypes.c_void_p
 u32 = ctypes.c_uint32
 u64 = ctypes.c_uint64
 
+
+class Tuning(ctypes.Structure):
+    """tcpcsum_tuning_t: a launch-shape override passed per call (None = built-in shapes)."""
+    _fields_ = [("max_blocks", ctypes.c_int32), ("unroll", ctypes.c_int32), ("shape", ctypes.c_int32),
+                ("flags", ctypes.c_int32)]
+
+
+tunep = ctypes.POINTER(Tuning)
+
 # name -> (restype, argtypes); must cover every function in include/tcpcsum.h
 SIGNATURES = {
     "tcpcsum_abi_version": (ctypes.c_int, []),
@@ -79,21 +88,27 @@ SIGNATURES = {
     "tcpcsum_device_check": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t]),
     "tcpcsum_pseudo": (ctypes.c_ulong, [u32, u32, ctypes.c_uint16]),
     "tcpcsum_continue": (ctypes.c_ushort, [ctypes.c_ulong, ctypes.c_char_p, ctypes.c_int]),
-    "tcpcsum_batch_uniform_dev": (ctypes.c_int, [vp, u64, u32, vp, u32, vp, u64, vp]),
-    "tcpcsum_batch_desc_dev": (ctypes.c_int, [vp, vp, u64, u32, vp, vp]),
-    "tcpcsum_ipv4_batch_dev": (ctypes.c_int, [vp, u64, vp, u64, u32, ctypes.c_int, vp, vp, vp]),
+    "tcpcsum_batch_uniform_dev": (ctypes.c_int, [vp, u64, u32, vp, u32, vp, u64, vp, tunep]),
+    "tcpcsum_batch_desc_dev": (ctypes.c_int, [vp, vp, u64, u32, vp, vp, tunep]),
+    "tcpcsum_ipv4_batch_dev": (ctypes.c_int, [vp, u64, vp, u64, u32, ctypes.c_int, vp, vp, vp, tunep]),
+    "tcpcsum_ipv4_batch_ptrs_dev": (ctypes.c_int, [vp, vp, u64, u32, ctypes.c_int, vp, vp, vp, tunep]),
     "tcpcsum_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_size_t, ctypes.POINTER(vp)]),
     "tcpcsum_ctx_destroy": (None, [vp]),
+    "tcpcsum_ctx_set_tuning": (ctypes.c_int, [vp, tunep]),
     "tcpcsum_host_alloc": (vp, [ctypes.c_size_t]),
     "tcpcsum_host_free": (None, [vp]),
     "tcpcsum_batch_uniform_host": (ctypes.c_int, [vp, vp, u64, u32, vp, u32, vp, u64]),
     "tcpcsum_ipv4_batch_host": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp, u64, u32, ctypes.c_int, vp, vp]),
-    "tcpcsum_tx_build_dev": (ctypes.c_int, [vp, vp, u64, u32, vp, ctypes.c_int, vp, vp]),
+    "tcpcsum_ipv4_batch_ptrs_host": (ctypes.c_int, [vp, vp, vp, u64, ctypes.c_int, vp, vp]),
+    "tcpcsum_ctx_register_host": (ctypes.c_int, [vp, vp, ctypes.c_size_t]),
+    "tcpcsum_ctx_unregister_host": (ctypes.c_int, [vp, vp, ctypes.c_size_t]),
+    "tcpcsum_ctx_registered": (ctypes.c_int, [vp, c_u64p, c_u64p]),
+    "tcpcsum_tx_build_dev": (ctypes.c_int, [vp, vp, u64, u32, vp, ctypes.c_int, vp, vp, tunep]),
     "tcpcsum_synth_fill_dev": (ctypes.c_int, [vp, u64, u64, vp]),
     "tcpcsum_synth_pseudo_dev": (ctypes.c_int, [vp, u64, u64, u32, vp]),
-    "tcpcsum_stream_probe_dev": (ctypes.c_int, [vp, u64, vp, ctypes.POINTER(ctypes.c_int), vp]),
-    "tcpcsum_set_tuning": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
-    "tcpcsum_plan_uniform": (ctypes.c_int, [u64, u64, u32, u64, ctypes.POINTER(ctypes.c_int),
+    "tcpcsum_stream_probe_dev": (ctypes.c_int, [vp, u64, vp, ctypes.POINTER(ctypes.c_int), vp, tunep]),
+    "tcpcsum_tuning_check": (ctypes.c_int, [tunep]),
+    "tcpcsum_plan_uniform": (ctypes.c_int, [u64, u64, u32, u64, tunep, ctypes.POINTER(ctypes.c_int),
                                             ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                                             ctypes.POINTER(ctypes.c_int)]),
 }
@@ -155,15 +170,48 @@ TUNE_PIPE_ON, TUNE_PIPE_OFF, TUNE_NT_ON, TUNE_NT_OFF = 1, 2, 4, 8
 TUNE_WIRE_CACHED, TUNE_WIN16 = 32, 64   # wire kernel variants (tcpcsum.h)
 
 
+# The C library holds no tuning state: every device call takes an explicit
+# tcpcsum_tuning_t* (NULL = built-in shapes). For the test / tool front end the
+# wrappers below pass `tune=` when given, else this thread's default set with
+# set_tuning() — per thread, so one thread's sweep never reshapes another's.
+_tls = threading.local()
+
+
+def make_tuning(max_blocks: int = 0, unroll: int = 0, shape: int = -1, flags: int = 0) -> Optional[Tuning]:
+    """A validated Tuning, or None for the built-in shapes (all defaults)."""
+    t = Tuning(int(max_blocks), int(unroll), int(shape), int(flags))
+    _check(lib().tcpcsum_tuning_check(ctypes.byref(t)), "tcpcsum_tuning_check")
+    if (t.max_blocks, t.unroll, t.shape, t.flags) == (0, 0, -1, 0):
+        return None
+    return t
+
+
 def set_tuning(max_blocks: int = 0, unroll: int = 0, shape: int = -1, flags: int = 0) -> None:
-    _check(lib().tcpcsum_set_tuning(int(max_blocks), int(unroll), int(shape), int(flags)), "tcpcsum_set_tuning")
+    """This thread's default tuning for the wrappers (raises TcpCsumError on invalid values)."""
+    _tls.tune = make_tuning(max_blocks, unroll, shape, flags)
 
 
-def plan_uniform(base_addr: int, stride: int, length: int, n: int) -> tuple[int, int, int, int]:
+def get_tuning() -> Optional[Tuning]:
+    return getattr(_tls, "tune", None)
+
+
+def _tune(tune):
+    t = get_tuning() if tune is None else tune
+    if t is None:
+        return None
+    if isinstance(t, tuple):
+        t = make_tuning(*t)
+        if t is None:
+            return None
+    return ctypes.byref(t)
+
+
+def plan_uniform(base_addr: int, stride: int, length: int, n: int, tune=None) -> tuple[int, int, int, int]:
     """(mode, shape, unroll, max_blocks) the library picks for a uniform batch — host logic only."""
     mode, shape, unroll, mb = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-    _check(lib().tcpcsum_plan_uniform(base_addr, stride, length, n, ctypes.byref(mode), ctypes.byref(shape),
-                                      ctypes.byref(unroll), ctypes.byref(mb)), "tcpcsum_plan_uniform")
+    _check(lib().tcpcsum_plan_uniform(base_addr, stride, length, n, _tune(tune), ctypes.byref(mode),
+                                      ctypes.byref(shape), ctypes.byref(unroll), ctypes.byref(mb)),
+           "tcpcsum_plan_uniform")
     return mode.value, shape.value, unroll.value, mb.value
 
 
@@ -185,7 +233,7 @@ def _dev_ptr(t, what: str) -> int:
 
 
 def batch_uniform(data, stride: int, length: int, n: int, sum_start=0, out=None, offset: int = 0,
-                  stream=None):
+                  stream=None, tune=None):
     """d_out[i] = csum_continue(start_i, data[offset+i*stride : +length], length) on the GPU.
 
     ``sum_start``: an int (same start for every segment) or a device int32 tensor of n entries.
@@ -203,36 +251,47 @@ def batch_uniform(data, stride: int, length: int, n: int, sum_start=0, out=None,
             raise ValueError("sum_start too short")
         ss_ptr, ss0 = _dev_ptr(sum_start, "sum_start"), 0
     rc = lib().tcpcsum_batch_uniform_dev(_dev_ptr(data, "data") + offset, stride, length, ss_ptr, ss0,
-                                         _dev_ptr(out, "out"), n, _stream_handle(stream))
+                                         _dev_ptr(out, "out"), n, _stream_handle(stream), _tune(tune))
     _check(rc, "tcpcsum_batch_uniform_dev")
     return out
 
 
-def batch_desc(data, desc, n: int, max_len: int, out=None, stream=None):
+def batch_desc(data, desc, n: int, max_len: int, out=None, stream=None, tune=None):
     """Ragged batch; ``desc`` is a device uint8/int64 tensor holding n tcpcsum_desc_t records."""
     if out is None:
         out = torch.empty(n, dtype=torch.int16, device=data.device)
     rc = lib().tcpcsum_batch_desc_dev(_dev_ptr(data, "data"), _dev_ptr(desc, "desc"), n, max_len,
-                                      _dev_ptr(out, "out"), _stream_handle(stream))
+                                      _dev_ptr(out, "out"), _stream_handle(stream), _tune(tune))
     _check(rc, "tcpcsum_batch_desc_dev")
     return out
 
 
-def ipv4_batch(pkts, pkt_off, n: int, cap: int, mode: int, out=None, status=None, stream=None):
+def ipv4_batch(pkts, pkt_off, n: int, cap: int, mode: int, out=None, status=None, stream=None, tune=None):
     """Wire batch over the device tensor ``pkts`` (its whole size is the region)."""
     region = pkts.numel() * pkts.element_size()
     rc = lib().tcpcsum_ipv4_batch_dev(_dev_ptr(pkts, "pkts"), region, _dev_ptr(pkt_off, "pkt_off"), n, cap, mode,
-                                      _dev_ptr(out, "out"), _dev_ptr(status, "status"), _stream_handle(stream))
+                                      _dev_ptr(out, "out"), _dev_ptr(status, "status"), _stream_handle(stream),
+                                      _tune(tune))
     _check(rc, "tcpcsum_ipv4_batch_dev")
     return out, status
 
 
-def tx_build(payload, segs, n: int, max_len: int, out_pkts, mode: int = 0, checks=None, stream=None):
+def ipv4_batch_ptrs(pkt_ptrs, lens, n: int, cap: int, mode: int, out=None, status=None, stream=None, tune=None):
+    """Scatter-gather wire batch: ``pkt_ptrs`` a device int64 tensor of packet addresses (device-accessible),
+    ``lens`` a device int32 tensor of per-packet readable bytes."""
+    rc = lib().tcpcsum_ipv4_batch_ptrs_dev(_dev_ptr(pkt_ptrs, "pkt_ptrs"), _dev_ptr(lens, "lens"), n, cap, mode,
+                                           _dev_ptr(out, "out"), _dev_ptr(status, "status"), _stream_handle(stream),
+                                           _tune(tune))
+    _check(rc, "tcpcsum_ipv4_batch_ptrs_dev")
+    return out, status
+
+
+def tx_build(payload, segs, n: int, max_len: int, out_pkts, mode: int = 0, checks=None, stream=None, tune=None):
     """Assemble + checksum n IPv4/TCP packets on the GPU (device-side context.c:150-213).
     ``segs``: device tensor holding n TXSEG_DTYPE records (16-B aligned)."""
     rc = lib().tcpcsum_tx_build_dev(_dev_ptr(payload, "payload"), _dev_ptr(segs, "segs"), n, max_len,
                                     _dev_ptr(out_pkts, "out_pkts"), mode, _dev_ptr(checks, "checks"),
-                                    _stream_handle(stream))
+                                    _stream_handle(stream), _tune(tune))
     _check(rc, "tcpcsum_tx_build_dev")
     return checks
 
@@ -251,14 +310,15 @@ def synth_pseudo(dst, seg0: int, n: int, seg_len: int, stream=None) -> None:
            "tcpcsum_synth_pseudo_dev")
 
 
-def stream_probe(src, nbytes: int, partials, stream=None) -> int:
+def stream_probe(src, nbytes: int, partials, stream=None, tune=None) -> int:
     """Launch the read-only probe; ``partials`` is a device int64 tensor of >= PROBE_SLOTS.
     Returns how many leading partials the launch writes (their sum = lo16+hi16 word sum)."""
     if partials.numel() < PROBE_SLOTS:
         raise ValueError("partials needs PROBE_SLOTS entries")
     n = ctypes.c_int()
     _check(lib().tcpcsum_stream_probe_dev(_dev_ptr(src, "src"), nbytes, _dev_ptr(partials, "partials"),
-                                          ctypes.byref(n), _stream_handle(stream)), "tcpcsum_stream_probe_dev")
+                                          ctypes.byref(n), _stream_handle(stream), _tune(tune)),
+           "tcpcsum_stream_probe_dev")
     return n.value
 
 
@@ -319,6 +379,12 @@ class HostContext:
         except Exception:
             pass
 
+    def set_tuning(self, max_blocks: int = 0, unroll: int = 0, shape: int = -1, flags: int = 0) -> None:
+        """Launch shapes of this context's batches only (tcpcsum_ctx_set_tuning)."""
+        t = make_tuning(max_blocks, unroll, shape, flags)
+        _check(lib().tcpcsum_ctx_set_tuning(self._h, None if t is None else ctypes.byref(t)),
+               "tcpcsum_ctx_set_tuning")
+
     def batch_uniform(self, data: np.ndarray, stride: int, length: int, n: int, sum_start=0,
                       offset: int = 0) -> np.ndarray:
         data = np.ascontiguousarray(data).view(np.uint8)
@@ -345,3 +411,30 @@ class HostContext:
                                            mode, out.ctypes.data, status.ctypes.data)
         _check(rc, "tcpcsum_ipv4_batch_host")
         return out, status
+
+    def ipv4_batch_ptrs(self, ptrs, lens, mode: int):
+        """Scatter-gather wire batch over host buffers: ``ptrs`` host addresses (ints), ``lens`` readable
+        bytes per packet. Pageable buffers are page-locked on first use and stay registered with this
+        context (FILL patches the checks in place)."""
+        p = np.ascontiguousarray(np.asarray(ptrs, dtype=np.uint64))
+        ln = np.ascontiguousarray(np.asarray(lens, dtype=np.uint32))
+        if p.size != ln.size:
+            raise ValueError("ptrs and lens differ in length")
+        n = p.size
+        out = np.empty(n, np.uint16)
+        status = np.empty(n, np.uint8)
+        rc = lib().tcpcsum_ipv4_batch_ptrs_host(self._h, p.ctypes.data, ln.ctypes.data, n, mode, out.ctypes.data,
+                                                status.ctypes.data)
+        _check(rc, "tcpcsum_ipv4_batch_ptrs_host")
+        return out, status
+
+    def register_host(self, addr: int, nbytes: int) -> None:
+        _check(lib().tcpcsum_ctx_register_host(self._h, addr, nbytes), "tcpcsum_ctx_register_host")
+
+    def unregister_host(self, addr: int = 0, nbytes: int = 0) -> None:
+        _check(lib().tcpcsum_ctx_unregister_host(self._h, addr or None, nbytes), "tcpcsum_ctx_unregister_host")
+
+    def registered(self) -> tuple[int, int]:
+        r, b = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib().tcpcsum_ctx_registered(self._h, ctypes.byref(r), ctypes.byref(b)), "tcpcsum_ctx_registered")
+        return r.value, b.value

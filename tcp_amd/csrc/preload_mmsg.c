@@ -22,11 +22,20 @@
  *   TCPCSUM_PRELOAD_ANY_SOCKET=1 act on every socket, not only SOCK_RAW ones
  *                                (tests run it over UDP loopback, no root)
  *   TCPCSUM_PRELOAD_STATS=1      print counters to stderr at exit
+ *   TCPCSUM_PRELOAD_COPY=1       gather packets into a page-locked staging
+ *                                area instead (for applications that free()
+ *                                their packet buffers; see below)
  *
- * Packets are gathered into a page-locked staging area (the kernels then read
- * it over PCIe, zero-copy) and only the 2-byte check fields are written back.
- * If the GPU path cannot run, the call fails with errno = ENXIO rather than
- * sending packets with unchecked checksums: there is no silent CPU fallback.
+ * Default: the kernel works on the caller's own buffers — one iov_base per
+ * message, each buffer page-locked on first use and kept registered for the
+ * life of the process (tcpcsum_ipv4_batch_ptrs_host) — reading the packets
+ * over PCIe and storing the checks in place: no CPU pass over packet bytes.
+ * This suits the reference, which allocates its 2 x 1024 packet buffers once
+ * and never frees them (loop.c:180-183). With TCPCSUM_PRELOAD_COPY=1 packets
+ * are copied into pinned staging and only the 2-byte check fields are
+ * written back. If the GPU path cannot run, the call fails with errno = ENXIO
+ * rather than sending packets with unchecked checksums: there is no silent
+ * CPU fallback.
  */
 #define _GNU_SOURCE
 #include <dlfcn.h>
@@ -56,7 +65,7 @@ static pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;
 static pthread_once_t g_once = PTHREAD_ONCE_INIT;
 static sendmmsg_fn real_sendmmsg;
 static recvmmsg_fn real_recvmmsg;
-static int g_tx = MODE_FILL, g_rx = MODE_OFF, g_iphdr, g_any, g_stats;
+static int g_tx = MODE_FILL, g_rx = MODE_OFF, g_iphdr, g_any, g_stats, g_copy;
 static tcpcsum_ctx_t *g_ctx;
 static int g_ctx_failed;
 static uint8_t *g_stage;   /* pinned */
@@ -95,6 +104,7 @@ static void init_once(void) {
     g_iphdr = getenv("TCPCSUM_PRELOAD_IPHDR") && atoi(getenv("TCPCSUM_PRELOAD_IPHDR"));
     g_any = getenv("TCPCSUM_PRELOAD_ANY_SOCKET") && atoi(getenv("TCPCSUM_PRELOAD_ANY_SOCKET"));
     g_stats = getenv("TCPCSUM_PRELOAD_STATS") && atoi(getenv("TCPCSUM_PRELOAD_STATS"));
+    g_copy = getenv("TCPCSUM_PRELOAD_COPY") && atoi(getenv("TCPCSUM_PRELOAD_COPY"));
     atexit(print_stats);
 }
 
@@ -152,10 +162,60 @@ static int ensure_ctx(size_t bytes, size_t npkts) {
     return 0;
 }
 
+/* g_mu held. Count one message of a finished batch (k: its slot in the
+ * batch arrays). */
+static void account(int k, int fill, int is_tx) {
+    const int skipped = (g_status[k] & TCPCSUM_PKT_SKIPPED) != 0;
+    if (skipped) {
+        if (is_tx) g_st.tx_skipped++; else g_st.rx_skipped++;
+    } else if (fill) {
+        g_st.tx_filled++;
+    } else {
+        /* CHECKSUM_PARTIAL segments (checksum left to offload, e.g. Linux
+         * loopback) are counted apart, not as corrupt */
+        const int partial = (g_status[k] & TCPCSUM_PKT_CSUM_PARTIAL) != 0;
+        const int bad = (g_out[k] != 0 && !partial) || (g_status[k] & TCPCSUM_PKT_IPHDR_BAD);
+        if (is_tx) { g_st.tx_verified++; if (bad) g_st.tx_verify_failed++; }
+        else { g_st.rx_verified++; if (bad) g_st.rx_verify_failed++; if (partial) g_st.rx_partial++; }
+    }
+}
+
+/* Default path: the GPU reads the caller's buffers in place (scatter-gather,
+ * each buffer page-locked once) and FILL stores the checks there. */
+static int gpu_batch_inplace(struct mmsghdr *vec, unsigned int vlen, const unsigned int *lens, int fill, int is_tx) {
+    void *ptrs[1024];
+    uint32_t plen[1024];
+    for (unsigned int i = 0; i < vlen; ++i) {
+        const int one = vec[i].msg_hdr.msg_iovlen == 1;
+        ptrs[i] = one ? vec[i].msg_hdr.msg_iov[0].iov_base : NULL;
+        plen[i] = one ? lens[i] : 0;   /* < 20 bytes: SKIPPED, nothing read */
+    }
+    pthread_mutex_lock(&g_mu);
+    if (ensure_ctx(0, vlen)) {
+        g_st.errors++;
+        pthread_mutex_unlock(&g_mu);
+        errno = ENXIO;
+        return -1;
+    }
+    int mode = (fill ? TCPCSUM_IPV4_FILL : TCPCSUM_IPV4_VERIFY) | (g_iphdr ? TCPCSUM_IPV4_IPHDR : 0);
+    int rc = tcpcsum_ipv4_batch_ptrs_host(g_ctx, ptrs, plen, vlen, mode, g_out, g_status);
+    if (rc) {
+        g_st.errors++;
+        pthread_mutex_unlock(&g_mu);
+        fprintf(stderr, "tcpcsum_preload: batch failed: %s\n", tcpcsum_strerror(rc));
+        errno = ENXIO;
+        return -1;
+    }
+    for (unsigned int i = 0; i < vlen; ++i) account((int) i, fill, is_tx);
+    pthread_mutex_unlock(&g_mu);
+    return 0;
+}
+
 /* Checksum a batch of single-iovec messages on the GPU. fill: write the check
  * fields back into the caller's buffers. Returns 0, or -1 (errno set). lens
  * gives each message's byte count (iov_len for tx, msg_len for rx). */
 static int gpu_batch(struct mmsghdr *vec, unsigned int vlen, const unsigned int *lens, int fill, int is_tx) {
+    if (!g_copy) return gpu_batch_inplace(vec, vlen, lens, fill, is_tx);
     size_t total = 0;
     unsigned int m = 0;
     for (unsigned int i = 0; i < vlen; ++i) {
@@ -200,22 +260,13 @@ static int gpu_batch(struct mmsghdr *vec, unsigned int vlen, const unsigned int 
         const uint8_t *sp = g_stage + g_off[k];
         uint8_t *dp = (uint8_t *) vec[i].msg_hdr.msg_iov[0].iov_base;
         const unsigned int tot = ((unsigned) sp[2] << 8) | sp[3];
-        const int ok = !(g_status[k] & TCPCSUM_PKT_SKIPPED) && tot <= lens[i];
-        if (!ok) {
-            if (is_tx) g_st.tx_skipped++; else g_st.rx_skipped++;
-        } else if (fill) {
+        if (tot > lens[i]) g_status[k] |= TCPCSUM_PKT_SKIPPED;   /* claims more than was handed over */
+        if (fill && !(g_status[k] & TCPCSUM_PKT_SKIPPED)) {
             const unsigned int tcp = (sp[0] & 15u) * 4u;
             memcpy(dp + tcp + 16, sp + tcp + 16, 2);
             if (g_iphdr) memcpy(dp + 10, sp + 10, 2);
-            g_st.tx_filled++;
-        } else {
-            /* CHECKSUM_PARTIAL segments (checksum left to offload, e.g. Linux
-             * loopback) are counted apart, not as corrupt */
-            const int partial = (g_status[k] & TCPCSUM_PKT_CSUM_PARTIAL) != 0;
-            const int bad = (g_out[k] != 0 && !partial) || (g_status[k] & TCPCSUM_PKT_IPHDR_BAD);
-            if (is_tx) { g_st.tx_verified++; if (bad) g_st.tx_verify_failed++; }
-            else { g_st.rx_verified++; if (bad) g_st.rx_verify_failed++; if (partial) g_st.rx_partial++; }
         }
+        account((int) k, fill, is_tx);
         ++k;
     }
     pthread_mutex_unlock(&g_mu);

@@ -9,10 +9,12 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
 #include <atomic>
 #include <climits>
 #include <mutex>
 #include <new>
+#include <vector>
 
 #include "tcpcsum.h"
 #include "tcpcsum_internal.h"
@@ -22,11 +24,9 @@ static_assert(sizeof(tcpcsum_txseg_t) == 48, "tx descriptor is read as three 16-
 
 namespace {
 
+// Diagnostics only (the hipError_t behind the last TCPCSUM_EHIP) and the
+// per-device arch cache below; nothing that changes what a launch does.
 std::atomic<int> g_last_hip_error{0};
-std::atomic<int> g_max_blocks{0};
-std::atomic<int> g_unroll{0};
-std::atomic<int> g_shape{-1};
-std::atomic<int> g_flags{0};
 
 constexpr int kMaxDevices = 64;
 std::atomic<int> g_dev_ok[kMaxDevices];   // 0 unknown, 1 gfx950, -1 unusable
@@ -36,13 +36,21 @@ int hip_fail(hipError_t e) {
     return TCPCSUM_EHIP;
 }
 
-tcpcsum::Tuning tuning() {
-    tcpcsum::Tuning t;
-    t.max_blocks = g_max_blocks.load(std::memory_order_relaxed);
-    t.unroll = g_unroll.load(std::memory_order_relaxed);
-    t.shape = g_shape.load(std::memory_order_relaxed);
-    t.flags = g_flags.load(std::memory_order_relaxed);
-    return t;
+// The launch shapes of one call: *t, or the built-in defaults for NULL.
+int get_tuning(const tcpcsum_tuning_t* t, tcpcsum::Tuning* out) {
+    tcpcsum::Tuning r;
+    if (t) {
+        const int u = t->unroll;
+        if (t->max_blocks < 0 || !(u == 0 || u == 1 || u == 2 || u == 4 || u == 8) || t->shape < -1 ||
+            t->shape > 12 || (t->flags & ~255) || (t->flags & 3) == 3 || (t->flags & 12) == 12)
+            return TCPCSUM_EINVAL;
+        r.max_blocks = t->max_blocks;
+        r.unroll = t->unroll;
+        r.shape = t->shape;
+        r.flags = t->flags;
+    }
+    *out = r;
+    return TCPCSUM_OK;
 }
 
 // The current device must be a gfx950 (the only code object in this library).
@@ -108,21 +116,17 @@ int tcpcsum_device_check(char* arch, size_t arch_len) {
     return require_device(arch, arch_len);
 }
 
-int tcpcsum_set_tuning(int max_blocks, int unroll, int shape, int flags) {
-    if (max_blocks < 0 || !(unroll == 0 || unroll == 1 || unroll == 2 || unroll == 4 || unroll == 8) ||
-        shape < -1 || shape > 12 || (flags & ~255) || (flags & 3) == 3 || (flags & 12) == 12)
-        return TCPCSUM_EINVAL;
-    g_max_blocks.store(max_blocks);
-    g_unroll.store(unroll);
-    g_shape.store(shape);
-    g_flags.store(flags);
-    return TCPCSUM_OK;
+int tcpcsum_tuning_check(const tcpcsum_tuning_t* tune) {
+    tcpcsum::Tuning t;
+    return get_tuning(tune, &t);
 }
 
-int tcpcsum_plan_uniform(uint64_t base, uint64_t stride, uint32_t len, uint64_t n, int* mode, int* shape,
-                         int* unroll, int* max_blocks) {
+int tcpcsum_plan_uniform(uint64_t base, uint64_t stride, uint32_t len, uint64_t n, const tcpcsum_tuning_t* tune,
+                         int* mode, int* shape, int* unroll, int* max_blocks) {
     if (!mode || !shape || !unroll || !max_blocks || len > (uint32_t)INT_MAX) return TCPCSUM_EINVAL;
-    const tcpcsum::UniformPlan p = tcpcsum::plan_uniform((uintptr_t)base, stride, len, n, tuning());
+    tcpcsum::Tuning tu;
+    if (get_tuning(tune, &tu)) return TCPCSUM_EINVAL;
+    const tcpcsum::UniformPlan p = tcpcsum::plan_uniform((uintptr_t)base, stride, len, n, tu);
     *mode = p.mode;
     *shape = p.shape;
     *unroll = p.unroll;
@@ -131,49 +135,73 @@ int tcpcsum_plan_uniform(uint64_t base, uint64_t stride, uint32_t len, uint64_t 
 }
 
 int tcpcsum_batch_uniform_dev(const void* d_base, uint64_t stride, uint32_t len, const uint32_t* d_sum_start,
-                              uint32_t sum_start, uint16_t* d_out, uint64_t n, void* stream) {
+                              uint32_t sum_start, uint16_t* d_out, uint64_t n, void* stream,
+                              const tcpcsum_tuning_t* tune) {
+    tcpcsum::Tuning tu;
+    if (get_tuning(tune, &tu)) return TCPCSUM_EINVAL;
     if (n == 0) return TCPCSUM_OK;
     if (!d_base || !d_out || len > (uint32_t)INT_MAX) return TCPCSUM_EINVAL;
     int rc = require_device(nullptr, 0);
     if (rc) return rc;
     tcpcsum::launch_uniform((const uint8_t*)d_base, stride, len, d_sum_start, sum_start, d_out, n,
-                            (hipStream_t)stream, tuning());
+                            (hipStream_t)stream, tu);
     return check_launch();
 }
 
 int tcpcsum_batch_desc_dev(const void* d_base, const tcpcsum_desc_t* d_desc, uint64_t n, uint32_t max_len,
-                           uint16_t* d_out, void* stream) {
+                           uint16_t* d_out, void* stream, const tcpcsum_tuning_t* tune) {
+    tcpcsum::Tuning tu;
+    if (get_tuning(tune, &tu)) return TCPCSUM_EINVAL;
     if (n == 0) return TCPCSUM_OK;
     if (!d_base || !d_desc || !d_out || max_len > (uint32_t)INT_MAX) return TCPCSUM_EINVAL;
     if (((uintptr_t)d_desc) & 15u) return TCPCSUM_EINVAL;   // descriptors are read as one 16-B load
     int rc = require_device(nullptr, 0);
     if (rc) return rc;
-    tcpcsum::launch_desc((const uint8_t*)d_base, d_desc, n, max_len, d_out, (hipStream_t)stream, tuning());
+    tcpcsum::launch_desc((const uint8_t*)d_base, d_desc, n, max_len, d_out, (hipStream_t)stream, tu);
     return check_launch();
 }
 
 int tcpcsum_ipv4_batch_dev(void* d_pkts, uint64_t region_bytes, const uint64_t* d_pkt_off, uint64_t n, uint32_t cap,
-                           int mode, uint16_t* d_out, uint8_t* d_status, void* stream) {
+                           int mode, uint16_t* d_out, uint8_t* d_status, void* stream, const tcpcsum_tuning_t* tune) {
+    tcpcsum::Tuning tu;
+    if (get_tuning(tune, &tu)) return TCPCSUM_EINVAL;
     if (n == 0) return TCPCSUM_OK;
     if (!d_pkts || !d_pkt_off || !region_bytes || (mode & ~3)) return TCPCSUM_EINVAL;
     if (cap > 65535u) cap = 65535u;   // tot_len is a u16
     int rc = require_device(nullptr, 0);
     if (rc) return rc;
-    tcpcsum::launch_ipv4((uint8_t*)d_pkts, d_pkt_off, n, cap, region_bytes, mode, d_out, d_status, nullptr,
-                         (hipStream_t)stream,
-                         tuning());
+    tcpcsum::launch_ipv4((uint8_t*)d_pkts, d_pkt_off, nullptr, n, cap, region_bytes, region_bytes, mode, d_out,
+                         d_status, nullptr, (hipStream_t)stream, tu);
+    return check_launch();
+}
+
+int tcpcsum_ipv4_batch_ptrs_dev(void* const* d_pkt_ptrs, const uint32_t* d_lens, uint64_t n, uint32_t cap, int mode,
+                                uint16_t* d_out, uint8_t* d_status, void* stream, const tcpcsum_tuning_t* tune) {
+    tcpcsum::Tuning tu;
+    if (get_tuning(tune, &tu)) return TCPCSUM_EINVAL;
+    if (n == 0) return TCPCSUM_OK;
+    if (!d_pkt_ptrs || !d_lens || (mode & ~3) || (((uintptr_t)d_pkt_ptrs) & 7u) || (((uintptr_t)d_lens) & 3u))
+        return TCPCSUM_EINVAL;
+    if (cap > 65535u) cap = 65535u;
+    int rc = require_device(nullptr, 0);
+    if (rc) return rc;
+    // addresses as offsets from 0, bounded per packet by d_lens
+    tcpcsum::launch_ipv4(nullptr, (const uint64_t*)d_pkt_ptrs, d_lens, n, cap, ~0ull, n * (uint64_t)cap, mode, d_out,
+                         d_status, nullptr, (hipStream_t)stream, tu);
     return check_launch();
 }
 
 int tcpcsum_tx_build_dev(const void* d_payload, const tcpcsum_txseg_t* d_segs, uint64_t n, uint32_t max_len,
-                         void* d_out_pkts, int mode, uint16_t* d_check, void* stream) {
+                         void* d_out_pkts, int mode, uint16_t* d_check, void* stream, const tcpcsum_tuning_t* tune) {
+    tcpcsum::Tuning tu;
+    if (get_tuning(tune, &tu)) return TCPCSUM_EINVAL;
     if (n == 0) return TCPCSUM_OK;
     if (!d_segs || !d_out_pkts || (mode & ~TCPCSUM_IPV4_IPHDR) || (((uintptr_t)d_segs) & 15u))
         return TCPCSUM_EINVAL;
     int rc = require_device(nullptr, 0);
     if (rc) return rc;
     tcpcsum::launch_tx_build((const uint8_t*)d_payload, d_segs, n, max_len, (uint8_t*)d_out_pkts, mode, d_check,
-                             (hipStream_t)stream, tuning());
+                             (hipStream_t)stream, tu);
     return check_launch();
 }
 
@@ -196,12 +224,14 @@ int tcpcsum_synth_pseudo_dev(uint32_t* d_sum_start, uint64_t seg0, uint64_t n, u
 }
 
 int tcpcsum_stream_probe_dev(const void* d_src, uint64_t nbytes, uint64_t* d_partials, int* n_partials,
-                             void* stream) {
+                             void* stream, const tcpcsum_tuning_t* tune) {
+    tcpcsum::Tuning tu;
+    if (get_tuning(tune, &tu)) return TCPCSUM_EINVAL;
     if (!d_src || !d_partials || !n_partials || (nbytes & 15u) || (((uintptr_t)d_src) & 15u))
         return TCPCSUM_EINVAL;
     int rc = require_device(nullptr, 0);
     if (rc) return rc;
-    *n_partials = tcpcsum::launch_probe((const uint8_t*)d_src, nbytes, d_partials, (hipStream_t)stream, tuning());
+    *n_partials = tcpcsum::launch_probe((const uint8_t*)d_src, nbytes, d_partials, (hipStream_t)stream, tu);
     return check_launch();
 }
 
@@ -231,7 +261,26 @@ struct tcpcsum_ctx {
     uint16_t* k_wout = nullptr;
     uint8_t* k_wstat = nullptr;
     uint16_t* k_wip = nullptr;
+    uint32_t* h_len = nullptr;   // scatter-gather batches: per-packet readable bytes
+    uint32_t* k_len = nullptr;
     size_t pkt_cap = 0;
+    // launch shapes of this context's batches (tcpcsum_ctx_set_tuning)
+    tcpcsum::Tuning tune;
+    // Host memory this context page-locked (hipHostRegister), one entry per
+    // registration: disjoint whole pages. `view` is the lookup table derived
+    // from them and from memory found already page-locked by someone else:
+    // sorted, disjoint intervals [lo, hi) with device address = host + delta,
+    // touching intervals of equal delta merged. `finger`: the last hit (packets
+    // of a batch mostly come in pool order).
+    struct Reg {
+        uintptr_t lo, hi;
+        intptr_t delta;
+        bool owned;
+    };
+    std::vector<Reg> regs;
+    std::vector<Reg> view;
+    size_t finger = 0;
+    uint64_t reg_bytes = 0;
     std::mutex mu;
 };
 
@@ -323,9 +372,21 @@ void tcpcsum_ctx_destroy(tcpcsum_ctx_t* c) {
     if (c->h_wout) hipHostFree(c->h_wout);
     if (c->h_wstat) hipHostFree(c->h_wstat);
     if (c->h_wip) hipHostFree(c->h_wip);
+    if (c->h_len) hipHostFree(c->h_len);
+    for (const auto& r : c->regs)
+        if (r.owned) (void)hipHostUnregister((void*)r.lo);
     for (int i = 0; i < 2; ++i)
         if (c->st[i]) hipStreamDestroy(c->st[i]);
     delete c;
+}
+
+int tcpcsum_ctx_set_tuning(tcpcsum_ctx_t* c, const tcpcsum_tuning_t* tune) {
+    if (!c) return TCPCSUM_EINVAL;
+    tcpcsum::Tuning tu;
+    if (get_tuning(tune, &tu)) return TCPCSUM_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->tune = tu;
+    return TCPCSUM_OK;
 }
 
 void* tcpcsum_host_alloc(size_t bytes) {
@@ -367,19 +428,23 @@ int ensure_pkt_staging(tcpcsum_ctx* c, uint64_t n, hipStream_t st) {
     if (c->h_wout) (void)hipHostFree(c->h_wout);
     if (c->h_wstat) (void)hipHostFree(c->h_wstat);
     if (c->h_wip) (void)hipHostFree(c->h_wip);
-    c->h_off = nullptr; c->h_wout = nullptr; c->h_wstat = nullptr; c->h_wip = nullptr; c->pkt_cap = 0;
+    if (c->h_len) (void)hipHostFree(c->h_len);
+    c->h_off = nullptr; c->h_wout = nullptr; c->h_wstat = nullptr; c->h_wip = nullptr; c->h_len = nullptr;
+    c->pkt_cap = 0;
     size_t cap = 1024;
     while (cap < n) cap *= 2;
     hipError_t e = hipHostMalloc((void**)&c->h_off, cap * sizeof(uint64_t), hipHostMallocDefault);
     if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_wout, cap * sizeof(uint16_t), hipHostMallocDefault);
     if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_wstat, cap, hipHostMallocDefault);
     if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_wip, cap * sizeof(uint16_t), hipHostMallocDefault);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_len, cap * sizeof(uint32_t), hipHostMallocDefault);
     if (e != hipSuccess) { g_last_hip_error.store((int)e); return TCPCSUM_ENOMEM; }
     c->k_off = (uint64_t*)pinned_dev_ptr(c->h_off);
     c->k_wout = (uint16_t*)pinned_dev_ptr(c->h_wout);
     c->k_wstat = (uint8_t*)pinned_dev_ptr(c->h_wstat);
     c->k_wip = (uint16_t*)pinned_dev_ptr(c->h_wip);
-    if (!c->k_off || !c->k_wout || !c->k_wstat || !c->k_wip) return TCPCSUM_ENOMEM;
+    c->k_len = (uint32_t*)pinned_dev_ptr(c->h_len);
+    if (!c->k_off || !c->k_wout || !c->k_wstat || !c->k_wip || !c->k_len) return TCPCSUM_ENOMEM;
     c->pkt_cap = cap;
     return TCPCSUM_OK;
 }
@@ -397,7 +462,7 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t st
     if (!h_base || !h_out || len > (uint32_t)INT_MAX) return TCPCSUM_EINVAL;
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard g(c->device);
-    const tcpcsum::Tuning tu = tuning();
+    const tcpcsum::Tuning tu = c->tune;
     hipError_t e;
     int rc;
     if (const uint8_t* zb = (const uint8_t*)pinned_dev_ptr(h_base)) {
@@ -502,9 +567,10 @@ int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t* c, void* h_pkts, size_t region_bytes,
         // zero-copy over PCIe: 16-lane groups, 512 B per round (more waves with
         // reads in flight) beat the HBM-tuned MTU shape — 1024 x 1500-B FILL
         // batch 49 vs 59 us on MI355X (tools/e2e.py --sweep)
-        tcpcsum::Tuning tu = tuning();
+        tcpcsum::Tuning tu = c->tune;
         if (tu.shape < 0 && n < 65536u) tu.shape = 3;
-        tcpcsum::launch_ipv4(zp, koff, n, cap, (uint64_t)region_bytes, mode, kout, kst, nullptr, st, tu);
+        tcpcsum::launch_ipv4(zp, koff, nullptr, n, cap, (uint64_t)region_bytes, (uint64_t)region_bytes, mode, kout,
+                             kst, nullptr, st, tu);
         rc = check_launch();
         if (rc) return rc;
         e = hipStreamSynchronize(st);
@@ -524,8 +590,8 @@ int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t* c, void* h_pkts, size_t region_bytes,
         e = hipMemcpyAsync(c->d_region + mis, h_pkts, region_bytes, hipMemcpyHostToDevice, st);
         if (e != hipSuccess) return hip_fail(e);
         const bool ipfill = fill && (mode & TCPCSUM_IPV4_IPHDR);
-        tcpcsum::launch_ipv4(c->d_region + mis, koff, n, cap, (uint64_t)region_bytes, mode, kout, kst,
-                             ipfill ? c->k_wip : nullptr, st, tuning());
+        tcpcsum::launch_ipv4(c->d_region + mis, koff, nullptr, n, cap, (uint64_t)region_bytes,
+                             (uint64_t)region_bytes, mode, kout, kst, ipfill ? c->k_wip : nullptr, st, c->tune);
         rc = check_launch();
         if (rc) return rc;
         e = hipStreamSynchronize(st);
@@ -547,6 +613,233 @@ int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t* c, void* h_pkts, size_t region_bytes,
     }
     if (h_out && !zout) memcpy(h_out, c->h_wout, n * sizeof(uint16_t));
     if (h_status && !zst) memcpy(h_status, c->h_wstat, n);
+    return TCPCSUM_OK;
+}
+
+
+// ------------------------------------------------- scatter-gather host batches
+
+namespace {
+
+constexpr uintptr_t kPage = 4096;
+
+bool reg_less(const tcpcsum_ctx::Reg& a, const tcpcsum_ctx::Reg& b) { return a.lo < b.lo; }
+
+// The lookup view: registrations sorted by address, touching intervals with
+// the same host->device offset merged (on MI355X hosts every registration maps
+// at its host address, so a pool registered buffer by buffer becomes one
+// interval wherever the buffers touch).
+void rebuild_view(tcpcsum_ctx* c) {
+    std::sort(c->regs.begin(), c->regs.end(), reg_less);
+    c->view.clear();
+    for (const auto& r : c->regs) {
+        if (!c->view.empty() && c->view.back().hi == r.lo && c->view.back().delta == r.delta)
+            c->view.back().hi = r.hi;
+        else
+            c->view.push_back(r);
+    }
+    c->finger = 0;
+}
+
+// [p, e) inside one interval of the view: its device address.
+bool view_find(tcpcsum_ctx* c, uintptr_t p, uintptr_t e, uintptr_t* dev) {
+    const std::vector<tcpcsum_ctx::Reg>& v = c->view;
+    if (v.empty()) return false;
+    auto hit = [&](size_t j) { return j < v.size() && v[j].lo <= p && e <= v[j].hi; };
+    size_t k = c->finger;
+    if (!hit(k)) {
+        if (hit(k + 1)) {
+            k = k + 1;
+        } else {   // last interval starting at or before p
+            size_t lo = 0, hi = v.size();
+            while (hi - lo > 1) {
+                const size_t mid = (lo + hi) / 2;
+                if (v[mid].lo <= p) lo = mid; else hi = mid;
+            }
+            if (!hit(lo)) return false;
+            k = lo;
+        }
+    }
+    c->finger = k;
+    *dev = (uintptr_t)((intptr_t)p + v[k].delta);
+    return true;
+}
+
+// Page-lock the pages of [lo, hi) (page-aligned) that no registration of this
+// context covers yet.
+int reg_pages(tcpcsum_ctx* c, uintptr_t lo, uintptr_t hi) {
+    std::vector<std::pair<uintptr_t, uintptr_t>> gaps;
+    uintptr_t cur = lo;
+    for (const auto& r : c->regs) {   // sorted by lo
+        if (r.hi <= cur) continue;
+        if (r.lo >= hi) break;
+        if (r.lo > cur) gaps.push_back({cur, r.lo});
+        if (r.hi > cur) cur = r.hi;
+        if (cur >= hi) break;
+    }
+    if (cur < hi) gaps.push_back({cur, hi});
+    for (const auto& g : gaps) {
+        hipError_t e = hipHostRegister((void*)g.first, g.second - g.first, hipHostRegisterMapped);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            rebuild_view(c);
+            return hip_fail(e);
+        }
+        void* d = nullptr;
+        e = hipHostGetDevicePointer(&d, (void*)g.first, 0);
+        if (e != hipSuccess || !d) {
+            (void)hipGetLastError();
+            (void)hipHostUnregister((void*)g.first);
+            rebuild_view(c);
+            return hip_fail(e != hipSuccess ? e : hipErrorInvalidValue);
+        }
+        c->regs.push_back({g.first, g.second, (intptr_t)d - (intptr_t)g.first, true});
+        c->reg_bytes += g.second - g.first;
+    }
+    rebuild_view(c);
+    return TCPCSUM_OK;
+}
+
+// Device address of the host bytes [p, p + len), page-locking them on first use.
+int resolve_host(tcpcsum_ctx* c, uintptr_t p, uint32_t len, uintptr_t* dev) {
+    const uintptr_t e = p + len;
+    if (view_find(c, p, e, dev)) return TCPCSUM_OK;
+    // page-locked by someone else (tcpcsum_host_alloc, the application's own
+    // registration): use that mapping over the allocation's whole extent
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, (const void*)p) == hipSuccess && a.type == hipMemoryTypeHost && a.devicePointer) {
+        uintptr_t rs = 0;
+        size_t rsz = 0;
+        if (hipPointerGetAttribute(&rs, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, (hipDeviceptr_t)p) != hipSuccess ||
+            hipPointerGetAttribute(&rsz, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, (hipDeviceptr_t)p) != hipSuccess ||
+            rs > p || rs + rsz < e) {
+            rs = p;
+            rsz = len;
+        }
+        (void)hipGetLastError();
+        const intptr_t delta = (intptr_t)a.devicePointer - (intptr_t)p;
+        bool known = false;
+        for (const auto& r : c->regs) known = known || (r.lo == rs && r.hi == rs + rsz);
+        if (!known) {
+            c->regs.push_back({rs, rs + rsz, delta, false});
+            rebuild_view(c);
+        }
+        if (view_find(c, p, e, dev)) return TCPCSUM_OK;
+    }
+    (void)hipGetLastError();   // pageable memory: not an error for us
+    const uintptr_t lo = p & ~(kPage - 1), hi = (e + kPage - 1) & ~(kPage - 1);
+    int rc = reg_pages(c, lo, hi);
+    if (rc) return rc;
+    if (view_find(c, p, e, dev)) return TCPCSUM_OK;
+    // The packet spans registrations mapped at unrelated device addresses (a
+    // host whose registrations do not map at their host address): replace the
+    // ones under it by a single registration of their union.
+    uintptr_t ulo = lo, uhi = hi;
+    std::vector<tcpcsum_ctx::Reg> keep;
+    for (const auto& r : c->regs) {
+        if (r.owned && r.lo < hi && r.hi > lo) {
+            ulo = r.lo < ulo ? r.lo : ulo;
+            uhi = r.hi > uhi ? r.hi : uhi;
+            (void)hipHostUnregister((void*)r.lo);
+            c->reg_bytes -= r.hi - r.lo;
+        } else {
+            keep.push_back(r);
+        }
+    }
+    c->regs.swap(keep);
+    std::sort(c->regs.begin(), c->regs.end(), reg_less);
+    rc = reg_pages(c, ulo, uhi);
+    if (rc) return rc;
+    return view_find(c, p, e, dev) ? TCPCSUM_OK : TCPCSUM_EINVAL;
+}
+
+}  // namespace
+
+int tcpcsum_ipv4_batch_ptrs_host(tcpcsum_ctx_t* c, void* const* h_pkts, const uint32_t* h_lens, uint64_t n, int mode,
+                                 uint16_t* h_out, uint8_t* h_status) {
+    if (!c) return TCPCSUM_EINVAL;
+    if (n == 0) return TCPCSUM_OK;
+    if (!h_pkts || !h_lens || (mode & ~3)) return TCPCSUM_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    hipStream_t st = c->st[0];
+    int rc = ensure_pkt_staging(c, n, st);
+    if (rc) return rc;
+    // per-packet device addresses and bounds, straight into the pinned staging
+    // the kernel reads (no copy of packet bytes anywhere)
+    uint64_t foot = 0;
+    uint32_t cap = 20;
+    for (uint64_t i = 0; i < n; ++i) {
+        uint32_t len = h_lens[i] > 65535u ? 65535u : h_lens[i];   // tot_len is a u16
+        const uintptr_t p = (uintptr_t)h_pkts[i];
+        uintptr_t dev = 0;
+        if (len >= 20u && p) {
+            rc = resolve_host(c, p, len, &dev);
+            if (rc) return rc;
+        } else {
+            len = 0;   // too short for an IP header: SKIPPED, nothing is read
+        }
+        c->h_off[i] = dev;
+        c->h_len[i] = len;
+        foot += len;
+        cap = len > cap ? len : cap;
+    }
+    uint16_t* zout = h_out ? (uint16_t*)pinned_dev_ptr(h_out) : nullptr;
+    uint8_t* zst = h_status ? (uint8_t*)pinned_dev_ptr(h_status) : nullptr;
+    // zero-copy over PCIe: the 16-lane group shape for latency-bound batches
+    // (as tcpcsum_ipv4_batch_host on a pinned pool)
+    tcpcsum::Tuning tu = c->tune;
+    if (tu.shape < 0 && n < 65536u) tu.shape = 3;
+    tcpcsum::launch_ipv4(nullptr, c->k_off, c->k_len, n, cap, ~0ull, foot, mode, zout ? zout : c->k_wout,
+                         zst ? zst : c->k_wstat, nullptr, st, tu);
+    rc = check_launch();
+    if (rc) return rc;
+    hipError_t e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return hip_fail(e);
+    if (h_out && !zout) memcpy(h_out, c->h_wout, n * sizeof(uint16_t));
+    if (h_status && !zst) memcpy(h_status, c->h_wstat, n);
+    return TCPCSUM_OK;
+}
+
+int tcpcsum_ctx_register_host(tcpcsum_ctx_t* c, void* p, size_t bytes) {
+    if (!c || !p || !bytes) return TCPCSUM_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    const uintptr_t lo = (uintptr_t)p & ~(kPage - 1), hi = ((uintptr_t)p + bytes + kPage - 1) & ~(kPage - 1);
+    return reg_pages(c, lo, hi);
+}
+
+int tcpcsum_ctx_unregister_host(tcpcsum_ctx_t* c, void* p, size_t bytes) {
+    if (!c) return TCPCSUM_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    for (int i = 0; i < 2; ++i) (void)hipStreamSynchronize(c->st[i]);
+    const uintptr_t lo = (uintptr_t)p, hi = p ? (uintptr_t)p + bytes : UINTPTR_MAX;
+    std::vector<tcpcsum_ctx::Reg> keep;
+    int rc = TCPCSUM_OK;
+    for (const auto& r : c->regs) {
+        if (r.lo < hi && r.hi > lo) {
+            if (r.owned) {
+                const hipError_t e = hipHostUnregister((void*)r.lo);
+                if (e != hipSuccess) rc = hip_fail(e);
+                c->reg_bytes -= r.hi - r.lo;
+            }
+        } else {
+            keep.push_back(r);
+        }
+    }
+    c->regs.swap(keep);
+    rebuild_view(c);
+    return rc;
+}
+
+int tcpcsum_ctx_registered(tcpcsum_ctx_t* c, uint64_t* ranges, uint64_t* bytes) {
+    if (!c) return TCPCSUM_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    uint64_t k = 0;
+    for (const auto& r : c->regs) k += r.owned ? 1u : 0u;
+    if (ranges) *ranges = k;
+    if (bytes) *bytes = c->reg_bytes;
     return TCPCSUM_OK;
 }
 

@@ -37,9 +37,13 @@ void launch_uniform(const uint8_t* base, uint64_t stride, uint32_t len, const ui
                     uint16_t* out, uint64_t n, hipStream_t s, const Tuning& tu);
 void launch_desc(const uint8_t* base, const tcpcsum_desc_t* d, uint64_t n, uint32_t max_len, uint16_t* out,
                  hipStream_t s, const Tuning& tu);
-// ipout (nullable): per-packet IPv4 header checksum when mode has TCPCSUM_IPV4_IPHDR
-void launch_ipv4(uint8_t* pkts, const uint64_t* off, uint64_t n, uint32_t cap, uint64_t limit, int mode,
-                 uint16_t* out, uint8_t* status, uint16_t* ipout, hipStream_t s, const Tuning& tu);
+// Wire batch: packet i at pkts + off[i], readable up to min(limit - off[i], plen[i])
+// (plen nullable). footprint: bytes the batch spans (region size, or summed
+// lengths), for the shape choice. ipout (nullable): per-packet IPv4 header
+// checksum when mode has TCPCSUM_IPV4_IPHDR.
+void launch_ipv4(uint8_t* pkts, const uint64_t* off, const uint32_t* plen, uint64_t n, uint32_t cap, uint64_t limit,
+                 uint64_t footprint, int mode, uint16_t* out, uint8_t* status, uint16_t* ipout, hipStream_t s,
+                 const Tuning& tu);
 void launch_tx_build(const uint8_t* payload, const tcpcsum_txseg_t* segs, uint64_t n, uint32_t max_len,
                      uint8_t* outp, int mode, uint16_t* checks, hipStream_t s, const Tuning& tu);
 void launch_synth_fill(uint8_t* dst, uint64_t off, uint64_t nbytes, hipStream_t s);

@@ -696,8 +696,9 @@ struct IpPkt {
     uint64_t o;
     uint32_t m;      // ip & 15
     uint32_t spec;   // chunks loaded speculatively
+    uint32_t room;   // readable bytes at ip: min(region end, the packet's own bound), clamped
     bool live;    // a packet of the batch
-    bool hdr;     // its 20-byte IP header lies inside the region
+    bool hdr;     // its 20-byte IP header is readable
 };
 
 // A native u16 at p: one 2-byte store when p is even, two byte stores otherwise.
@@ -756,8 +757,12 @@ struct IpDone {
     bool fill;  // checks are stored in place
 };
 
-template <int G, int C, int U, bool NT>
+// plen (nullable): per-packet readable bytes (scatter-gather batches: pkts = 0,
+// off[i] = the packet's address, limit = ~0). A packet never reads past
+// min(limit - off[i], plen[i]).
+template <int G, int C, int U, bool NT, bool PL>
 __global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const uint64_t* __restrict__ off,
+                                              const uint32_t* __restrict__ plen,
                                               uint64_t n, uint32_t cap, uint64_t limit, int mode,
                                               uint16_t* __restrict__ out, uint8_t* __restrict__ status,
                                               uint16_t* __restrict__ ipout, uint32_t amask) {
@@ -779,12 +784,17 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const 
     uint64_t t = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
     // offsets of packet i and of packet i + 1 (0 past the end: no bound)
     uint64_t on[U], on1[U];
+    uint32_t pn[U];
     auto load_off = [&](uint64_t tile) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint64_t i = tile * SPT + (uint64_t)(u * GPW + q);
             on[u] = *reinterpret_cast<const uint64_t*>(zsel(i < n, reinterpret_cast<const uint8_t*>(off + i)));
             on1[u] = *reinterpret_cast<const uint64_t*>(zsel(i + 1 < n, reinterpret_cast<const uint8_t*>(off + i + 1)));
+            if constexpr (PL)
+                pn[u] = *reinterpret_cast<const uint32_t*>(zsel(i < n, reinterpret_cast<const uint8_t*>(plen + i)));
+            else
+                pn[u] = 0xffffffffu;
         }
     };
     IpPkt p[U];
@@ -796,15 +806,26 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const 
             const uint64_t i = tile * SPT + (uint64_t)(u * GPW + q);
             p[u].live = i < n;
             p[u].o = on[u];
-            uint8_t* ip = pkts + p[u].o;
+            // scatter-gather (PL): pkts is 0 and off[i] the address — integer
+            // arithmetic, not a pointer offset from null
+            uint8_t* ip = PL ? reinterpret_cast<uint8_t*>((uintptr_t)pkts + p[u].o) : pkts + p[u].o;
             p[u].ip = ip;
             p[u].m = (uint32_t)((uintptr_t)ip & amask);
-            p[u].hdr = p[u].live && p[u].o < limit && limit - p[u].o >= 20u;
+            uint64_t span;
+            if constexpr (PL) {   // bounded by the region and by the packet's own length
+                const uint64_t rr = p[u].live && p[u].o < limit ? limit - p[u].o : 0u;
+                const uint32_t room = (uint32_t)(rr < (uint64_t)pn[u] ? rr : (uint64_t)pn[u]);
+                p[u].hdr = room >= 20u;
+                p[u].room = room;
+                span = p[u].hdr ? (room < cap ? room : cap) : 0u;
+            } else {              // bounded by the region
+                p[u].hdr = p[u].live && p[u].o < limit && limit - p[u].o >= 20u;
+                const uint64_t room = p[u].hdr ? limit - p[u].o : 0u;
+                span = room < cap ? room : cap;
+            }
             const bool live = p[u].hdr;   // a dead slot reads zeros: ver 0, skipped
             // speculative payload chunks: the aligned hull of [ip, ip + span); at
-            // least 80 bytes (any IP header and the TCP check) when the region has them
-            const uint64_t room = live ? limit - p[u].o : 0u;
-            uint64_t span = room < cap ? room : cap;
+            // least 80 bytes (any IP header and the TCP check) when the packet has them
             const uint64_t gap = on1[u] > p[u].o ? on1[u] - p[u].o : ~0ull;
             const uint64_t hint = gap > 80u ? gap : 80u;
             span = span < hint ? span : hint;
@@ -838,8 +859,9 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const 
         const uint32_t ver = (h0 >> 4) & 15u, ihl = h0 & 15u;
         const uint32_t tot = ((h0 >> 8) & 0xff00u) | (h0 >> 24);
         const uint32_t proto = (h8 >> 8) & 0xffu;
+        const bool fits = PL ? tot <= p[u].room : p[u].o + tot <= limit;
         const bool ok = p[u].hdr && ver == 4u && proto == 6u && ihl >= 5u && tot >= ihl * 4u + 20u && tot <= cap &&
-                        p[u].o + tot <= limit;
+                        fits;
         if (!ok) return d;   // group-uniform: skipped, out = 0
         const uint32_t th = ihl * 4u;   // TCP start, packet-relative (even)
         const bool odd = (m & 1u) != 0;
@@ -944,8 +966,9 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const 
 // summed by lb_sums — FILL then subtracts the check word (what zeroing it
 // does). The IPv4 header checksum (IPHDR) is summed per lane from the
 // header dwords: relative dwords, so its u16 halves are the reference's words.
-template <int C>
+template <int C, bool PL>
 __global__ __launch_bounds__(256) void k_ipv4_lb(uint8_t* __restrict__ pkts, const uint64_t* __restrict__ off,
+                                                 const uint32_t* __restrict__ plen,
                                                  uint64_t n, uint32_t cap, uint64_t limit, int mode,
                                                  uint16_t* __restrict__ out, uint8_t* __restrict__ status,
                                                  uint16_t* __restrict__ ipout) {
@@ -959,8 +982,17 @@ __global__ __launch_bounds__(256) void k_ipv4_lb(uint8_t* __restrict__ pkts, con
         const uint64_t i = t * 64 + lane;
         const bool live = i < n;
         const uint64_t o = *reinterpret_cast<const uint64_t*>(zsel(live, reinterpret_cast<const uint8_t*>(off + i)));
-        const bool hdr = live && o < limit && limit - o >= 20u;
-        uint8_t* ip = pkts + o;
+        uint32_t room = 0;   // PL: readable bytes at the packet (region end, its own length)
+        bool hdr;
+        if constexpr (PL) {
+            const uint32_t pl = *reinterpret_cast<const uint32_t*>(zsel(live, reinterpret_cast<const uint8_t*>(plen + i)));
+            const uint64_t rr = live && o < limit ? limit - o : 0u;
+            room = (uint32_t)(rr < (uint64_t)pl ? rr : (uint64_t)pl);
+            hdr = room >= 20u;
+        } else {
+            hdr = live && o < limit && limit - o >= 20u;
+        }
+        uint8_t* ip = PL ? reinterpret_cast<uint8_t*>((uintptr_t)pkts + o) : pkts + o;
         const uint32_t sh = (uint32_t)((uintptr_t)ip & 3u);
         const uint8_t* d0 = ip - sh;
         // the dwords under header bytes [0, 20): D[5] only when ip is not 4-B aligned
@@ -974,8 +1006,8 @@ __global__ __launch_bounds__(256) void k_ipv4_lb(uint8_t* __restrict__ pkts, con
         const uint32_t ver = (h0 >> 4) & 15u, ihl = h0 & 15u;
         const uint32_t tot = ((h0 >> 8) & 0xff00u) | (h0 >> 24);
         const uint32_t proto = (h8 >> 8) & 0xffu;
-        const bool ok = hdr && ver == 4u && proto == 6u && ihl >= 5u && tot >= ihl * 4u + 20u && tot <= cap &&
-                        o + tot <= limit;
+        const bool fits = PL ? tot <= room : o + tot <= limit;
+        const bool ok = hdr && ver == 4u && proto == 6u && ihl >= 5u && tot >= ihl * 4u + 20u && tot <= cap && fits;
         const uint32_t th = ihl * 4u;
         const uint32_t len = ok ? tot - th : 0u;
         uint8_t* tcp = ip + th;
@@ -1578,37 +1610,50 @@ void launch_desc(const uint8_t* base, const tcpcsum_desc_t* d, uint64_t n, uint3
 }
 
 template <int G, int C, int U>
-static void launch_ipv4_t(uint8_t* pkts, const uint64_t* off, uint64_t n, uint32_t cap, uint64_t limit, int mode,
-                          uint16_t* out, uint8_t* status, uint16_t* ipout, hipStream_t s, int max_blocks, bool nt,
-                          uint32_t amask) {
+static void launch_ipv4_t(uint8_t* pkts, const uint64_t* off, const uint32_t* plen, uint64_t n, uint32_t cap,
+                          uint64_t limit, int mode, uint16_t* out, uint8_t* status, uint16_t* ipout, hipStream_t s,
+                          int max_blocks, bool nt, uint32_t amask) {
     constexpr int SPT = (64 / G) * U;
     const dim3 grid(grid_for((n + SPT - 1) / SPT, max_blocks));
-    if (nt)
-        hipLaunchKernelGGL((k_ipv4<G, C, U, true>), grid, dim3(256), 0, s, pkts, off, n, cap, limit, mode, out,
-                           status, ipout, amask);
+    // per-packet bounds only when given: the extra load and register cost the
+    // region-bounded MTU batches 4-8 % (tools/wire_ab.py)
+    if (plen && nt)
+        hipLaunchKernelGGL((k_ipv4<G, C, U, true, true>), grid, dim3(256), 0, s, pkts, off, plen, n, cap, limit, mode,
+                           out, status, ipout, amask);
+    else if (plen)
+        hipLaunchKernelGGL((k_ipv4<G, C, U, false, true>), grid, dim3(256), 0, s, pkts, off, plen, n, cap, limit, mode,
+                           out, status, ipout, amask);
+    else if (nt)
+        hipLaunchKernelGGL((k_ipv4<G, C, U, true, false>), grid, dim3(256), 0, s, pkts, off, plen, n, cap, limit, mode,
+                           out, status, ipout, amask);
     else
-        hipLaunchKernelGGL((k_ipv4<G, C, U, false>), grid, dim3(256), 0, s, pkts, off, n, cap, limit, mode, out,
-                           status, ipout, amask);
+        hipLaunchKernelGGL((k_ipv4<G, C, U, false, false>), grid, dim3(256), 0, s, pkts, off, plen, n, cap, limit,
+                           mode, out, status, ipout, amask);
 }
 
-void launch_ipv4(uint8_t* pkts, const uint64_t* off, uint64_t n, uint32_t cap, uint64_t limit, int mode,
-                 uint16_t* out, uint8_t* status, uint16_t* ipout, hipStream_t s, const Tuning& tu) {
+void launch_ipv4(uint8_t* pkts, const uint64_t* off, const uint32_t* plen, uint64_t n, uint32_t cap, uint64_t limit,
+                 uint64_t footprint, int mode, uint16_t* out, uint8_t* status, uint16_t* ipout, hipStream_t s,
+                 const Tuning& tu) {
     const int max_blocks = tu.max_blocks > 0 ? tu.max_blocks : 8192;
     const int unroll = tu.unroll ? tu.unroll : 1;
     const bool nt = (tu.flags & TCPCSUM_TUNE_WIRE_CACHED) == 0;
     const uint32_t amask = (tu.flags & TCPCSUM_TUNE_WIN16) ? 15u : 127u;
-    // shape by the cap and by the mean packet footprint limit / n (packed small
-    // packets: one chunk per lane; MTU slots: one round of 96 chunks per packet)
+    // shape by the cap and by the mean packet footprint (region bytes / n; the
+    // summed lengths for scatter-gather batches): packed small packets one
+    // chunk per lane, MTU slots one round of 96 chunks per packet
     const uint64_t nch = ((uint64_t)cap + 15u) >> 4;   // an odd start takes one extra round
-    const uint64_t mean = n ? limit / n : 0;
-#define IP_U(G, C)                                                                                                 \
-    do {                                                                                                           \
-        if (unroll <= 1)                                                                                           \
-            launch_ipv4_t<G, C, 1>(pkts, off, n, cap, limit, mode, out, status, ipout, s, max_blocks, nt, amask); \
-        else if (unroll == 2)                                                                                      \
-            launch_ipv4_t<G, C, 2>(pkts, off, n, cap, limit, mode, out, status, ipout, s, max_blocks, nt, amask); \
-        else                                                                                                       \
-            launch_ipv4_t<G, C, 4>(pkts, off, n, cap, limit, mode, out, status, ipout, s, max_blocks, nt, amask); \
+    const uint64_t mean = n ? footprint / n : 0;
+#define IP_U(G, C)                                                                                                   \
+    do {                                                                                                             \
+        if (unroll <= 1)                                                                                             \
+            launch_ipv4_t<G, C, 1>(pkts, off, plen, n, cap, limit, mode, out, status, ipout, s, max_blocks, nt,     \
+                                   amask);                                                                           \
+        else if (unroll == 2)                                                                                        \
+            launch_ipv4_t<G, C, 2>(pkts, off, plen, n, cap, limit, mode, out, status, ipout, s, max_blocks, nt,     \
+                                   amask);                                                                           \
+        else                                                                                                         \
+            launch_ipv4_t<G, C, 4>(pkts, off, plen, n, cap, limit, mode, out, status, ipout, s, max_blocks, nt,     \
+                                   amask);                                                                           \
     } while (0)
     // forced: 0 (8,1), 1 (32,3), 2 (64,4), 3 (16,2), 4 (16,6), 5 (8,12), 6 (8,2), 7 (8,4),
     // 8 / 9: balanced chunk space (k_ipv4_lb) with 4 / 8 loads per lane in flight
@@ -1622,10 +1667,18 @@ void launch_ipv4(uint8_t* pkts, const uint64_t* off, uint64_t n, uint32_t cap, u
         sh = (n >= 65536u && mean <= 1024u) ? 8 : (nch <= 8 || mean <= 112u) ? 0 : nch <= 96 ? 5 : 1;
     if (sh == 8 || sh == 9) {
         const dim3 grid(grid_for((n + 63) / 64, max_blocks));
-        if (sh == 8)
-            hipLaunchKernelGGL(k_ipv4_lb<4>, grid, dim3(256), 0, s, pkts, off, n, cap, limit, mode, out, status, ipout);
+        if (sh == 8 && plen)
+            hipLaunchKernelGGL((k_ipv4_lb<4, true>), grid, dim3(256), 0, s, pkts, off, plen, n, cap, limit, mode, out,
+                               status, ipout);
+        else if (sh == 8)
+            hipLaunchKernelGGL((k_ipv4_lb<4, false>), grid, dim3(256), 0, s, pkts, off, plen, n, cap, limit, mode, out,
+                               status, ipout);
+        else if (plen)
+            hipLaunchKernelGGL((k_ipv4_lb<8, true>), grid, dim3(256), 0, s, pkts, off, plen, n, cap, limit, mode, out,
+                               status, ipout);
         else
-            hipLaunchKernelGGL(k_ipv4_lb<8>, grid, dim3(256), 0, s, pkts, off, n, cap, limit, mode, out, status, ipout);
+            hipLaunchKernelGGL((k_ipv4_lb<8, false>), grid, dim3(256), 0, s, pkts, off, plen, n, cap, limit, mode, out,
+                               status, ipout);
         return;
     }
     switch (sh) {

@@ -30,8 +30,8 @@ int main(int argc, char **argv) {
     CHECK(tcpcsum_pseudo(htonl(0x0A000000), htonl(0xC0A80000), htons(1500)) == 101071);
     CHECK(tcpcsum_pseudo(htonl(0x0A000000), htonl(0xC0A80000), htons(64)) == 61130);
     CHECK(tcpcsum_pseudo(htonl(0x0A000000), htonl(0xC0A80000), 0) == 44746);
-    CHECK(tcpcsum_batch_uniform_dev(NULL, 0, 0, NULL, 0, NULL, 1, NULL) == TCPCSUM_EINVAL);
-    CHECK(tcpcsum_batch_uniform_dev(NULL, 0, 0, NULL, 0, NULL, 0, NULL) == TCPCSUM_OK);
+    CHECK(tcpcsum_batch_uniform_dev(NULL, 0, 0, NULL, 0, NULL, 1, NULL, NULL) == TCPCSUM_EINVAL);
+    CHECK(tcpcsum_batch_uniform_dev(NULL, 0, 0, NULL, 0, NULL, 0, NULL, NULL) == TCPCSUM_OK);
     CHECK(strcmp(tcpcsum_strerror(TCPCSUM_ENODEV), "no usable gfx950 device") == 0);
     char arch[64];
     int dc = tcpcsum_device_check(arch, sizeof arch);

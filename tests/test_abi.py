@@ -86,22 +86,36 @@ def test_scalar_kats(golden):
 
 def test_argument_errors_need_no_device():
     L = tcp_amd.lib()
-    assert L.tcpcsum_batch_uniform_dev(None, 0, 0, None, 0, None, 0, None) == api.OK      # n == 0
-    assert L.tcpcsum_batch_uniform_dev(None, 0, 10, None, 0, None, 5, None) == api.EINVAL
-    assert L.tcpcsum_batch_uniform_dev(1 << 20, 0, 2**31, None, 0, 1 << 20, 5, None) == api.EINVAL
-    assert L.tcpcsum_batch_desc_dev(1 << 20, (1 << 20) + 8, 5, 64, 1 << 20, None) == api.EINVAL   # unaligned desc
-    assert L.tcpcsum_ipv4_batch_dev(1 << 20, 1 << 20, 1 << 20, 5, 1500, 7, None, None, None) == api.EINVAL
-    assert L.tcpcsum_ipv4_batch_dev(1 << 20, 1 << 20, 1 << 20, 5, 1500, 4, None, None, None) == api.EINVAL
-    assert L.tcpcsum_ipv4_batch_dev(1 << 20, 0, 1 << 20, 5, 1500, 0, None, None, None) == api.EINVAL
+    assert L.tcpcsum_batch_uniform_dev(None, 0, 0, None, 0, None, 0, None, None) == api.OK      # n == 0
+    assert L.tcpcsum_batch_uniform_dev(None, 0, 10, None, 0, None, 5, None, None) == api.EINVAL
+    assert L.tcpcsum_batch_uniform_dev(1 << 20, 0, 2**31, None, 0, 1 << 20, 5, None, None) == api.EINVAL
+    assert L.tcpcsum_batch_desc_dev(1 << 20, (1 << 20) + 8, 5, 64, 1 << 20, None, None) == api.EINVAL   # unaligned
+    assert L.tcpcsum_ipv4_batch_dev(1 << 20, 1 << 20, 1 << 20, 5, 1500, 7, None, None, None, None) == api.EINVAL
+    assert L.tcpcsum_ipv4_batch_dev(1 << 20, 1 << 20, 1 << 20, 5, 1500, 4, None, None, None, None) == api.EINVAL
+    assert L.tcpcsum_ipv4_batch_dev(1 << 20, 0, 1 << 20, 5, 1500, 0, None, None, None, None) == api.EINVAL
+    assert L.tcpcsum_ipv4_batch_ptrs_dev(None, 1 << 20, 5, 1500, 0, None, None, None, None) == api.EINVAL
+    assert L.tcpcsum_ipv4_batch_ptrs_dev((1 << 20) + 4, 1 << 20, 5, 1500, 0, None, None, None, None) == api.EINVAL
+    assert L.tcpcsum_ipv4_batch_ptrs_dev(1 << 20, 1 << 20, 5, 1500, 8, None, None, None, None) == api.EINVAL
+    assert L.tcpcsum_ipv4_batch_ptrs_host(None, 1 << 20, 1 << 20, 5, 0, None, None) == api.EINVAL
+    assert L.tcpcsum_ctx_register_host(None, 1 << 20, 4096) == api.EINVAL
+    assert L.tcpcsum_ctx_unregister_host(None, None, 0) == api.EINVAL
+    assert L.tcpcsum_ctx_registered(None, None, None) == api.EINVAL
+    assert L.tcpcsum_ctx_set_tuning(None, None) == api.EINVAL
     ng = ctypes.c_int()
-    assert L.tcpcsum_stream_probe_dev(1 << 20, 17, 1 << 20, ctypes.byref(ng), None) == api.EINVAL
-    assert L.tcpcsum_set_tuning(-1, 0, -1, 0) == api.EINVAL
-    assert L.tcpcsum_set_tuning(0, 3, -1, 0) == api.EINVAL
-    assert L.tcpcsum_set_tuning(0, 0, 13, 0) == api.EINVAL
-    assert L.tcpcsum_set_tuning(0, 0, -1, 3) == api.EINVAL      # PIPE_ON | PIPE_OFF
-    assert L.tcpcsum_set_tuning(0, 0, -1, 12) == api.EINVAL     # NT_ON | NT_OFF
-    assert L.tcpcsum_set_tuning(0, 0, -1, 256) == api.EINVAL
-    assert L.tcpcsum_set_tuning(0, 0, -1, 0) == api.OK
+    assert L.tcpcsum_stream_probe_dev(1 << 20, 17, 1 << 20, ctypes.byref(ng), None, None) == api.EINVAL
+    T = api.Tuning
+    for bad in (T(-1, 0, -1, 0), T(0, 3, -1, 0), T(0, 0, 13, 0), T(0, 0, -2, 0),
+                T(0, 0, -1, 3),      # PIPE_ON | PIPE_OFF
+                T(0, 0, -1, 12),     # NT_ON | NT_OFF
+                T(0, 0, -1, 256)):
+        assert L.tcpcsum_tuning_check(ctypes.byref(bad)) == api.EINVAL
+        # every entry point rejects it before touching anything else (n == 0 included)
+        assert L.tcpcsum_batch_uniform_dev(None, 0, 0, None, 0, None, 0, None, ctypes.byref(bad)) == api.EINVAL
+        assert L.tcpcsum_ipv4_batch_dev(None, 0, None, 0, 0, 0, None, None, None, ctypes.byref(bad)) == api.EINVAL
+        assert L.tcpcsum_plan_uniform(0, 1500, 1500, 10, ctypes.byref(bad), ctypes.byref(ng), ctypes.byref(ng),
+                                      ctypes.byref(ng), ctypes.byref(ng)) == api.EINVAL
+    assert L.tcpcsum_tuning_check(ctypes.byref(T(0, 0, -1, 0))) == api.OK
+    assert L.tcpcsum_tuning_check(None) == api.OK
     assert L.tcpcsum_batch_uniform_host(None, None, 0, 0, None, 0, None, 0) == api.EINVAL
     assert L.tcpcsum_strerror(api.EHIP) == b"HIP runtime error"
 
@@ -113,7 +127,7 @@ def test_no_device_is_reported_not_faked():
         pytest.skip(f"a {arch} GPU is present")
     assert rc == api.ENODEV
     L = tcp_amd.lib()
-    assert L.tcpcsum_batch_uniform_dev(1 << 20, 1500, 1500, None, 0, 1 << 20, 4, None) == api.ENODEV
+    assert L.tcpcsum_batch_uniform_dev(1 << 20, 1500, 1500, None, 0, 1 << 20, 4, None, None) == api.ENODEV
     with pytest.raises(tcp_amd.TcpCsumError):
         tcp_amd.HostContext(0)
 
@@ -144,6 +158,31 @@ def test_plan_respects_overrides():
         assert api.plan_uniform(0, 1500, 1500, 1000)[1] == 5
     finally:
         api.set_tuning(0, 0, -1, 0)
+
+
+def test_tuning_is_per_call_not_global():
+    """The library keeps no tuning state: a tuned call never reshapes a later untuned one,
+    and the Python default set by set_tuning() is per thread."""
+    import threading
+    t = api.make_tuning(0, 0, 6)
+    assert api.plan_uniform(0, 1500, 1500, 1000, tune=t)[1] == 6
+    assert api.plan_uniform(0, 1500, 1500, 1000)[1] == 5        # nothing stuck in the library
+    seen = {}
+    try:
+        api.set_tuning(0, 0, 6)
+
+        def other():
+            seen["other"] = api.plan_uniform(0, 1500, 1500, 1000)[1]
+
+        th = threading.Thread(target=other)
+        th.start()
+        th.join()
+        seen["mine"] = api.plan_uniform(0, 1500, 1500, 1000)[1]
+    finally:
+        api.set_tuning(0, 0, -1, 0)
+    assert seen == {"other": 5, "mine": 6}
+    with pytest.raises(tcp_amd.TcpCsumError):
+        api.make_tuning(0, 3)
 
 
 def test_c_program_links_the_abi():

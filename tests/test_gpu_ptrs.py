@@ -1,0 +1,237 @@
+"""GPU parity for scatter-gather wire batches (one buffer per packet).
+
+The reference keeps every outgoing packet in its own malloc'd 32 KiB buffer
+(/root/reference/loop.c:180-183) and hands sendmmsg one iov_base per message
+(loop.c:53-54). tcpcsum_ipv4_batch_ptrs_dev / _host checksum such batches in
+place, with a per-packet byte bound (iov_len / msg_len). Every result is
+compared with the oracle's FILL / VERIFY of the same packet bytes
+(context.c:104-145 framing of context.c:169-209), bit for bit.
+"""
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    import tcp_amd
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rc, arch = tcp_amd.device_check()
+    assert rc == 0, f"tcpcsum_device_check -> {rc} ({arch}); the HIP path must run on gfx950"
+    return torch.device("cuda:0")
+
+
+def to_dev(a: np.ndarray, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def u16(t) -> np.ndarray:
+    return t.cpu().numpy().view(np.uint16)
+
+
+def tot_len(buf: np.ndarray, o: int) -> int:
+    return (int(buf[o + 2]) << 8) | int(buf[o + 3])
+
+
+def expected(region: np.ndarray, off: np.ndarray, lens: np.ndarray, mode: int):
+    """Oracle per packet, with the per-packet bound: tot_len > lens[i] or lens[i] < 20 -> SKIPPED,
+    untouched, out 0. Mutates region (FILL) like the device."""
+    import tcp_amd
+    ok = np.array([l >= 20 and tot_len(region, int(o)) <= l for o, l in zip(off, lens)], bool)
+    want_out = np.zeros(off.size, np.uint16)
+    want_st = np.full(off.size, tcp_amd.PKT_SKIPPED, np.uint8)
+    if ok.any():
+        o2, s2 = oracle.ipv4_batch(region, off[ok], 65535, mode)
+        want_out[ok] = o2
+        want_st[ok] = s2
+    return want_out, want_st
+
+
+@pytest.mark.parametrize("shape", [-1, 0, 1, 3, 5, 8, 9])
+def test_ipv4_ptrs_dev_vs_oracle(dev, shape):
+    """Packets scattered through one device allocation, addressed by pointer in shuffled order,
+    each bounded by its own length: exact, checks patched in place, nothing else touched."""
+    import tcp_amd
+    from tests.packets import build_batch
+    rng = np.random.default_rng(77)
+    n = 1500
+    region, off, _ = build_batch(rng, n, slot=2048, malformed=True)
+    perm = rng.permutation(n)
+    off = off[perm]
+    lens = np.array([tot_len(region, int(o)) for o in off], np.int64)
+    lens[::7] += rng.integers(1, 500, lens[::7].size)      # more room than the packet needs
+    lens[3::13] -= 1                                        # tot_len one past the bound: SKIPPED
+    lens[5::17] = rng.integers(0, 20, lens[5::17].size)     # no room for an IP header: SKIPPED
+    lens = np.clip(lens, 0, 2048).astype(np.uint32)
+    ref = region.copy()
+    want_out, want_st = expected(ref, off, lens, tcp_amd.IPV4_FILL)
+    dreg = to_dev(region, dev)
+    ptrs = to_dev((off + np.uint64(dreg.data_ptr())).view(np.int64), dev)
+    dl = to_dev(lens.view(np.int32), dev)
+    out = torch.empty(n, dtype=torch.int16, device=dev)
+    st = torch.empty(n, dtype=torch.uint8, device=dev)
+    tcp_amd.ipv4_batch_ptrs(ptrs, dl, n, 65535, tcp_amd.IPV4_FILL, out, st,
+                            tune=tcp_amd.make_tuning(0, 0, shape, 0))
+    assert np.array_equal(st.cpu().numpy(), want_st)
+    assert np.array_equal(u16(out), want_out)
+    assert np.array_equal(dreg.cpu().numpy(), ref)
+    # verify round trip: every filled packet verifies to 0
+    tcp_amd.ipv4_batch_ptrs(ptrs, dl, n, 65535, tcp_amd.IPV4_VERIFY, out, st,
+                            tune=tcp_amd.make_tuning(0, 0, shape, 0))
+    want_v, want_vs = expected(ref.copy(), off, lens, tcp_amd.IPV4_VERIFY)
+    assert np.array_equal(u16(out), want_v)
+    assert np.array_equal(st.cpu().numpy(), want_vs)
+    assert np.all(want_v[want_vs == tcp_amd.PKT_OK] == 0)
+
+
+def test_ipv4_ptrs_dev_iphdr_and_tail(dev):
+    """IPv4 header checksum through pointers; packets ending exactly at their bound, at the end of
+    the allocation."""
+    import tcp_amd
+    from tests.packets import ip_packet
+    rng = np.random.default_rng(3)
+    pkts = [ip_packet(rng, int(rng.integers(0, 1456)), ihl=5 + (i % 3)) for i in range(300)]
+    offs, pos = [], 0
+    for p in pkts:
+        pos += int(rng.integers(0, 9))
+        offs.append(pos)
+        pos += len(p)
+    region = np.zeros(pos, np.uint8)        # the last packet ends at the last byte
+    for o, p in zip(offs, pkts):
+        region[o:o + len(p)] = np.frombuffer(p, np.uint8)
+    off = np.array(offs, np.uint64)
+    lens = np.array([len(p) for p in pkts], np.uint32)
+    mode = tcp_amd.IPV4_FILL | tcp_amd.IPV4_IPHDR
+    ref = region.copy()
+    want_out, want_st = expected(ref, off, lens, mode)
+    dreg = to_dev(region, dev)
+    ptrs = to_dev((off + np.uint64(dreg.data_ptr())).view(np.int64), dev)
+    out = torch.empty(off.size, dtype=torch.int16, device=dev)
+    st = torch.empty(off.size, dtype=torch.uint8, device=dev)
+    tcp_amd.ipv4_batch_ptrs(ptrs, to_dev(lens.view(np.int32), dev), off.size, 65535, mode, out, st)
+    assert np.array_equal(st.cpu().numpy(), want_st)
+    assert np.array_equal(u16(out), want_out)
+    assert np.array_equal(dreg.cpu().numpy(), ref)
+    tcp_amd.ipv4_batch_ptrs(ptrs, to_dev(lens.view(np.int32), dev), off.size, 65535,
+                            tcp_amd.IPV4_VERIFY | tcp_amd.IPV4_IPHDR, out, st)
+    assert np.all(u16(out) == 0) and np.all(st.cpu().numpy() == tcp_amd.PKT_OK)
+
+
+def _loop_pool(rng, n, slot=32768, payload=None):
+    """The reference's out-buffer pool: n separately allocated pageable 32 KiB buffers, each holding
+    one packet at its start (loop.c:180-183, context.c:169-209)."""
+    from tests.packets import ip_packet
+    bufs, lens = [], []
+    for i in range(n):
+        pl = int(rng.integers(0, 1457)) if payload is None else payload
+        p = ip_packet(rng, pl)
+        b = np.empty(slot, np.uint8)      # malloc'd by numpy, pageable
+        b[:] = rng.integers(0, 256, slot, dtype=np.uint8)
+        b[:len(p)] = np.frombuffer(p, np.uint8)
+        bufs.append(b)
+        lens.append(len(p))
+    return bufs, np.array(lens, np.uint32)
+
+
+def test_ipv4_ptrs_host_loop_layout(dev):
+    """1024 separate pageable buffers: FILL in place, then VERIFY; registrations are cached across
+    batches and released on request; bytes outside the check fields never change."""
+    import tcp_amd
+    rng = np.random.default_rng(11)
+    bufs, lens = _loop_pool(rng, 1024)
+    refs = [b.copy() for b in bufs]
+    want = []
+    for r, l in zip(refs, lens):
+        o, s = expected(r, np.array([0], np.uint64), np.array([l], np.uint32), tcp_amd.IPV4_FILL)
+        want.append((o[0], s[0]))
+    ptrs = [b.ctypes.data for b in bufs]
+    with tcp_amd.HostContext(0) as ctx:
+        try:
+            out, st = ctx.ipv4_batch_ptrs(ptrs, lens, tcp_amd.IPV4_FILL)
+            assert [(int(a), int(b)) for a, b in zip(out, st)] == [(int(a), int(b)) for a, b in want]
+            for b, r in zip(bufs, refs):
+                assert np.array_equal(b, r)
+            nreg, nbytes = ctx.registered()
+            assert nreg >= 1 and nbytes >= 1024 * 4096
+            # same buffers again (a second releaseSend): no new registrations, same results
+            out2, _ = ctx.ipv4_batch_ptrs(ptrs, lens, tcp_amd.IPV4_FILL)
+            assert np.array_equal(out2, out)
+            assert ctx.registered() == (nreg, nbytes)
+            v, vs = ctx.ipv4_batch_ptrs(ptrs, lens, tcp_amd.IPV4_VERIFY)
+            assert np.all(v == 0) and np.all(vs == tcp_amd.PKT_OK)
+            # a sub-batch in another order, with a bound one byte short on some packets
+            idx = rng.permutation(1024)[:300]
+            sl = lens[idx].copy()
+            sl[::5] -= 1
+            v, vs = ctx.ipv4_batch_ptrs([ptrs[i] for i in idx], sl, tcp_amd.IPV4_VERIFY)
+            short = np.zeros(300, bool)
+            short[::5] = True
+            assert np.all(vs[short] == tcp_amd.PKT_SKIPPED) and np.all(v[short] == 0)
+            assert np.all(vs[~short] == tcp_amd.PKT_OK) and np.all(v[~short] == 0)
+        finally:
+            ctx.unregister_host()
+        assert ctx.registered() == (0, 0)
+
+
+def test_ipv4_ptrs_host_pinned_and_mixed(dev):
+    """Packets in page-locked memory (tcpcsum_host_alloc) are used through their existing mapping
+    (no registration); mixed with pageable buffers and NULL / short messages in one batch."""
+    import tcp_amd
+    rng = np.random.default_rng(12)
+    pinned = tcp_amd.pinned_empty(64 * 2048)
+    pinned[:] = 0
+    from tests.packets import ip_packet
+    ptrs, lens, refs = [], [], []
+    pageable, _ = _loop_pool(rng, 64, slot=4096)
+    for i in range(64):
+        p = ip_packet(rng, int(rng.integers(0, 1400)))
+        pinned[i * 2048:i * 2048 + len(p)] = np.frombuffer(p, np.uint8)
+    ref_pinned = pinned.copy()
+    for i in range(64):
+        ptrs += [pinned.ctypes.data + i * 2048, pageable[i].ctypes.data]
+        lens += [tot_len(pinned, i * 2048), tot_len(pageable[i], 0)]
+    ptrs += [0, pageable[0].ctypes.data]
+    lens += [1500, 10]
+    ref_page = [b.copy() for b in pageable]
+    with tcp_amd.HostContext(0) as ctx:
+        try:
+            out, st = ctx.ipv4_batch_ptrs(ptrs, np.array(lens, np.uint32), tcp_amd.IPV4_FILL)
+            w1, s1 = expected(ref_pinned, np.arange(64, dtype=np.uint64) * 2048,
+                              np.array(lens[0:128:2], np.uint32), tcp_amd.IPV4_FILL)
+            assert np.array_equal(out[0:128:2], w1) and np.array_equal(st[0:128:2], s1)
+            for i in range(64):
+                w2, s2 = expected(ref_page[i], np.array([0], np.uint64), np.array([lens[2 * i + 1]], np.uint32),
+                                  tcp_amd.IPV4_FILL)
+                assert out[2 * i + 1] == w2[0] and st[2 * i + 1] == s2[0]
+                assert np.array_equal(pageable[i], ref_page[i])
+            assert np.array_equal(pinned, ref_pinned)
+            assert list(st[-2:]) == [tcp_amd.PKT_SKIPPED] * 2 and list(out[-2:]) == [0, 0]
+            nreg, nbytes = ctx.registered()
+            assert nreg >= 1 and nbytes <= 64 * 2 * 4096     # only the pageable buffers were page-locked
+        finally:
+            ctx.unregister_host()
+
+
+def test_ipv4_ptrs_host_context_tuning(dev):
+    """Tuning set on one context shapes only that context's batches (results identical)."""
+    import tcp_amd
+    rng = np.random.default_rng(13)
+    bufs, lens = _loop_pool(rng, 200, slot=4096)
+    ptrs = [b.ctypes.data for b in bufs]
+    with tcp_amd.HostContext(0) as a, tcp_amd.HostContext(0) as b:
+        try:
+            b.set_tuning(0, 0, 5, tcp_amd.TUNE_WIN16)
+            va, sa = a.ipv4_batch_ptrs(ptrs, lens, tcp_amd.IPV4_VERIFY)
+            vb, sb = b.ipv4_batch_ptrs(ptrs, lens, tcp_amd.IPV4_VERIFY)
+            assert np.array_equal(va, vb) and np.array_equal(sa, sb)
+            with pytest.raises(tcp_amd.TcpCsumError):
+                b.set_tuning(0, 3)
+        finally:
+            a.unregister_host()
+            b.unregister_host()

@@ -77,8 +77,11 @@ def test_fails_loudly_without_gpu(tmp_path):
 
 
 @pytest.mark.gpu
-def test_tx_fill_on_gpu(tmp_path):
-    r, pkts, stats = run_loop(tmp_path, 3000, {"TCPCSUM_PRELOAD_TX": "fill", "TCPCSUM_PRELOAD_RX": "verify"})
+@pytest.mark.parametrize("copy", ["0", "1"])
+def test_tx_fill_on_gpu(tmp_path, copy):
+    """Default: in place on the caller's 32 KiB buffers (scatter-gather); COPY=1: gather into staging."""
+    r, pkts, stats = run_loop(tmp_path, 3000, {"TCPCSUM_PRELOAD_TX": "fill", "TCPCSUM_PRELOAD_RX": "verify",
+                                               "TCPCSUM_PRELOAD_COPY": copy})
     assert r.returncode == 0, r.stderr
     assert len(pkts) == 3000
     for built, got in pkts:
@@ -100,9 +103,10 @@ def test_tx_verify_live_parity_with_cpu_checks(tmp_path):
 
 
 @pytest.mark.gpu
-def test_tx_fill_with_ip_header(tmp_path):
+@pytest.mark.parametrize("copy", ["0", "1"])
+def test_tx_fill_with_ip_header(tmp_path, copy):
     r, pkts, stats = run_loop(tmp_path, 700, {"TCPCSUM_PRELOAD_TX": "fill", "TCPCSUM_PRELOAD_IPHDR": "1",
-                                              "TCPCSUM_PRELOAD_RX": "verify"})
+                                              "TCPCSUM_PRELOAD_RX": "verify", "TCPCSUM_PRELOAD_COPY": copy})
     assert r.returncode == 0, r.stderr
     for built, got in pkts:
         assert got == oracle_fill(built, 2)

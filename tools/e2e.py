@@ -9,8 +9,13 @@ This measures the library's host entry points on MI355X:
   * tcpcsum_ipv4_batch_host FILL on one releaseSend-sized batch (1024 packets
     of 1500 B, loop.c:27-94) in the reference's pool layout (32 KiB slots) and
     packed, pageable vs pinned — per-batch latency (--sweep: per wire kernel
-    shape / window flag).
-GPU path only; CPU rates come from bench.py's cpu_baseline.
+    shape / window flag);
+  * tcpcsum_ipv4_batch_ptrs_host FILL over 1024 separately allocated pageable
+    buffers (the loop's own layout, loop.c:180-183): first batch (page-locks
+    the buffers) and steady state;
+  * the sendmmsg seam itself (tools/mmsg_bench under libtcpcsum_preload.so,
+    in place and with TCPCSUM_PRELOAD_COPY=1) beside the reference's CPU path
+    for the same batch (one csum_continue per packet, -O2, one core).
 
   python tools/e2e.py  -> one JSON line per measurement
 """
@@ -83,7 +88,7 @@ def main():
                     if "--sweep" in sys.argv else [(-1, 0)])
         for name, r in (("pageable", reg), ("pinned_zero_copy", pin)):
             for sh, fl in variants:
-                tcp_amd.set_tuning(0, 0, sh, fl)
+                ctx.set_tuning(0, 0, sh, fl)
                 ctx.ipv4_batch(r, offs, 32768, tcp_amd.IPV4_FILL)
                 tmin, tmed = best_of(lambda: ctx.ipv4_batch(r, offs, 32768, tcp_amd.IPV4_FILL), 50)
                 print(json.dumps({"measure": "ipv4_fill_host_1024x1500", "layout": layout, "memory": name,
@@ -92,8 +97,58 @@ def main():
                                   "region_bytes": int(r.size),
                                   "GiB/s_packet_bytes_median": round(1024 * 1500 / tmed / 2**30, 2)}),
                       flush=True)
-            tcp_amd.set_tuning(0, 0, -1, 0)
+            ctx.set_tuning(0, 0, -1, 0)
+
+    # the loop's own layout: 1024 separate pageable buffers, in and out alternating
+    bufs = []
+    for i in range(2048):
+        b = np.empty(32768, np.uint8)
+        if i & 1:
+            p = np.frombuffer(ip_packet(rng, 1456), np.uint8)
+            b[:p.size] = p
+        bufs.append(b)
+    outb = bufs[1::2]
+    ptrs = [b.ctypes.data for b in outb]
+    lens = np.full(1024, 1500, np.uint32)
+    t0 = time.perf_counter()
+    ctx.ipv4_batch_ptrs(ptrs, lens, tcp_amd.IPV4_FILL)
+    first = time.perf_counter() - t0
+    tmin, tmed = best_of(lambda: ctx.ipv4_batch_ptrs(ptrs, lens, tcp_amd.IPV4_FILL), 200)
+    nreg, nbytes = ctx.registered()
+    print(json.dumps({"measure": "ipv4_fill_ptrs_host_1024x1500", "layout": "1024 separate 32 KiB buffers (pageable)",
+                      "first_batch_us": round(first * 1e6, 1), "us_best": round(tmin * 1e6, 1),
+                      "us_median": round(tmed * 1e6, 1), "registrations": nreg, "registered_bytes": nbytes,
+                      "GiB/s_packet_bytes_median": round(1024 * 1500 / tmed / 2**30, 2)}), flush=True)
+    if "--sweep" in sys.argv:
+        for sh in (0, 1, 3, 4, 5, 6, 7, 8):
+            for fl in (0, tcp_amd.TUNE_WIN16, tcp_amd.TUNE_WIRE_CACHED):
+                ctx.set_tuning(0, 0, sh, fl)
+                tmin, tmed = best_of(lambda: ctx.ipv4_batch_ptrs(ptrs, lens, tcp_amd.IPV4_FILL), 100)
+                print(json.dumps({"measure": "ipv4_fill_ptrs_host_1024x1500", "shape": sh, "flags": fl,
+                                  "us_best": round(tmin * 1e6, 1), "us_median": round(tmed * 1e6, 1)}), flush=True)
+        ctx.set_tuning(0, 0, -1, 0)
+    ctx.unregister_host()
     ctx.close()
+
+    # the seam itself: the interposer's per-batch latency vs the reference's CPU path
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(repo, "tools", "mmsg_bench")
+    pre = os.path.join(repo, "tcp_amd", "libtcpcsum_preload.so")
+    import subprocess
+    for label, mode, env_extra in (("cpu_reference_O2", "cpu", {}),
+                                   ("preload_off", "gpu", {"TCPCSUM_PRELOAD_TX": "off"}),
+                                   ("preload_fill_inplace", "gpu", {"TCPCSUM_PRELOAD_TX": "fill"}),
+                                   ("preload_fill_copy", "gpu", {"TCPCSUM_PRELOAD_TX": "fill",
+                                                                 "TCPCSUM_PRELOAD_COPY": "1"})):
+        env = dict(os.environ)
+        if mode == "gpu":
+            env.update({"LD_PRELOAD": pre, "TCPCSUM_PRELOAD_ANY_SOCKET": "1"})
+        env.update(env_extra)
+        r = subprocess.run([exe, mode, "300"], env=env, capture_output=True, text=True, timeout=300)
+        line = r.stdout.strip().splitlines()[-1] if r.stdout.strip() else "{}"
+        d = json.loads(line)
+        d.update({"measure": "sendmmsg_seam_1024x1500", "variant": label, "rc": r.returncode})
+        print(json.dumps(d), flush=True)
 
 
 if __name__ == "__main__":

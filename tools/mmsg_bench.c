@@ -1,0 +1,129 @@
+/*
+ * mmsg_bench.c — per-batch latency of the sendmmsg seam on the reference's own
+ * buffer layout: 1024 in/out buffers malloc'd alternately, 32 KiB each
+ * (/root/reference/loop.c:180-183), one finished 1500-byte IPv4/TCP packet at
+ * the start of each out-buffer (context.c:169-206, check = 0 as at :182), and
+ * one sendmmsg of all 1024 messages, one iov_base each (loop.c:44-75).
+ *
+ *   mmsg_bench gpu <iters>   time sendmmsg; run under LD_PRELOAD=libtcpcsum_preload.so
+ *                            with TCPCSUM_PRELOAD_ANY_SOCKET=1 (the socket is an
+ *                            unconnected UDP socket, so the real sendmmsg returns
+ *                            EDESTADDRREQ at once: the time is the interposer's)
+ *   mmsg_bench cpu <iters>   the reference's CPU path for the same batch: one
+ *                            csum_continue(getPseudoHeaderSum(...)) per packet
+ *                            (tcpcsum_continue / tcpcsum_pseudo == context.c:104-145,
+ *                            gcc -O2), stored at TCP+16 as context.c:208 does
+ *
+ * Prints one JSON line: first-call and steady-state (min / median) latency
+ * per 1024-packet batch, and whether every check equals the CPU's.
+ */
+#define _GNU_SOURCE
+#include <arpa/inet.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/socket.h>
+#include <time.h>
+#include <unistd.h>
+
+#include "tcpcsum.h"
+
+enum { NPKT = 1024, SLOT = 32768, PAYLOAD = 1456 };
+
+static uint64_t rng = 0x243F6A8885A308D3ull;
+static uint32_t next32(void) {
+    rng ^= rng << 13; rng ^= rng >> 7; rng ^= rng << 17;
+    return (uint32_t) (rng >> 16);
+}
+
+static void build(uint8_t *b, int i) {
+    const size_t tot = 20 + 24 + PAYLOAD;
+    memset(b, 0, 44);
+    b[0] = 0x45;
+    b[2] = (uint8_t) (tot >> 8); b[3] = (uint8_t) tot;
+    b[4] = 0xd4; b[5] = 0x31;
+    b[8] = 255; b[9] = 6;
+    uint32_t sa = htonl(0x7F000001u), da = htonl(0x0A000000u | (uint32_t) i);
+    memcpy(b + 12, &sa, 4); memcpy(b + 16, &da, 4);
+    uint8_t *t = b + 20;
+    t[0] = 4000 >> 8; t[1] = 4000 & 255; t[2] = 45001 >> 8; t[3] = 45001 & 255;
+    uint32_t seq = htonl(next32()), ack = htonl(next32());
+    memcpy(t + 4, &seq, 4); memcpy(t + 8, &ack, 4);
+    t[12] = 6 << 4; t[13] = 0x18;
+    t[14] = 8192 >> 8;
+    t[20] = 3; t[21] = 3; t[22] = 5;
+    for (size_t k = 0; k < PAYLOAD; ++k) t[24 + k] = (uint8_t) next32();
+}
+
+/* The reference's per-packet check (context.c:208), on the CPU. */
+static uint16_t cpu_check(const uint8_t *ip) {
+    uint32_t sa, da;
+    memcpy(&sa, ip + 12, 4);
+    memcpy(&da, ip + 16, 4);
+    const int len = 24 + PAYLOAD;
+    return tcpcsum_continue(tcpcsum_pseudo(sa, da, htons((uint16_t) len)), (const char *) ip + 20, len);
+}
+
+static double now_us(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec * 1e6 + ts.tv_nsec * 1e-3;
+}
+
+static int cmp_d(const void *a, const void *b) {
+    const double x = *(const double *) a, y = *(const double *) b;
+    return x < y ? -1 : x > y;
+}
+
+int main(int argc, char **argv) {
+    if (argc < 3) { fprintf(stderr, "usage: %s gpu|cpu iters\n", argv[0]); return 2; }
+    const int gpu = !strcmp(argv[1], "gpu");
+    const int iters = atoi(argv[2]) > 1 ? atoi(argv[2]) : 2;
+    static uint8_t *inb[NPKT], *outb[NPKT];
+    for (int i = 0; i < NPKT; ++i) {   /* loop.c:180-183: in and out buffers alternate */
+        inb[i] = malloc(SLOT);
+        memset(inb[i], 0, SLOT);          /* the rx buffers, touched as recvmmsg would */
+        outb[i] = malloc(SLOT);
+        build(outb[i], i);
+    }
+    static struct iovec iov[NPKT];
+    static struct mmsghdr vec[NPKT];
+    for (int i = 0; i < NPKT; ++i) {
+        iov[i].iov_base = outb[i];
+        iov[i].iov_len = 20 + 24 + PAYLOAD;   /* = tot_len, as loop.c:47,54 */
+        vec[i].msg_hdr.msg_iov = &iov[i];
+        vec[i].msg_hdr.msg_iovlen = 1;
+    }
+    const int fd = socket(AF_INET, SOCK_DGRAM, 0);
+    double *t = malloc(sizeof(double) * (size_t) iters);
+    for (int k = 0; k < iters; ++k) {
+        for (int i = 0; i < NPKT; ++i) memset(outb[i] + 36, 0, 2);   /* check = 0 (context.c:182) */
+        const double t0 = now_us();
+        if (gpu) {
+            (void) sendmmsg(fd, vec, NPKT, 0);
+        } else {
+            for (int i = 0; i < NPKT; ++i) {
+                const uint16_t c = cpu_check(outb[i]);
+                memcpy(outb[i] + 36, &c, 2);
+            }
+        }
+        t[k] = now_us() - t0;
+    }
+    int mismatches = 0;
+    for (int i = 0; i < NPKT; ++i) {
+        uint16_t got;
+        memcpy(&got, outb[i] + 36, 2);
+        memset(outb[i] + 36, 0, 2);
+        mismatches += got != cpu_check(outb[i]);
+    }
+    const double first = t[0];
+    qsort(t + 1, (size_t) (iters - 1), sizeof(double), cmp_d);
+    printf("{\"path\": \"%s\", \"batch\": \"1024 x 1500-B packets, separate 32 KiB malloc'd buffers (loop.c:180-183)\", "
+           "\"first_us\": %.1f, \"min_us\": %.1f, \"median_us\": %.1f, \"iters\": %d, \"checks_match_cpu\": %s, "
+           "\"mismatches\": %d}\n",
+           gpu ? "sendmmsg under libtcpcsum_preload.so" : "cpu csum_continue per packet (-O2)", first, t[1],
+           t[1 + (iters - 1) / 2], iters, mismatches ? "false" : "true", mismatches);
+    close(fd);
+    return 0;
+}
