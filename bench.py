@@ -12,8 +12,11 @@ of the batch) over the GPU's whole shard.
 
 Multi-GPU: one process per GPU, each owns a contiguous shard of segments
 (weak scaling: 1M segments per GPU; N=8 is BASELINE's 8M x 1500 config). No
-collective touches the data path; torch.distributed (RCCL) is used only for the
-barriers around the timed region and the max-over-ranks of its duration.
+collective touches the data path (north_star: independent segment batches, no
+RCCL): torch.distributed over gloo (CPU) only brackets the timed region with
+barriers and takes the max over ranks of its duration and the min of the
+per-rank digest checks. `python bench.py --gpus N` without a launcher starts
+the N rank processes itself (before any GPU call) and relays rank 0's line.
 
 Rank 0 prints one JSON line. ``roofline.achieved`` = algorithmic bytes per
 launch (segments x segment bytes) / the kernel's average duration, measured
@@ -104,37 +107,64 @@ def load_traffic(config: str):
         return None
 
 
+def host_cpu_info() -> dict:
+    """Model, sockets, physical cores and hardware threads of this host; the cgroup CPU quota."""
+    model, sockets, cores = "", set(), set()
+    phys = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                k, _, v = line.partition(":")
+                k, v = k.strip(), v.strip()
+                if k == "model name" and not model:
+                    model = v
+                elif k == "physical id":
+                    phys = v
+                    sockets.add(v)
+                elif k == "core id":
+                    cores.add((phys, v))
+    except OSError:
+        pass
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    return {"host_cpu": model, "sockets": len(sockets) or None, "physical_cores": len(cores) or None,
+            "hw_threads": os.cpu_count(), "threads_in_affinity": avail, "cgroup_cpu_quota": quota}
+
+
 def cpu_baseline(seg_len: int, seconds: float) -> dict:
-    """The reference's scalar checksum (C restatement, oracle/) on this host, bounded sample."""
+    """The reference's scalar checksum (C restatement of context.c:104-145, oracle/) on this host,
+    as BASELINE.md plans it: gcc -O0 -g (the reference Makefile sets no CFLAGS, Makefile:3) and
+    -O2, on 1 thread and on every hardware thread of the affinity mask (nproc), best of >= 5 passes
+    over the same host-resident batch (bounded sample). Persistent threads, contiguous shards."""
     import oracle
     # the same batch as the GPU step when it fits in 1.5 GiB (1M x 1500 B: exactly it), so the
     # sample streams from host DRAM like the GPU's does from HBM
     nseg = max(1, min(1 << 20, (3 << 29) // seg_len))
-    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    threads = max(1, min(16, avail))
+    info = host_cpu_info()
+    nproc = max(1, info["threads_in_affinity"])
     res = {}
-    for key, th, opt, secs in (("o2_all", threads, "O2", seconds * 0.4), ("o2_1", 1, "O2", seconds * 0.35),
-                               ("o0_1", 1, "O0", seconds * 0.25)):
-        gibs, _, passes = oracle.cpu_bench(th, seg_len, nseg, secs, opt)
-        res[key] = (gibs, th, passes)
-    gibs, th, _ = res["o2_all"]
-    model = ""
-    try:
-        with open("/proc/cpuinfo") as f:
-            for line in f:
-                if line.startswith("model name"):
-                    model = line.split(":", 1)[1].strip()
-                    break
-    except OSError:
-        pass
+    plan = (("O2", nproc, 0.15), ("O2", 1, 0.25), ("O0", 1, 0.45), ("O0", nproc, 0.15))
+    for opt, th, share in plan:
+        gibs, digest, passes, mean = oracle.cpu_bench(th, seg_len, nseg, seconds * share, opt, mean=True)
+        res[(opt, th)] = {"GiB/s": round(gibs, 3), "passes": passes, "digest": digest, "mean": round(mean, 3)}
+    best = res[("O2", nproc)]
     return {
-        "value": round(gibs, 3), "unit": "GiB/s", "cores": th, "kind": "port",
-        "sample": f"{nseg} x {seg_len}-byte segments (Appendix B stream, host DRAM), gcc -O2, "
-                  f"{th} pthreads, best pass of >=3 over ~{seconds * 0.4:.0f}s",
-        "single_core_O2": round(res["o2_1"][0], 3),
-        "single_core_O0_makefile_flags": round(res["o0_1"][0], 3),
-        "host_cpu": model,
-        "threads_available": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count(),
+        "value": best["GiB/s"], "unit": "GiB/s", "cores": nproc, "kind": "port",
+        "sample": f"{nseg} x {seg_len}-byte segments (Appendix B stream, host DRAM), gcc -O2, {nproc} threads "
+                  f"(nproc), best of >= {best['passes']} passes",
+        "threads": nproc,
+        "O2_nproc": best["GiB/s"], "O2_1thread": res[("O2", 1)]["GiB/s"],
+        "O0_nproc": res[("O0", nproc)]["GiB/s"], "O0_1thread": res[("O0", 1)]["GiB/s"],
+        "passes": {f"{o}_{'1thread' if t == 1 else 'nproc'}": r["passes"] for (o, t), r in res.items()},
+        # mean over all passes: below the best pass where a cgroup CPU quota throttles the threads
+        "O2_nproc_mean_over_passes": best["mean"],
+        "digests_agree": len({r["digest"] for r in res.values()}) == 1,
+        **info,
     }
 
 
@@ -215,6 +245,51 @@ def run_config(config: str, steps: int, warmup: int, rank: int, world: int, dist
     return r, bufs, rot
 
 
+def spawn_ranks(args, argv, script=None) -> int:
+    """`bench.py --gpus N` with no launcher: start ranks 0..N-1 as child processes (this process
+    has made no GPU call), rendezvous on 127.0.0.1, relay rank 0's JSON line, return the worst
+    exit code. If a rank fails the others are stopped (by PID) instead of waiting in a barrier."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, script or os.path.abspath(__file__)] + list(argv if argv is not None else sys.argv[1:])
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            failed = [c for c in codes if c not in (None, 0)]
+            if failed:   # a rank died: the others would wait in a barrier for ever
+                rc = failed[0]
+                for p in procs:
+                    if p.poll() is None:
+                        p.terminate()
+                break
+            if all(c == 0 for c in codes):
+                break
+            time.sleep(0.05)
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    out0 = procs[0].stdout.read() if procs[0].stdout else b""
+    sys.stdout.write(out0.decode())
+    sys.stdout.flush()
+    return rc
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -233,18 +308,19 @@ def main(argv=None) -> int:
     ap.add_argument("--rotate", type=int, default=0, help="distinct batches to rotate (0 = auto)")
     args = ap.parse_args(argv)
 
+    rank, world, local = dist_env()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn_ranks(args, argv)   # before any GPU call in this process
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 2
+
     import numpy as np
     import torch
     import tcp_amd
 
-    rank, world, local = dist_env()
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            print("bench.py: --gpus > 1 needs torch.distributed.run with one process per GPU", file=sys.stderr)
-            return 2
-    # Rehearsal knobs for a 1-GPU box (never needed on an N-GPU node):
-    # TCPCSUM_BENCH_SHARE_DEVICE=1 puts every rank on GPU 0, TCPCSUM_BENCH_BACKEND=gloo
-    # runs the barriers / max-reduce on the CPU (RCCL refuses two ranks on one GPU).
+    # Rehearsal knob for a 1-GPU box (never needed on an N-GPU node):
+    # TCPCSUM_BENCH_SHARE_DEVICE=1 puts every rank on GPU 0.
     if os.environ.get("TCPCSUM_BENCH_SHARE_DEVICE") == "1":
         local = 0
     torch.cuda.set_device(local)
@@ -252,7 +328,9 @@ def main(argv=None) -> int:
     dist = None
     if world > 1:
         import torch.distributed as tdist
-        backend = os.environ.get("TCPCSUM_BENCH_BACKEND", "nccl")
+        # no data-path collective: gloo (CPU) carries the barriers and the two reductions;
+        # TCPCSUM_BENCH_BACKEND=nccl selects RCCL instead
+        backend = os.environ.get("TCPCSUM_BENCH_BACKEND", "gloo")
         if backend == "nccl":
             tdist.init_process_group("nccl", device_id=device)
         else:
@@ -333,6 +411,9 @@ def main(argv=None) -> int:
                          "algorithmic_bytes_per_launch": batch_bytes},
             "digest_check": check,
         }
+        if dist is not None:
+            line["barrier_backend"] = dist.get_backend()
+            line["ranks_share_one_gpu"] = os.environ.get("TCPCSUM_BENCH_SHARE_DEVICE") == "1"
         if probe:
             line["stream_probe"] = probe
         if extra:

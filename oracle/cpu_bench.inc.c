@@ -46,14 +46,36 @@ struct cb_job {
     uint16_t *out;
 };
 
-static void *cb_worker(void *arg) {
-    struct cb_job *j = (struct cb_job *) arg;
+static void cb_work(const struct cb_job *j) {
     const uint16_t len_be = htons((uint16_t) j->seg_len);
     for (uint64_t i = j->s0; i < j->s1; ++i) {
         uint32_t sa = htonl(0x0A000000u | (uint32_t) (i & 0xFFFFFFu));
         uint32_t da = htonl(0xC0A80000u | (uint32_t) ((i * 7u) & 0xFFFFu));
         j->out[i] = CB_CSUM(CB_PSEUDO(sa, da, len_be),
                             (char *) (j->buf + i * (uint64_t) j->seg_len), (int) j->seg_len);
+    }
+}
+
+/* A persistent pool: every pass is [barrier, work, barrier], so thread
+ * creation is outside the timed passes (it would dominate at hundreds of
+ * threads). Thread 0 is the caller. */
+struct cb_pool {
+    pthread_barrier_t start, done;
+    volatile int stop;
+};
+
+struct cb_arg {
+    struct cb_pool *pool;
+    struct cb_job job;
+};
+
+static void *cb_worker(void *arg) {
+    struct cb_arg *a = (struct cb_arg *) arg;
+    for (;;) {
+        pthread_barrier_wait(&a->pool->start);
+        if (a->pool->stop) break;
+        cb_work(&a->job);
+        pthread_barrier_wait(&a->pool->done);
     }
     return 0;
 }
@@ -64,39 +86,51 @@ static double cb_now(void) {
     return (double) ts.tv_sec + 1e-9 * (double) ts.tv_nsec;
 }
 
+#define CB_MAX_THREADS 1024
+
+/* Best pass (GiB/s) over at least 5 passes and min_seconds of passes. */
 double CB_BENCH_NAME(int nthreads, uint32_t seg_len, uint64_t nseg, double min_seconds,
-                     uint64_t *digest_out, int *passes_out) {
+                     uint64_t *digest_out, int *passes_out, double *total_out) {
     if (nthreads < 1) nthreads = 1;
-    if (nthreads > 256) nthreads = 256;
+    if (nthreads > CB_MAX_THREADS) nthreads = CB_MAX_THREADS;
     uint64_t bytes = nseg * (uint64_t) seg_len;
     uint8_t *buf = (uint8_t *) aligned_alloc(64, (bytes + 63) & ~63ull);
     uint16_t *out = (uint16_t *) calloc(nseg ? nseg : 1, sizeof(uint16_t));
-    if (!buf || !out) { free(buf); free(out); return -1.0; }
+    pthread_t *th = (pthread_t *) calloc((size_t) nthreads, sizeof(pthread_t));
+    struct cb_arg *args = (struct cb_arg *) calloc((size_t) nthreads, sizeof(struct cb_arg));
+    if (!buf || !out || !th || !args) { free(buf); free(out); free(th); free(args); return -1.0; }
     cb_fill(buf, bytes);
-    /* first-touch the output */
-    memset(out, 0, nseg * sizeof(uint16_t));
+    memset(out, 0, nseg * sizeof(uint16_t));   /* first-touch the output */
 
-    pthread_t th[256];
-    struct cb_job jobs[256];
+    struct cb_pool pool;
+    pool.stop = 0;
+    pthread_barrier_init(&pool.start, 0, (unsigned) nthreads);
+    pthread_barrier_init(&pool.done, 0, (unsigned) nthreads);
+    for (int t = 0; t < nthreads; ++t) {
+        args[t].pool = &pool;
+        args[t].job.buf = buf; args[t].job.seg_len = seg_len; args[t].job.out = out;
+        args[t].job.s0 = nseg * (uint64_t) t / (uint64_t) nthreads;
+        args[t].job.s1 = nseg * (uint64_t) (t + 1) / (uint64_t) nthreads;
+        if (t) pthread_create(&th[t], 0, cb_worker, &args[t]);
+    }
     double best = 1e300, total = 0.0;
     int passes = 0;
-    while (passes < 3 || total < min_seconds) {
+    while (passes < 5 || total < min_seconds) {
+        pthread_barrier_wait(&pool.start);
         double t0 = cb_now();
-        for (int t = 0; t < nthreads; ++t) {
-            jobs[t].buf = buf; jobs[t].seg_len = seg_len; jobs[t].out = out;
-            jobs[t].s0 = nseg * (uint64_t) t / (uint64_t) nthreads;
-            jobs[t].s1 = nseg * (uint64_t) (t + 1) / (uint64_t) nthreads;
-            if (nthreads == 1) cb_worker(&jobs[t]);
-            else pthread_create(&th[t], 0, cb_worker, &jobs[t]);
-        }
-        if (nthreads > 1)
-            for (int t = 0; t < nthreads; ++t) pthread_join(th[t], 0);
+        cb_work(&args[0].job);
+        pthread_barrier_wait(&pool.done);
         double dt = cb_now() - t0;
         total += dt;
         if (dt < best) best = dt;
         ++passes;
         if (passes > 100000) break;
     }
+    pool.stop = 1;
+    pthread_barrier_wait(&pool.start);
+    for (int t = 1; t < nthreads; ++t) pthread_join(th[t], 0);
+    pthread_barrier_destroy(&pool.start);
+    pthread_barrier_destroy(&pool.done);
     if (digest_out) {
         uint64_t h = 0xcbf29ce484222325ull;
         for (uint64_t i = 0; i < nseg; ++i) {
@@ -106,7 +140,10 @@ double CB_BENCH_NAME(int nthreads, uint32_t seg_len, uint64_t nseg, double min_s
         *digest_out = h;
     }
     if (passes_out) *passes_out = passes;
+    if (total_out) *total_out = total;
     free(buf);
     free(out);
+    free(th);
+    free(args);
     return (double) bytes / best / (double) (1ull << 30);
 }

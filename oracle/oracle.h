@@ -71,10 +71,11 @@ void oracle_digest(const uint16_t *out, uint64_t n, uint64_t *fnv, uint64_t *sum
 /* CPU throughput harness (CLOCK_MONOTONIC, pthreads, contiguous shards).
  * Times the checksum of nseg synthetic segments of seg_len bytes held in
  * host memory, pseudo-header sum computed per segment as context.c:208 does.
- * Repeats passes until min_seconds elapsed (>= 3 passes); returns the best
- * pass in GiB/s and the fnv1a64 digest of that pass's outputs. */
+ * Repeats passes until min_seconds elapsed (>= 5 passes, persistent threads);
+ * returns the best pass in GiB/s, the fnv1a64 digest of the outputs and the
+ * summed duration of all passes (mean rate = passes * bytes / total). */
 double oracle_cpu_bench(int nthreads, uint32_t seg_len, uint64_t nseg, double min_seconds,
-                        uint64_t *digest_out, int *passes_out);
+                        uint64_t *digest_out, int *passes_out, double *total_out);
 
 #ifdef __cplusplus
 }

@@ -81,3 +81,53 @@ def test_shard_range_matches_appendix_b_shards(golden):
     for k in range(8):
         g = golden["digests"][f"8Mx1500_shard{k}"]
         assert bench.shard_range(8 << 20, 8, k) == (g["seg0"], g["n"])
+
+
+STUB = """
+import json, os, sys, time
+sys.path.insert(0, {repo!r})
+import torch, torch.distributed as dist
+import bench
+rank, world, _ = bench.dist_env()
+dist.init_process_group("gloo")
+if os.environ.get("STUB_FAIL_RANK") == str(rank):
+    sys.exit(7)
+wall = bench.timed_region(lambda: time.sleep(0.001 * (rank + 1)), 3, 1, dist, lambda: None)
+wmax = bench.max_over_ranks(wall, dist, torch.device("cpu"))
+if rank == 0:
+    print(json.dumps({{"world": world, "wall_max": wmax, "mine": wall}}))
+dist.destroy_process_group()
+"""
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_spawn_ranks_relays_rank0_line(tmp_path, world):
+    """bench.py --gpus N without a launcher: N rank processes on 127.0.0.1, rank 0's line relayed,
+    the max over ranks is the slowest rank's time."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    stub = tmp_path / "stub.py"
+    stub.write_text(STUB.format(repo=repo))
+    code = ("import sys, argparse; sys.path.insert(0, %r); import bench; "
+            "sys.exit(bench.spawn_ranks(argparse.Namespace(gpus=%d), [], script=%r))" % (repo, world, str(stub)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=180, env=env)
+    assert r.returncode == 0, r.stderr
+    import json
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["world"] == world and d["wall_max"] >= d["mine"] > 0
+
+
+def test_spawn_ranks_stops_the_others_when_one_fails(tmp_path):
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    stub = tmp_path / "stub.py"
+    stub.write_text(STUB.format(repo=repo))
+    code = ("import sys, argparse; sys.path.insert(0, %r); import bench; "
+            "sys.exit(bench.spawn_ranks(argparse.Namespace(gpus=2), [], script=%r))" % (repo, str(stub)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    env["STUB_FAIL_RANK"] = "1"
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 7
