@@ -17,12 +17,12 @@ CFLAGS_LIB ?= -O2 -fPIC -Wall -Wextra
 
 LIB := tcp_amd/libtcpcsum.so
 HIP_SRCS := tcp_amd/csrc/tcpcsum_kernels.hip tcp_amd/csrc/tcpcsum_api.hip
-HDRS := include/tcpcsum.h tcp_amd/csrc/tcpcsum_internal.h
+HDRS := include/tcpcsum.h tcp_amd/csrc/tcpcsum_internal.h tcp_amd/csrc/host_registry.h
 OBJDIR := build/obj
 
 PRELOAD := tcp_amd/libtcpcsum_preload.so
 
-all: $(LIB) $(PRELOAD) oracle tests/c/abi_smoke tests/c/mmsg_loop tools/mmsg_bench
+all: $(LIB) $(PRELOAD) oracle tests/c/abi_smoke tests/c/mmsg_loop tests/c/raw_echo tools/mmsg_bench
 
 $(OBJDIR)/%.o: tcp_amd/csrc/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
@@ -56,10 +56,13 @@ tests/c/abi_smoke: tests/c/abi_smoke.c include/tcpcsum.h $(LIB)
 tests/c/mmsg_loop: tests/c/mmsg_loop.c include/tcpcsum.h $(LIB)
 	$(CC) -O2 -Wall -Wextra -Iinclude -o $@ $< -Ltcp_amd -ltcpcsum -Wl,-rpath,'$$ORIGIN/../../tcp_amd'
 
+tests/c/raw_echo: tests/c/raw_echo.c include/tcpcsum.h $(LIB)
+	$(CC) -O2 -Wall -Wextra -Iinclude -o $@ $< -Ltcp_amd -ltcpcsum -Wl,-rpath,'$$ORIGIN/../../tcp_amd'
+
 tools/mmsg_bench: tools/mmsg_bench.c include/tcpcsum.h $(LIB)
 	$(CC) -O2 -Wall -Wextra -Iinclude -o $@ $< -Ltcp_amd -ltcpcsum -Wl,-rpath,'$$ORIGIN/../tcp_amd'
 
 clean:
-	rm -rf build oracle/build $(LIB) $(PRELOAD) tests/c/abi_smoke tests/c/mmsg_loop tools/mmsg_bench
+	rm -rf build oracle/build $(LIB) $(PRELOAD) tests/c/abi_smoke tests/c/mmsg_loop tests/c/raw_echo tools/mmsg_bench
 
 .PHONY: all oracle clean

@@ -279,8 +279,8 @@ int tcpcsum_stream_probe_dev(const void *d_src, uint64_t nbytes, uint64_t *d_par
 int tcpcsum_plan_uniform(uint64_t base, uint64_t stride, uint32_t len, uint64_t n,
                          const tcpcsum_tuning_t *tune, int *mode, int *shape, int *unroll, int *max_blocks);
 
-/* tcpcsum_tuning_t.shape, read per entry point: uniform 0..12 (a forced shape that cannot cover the segments is
- * ignored), ragged 0..6 = (G,C) (4,1) (8,1) (16,1) (32,1) (32,3) (64,4) (64,8)
+/* tcpcsum_tuning_t.shape, read per entry point: uniform 0..12 (a forced shape
+ * that cannot cover the segments is ignored), ragged 0..6 = (G,C) (4,1) (8,1) (16,1) (32,1) (32,3) (64,4) (64,8)
  * and 7..8 = balanced chunk space (4 / 8 loads per lane in flight),
  * wire 0..7 = (8,1) (32,3) (64,4) (16,2) (16,6) (8,12) (8,2) (8,4) and 8..9 =
  * balanced (4 / 8 loads per lane), builder 0..4. tcpcsum_tuning_t.flags: */
@@ -293,6 +293,7 @@ int tcpcsum_plan_uniform(uint64_t base, uint64_t stride, uint32_t len, uint64_t 
 #define TCPCSUM_TUNE_WIRE_CACHED 32  /* wire: default-policy (not non-temporal) packet loads */
 #define TCPCSUM_TUNE_WIN16 64    /* wire: 16-B (not 128-B) aligned packet windows */
 #define TCPCSUM_TUNE_TX_NT_STORE 128  /* builder: non-temporal payload stores */
+#define TCPCSUM_TUNE_FILL_DWORD 256   /* wire FILL: store check|urg_ptr as one dword when TCP+16 is 4-B aligned */
 /* 0 if *tune is a valid tuning (NULL counts as valid), else TCPCSUM_EINVAL. */
 int tcpcsum_tuning_check(const tcpcsum_tuning_t *tune);
 

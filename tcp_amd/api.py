@@ -168,6 +168,7 @@ def device_check() -> tuple[int, str]:
 PROBE_SLOTS = 8192
 TUNE_PIPE_ON, TUNE_PIPE_OFF, TUNE_NT_ON, TUNE_NT_OFF = 1, 2, 4, 8
 TUNE_WIRE_CACHED, TUNE_WIN16 = 32, 64   # wire kernel variants (tcpcsum.h)
+TUNE_TX_NT_STORE, TUNE_FILL_DWORD = 128, 256
 
 
 # The C library holds no tuning state: every device call takes an explicit

@@ -16,8 +16,53 @@
 #include <new>
 #include <vector>
 
+#include "host_registry.h"
 #include "tcpcsum.h"
 #include "tcpcsum_internal.h"
+
+namespace tcpcsum {
+
+// HostRegistry backend over HIP: hipHostRegister'ed pages are mapped for the
+// device (on MI355X hosts at their host address: tools/hostreg_probe.py).
+struct HipHostBackend {
+    int last_error = 0;
+    int lock(uintptr_t lo, size_t bytes, intptr_t* delta) {
+        hipError_t e = hipHostRegister((void*)lo, bytes, hipHostRegisterMapped);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            last_error = (int)e;
+            return TCPCSUM_EHIP;
+        }
+        void* d = nullptr;
+        e = hipHostGetDevicePointer(&d, (void*)lo, 0);
+        if (e != hipSuccess || !d) {
+            (void)hipGetLastError();
+            (void)hipHostUnregister((void*)lo);
+            last_error = (int)(e != hipSuccess ? e : hipErrorInvalidValue);
+            return TCPCSUM_EHIP;
+        }
+        *delta = (intptr_t)d - (intptr_t)lo;
+        return 0;
+    }
+    void unlock(uintptr_t lo) { (void)hipHostUnregister((void*)lo); }
+    bool pinned_extent(uintptr_t p, uintptr_t* lo, uintptr_t* hi, intptr_t* delta) {
+        hipPointerAttribute_t a;
+        bool ok = hipPointerGetAttributes(&a, (const void*)p) == hipSuccess && a.type == hipMemoryTypeHost &&
+                  a.devicePointer;
+        uintptr_t rs = 0;
+        size_t rsz = 0;
+        ok = ok && hipPointerGetAttribute(&rs, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, (hipDeviceptr_t)p) == hipSuccess &&
+             hipPointerGetAttribute(&rsz, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, (hipDeviceptr_t)p) == hipSuccess;
+        (void)hipGetLastError();   // pageable memory: not an error for us
+        if (!ok) return false;
+        *lo = rs;
+        *hi = rs + rsz;
+        *delta = (intptr_t)a.devicePointer - (intptr_t)p;
+        return true;
+    }
+};
+
+}  // namespace tcpcsum
 
 static_assert(sizeof(tcpcsum_desc_t) == 16, "descriptor is read as one 16-B load");
 static_assert(sizeof(tcpcsum_txseg_t) == 48, "tx descriptor is read as three 16-B loads");
@@ -42,7 +87,7 @@ int get_tuning(const tcpcsum_tuning_t* t, tcpcsum::Tuning* out) {
     if (t) {
         const int u = t->unroll;
         if (t->max_blocks < 0 || !(u == 0 || u == 1 || u == 2 || u == 4 || u == 8) || t->shape < -1 ||
-            t->shape > 12 || (t->flags & ~255) || (t->flags & 3) == 3 || (t->flags & 12) == 12)
+            t->shape > 12 || (t->flags & ~511) || (t->flags & 3) == 3 || (t->flags & 12) == 12)
             return TCPCSUM_EINVAL;
         r.max_blocks = t->max_blocks;
         r.unroll = t->unroll;
@@ -266,21 +311,9 @@ struct tcpcsum_ctx {
     size_t pkt_cap = 0;
     // launch shapes of this context's batches (tcpcsum_ctx_set_tuning)
     tcpcsum::Tuning tune;
-    // Host memory this context page-locked (hipHostRegister), one entry per
-    // registration: disjoint whole pages. `view` is the lookup table derived
-    // from them and from memory found already page-locked by someone else:
-    // sorted, disjoint intervals [lo, hi) with device address = host + delta,
-    // touching intervals of equal delta merged. `finger`: the last hit (packets
-    // of a batch mostly come in pool order).
-    struct Reg {
-        uintptr_t lo, hi;
-        intptr_t delta;
-        bool owned;
-    };
-    std::vector<Reg> regs;
-    std::vector<Reg> view;
-    size_t finger = 0;
-    uint64_t reg_bytes = 0;
+    // host pages this context page-locked for scatter-gather batches
+    tcpcsum::HipHostBackend backend;
+    tcpcsum::HostRegistry<tcpcsum::HipHostBackend> reg{backend};
     std::mutex mu;
 };
 
@@ -373,8 +406,7 @@ void tcpcsum_ctx_destroy(tcpcsum_ctx_t* c) {
     if (c->h_wstat) hipHostFree(c->h_wstat);
     if (c->h_wip) hipHostFree(c->h_wip);
     if (c->h_len) hipHostFree(c->h_len);
-    for (const auto& r : c->regs)
-        if (r.owned) (void)hipHostUnregister((void*)r.lo);
+    c->reg.release(0, 0);
     for (int i = 0; i < 2; ++i)
         if (c->st[i]) hipStreamDestroy(c->st[i]);
     delete c;
@@ -619,142 +651,6 @@ int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t* c, void* h_pkts, size_t region_bytes,
 
 // ------------------------------------------------- scatter-gather host batches
 
-namespace {
-
-constexpr uintptr_t kPage = 4096;
-
-bool reg_less(const tcpcsum_ctx::Reg& a, const tcpcsum_ctx::Reg& b) { return a.lo < b.lo; }
-
-// The lookup view: registrations sorted by address, touching intervals with
-// the same host->device offset merged (on MI355X hosts every registration maps
-// at its host address, so a pool registered buffer by buffer becomes one
-// interval wherever the buffers touch).
-void rebuild_view(tcpcsum_ctx* c) {
-    std::sort(c->regs.begin(), c->regs.end(), reg_less);
-    c->view.clear();
-    for (const auto& r : c->regs) {
-        if (!c->view.empty() && c->view.back().hi == r.lo && c->view.back().delta == r.delta)
-            c->view.back().hi = r.hi;
-        else
-            c->view.push_back(r);
-    }
-    c->finger = 0;
-}
-
-// [p, e) inside one interval of the view: its device address.
-bool view_find(tcpcsum_ctx* c, uintptr_t p, uintptr_t e, uintptr_t* dev) {
-    const std::vector<tcpcsum_ctx::Reg>& v = c->view;
-    if (v.empty()) return false;
-    auto hit = [&](size_t j) { return j < v.size() && v[j].lo <= p && e <= v[j].hi; };
-    size_t k = c->finger;
-    if (!hit(k)) {
-        if (hit(k + 1)) {
-            k = k + 1;
-        } else {   // last interval starting at or before p
-            size_t lo = 0, hi = v.size();
-            while (hi - lo > 1) {
-                const size_t mid = (lo + hi) / 2;
-                if (v[mid].lo <= p) lo = mid; else hi = mid;
-            }
-            if (!hit(lo)) return false;
-            k = lo;
-        }
-    }
-    c->finger = k;
-    *dev = (uintptr_t)((intptr_t)p + v[k].delta);
-    return true;
-}
-
-// Page-lock the pages of [lo, hi) (page-aligned) that no registration of this
-// context covers yet.
-int reg_pages(tcpcsum_ctx* c, uintptr_t lo, uintptr_t hi) {
-    std::vector<std::pair<uintptr_t, uintptr_t>> gaps;
-    uintptr_t cur = lo;
-    for (const auto& r : c->regs) {   // sorted by lo
-        if (r.hi <= cur) continue;
-        if (r.lo >= hi) break;
-        if (r.lo > cur) gaps.push_back({cur, r.lo});
-        if (r.hi > cur) cur = r.hi;
-        if (cur >= hi) break;
-    }
-    if (cur < hi) gaps.push_back({cur, hi});
-    for (const auto& g : gaps) {
-        hipError_t e = hipHostRegister((void*)g.first, g.second - g.first, hipHostRegisterMapped);
-        if (e != hipSuccess) {
-            (void)hipGetLastError();
-            rebuild_view(c);
-            return hip_fail(e);
-        }
-        void* d = nullptr;
-        e = hipHostGetDevicePointer(&d, (void*)g.first, 0);
-        if (e != hipSuccess || !d) {
-            (void)hipGetLastError();
-            (void)hipHostUnregister((void*)g.first);
-            rebuild_view(c);
-            return hip_fail(e != hipSuccess ? e : hipErrorInvalidValue);
-        }
-        c->regs.push_back({g.first, g.second, (intptr_t)d - (intptr_t)g.first, true});
-        c->reg_bytes += g.second - g.first;
-    }
-    rebuild_view(c);
-    return TCPCSUM_OK;
-}
-
-// Device address of the host bytes [p, p + len), page-locking them on first use.
-int resolve_host(tcpcsum_ctx* c, uintptr_t p, uint32_t len, uintptr_t* dev) {
-    const uintptr_t e = p + len;
-    if (view_find(c, p, e, dev)) return TCPCSUM_OK;
-    // page-locked by someone else (tcpcsum_host_alloc, the application's own
-    // registration): use that mapping over the allocation's whole extent
-    hipPointerAttribute_t a;
-    if (hipPointerGetAttributes(&a, (const void*)p) == hipSuccess && a.type == hipMemoryTypeHost && a.devicePointer) {
-        uintptr_t rs = 0;
-        size_t rsz = 0;
-        if (hipPointerGetAttribute(&rs, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, (hipDeviceptr_t)p) != hipSuccess ||
-            hipPointerGetAttribute(&rsz, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, (hipDeviceptr_t)p) != hipSuccess ||
-            rs > p || rs + rsz < e) {
-            rs = p;
-            rsz = len;
-        }
-        (void)hipGetLastError();
-        const intptr_t delta = (intptr_t)a.devicePointer - (intptr_t)p;
-        bool known = false;
-        for (const auto& r : c->regs) known = known || (r.lo == rs && r.hi == rs + rsz);
-        if (!known) {
-            c->regs.push_back({rs, rs + rsz, delta, false});
-            rebuild_view(c);
-        }
-        if (view_find(c, p, e, dev)) return TCPCSUM_OK;
-    }
-    (void)hipGetLastError();   // pageable memory: not an error for us
-    const uintptr_t lo = p & ~(kPage - 1), hi = (e + kPage - 1) & ~(kPage - 1);
-    int rc = reg_pages(c, lo, hi);
-    if (rc) return rc;
-    if (view_find(c, p, e, dev)) return TCPCSUM_OK;
-    // The packet spans registrations mapped at unrelated device addresses (a
-    // host whose registrations do not map at their host address): replace the
-    // ones under it by a single registration of their union.
-    uintptr_t ulo = lo, uhi = hi;
-    std::vector<tcpcsum_ctx::Reg> keep;
-    for (const auto& r : c->regs) {
-        if (r.owned && r.lo < hi && r.hi > lo) {
-            ulo = r.lo < ulo ? r.lo : ulo;
-            uhi = r.hi > uhi ? r.hi : uhi;
-            (void)hipHostUnregister((void*)r.lo);
-            c->reg_bytes -= r.hi - r.lo;
-        } else {
-            keep.push_back(r);
-        }
-    }
-    c->regs.swap(keep);
-    std::sort(c->regs.begin(), c->regs.end(), reg_less);
-    rc = reg_pages(c, ulo, uhi);
-    if (rc) return rc;
-    return view_find(c, p, e, dev) ? TCPCSUM_OK : TCPCSUM_EINVAL;
-}
-
-}  // namespace
-
 int tcpcsum_ipv4_batch_ptrs_host(tcpcsum_ctx_t* c, void* const* h_pkts, const uint32_t* h_lens, uint64_t n, int mode,
                                  uint16_t* h_out, uint8_t* h_status) {
     if (!c) return TCPCSUM_EINVAL;
@@ -774,8 +670,9 @@ int tcpcsum_ipv4_batch_ptrs_host(tcpcsum_ctx_t* c, void* const* h_pkts, const ui
         const uintptr_t p = (uintptr_t)h_pkts[i];
         uintptr_t dev = 0;
         if (len >= 20u && p) {
-            rc = resolve_host(c, p, len, &dev);
-            if (rc) return rc;
+            rc = c->reg.resolve(p, len, &dev);
+            if (rc == TCPCSUM_EHIP) g_last_hip_error.store(c->backend.last_error);
+            if (rc) return rc == TCPCSUM_EHIP ? rc : TCPCSUM_EINVAL;
         } else {
             len = 0;   // too short for an IP header: SKIPPED, nothing is read
         }
@@ -805,8 +702,9 @@ int tcpcsum_ctx_register_host(tcpcsum_ctx_t* c, void* p, size_t bytes) {
     if (!c || !p || !bytes) return TCPCSUM_EINVAL;
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard g(c->device);
-    const uintptr_t lo = (uintptr_t)p & ~(kPage - 1), hi = ((uintptr_t)p + bytes + kPage - 1) & ~(kPage - 1);
-    return reg_pages(c, lo, hi);
+    const int rc = c->reg.lock_range((uintptr_t)p, bytes);
+    if (rc == TCPCSUM_EHIP) g_last_hip_error.store(c->backend.last_error);
+    return rc;
 }
 
 int tcpcsum_ctx_unregister_host(tcpcsum_ctx_t* c, void* p, size_t bytes) {
@@ -814,32 +712,15 @@ int tcpcsum_ctx_unregister_host(tcpcsum_ctx_t* c, void* p, size_t bytes) {
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard g(c->device);
     for (int i = 0; i < 2; ++i) (void)hipStreamSynchronize(c->st[i]);
-    const uintptr_t lo = (uintptr_t)p, hi = p ? (uintptr_t)p + bytes : UINTPTR_MAX;
-    std::vector<tcpcsum_ctx::Reg> keep;
-    int rc = TCPCSUM_OK;
-    for (const auto& r : c->regs) {
-        if (r.lo < hi && r.hi > lo) {
-            if (r.owned) {
-                const hipError_t e = hipHostUnregister((void*)r.lo);
-                if (e != hipSuccess) rc = hip_fail(e);
-                c->reg_bytes -= r.hi - r.lo;
-            }
-        } else {
-            keep.push_back(r);
-        }
-    }
-    c->regs.swap(keep);
-    rebuild_view(c);
-    return rc;
+    c->reg.release((uintptr_t)p, bytes);
+    return TCPCSUM_OK;
 }
 
 int tcpcsum_ctx_registered(tcpcsum_ctx_t* c, uint64_t* ranges, uint64_t* bytes) {
     if (!c) return TCPCSUM_EINVAL;
     std::lock_guard<std::mutex> lk(c->mu);
-    uint64_t k = 0;
-    for (const auto& r : c->regs) k += r.owned ? 1u : 0u;
-    if (ranges) *ranges = k;
-    if (bytes) *bytes = c->reg_bytes;
+    if (ranges) *ranges = c->reg.owned_ranges();
+    if (bytes) *bytes = c->reg.owned_bytes();
     return TCPCSUM_OK;
 }
 

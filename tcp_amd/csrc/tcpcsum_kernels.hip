@@ -751,6 +751,7 @@ struct IpDone {
     uint8_t* ip;
     uint64_t i;
     uint32_t th;
+    uint32_t urg;   // urg_ptr (TCP+18) in the high half, for a check|urg_ptr dword store
     uint16_t c, ic;
     uint8_t st;
     bool w;     // a packet of the batch: out / status are written
@@ -765,7 +766,7 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const 
                                               const uint32_t* __restrict__ plen,
                                               uint64_t n, uint32_t cap, uint64_t limit, int mode,
                                               uint16_t* __restrict__ out, uint8_t* __restrict__ status,
-                                              uint16_t* __restrict__ ipout, uint32_t amask) {
+                                              uint16_t* __restrict__ ipout, uint32_t amask, bool dword_store) {
     // amask: window alignment - 1. Lane gl of a group loads window chunks k*G+gl,
     // so with 128-B windows every group load instruction covers whole 128-B
     // lines however the packet is aligned. Header fields lie in window bytes
@@ -847,6 +848,7 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const 
         d.i = i;
         d.ip = p[u].ip;
         d.th = 0;
+        d.urg = 0;
         d.c = 0;
         d.ic = 0;
         d.st = TCPCSUM_PKT_SKIPPED;
@@ -866,7 +868,8 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const 
         const uint32_t th = ihl * 4u;   // TCP start, packet-relative (even)
         const bool odd = (m & 1u) != 0;
         const uint32_t sa = grp_bytes4<G, C>(v[u], gbase, m + 12u), da = grp_bytes4<G, C>(v[u], gbase, m + 16u);
-        const uint32_t check_word = grp_bytes4<G, C>(v[u], gbase, m + th + 16u) & 0xffffu;
+        const uint32_t check_dw = grp_bytes4<G, C>(v[u], gbase, m + th + 16u);   // check | urg_ptr
+        const uint32_t check_word = check_dw & 0xffffu;
         const uint32_t nch_tot = (m + tot + 15u) >> 4;
         if (nch_tot > p[u].spec) {   // longer than its span hint (group-uniform, rare)
 #pragma unroll
@@ -898,15 +901,34 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const 
             if (iphdr && pos < (int32_t)th) chunk_wo_bytes(x, (int64_t)pos, (int64_t)th, odd, wi, oi);
         }
         uint64_t W = w, O = o;
-        // packets longer than the group's first G*C chunks
+        // packets longer than the group's first G*C chunks (jumbo frames): the same
+        // split — whole chunks unmasked, the tail chunk masked behind a wave-uniform
+        // branch; chunks past the packet read the zero buffer (no predicated loads)
         for (uint32_t r = (uint32_t)(G * C); r < nch_tot; r += (uint32_t)(G * C)) {
             uint32_t w2 = 0, o2 = 0;
+            u32x4 xs[C];
 #pragma unroll
             for (int k = 0; k < C; ++k) {
                 const uint32_t idx = r + (uint32_t)(k * G + gl);
-                if (idx >= nch_tot) continue;
-                const u32x4 x = ldq<NT>(ip - m + (uint64_t)idx * 16u);
-                chunk_wo_bytes(x, (int64_t)idx * 16 - m - th, (int64_t)(tot - th), odd, w2, o2);
+                xs[k] = ldq<NT>(zsel(idx < nch_tot, ip - m + (uint64_t)idx * 16u));
+            }
+#pragma unroll
+            for (int k = 0; k < C; ++k) {
+                const uint32_t idx = r + (uint32_t)(k * G + gl);
+                const int32_t pos = (int32_t)(idx * 16u) - (int32_t)m;
+                const u32x4 x = xs[k];
+                const bool full = idx < nch_tot && pos >= (int32_t)th && pos + 16 <= (int32_t)tot;
+                const uint32_t wk = sad16(x.w, sad16(x.z, sad16(x.y, sad16(x.x, 0u))));
+                w2 += full ? wk : 0u;
+                if (odd) {
+                    const uint32_t ok8 = sad8(x.w & 0xff00ff00u, sad8(x.z & 0xff00ff00u,
+                                              sad8(x.y & 0xff00ff00u, sad8(x.x & 0xff00ff00u, 0u))));
+                    o2 += full ? ok8 : 0u;
+                }
+                const bool part = idx < nch_tot && !full && pos + 16 > (int32_t)th && pos < (int32_t)tot;
+                if (__builtin_amdgcn_ballot_w64(part) != 0) {
+                    if (part) chunk_wo_bytes(x, (int64_t)pos - th, (int64_t)(tot - th), odd, w2, o2);
+                }
             }
             W += w2;
             O += o2;
@@ -923,6 +945,7 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const 
         if (!verify) S -= check_word;
         d.c = fold_ref(S);
         d.th = th;
+        d.urg = check_dw & 0xffff0000u;
         d.fill = !verify;
         uint32_t st = TCPCSUM_PKT_OK;
         if (verify && d.c != 0 && check_word == (uint32_t)(uint16_t)~fold_ref(ps)) st |= TCPCSUM_PKT_CSUM_PARTIAL;
@@ -942,7 +965,11 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const 
     auto commit = [&](const IpDone& d) {
         if (!d.w || gl != 0) return;
         if (d.fill) {
-            store_u16(d.ip + d.th + 16, d.c);   // native u16 store, as context.c:208
+            uint8_t* cp = d.ip + d.th + 16;
+            if (dword_store && ((uintptr_t)cp & 3u) == 0)   // check and the unchanged urg_ptr in one dword
+                *reinterpret_cast<uint32_t*>(cp) = d.urg | d.c;
+            else
+                store_u16(cp, d.c);   // native u16 store, as context.c:208
             if (iphdr) store_u16(d.ip + 10, d.ic);
         }
         if (iphdr && ipout && d.st != TCPCSUM_PKT_SKIPPED) ipout[d.i] = d.ic;
@@ -1612,23 +1639,23 @@ void launch_desc(const uint8_t* base, const tcpcsum_desc_t* d, uint64_t n, uint3
 template <int G, int C, int U>
 static void launch_ipv4_t(uint8_t* pkts, const uint64_t* off, const uint32_t* plen, uint64_t n, uint32_t cap,
                           uint64_t limit, int mode, uint16_t* out, uint8_t* status, uint16_t* ipout, hipStream_t s,
-                          int max_blocks, bool nt, uint32_t amask) {
+                          int max_blocks, bool nt, uint32_t amask, bool dw) {
     constexpr int SPT = (64 / G) * U;
     const dim3 grid(grid_for((n + SPT - 1) / SPT, max_blocks));
     // per-packet bounds only when given: the extra load and register cost the
     // region-bounded MTU batches 4-8 % (tools/wire_ab.py)
     if (plen && nt)
         hipLaunchKernelGGL((k_ipv4<G, C, U, true, true>), grid, dim3(256), 0, s, pkts, off, plen, n, cap, limit, mode,
-                           out, status, ipout, amask);
+                           out, status, ipout, amask, dw);
     else if (plen)
         hipLaunchKernelGGL((k_ipv4<G, C, U, false, true>), grid, dim3(256), 0, s, pkts, off, plen, n, cap, limit, mode,
-                           out, status, ipout, amask);
+                           out, status, ipout, amask, dw);
     else if (nt)
         hipLaunchKernelGGL((k_ipv4<G, C, U, true, false>), grid, dim3(256), 0, s, pkts, off, plen, n, cap, limit, mode,
-                           out, status, ipout, amask);
+                           out, status, ipout, amask, dw);
     else
         hipLaunchKernelGGL((k_ipv4<G, C, U, false, false>), grid, dim3(256), 0, s, pkts, off, plen, n, cap, limit,
-                           mode, out, status, ipout, amask);
+                           mode, out, status, ipout, amask, dw);
 }
 
 void launch_ipv4(uint8_t* pkts, const uint64_t* off, const uint32_t* plen, uint64_t n, uint32_t cap, uint64_t limit,
@@ -1638,6 +1665,7 @@ void launch_ipv4(uint8_t* pkts, const uint64_t* off, const uint32_t* plen, uint6
     const int unroll = tu.unroll ? tu.unroll : 1;
     const bool nt = (tu.flags & TCPCSUM_TUNE_WIRE_CACHED) == 0;
     const uint32_t amask = (tu.flags & TCPCSUM_TUNE_WIN16) ? 15u : 127u;
+    const bool dw = (tu.flags & TCPCSUM_TUNE_FILL_DWORD) != 0;
     // shape by the cap and by the mean packet footprint (region bytes / n; the
     // summed lengths for scatter-gather batches): packed small packets one
     // chunk per lane, MTU slots one round of 96 chunks per packet
@@ -1647,13 +1675,13 @@ void launch_ipv4(uint8_t* pkts, const uint64_t* off, const uint32_t* plen, uint6
     do {                                                                                                             \
         if (unroll <= 1)                                                                                             \
             launch_ipv4_t<G, C, 1>(pkts, off, plen, n, cap, limit, mode, out, status, ipout, s, max_blocks, nt,     \
-                                   amask);                                                                           \
+                                   amask, dw);                                                                           \
         else if (unroll == 2)                                                                                        \
             launch_ipv4_t<G, C, 2>(pkts, off, plen, n, cap, limit, mode, out, status, ipout, s, max_blocks, nt,     \
-                                   amask);                                                                           \
+                                   amask, dw);                                                                           \
         else                                                                                                         \
             launch_ipv4_t<G, C, 4>(pkts, off, plen, n, cap, limit, mode, out, status, ipout, s, max_blocks, nt,     \
-                                   amask);                                                                           \
+                                   amask, dw);                                                                           \
     } while (0)
     // forced: 0 (8,1), 1 (32,3), 2 (64,4), 3 (16,2), 4 (16,6), 5 (8,12), 6 (8,2), 7 (8,4),
     // 8 / 9: balanced chunk space (k_ipv4_lb) with 4 / 8 loads per lane in flight

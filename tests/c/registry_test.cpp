@@ -1,0 +1,155 @@
+// registry_test.cpp — CPU unit test of tcp_amd/csrc/host_registry.h (the page
+// locking behind tcpcsum_ipv4_batch_ptrs_host) against a fake backend that
+// models a host: every resolved packet must lie entirely in locked pages
+// (ours or someone else's) under ONE device mapping, pages are never locked
+// twice, and release() unlocks exactly what was locked.
+//
+//   registry_test [seed]   exit 0 when every check holds
+#include <cstdio>
+#include <cstdlib>
+#include <map>
+#include <random>
+#include <set>
+#include <vector>
+
+#include "../../tcp_amd/csrc/host_registry.h"
+
+static int fails = 0;
+#define CHECK(c)                                                            \
+    do {                                                                    \
+        if (!(c)) {                                                         \
+            if (fails++ < 20) std::printf("FAIL %s:%d %s\n", __FILE__, __LINE__, #c); \
+        }                                                                   \
+    } while (0)
+
+using tcpcsum::kHostPage;
+
+struct Lock {
+    uintptr_t lo, hi;
+    intptr_t delta;
+};
+
+struct FakeHost {
+    bool flat = true;                  // locks map at their host address (MI355X hosts)
+    std::map<uintptr_t, Lock> locks;   // ours, by start
+    std::vector<Lock> foreign;         // page-locked by someone else (tcpcsum_host_alloc)
+    std::mt19937_64 rng{1};
+    uint64_t lock_calls = 0;
+
+    int lock(uintptr_t lo, size_t bytes, intptr_t* delta) {
+        CHECK(lo % kHostPage == 0 && bytes % kHostPage == 0 && bytes > 0);
+        for (const auto& kv : locks) CHECK(!(kv.second.lo < lo + bytes && kv.second.hi > lo));   // never twice
+        for (const auto& f : foreign) CHECK(!(f.lo < lo + bytes && f.hi > lo));
+        *delta = flat ? 0 : (intptr_t)((rng() % 1000 + 1) << 20);
+        locks[lo] = {lo, lo + bytes, *delta};
+        ++lock_calls;
+        return 0;
+    }
+    void unlock(uintptr_t lo) {
+        CHECK(locks.count(lo) == 1);
+        locks.erase(lo);
+    }
+    bool pinned_extent(uintptr_t p, uintptr_t* lo, uintptr_t* hi, intptr_t* delta) {
+        for (const auto& f : foreign)
+            if (f.lo <= p && p < f.hi) { *lo = f.lo; *hi = f.hi; *delta = f.delta; return true; }
+        for (const auto& kv : locks)
+            if (kv.second.lo <= p && p < kv.second.hi) {
+                *lo = kv.second.lo; *hi = kv.second.hi; *delta = kv.second.delta; return true;
+            }
+        return false;
+    }
+    // the mapping that holds byte a, or nullptr
+    const Lock* holder(uintptr_t a) const {
+        for (const auto& f : foreign) if (f.lo <= a && a < f.hi) return &f;
+        for (const auto& kv : locks) if (kv.second.lo <= a && a < kv.second.hi) return &kv.second;
+        return nullptr;
+    }
+};
+
+// [p, p+len) -> dev is safe: every byte's page is mapped, and dev + k is where byte p + k lives.
+static void check_mapping(const FakeHost& h, uintptr_t p, size_t len, uintptr_t dev) {
+    for (uintptr_t a = p; a < p + len; a = (a | (kHostPage - 1)) + 1) {
+        const Lock* l = h.holder(a);
+        CHECK(l != nullptr);
+        if (l) CHECK((intptr_t)dev - (intptr_t)p == l->delta);
+    }
+    const Lock* last = h.holder(p + len - 1);
+    CHECK(last != nullptr);
+    if (last) CHECK((intptr_t)dev - (intptr_t)p == last->delta);
+}
+
+static void scenario(bool flat, uint64_t seed) {
+    FakeHost h;
+    h.flat = flat;
+    h.rng.seed(seed);
+    std::mt19937_64 r(seed * 7 + 3);
+    tcpcsum::HostRegistry<FakeHost> reg(h);
+    // a heap: buffers laid end to end with 16-B headers, like malloc; some are
+    // "pinned" allocations (page-aligned, locked by someone else)
+    struct Buf { uintptr_t p; size_t n; };
+    std::vector<Buf> bufs;
+    uintptr_t cur = 0x7f0000001010ull;
+    for (int i = 0; i < 600; ++i) {
+        const int kind = (int)(r() % 10);
+        if (kind == 0) {   // a pinned allocation of a few pages
+            cur = (cur + kHostPage - 1) & ~(kHostPage - 1);
+            const size_t n = (r() % 8 + 1) * kHostPage;
+            h.foreign.push_back({cur, cur + n, flat ? 0 : (intptr_t)((r() % 1000 + 1) << 24)});
+            bufs.push_back({cur, n});
+            cur += n + kHostPage;
+        } else {
+            const size_t n = kind < 4 ? 32768 : kind < 8 ? 4096 : (size_t)(r() % 3000 + 64);
+            bufs.push_back({cur, n});
+            cur += n + 16;
+        }
+    }
+    for (int round = 0; round < 6; ++round) {
+        for (int k = 0; k < 1500; ++k) {
+            const Buf& b = bufs[r() % bufs.size()];
+            const size_t len = 20 + r() % (b.n - 20 < 1500 ? b.n - 20 : 1500);
+            const size_t off = r() % (b.n - len + 1);
+            uintptr_t dev = 0;
+            const int rc = reg.resolve(b.p + off, len, &dev);
+            CHECK(rc == 0);
+            if (rc == 0) check_mapping(h, b.p + off, len, dev);
+        }
+        // what the registry owns is what the backend has locked
+        uint64_t bytes = 0;
+        for (const auto& kv : h.locks) bytes += kv.second.hi - kv.second.lo;
+        CHECK(bytes == reg.owned_bytes());
+        CHECK(h.locks.size() == reg.owned_ranges());
+        // release a random stretch, as a caller freeing some buffers would
+        const Buf& b = bufs[r() % bufs.size()];
+        reg.release(b.p, 200000);
+        for (const auto& kv : h.locks) CHECK(!(kv.second.lo < b.p + 200000 && kv.second.hi > b.p));
+    }
+    // a second pass over the same packets locks nothing new (flat hosts)
+    if (flat) {
+        std::vector<std::pair<uintptr_t, size_t>> pk;
+        for (int k = 0; k < 500; ++k) {
+            const Buf& b = bufs[r() % bufs.size()];
+            pk.push_back({b.p, 20 + r() % (b.n - 20 < 1500 ? b.n - 20 : 1500)});
+        }
+        uintptr_t dev;
+        for (auto& x : pk) CHECK(reg.resolve(x.first, x.second, &dev) == 0);
+        const uint64_t calls = h.lock_calls;
+        for (auto& x : pk) {
+            CHECK(reg.resolve(x.first, x.second, &dev) == 0);
+            CHECK(dev == x.first);
+        }
+        CHECK(h.lock_calls == calls);
+    }
+    CHECK(reg.lock_range(bufs[3].p, 100000) == 0);
+    reg.release(0, 0);
+    CHECK(h.locks.empty() && reg.owned_bytes() == 0 && reg.owned_ranges() == 0);
+}
+
+int main(int argc, char** argv) {
+    const uint64_t seed = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : 1;
+    for (uint64_t s = seed; s < seed + 4; ++s) {
+        scenario(true, s);
+        scenario(false, s);
+    }
+    std::printf(fails ? "FAIL (%d)\n" : "OK\n", fails);
+    return fails ? 1 : 0;
+}

@@ -575,17 +575,21 @@ def test_ipv4_span_hint_mispredicted(dev, shape):
             reg = ref
 
 
-@pytest.mark.parametrize("shape,flags", [(-1, 0), (-1, 32), (-1, 64), (-1, 96), (8, 0), (9, 0)])
-@pytest.mark.parametrize("layout", ["odd", "slot64", "slot16", "packed"])
+@pytest.mark.parametrize("shape,flags", [(-1, 0), (-1, 32), (-1, 64), (-1, 96), (8, 0), (9, 0),
+                                         (-1, 256), (-1, 320), (0, 256), (1, 256)])
+@pytest.mark.parametrize("layout", ["odd", "slot64", "slot16", "packed", "jumbo"])
 def test_ipv4_window_and_store_variants(dev, shape, flags, layout):
-    """Wire kernel variants (128-B or 16-B packet windows; non-temporal or default-policy loads)
-    are exact and FILL rewrites nothing but the checks, in every layout: odd packed
-    offsets, 64-B aligned slots, 16-B (not 64-B) aligned slots, packed tiny packets."""
+    """Wire kernel variants (128-B or 16-B packet windows; non-temporal or default-policy loads;
+    check|urg_ptr dword stores) are exact and FILL rewrites nothing but the checks, in every
+    layout: odd packed offsets, 64-B aligned slots, 16-B (not 64-B) aligned slots, packed tiny
+    packets, 9000-B jumbo frames at odd offsets (the multi-round path)."""
     import tcp_amd
     from tests.packets import build_batch, ip_packet
     rng = np.random.default_rng(4242 + flags)
     if layout == "odd":
         region, off, _ = build_batch(rng, 600, malformed=True, odd_offsets=True)
+    elif layout == "jumbo":
+        region, off, _ = build_batch(rng, 120, malformed=True, odd_offsets=True, max_payload=8956)
     elif layout in ("slot64", "slot16"):
         region, off, _ = build_batch(rng, 400, slot=1536, malformed=True)
         if layout == "slot16":
@@ -599,14 +603,14 @@ def test_ipv4_window_and_store_variants(dev, shape, flags, layout):
             region[int(o):int(o) + len(p)] = np.frombuffer(p, np.uint8)
     for mode in (tcp_amd.IPV4_FILL, tcp_amd.IPV4_FILL | tcp_amd.IPV4_IPHDR, tcp_amd.IPV4_VERIFY | tcp_amd.IPV4_IPHDR):
         ref = region.copy()
-        want_out, want_st = oracle.ipv4_batch(ref, off, 1536 if layout != "odd" else 32768, mode)
+        want_out, want_st = oracle.ipv4_batch(ref, off, 1536 if layout not in ("odd", "jumbo") else 32768, mode)
         tcp_amd.set_tuning(0, 0, shape, flags)
         try:
             dreg = to_dev(region, dev)
             out = torch.empty(off.size, dtype=torch.int16, device=dev)
             st = torch.empty(off.size, dtype=torch.uint8, device=dev)
             tcp_amd.ipv4_batch(dreg, to_dev(off.view(np.int64), dev), off.size,
-                               1536 if layout != "odd" else 32768, mode, out, st)
+                               1536 if layout not in ("odd", "jumbo") else 32768, mode, out, st)
         finally:
             tcp_amd.set_tuning(0, 0, -1, 0)
         assert np.array_equal(st.cpu().numpy(), want_st), mode

@@ -34,3 +34,21 @@ def test_host_c_under_asan_ubsan(tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True, env=env, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "sanitize_host: ok" in r.stdout
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="g++ not available")
+def test_host_registry_under_asan_ubsan(tmp_path):
+    """The page-locking bookkeeping of tcpcsum_ipv4_batch_ptrs_host (tcp_amd/csrc/host_registry.h)
+    against a modelled host: every resolved packet lies wholly in locked pages under one device
+    mapping (flat and non-flat hosts), no page is locked twice, release() unlocks what was locked."""
+    exe = tmp_path / "registry_test"
+    cmd = ["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
+           "-fno-sanitize-recover=all", "-Wall", "-Wextra",
+           os.path.join(REPO, "tests", "c", "registry_test.cpp"), "-o", str(exe)]
+    b = subprocess.run(cmd, capture_output=True, text=True)
+    assert b.returncode == 0, b.stderr
+    env = dict(os.environ)
+    env["ASAN_OPTIONS"] = "detect_leaks=1:abort_on_error=0:verify_asan_link_order=0"
+    r = subprocess.run([str(exe), "11"], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.strip().endswith("OK")

@@ -5,6 +5,7 @@ tests/c/mmsg_loop builds packets with the reference's framing in separate
 (no root needed). With TCPCSUM_PRELOAD_TX=fill every received packet must equal
 the oracle's FILL of the packet as built (check computed per context.c:208).
 """
+import json
 import os
 import re
 import struct
@@ -111,3 +112,84 @@ def test_tx_fill_with_ip_header(tmp_path, copy):
     for built, got in pkts:
         assert got == oracle_fill(built, 2)
     assert stats["rx_verify_failed"] == 0
+
+
+# ----------------------------------------------------------------- raw sockets
+# The plumbing configuration (BASELINE configs[0]: stress over loopback, 1500-B
+# MTU): tests/c/raw_echo echoes data segments through SOCK_RAW/IPPROTO_RAW
+# sockets in a private network namespace, with the interposer in its DEFAULT
+# mode (SOCK_RAW sockets only — no TCPCSUM_PRELOAD_ANY_SOCKET).
+RAW = os.path.join(REPO, "tests", "c", "raw_echo")
+
+
+def run_raw(tmp_path, n, env_extra):
+    if not os.path.exists(RAW):
+        subprocess.run(["make", "-C", REPO, "tests/c/raw_echo", "tcp_amd/libtcpcsum_preload.so"], check=True)
+    out = tmp_path / "raw.bin"
+    env = {k: v for k, v in os.environ.items() if not k.startswith("TCPCSUM_PRELOAD")}
+    env.update({"LD_PRELOAD": PRELOAD, "TCPCSUM_PRELOAD_STATS": "1"})
+    env.update(env_extra)
+    r = subprocess.run([RAW, str(n), str(out)], env=env, capture_output=True, text=True, timeout=120)
+    if r.returncode == 77:
+        pytest.skip("no CAP_NET_RAW: neither user namespaces nor root: " + r.stdout.strip())
+    summary = json.loads(r.stdout.strip().splitlines()[-1]) if r.stdout.strip() else {}
+    pkts = []
+    if r.returncode == 0:
+        data = out.read_bytes()
+        pos = 0
+        while pos < len(data):
+            (lo,) = struct.unpack_from("<I", data, pos)
+            built = data[pos + 4:pos + 4 + lo]
+            pos += 4 + lo
+            (li,) = struct.unpack_from("<I", data, pos)
+            got = data[pos + 4:pos + 4 + li]
+            pos += 4 + li
+            pkts.append((built, got))
+    stats = {}
+    m = re.search(r"tcpcsum_preload: (.*)", r.stderr)
+    if m:
+        for side, body in zip(("tx", "rx"), m.group(1).split("|")[:2]):
+            for k, v in re.findall(r"(\w+)=(\d+)", body):
+                stats[f"{side}_{k}"] = int(v)
+    return r, summary, pkts, stats
+
+
+def ip_header_ok(pkt: bytes) -> bool:
+    """The kernel fills the IPv4 header checksum of IPPROTO_RAW sends: RFC 1071 verify."""
+    ihl = (pkt[0] & 15) * 4
+    return oracle.csum_continue(0, pkt[:ihl], ihl) == 0
+
+
+def same_but_kernel_fields(built: bytes, got: bytes) -> bool:
+    """Equal except what the kernel writes into a raw IP_HDRINCL send: id when zero (the
+    reference's (u16)htonl(54321) is 0 on little-endian) and the IP header checksum."""
+    return len(built) == len(got) and built[:4] == got[:4] and built[6:10] == got[6:10] and built[12:] == got[12:]
+
+
+def test_raw_echo_plumbing_passthrough(tmp_path):
+    """The raw-socket echo runs end to end with the interposer passing through (TX/RX off)."""
+    r, summary, pkts, stats = run_raw(tmp_path, 600, {"TCPCSUM_PRELOAD_TX": "off"})
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert summary["echoes_sniffed"] == 600 and len(pkts) == 600
+    for built, got in pkts:
+        assert same_but_kernel_fields(built, got) and ip_header_ok(got)
+        assert got[36:38] == b"\0\0"                 # nobody filled the TCP check
+
+
+@pytest.mark.gpu
+def test_raw_echo_plumbing_on_gpu(tmp_path):
+    """stress-style echo over SOCK_RAW: every echo's TCP check filled on the GPU at the server's
+    sendmmsg equals the oracle's (context.c:208), every received batch verified on the GPU, the
+    kernel's CHECKSUM_PARTIAL RSTs counted apart."""
+    n = 3000
+    r, summary, pkts, stats = run_raw(tmp_path, n, {"TCPCSUM_PRELOAD_RX": "verify"})
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert len(pkts) == n
+    for built, got in pkts:
+        assert same_but_kernel_fields(oracle_fill(built), got)
+        assert ip_header_ok(got)
+    assert stats["tx_filled"] == n and stats["tx_skipped"] == 0
+    # rx: client segments (CPU checks) + sniffed echoes (GPU checks) verify; RSTs are partial
+    assert stats["rx_verify_failed"] == 0
+    assert stats["rx_partial"] == summary["kernel_rst"]
+    assert stats["rx_verified"] >= 2 * n + summary["kernel_rst"]

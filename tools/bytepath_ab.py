@@ -1,14 +1,15 @@
 #!/usr/bin/env python3
 """Byte-granular paths (odd starts / odd lengths), device-resident: kernel time
 per workload for the library at $TCPCSUM_LIB (A/B of two builds: run once per
-build). Checked against the Appendix B digests' generator where it applies and
-against each other by the caller (prints an fnv1a64 of every output).
+build). The two builds' outputs are compared by the caller: every workload
+prints an fnv1a64 of its first 64 KiB of results. Workloads:
 
   * uniform M1: 1M segments of 1499 B at stride 1499 (odd starts and lengths);
   * uniform long M1: 64K segments of 16383 B at stride 16385;
   * ragged lane groups (forced shape 4, 64 chunks): 256K segments of 1499 B at
-    odd offsets, random order;
-  * wire FILL with packets at odd addresses: 512K × 1500 B in 1537-B slots.
+    odd offsets, random order.
+(The wire kernel at odd packet addresses is A/B'd by tools/wire_ab.py and
+tools/wiresweep.py, not here.)
 """
 import json
 import os
