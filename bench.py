@@ -147,25 +147,40 @@ def cpu_baseline(seg_len: int, seconds: float) -> dict:
     nseg = max(1, min(1 << 20, (3 << 29) // seg_len))
     info = host_cpu_info()
     nproc = max(1, info["threads_in_affinity"])
+    # where a cgroup quota grants fewer CPUs than the affinity mask shows (the GPU
+    # pool: 16 of 256), also time that many threads — what this job may sustain
+    quota = info["cgroup_cpu_quota"]
+    qthreads = int(quota) if quota and 1 < int(quota) < nproc else None
     res = {}
-    plan = (("O2", nproc, 0.15), ("O2", 1, 0.25), ("O0", 1, 0.45), ("O0", nproc, 0.15))
+    plan = [("O2", nproc, 0.15), ("O2", 1, 0.2), ("O0", 1, 0.4), ("O0", nproc, 0.1)]
+    if qthreads:
+        plan.append(("O2", qthreads, 0.15))
     for opt, th, share in plan:
         gibs, digest, passes, mean = oracle.cpu_bench(th, seg_len, nseg, seconds * share, opt, mean=True)
         res[(opt, th)] = {"GiB/s": round(gibs, 3), "passes": passes, "digest": digest, "mean": round(mean, 3)}
-    best = res[("O2", nproc)]
-    return {
-        "value": best["GiB/s"], "unit": "GiB/s", "cores": nproc, "kind": "port",
-        "sample": f"{nseg} x {seg_len}-byte segments (Appendix B stream, host DRAM), gcc -O2, {nproc} threads "
-                  f"(nproc), best of >= {best['passes']} passes",
-        "threads": nproc,
-        "O2_nproc": best["GiB/s"], "O2_1thread": res[("O2", 1)]["GiB/s"],
+    # value: the most favourable -O2 figure (nproc, or the quota's thread count if a
+    # throttled nproc run came out slower)
+    vth = nproc if not qthreads or res[("O2", nproc)]["GiB/s"] >= res[("O2", qthreads)]["GiB/s"] else qthreads
+    best = res[("O2", vth)]
+
+    def name(o, t):
+        return f"{o}_{'1thread' if t == 1 else 'nproc' if t == nproc else f'{t}threads'}"
+    out = {
+        "value": best["GiB/s"], "unit": "GiB/s", "cores": vth, "kind": "port",
+        "sample": f"{nseg} x {seg_len}-byte segments (Appendix B stream, host DRAM), gcc -O2, {vth} threads, "
+                  f"best of >= {best['passes']} passes (persistent threads, contiguous shards)",
+        "threads": vth,
+        "O2_nproc": res[("O2", nproc)]["GiB/s"], "O2_1thread": res[("O2", 1)]["GiB/s"],
         "O0_nproc": res[("O0", nproc)]["GiB/s"], "O0_1thread": res[("O0", 1)]["GiB/s"],
-        "passes": {f"{o}_{'1thread' if t == 1 else 'nproc'}": r["passes"] for (o, t), r in res.items()},
+        "passes": {name(o, t): r["passes"] for (o, t), r in res.items()},
         # mean over all passes: below the best pass where a cgroup CPU quota throttles the threads
-        "O2_nproc_mean_over_passes": best["mean"],
+        "mean_over_passes": {name(o, t): r["mean"] for (o, t), r in res.items()},
         "digests_agree": len({r["digest"] for r in res.values()}) == 1,
         **info,
     }
+    if qthreads:
+        out[f"O2_{qthreads}threads_quota"] = res[("O2", qthreads)]["GiB/s"]
+    return out
 
 
 def run_config(config: str, steps: int, warmup: int, rank: int, world: int, dist, device, rotate: int = 0,
