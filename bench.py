@@ -409,7 +409,8 @@ def main(argv=None) -> int:
             extra[cfg] = {"workload": e["desc"], "GiB/s": round(e["batch_bytes"] * steps / e["wall_max"] / (1 << 30), 2),
                           "kernel_avg_ms": round(e["kernel_ms"], 5), "achieved_GB/s": round(gbs, 1),
                           "roofline_frac": round(gbs / HBM_PEAK_GBS, 4), "steps": steps,
-                          "rotating_batches": e["rot"], "digest_check": e["check"]}
+                          "rotating_batches": e["rot"], "digest_check": e["check"],
+                          "traffic": load_traffic(cfg)}
             torch.cuda.empty_cache()
             if CONFIGS[cfg][1] < 4096:
                 # small segments: the per-launch ramp is a large share of a launch; the same
@@ -448,6 +449,9 @@ def main(argv=None) -> int:
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
+                         "traffic_source": ("profiles/traffic.json: HBM bytes per launch of this kernel from a "
+                                            "separate rocprofv3 --pmc FETCH_SIZE pass (x2 gfx950 correction), "
+                                            "committed, not measured in this run") if traffic else None,
                          "kernel": "tcpcsum::k_uniform (tcpcsum_batch_uniform_dev)",
                          "kernel_avg_ms": round(kernel_ms, 5), "kernel_avg_ms_max_rank": round(kernel_ms_max, 5),
                          "algorithmic_bytes_per_launch": batch_bytes},
