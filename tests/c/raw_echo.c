@@ -24,8 +24,10 @@
  * and the kernel's own RSTs (no listener owns these ports), which loopback
  * leaves CHECKSUM_PARTIAL (counted apart).
  *
- *   raw_echo <nsegs> <out-file>
- * Needs CAP_NET_RAW: it first moves itself into a fresh user + network
+ *   raw_echo <nsegs> <out-file> [cpu]
+ * cpu: the server fills each check on the CPU as the reference does (the
+ * plumbing config exactly, no GPU); otherwise checks are left 0 for the
+ * interposer to fill. Needs CAP_NET_RAW: it first moves itself into a fresh user + network
  * namespace (unshare(2) in-process, so the dynamic loader and LD_PRELOAD are
  * untouched; an ordinary user is root there), brings that namespace's lo up,
  * and runs there — nothing else on the host sees the traffic. Exit 0 ok; 77
@@ -128,8 +130,11 @@ static double now_s(void) {
 }
 
 int main(int argc, char **argv) {
-    if (argc < 3) { fprintf(stderr, "usage: %s nsegs out-file\n", argv[0]); return 2; }
+    if (argc < 3) { fprintf(stderr, "usage: %s nsegs out-file [cpu]\n", argv[0]); return 2; }
     const int nsegs = atoi(argv[1]);
+    /* cpu: the server computes each echo's check itself, as the reference does
+     * (context.c:208-209, csum_continue on the CPU) — BASELINE configs[0] as is */
+    const int cpu_checks = argc > 3 && !strcmp(argv[3], "cpu");
     FILE *f = fopen(argv[2], "wb");
     if (!f || nsegs <= 0) return 2;
     const char *ns = enter_netns();
@@ -220,6 +225,12 @@ int main(int argc, char **argv) {
                     const size_t ot = frame(o, lo_addr, lo_addr, SERVER_PORT, CLIENT_PORT, sseq,
                                             ntohl(cs) + dlen, t + doff, dlen);
                     sseq += dlen;
+                    if (cpu_checks) {
+                        const uint16_t c = tcpcsum_continue(
+                            tcpcsum_pseudo(lo_addr, lo_addr, htons((uint16_t) (24 + dlen))),
+                            (const char *) o + 20, (int) (24 + dlen));
+                        memcpy(o + 36, &c, 2);
+                    }
                     const int k = queued_total + queued;
                     if (k < nsegs) {
                         built[k] = malloc(ot);
@@ -289,8 +300,8 @@ int main(int argc, char **argv) {
         }
     }
     fclose(f);
-    printf("{\"namespace\": \"%s\", \"segments\": %d, \"client_seen\": %ld, \"echoed\": %d, \"echoes_sniffed\": %ld, \"kernel_rst\": %ld, "
+    printf("{\"namespace\": \"%s\", \"server_checks\": \"%s\", \"segments\": %d, \"client_seen\": %ld, \"echoed\": %d, \"echoes_sniffed\": %ld, \"kernel_rst\": %ld, "
            "\"other\": %ld, \"send_calls\": %ld, \"rx_batches\": %ld, \"seconds\": %.3f}\n",
-           ns, nsegs, client_seen, queued_total, echoes, kernel_rst, other, send_calls, batches_rx, now_s() - t_start);
+           ns, cpu_checks ? "cpu" : "left 0", nsegs, client_seen, queued_total, echoes, kernel_rst, other, send_calls, batches_rx, now_s() - t_start);
     return echoes >= nsegs ? 0 : 5;
 }

@@ -8,6 +8,7 @@ the oracle's FILL of the packet as built (check computed per context.c:208).
 import json
 import os
 import re
+import socket
 import struct
 import subprocess
 
@@ -122,14 +123,15 @@ def test_tx_fill_with_ip_header(tmp_path, copy):
 RAW = os.path.join(REPO, "tests", "c", "raw_echo")
 
 
-def run_raw(tmp_path, n, env_extra):
+def run_raw(tmp_path, n, env_extra, cpu=False):
     if not os.path.exists(RAW):
         subprocess.run(["make", "-C", REPO, "tests/c/raw_echo", "tcp_amd/libtcpcsum_preload.so"], check=True)
     out = tmp_path / "raw.bin"
     env = {k: v for k, v in os.environ.items() if not k.startswith("TCPCSUM_PRELOAD")}
     env.update({"LD_PRELOAD": PRELOAD, "TCPCSUM_PRELOAD_STATS": "1"})
     env.update(env_extra)
-    r = subprocess.run([RAW, str(n), str(out)], env=env, capture_output=True, text=True, timeout=120)
+    r = subprocess.run([RAW, str(n), str(out)] + (["cpu"] if cpu else []), env=env, capture_output=True,
+                       text=True, timeout=120)
     if r.returncode == 77:
         pytest.skip("no CAP_NET_RAW: neither user namespaces nor root: " + r.stdout.strip())
     summary = json.loads(r.stdout.strip().splitlines()[-1]) if r.stdout.strip() else {}
@@ -174,6 +176,44 @@ def test_raw_echo_plumbing_passthrough(tmp_path):
     for built, got in pkts:
         assert same_but_kernel_fields(built, got) and ip_header_ok(got)
         assert got[36:38] == b"\0\0"                 # nobody filled the TCP check
+    # Linux's own TCP receive path drops the unchecked echoes (no RST for them) and answers
+    # only the client's correctly checked segments
+    assert summary["kernel_rst"] == 600
+
+
+def test_raw_echo_plumbing_config_cpu(tmp_path):
+    """BASELINE configs[0] as the reference runs it: the echo server fills every check on the CPU
+    (context.c:208-209) and the packets cross loopback through raw sockets; every sniffed echo equals
+    the oracle's FILL and verifies to zero. No interposer."""
+    env = {k: v for k, v in os.environ.items() if k != "LD_PRELOAD"}
+    if not os.path.exists(RAW):
+        subprocess.run(["make", "-C", REPO, "tests/c/raw_echo"], check=True)
+    out = tmp_path / "raw.bin"
+    r = subprocess.run([RAW, "2000", str(out), "cpu"], env=env, capture_output=True, text=True, timeout=120)
+    if r.returncode == 77:
+        pytest.skip("no CAP_NET_RAW: " + r.stdout.strip())
+    assert r.returncode == 0, r.stdout + r.stderr
+    summary = json.loads(r.stdout.strip().splitlines()[-1])
+    data = out.read_bytes()
+    pos, n = 0, 0
+    while pos < len(data):
+        (lo,) = struct.unpack_from("<I", data, pos)
+        built = data[pos + 4:pos + 4 + lo]
+        pos += 4 + lo
+        (li,) = struct.unpack_from("<I", data, pos)
+        got = data[pos + 4:pos + 4 + li]
+        pos += 4 + li
+        assert built == oracle_fill(built)           # the server's CPU check is the reference's
+        assert same_but_kernel_fields(built, got) and ip_header_ok(got)
+        tcp = got[20:]
+        ps = oracle.pseudo(int.from_bytes(got[12:16], "little"), int.from_bytes(got[16:20], "little"),
+                           socket.htons(len(tcp)))
+        assert oracle.csum_continue(ps, tcp, len(tcp)) == 0
+        n += 1
+    assert n == 2000 and summary["echoes_sniffed"] == 2000 and summary["server_checks"] == "cpu"
+    # the Linux TCP stack accepts every echo's checksum: it answers each (no listener) with a RST,
+    # as it does the client's segments
+    assert summary["kernel_rst"] == 2 * 2000
 
 
 @pytest.mark.gpu
@@ -192,4 +232,7 @@ def test_raw_echo_plumbing_on_gpu(tmp_path):
     # rx: client segments (CPU checks) + sniffed echoes (GPU checks) verify; RSTs are partial
     assert stats["rx_verify_failed"] == 0
     assert stats["rx_partial"] == summary["kernel_rst"]
+    # independent check by the Linux TCP stack: it RSTs every echo (so it accepted the GPU's
+    # checksum) as well as every client segment
+    assert summary["kernel_rst"] == 2 * n
     assert stats["rx_verified"] >= 2 * n + summary["kernel_rst"]
