@@ -2,10 +2,12 @@
  * abi_smoke.c — proves include/tcpcsum.h is consumable from plain C, the way
  * the reference's C host code (context.c / loop.c) would call it.
  *   ./abi_smoke        : CPU-only checks (scalar drop-ins, error paths)
- *   ./abi_smoke --gpu  : also one uniform batch on the GPU vs the scalar path
+ *   ./abi_smoke --gpu  : also a uniform host batch and a pointer-per-packet wire
+ *                        batch (INTEGRATION.md level 2) on the GPU vs the scalar path
  * Exit status 0 on success.
  */
 #include <arpa/inet.h>
+#include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -55,6 +57,48 @@ int main(int argc, char **argv) {
         for (int i = 0; i < N; ++i) bad += got[i] != ref[i];
         CHECK(bad == 0);
         printf("gpu host-batch mismatches: %d / %d\n", bad, N);
+
+        /* INTEGRATION.md level 2, pointer form: the loop's separately malloc'd
+         * 32 KiB out-buffers (loop.c:180-183), each holding one packet framed as
+         * context.c:169-206 frames it with check 0, filled in place at the flush */
+        enum { P = 256 };
+        void *pkt[P];
+        uint32_t plen[P];
+        const tcpcsum_tuning_t tu = {0, 0, -1, 0};
+        CHECK(tcpcsum_ctx_set_tuning(ctx, &tu) == TCPCSUM_OK);
+        for (int i = 0; i < P; ++i) {
+            uint8_t *b = (uint8_t *) malloc(32768);
+            const unsigned pay = (unsigned) (rand() % 1457), tot = 44 + pay;
+            memset(b, 0, 44);
+            b[0] = 0x45; b[2] = (uint8_t) (tot >> 8); b[3] = (uint8_t) tot; b[8] = 255; b[9] = 6;
+            const uint32_t sa = htonl(0x7F000001u), da = htonl(0x0A000000u | (uint32_t) i);
+            memcpy(b + 12, &sa, 4); memcpy(b + 16, &da, 4);
+            b[32] = 6 << 4; b[33] = 0x18; b[34] = 0x20; b[40] = 3; b[41] = 3; b[42] = 5;
+            for (unsigned k = 0; k < pay; ++k) b[44 + k] = (uint8_t) rand();
+            pkt[i] = b;
+            plen[i] = tot;
+        }
+        uint16_t pout[P];
+        uint8_t pst[P];
+        CHECK(tcpcsum_ipv4_batch_ptrs_host(ctx, pkt, plen, P, TCPCSUM_IPV4_FILL, pout, pst) == TCPCSUM_OK);
+        int pbad = 0;
+        for (int i = 0; i < P; ++i) {
+            uint8_t *b = (uint8_t *) pkt[i];
+            uint16_t got, want;
+            uint32_t sa, da;
+            memcpy(&got, b + 36, 2);
+            memset(b + 36, 0, 2);
+            memcpy(&sa, b + 12, 4); memcpy(&da, b + 16, 4);
+            want = tcpcsum_continue(tcpcsum_pseudo(sa, da, htons((uint16_t) (plen[i] - 20))), (const char *) b + 20,
+                                    (int) plen[i] - 20);
+            pbad += got != want || pout[i] != want || pst[i] != TCPCSUM_PKT_OK;
+        }
+        uint64_t nreg = 0, nbytes = 0;
+        CHECK(tcpcsum_ctx_registered(ctx, &nreg, &nbytes) == TCPCSUM_OK && nreg > 0 && nbytes >= P * 4096u);
+        CHECK(pbad == 0);
+        printf("gpu pointer-batch mismatches: %d / %d (%llu registrations)\n", pbad, P, (unsigned long long) nreg);
+        CHECK(tcpcsum_ctx_unregister_host(ctx, NULL, 0) == TCPCSUM_OK);
+        for (int i = 0; i < P; ++i) free(pkt[i]);
         tcpcsum_ctx_destroy(ctx);
         free(h); free(ref); free(got); free(ss);
     }
