@@ -566,6 +566,9 @@ __device__ __forceinline__ void lb_sums(const uint8_t* a, uint32_t len, uint32_t
     const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     const uint64_t a0 = (uint64_t)(uintptr_t)a - m;
     const uint32_t a_lo = (uint32_t)a0, a_hi = (uint32_t)(a0 >> 32);
+    // every segment of the tile 4-B aligned in start and length (packed IPv4/TCP
+    // packets of 4-B multiples, IMIX): dword-granular masks, no byte masks
+    const bool a4 = __ballot(len != 0 && (((uint32_t)(uintptr_t)a | len) & 3u) != 0) == 0 && hole == kNoHole;
     accW[lane] = 0;
     if (want_odd) accO[lane] = 0;
     uint32_t carry = 0;   // segment owning the next window's first chunk
@@ -601,7 +604,17 @@ __device__ __forceinline__ void lb_sums(const uint8_t* a, uint32_t len, uint32_t
             const uint32_t lo = lmo & ((1u << 27) - 1u), mo = lmo >> 27;
             const uint32_t no = (mo + lo + 15u) >> 4;
             uint32_t w = 0, od = 0;
-            if (g < T) chunk_masked(v[k], (int32_t)(pc[k] * 16u) - (int32_t)mo, (int32_t)lo, (int32_t)hole, want_odd, w, od);
+            if (a4) {   // wave-uniform
+                const uint32_t rel = pc[k] * 16u - mo;   // dwords at rel + 4j: inside iff < lo (unsigned)
+                const u32x4 x = v[k];
+                const bool in = g < T;
+                w = sad16(in && rel < lo ? x.x : 0u, 0u);
+                w = sad16(in && rel + 4u < lo ? x.y : 0u, w);
+                w = sad16(in && rel + 8u < lo ? x.z : 0u, w);
+                w = sad16(in && rel + 12u < lo ? x.w : 0u, w);
+            } else if (g < T) {
+                chunk_masked(v[k], (int32_t)(pc[k] * 16u) - (int32_t)mo, (int32_t)lo, (int32_t)hole, want_odd, w, od);
+            }
             const bool end = g < T && (pc[k] + 1u == no || lane == 63u || g + 1u == T);
             const uint32_t sr = po[k] > W0 ? po[k] - W0 : 0u;   // the run's first lane in this window
             const uint32_t X = wave_scan_incl(w);

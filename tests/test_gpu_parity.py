@@ -542,6 +542,64 @@ def test_desc_forced_shapes(dev, shape):
             assert np.array_equal(got, want), (un, mb)
 
 
+@pytest.mark.parametrize("shape", [7, 8])
+@pytest.mark.parametrize("mix", ["all4", "one_odd_len", "one_odd_start"])
+def test_desc_balanced_dword_tiles(dev, shape, mix):
+    """Balanced kernels on tiles whose segments are all 4-B aligned in start and length (the
+    dword-mask path: packed IPv4/TCP, IMIX) and on tiles where one segment breaks it."""
+    import tcp_amd
+    rng = np.random.default_rng({"all4": 1, "one_odd_len": 2, "one_odd_start": 3}[mix] + 10 * shape)
+    size = 4 << 20
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    n = 3000
+    lens = rng.choice(np.array([0, 4, 20, 60, 64, 576, 1480, 1500, 9000], np.uint32), n)
+    off = (np.array([rng.integers(0, (size - l) // 4) for l in lens], np.uint64) * 4).astype(np.uint64)
+    if mix == "one_odd_len":
+        lens[::97] += 1
+    elif mix == "one_odd_start":
+        off[::89] += 2
+    ss = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    want = oracle.batch_desc(host, off, lens, ss)
+    d = to_dev(host, dev)
+    dd = to_dev(_desc(off, lens, ss), dev)
+    got = u16(tcp_amd.batch_desc(d, dd, n, 9001, tune=tcp_amd.make_tuning(0, 0, shape, 0)))
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("shape", [8, 9])
+def test_ipv4_balanced_dword_tiles(dev, shape):
+    """Packed packets whose lengths are multiples of 4 (every tile on the dword-mask path), mixed with
+    stretches of arbitrary lengths; FILL then VERIFY, against the oracle."""
+    import tcp_amd
+    from tests.packets import ip_packet
+    rng = np.random.default_rng(90 + shape)
+    pk, offs, pos = [], [], 0
+    for i in range(4000):
+        a4 = (i // 200) % 3 != 0
+        pl = int(rng.integers(0, 365)) * 4 if a4 else int(rng.integers(0, 1457))
+        if a4:
+            pos = (pos + 3) & ~3
+        pk.append(ip_packet(rng, pl))
+        offs.append(pos)
+        pos += len(pk[-1])
+    off = np.array(offs, np.uint64)
+    region = np.zeros(int(off[-1]) + len(pk[-1]) + 64, np.uint8)
+    for o, p in zip(off, pk):
+        region[int(o):int(o) + len(p)] = np.frombuffer(p, np.uint8)
+    for mode in (tcp_amd.IPV4_FILL, tcp_amd.IPV4_VERIFY):
+        ref = region.copy()
+        want_out, want_st = oracle.ipv4_batch(ref, off, 1536, mode)
+        dreg = to_dev(region, dev)
+        out = torch.empty(off.size, dtype=torch.int16, device=dev)
+        st = torch.empty(off.size, dtype=torch.uint8, device=dev)
+        tcp_amd.ipv4_batch(dreg, to_dev(off.view(np.int64), dev), off.size, 1536, mode, out, st,
+                           tune=tcp_amd.make_tuning(0, 0, shape, 0))
+        assert np.array_equal(st.cpu().numpy(), want_st), mode
+        assert np.array_equal(u16(out), want_out), mode
+        assert np.array_equal(dreg.cpu().numpy(), ref), mode
+        region = ref
+
+
 @pytest.mark.parametrize("shape", [-1, 1, 3, 8, 9])
 def test_ipv4_span_hint_mispredicted(dev, shape):
     """The next packet's offset only bounds the speculative span: shuffled offsets (gaps unrelated
