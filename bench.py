@@ -360,10 +360,20 @@ def main(argv=None) -> int:
         # no data-path collective: gloo (CPU) carries the barriers and the two reductions;
         # TCPCSUM_BENCH_BACKEND=nccl selects RCCL instead
         backend = os.environ.get("TCPCSUM_BENCH_BACKEND", "gloo")
-        if backend == "nccl":
-            tdist.init_process_group("nccl", device_id=device)
-        else:
-            tdist.init_process_group(backend)
+        # gloo announces its connections on stdout; the one JSON line must stay alone there
+        sys.stdout.flush()
+        saved, null = os.dup(1), os.open(os.devnull, os.O_WRONLY)
+        os.dup2(null, 1)
+        try:
+            if backend == "nccl":
+                tdist.init_process_group("nccl", device_id=device)
+            else:
+                tdist.init_process_group(backend)
+            tdist.barrier()
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
+            os.close(null)
         dist = tdist
     rc, arch = tcp_amd.device_check()
     if rc != 0:
