@@ -14,42 +14,6 @@ Reference path (``/root/reference``):
 """
 from __future__ import annotations
 
-from .api import (  # noqa: F401
-    DESC_DTYPE,
-    IPV4_FILL,
-    IPV4_IPHDR,
-    IPV4_VERIFY,
-    PKT_IPHDR_BAD,
-    PKT_OK,
-    PKT_SKIPPED,
-    TUNE_WIRE_CACHED,
-    TUNE_WIN16,
-    TcpCsumError,
-    HostContext,
-    batch_desc,
-    batch_uniform,
-    csum_continue,
-    device_check,
-    getPseudoHeaderSum,
-    ipv4_batch,
-    ipv4_batch_ptrs,
-    lib,
-    lib_path,
-    pinned_empty,
-    make_tuning,
-    set_tuning,
-    Tuning,
-    stream_probe,
-    synth_fill,
-    synth_pseudo,
-    tx_build,
-    TXSEG_DTYPE,
-)
-
-__all__ = [
-    "DESC_DTYPE", "IPV4_FILL", "IPV4_IPHDR", "PKT_IPHDR_BAD", "IPV4_VERIFY", "PKT_OK", "PKT_SKIPPED", "TcpCsumError",
-    "HostContext", "batch_desc", "batch_uniform", "csum_continue", "device_check",
-    "getPseudoHeaderSum", "ipv4_batch", "ipv4_batch_ptrs", "lib", "lib_path", "make_tuning", "pinned_empty",
-    "set_tuning", "Tuning", "stream_probe",
-    "synth_fill", "synth_pseudo", "tx_build", "TXSEG_DTYPE",
-]
+from . import api  # noqa: F401
+from .api import *  # noqa: F401,F403  (the public names: api.__all__)
+from .api import __all__  # noqa: F401

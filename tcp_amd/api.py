@@ -20,6 +20,14 @@ try:  # torch first: its HIP runtime must be the one the library binds to
 except Exception:  # pragma: no cover - torch is always present in this image
     torch = None
 
+__all__ = [
+    "DESC_DTYPE", "TXSEG_DTYPE", "IPV4_FILL", "IPV4_VERIFY", "IPV4_IPHDR", "PKT_OK", "PKT_SKIPPED",
+    "PKT_IPHDR_BAD", "PKT_CSUM_PARTIAL", "TUNE_WIRE_CACHED", "TUNE_WIN16", "TUNE_TX_NT_STORE", "TUNE_FILL_DWORD",
+    "TcpCsumError", "Tuning", "HostContext", "lib", "lib_path", "device_check", "make_tuning", "set_tuning",
+    "get_tuning", "plan_uniform", "getPseudoHeaderSum", "csum_continue", "batch_uniform", "batch_desc",
+    "ipv4_batch", "ipv4_batch_ptrs", "tx_build", "synth_fill", "synth_pseudo", "stream_probe", "pinned_empty",
+]
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_NAME = "libtcpcsum.so"
 
