@@ -511,6 +511,23 @@ __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
     return x;
 }
 
+// N independent inclusive scans stepped in lockstep: each DPP step of one scan
+// fills the other scans' DPP read-after-write wait states (one scan alone pads
+// every step with s_nop).
+template <int N>
+__device__ __forceinline__ void wave_scan_incl_n(uint32_t (&x)[N]) {
+#define TC_SCAN_STEP(ctrl, rmask)                                                                        \
+    _Pragma("unroll") for (int i = 0; i < N; ++i) x[i] +=                                                 \
+        (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x[i], ctrl, rmask, 0xF, false);
+    TC_SCAN_STEP(0x111, 0xF)   // row_shr:1
+    TC_SCAN_STEP(0x112, 0xF)   // row_shr:2
+    TC_SCAN_STEP(0x114, 0xF)   // row_shr:4
+    TC_SCAN_STEP(0x118, 0xF)   // row_shr:8
+    TC_SCAN_STEP(0x142, 0xA)   // row_bcast:15 -> rows 1, 3
+    TC_SCAN_STEP(0x143, 0xC)   // row_bcast:31 -> rows 2, 3
+#undef TC_SCAN_STEP
+}
+
 __device__ __forceinline__ uint32_t bperm(uint32_t x, uint32_t src_lane) {
     return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src_lane << 2), (int)x);
 }
@@ -595,6 +612,8 @@ __device__ __forceinline__ void lb_sums(const uint8_t* a, uint32_t len, uint32_t
             const uint64_t base = (uint64_t)bperm(a_lo, o) | ((uint64_t)bperm(a_hi, o) << 32);
             v[k] = ld16(zsel(g < T, reinterpret_cast<const uint8_t*>(base + (uint64_t)pc[k] * 16u)));
         }
+        uint32_t w[C], od[C], sr[C];
+        bool end[C];
 #pragma unroll
         for (int k = 0; k < C; ++k) {
             const uint32_t W0 = R + 64u * k;
@@ -603,27 +622,40 @@ __device__ __forceinline__ void lb_sums(const uint8_t* a, uint32_t len, uint32_t
             const uint32_t lmo = bperm(lm, o);
             const uint32_t lo = lmo & ((1u << 27) - 1u), mo = lmo >> 27;
             const uint32_t no = (mo + lo + 15u) >> 4;
-            uint32_t w = 0, od = 0;
+            w[k] = 0;
+            od[k] = 0;
             if (a4) {   // wave-uniform
                 const uint32_t rel = pc[k] * 16u - mo;   // dwords at rel + 4j: inside iff < lo (unsigned)
                 const u32x4 x = v[k];
                 const bool in = g < T;
-                w = sad16(in && rel < lo ? x.x : 0u, 0u);
-                w = sad16(in && rel + 4u < lo ? x.y : 0u, w);
-                w = sad16(in && rel + 8u < lo ? x.z : 0u, w);
-                w = sad16(in && rel + 12u < lo ? x.w : 0u, w);
+                uint32_t t = sad16(in && rel < lo ? x.x : 0u, 0u);
+                t = sad16(in && rel + 4u < lo ? x.y : 0u, t);
+                t = sad16(in && rel + 8u < lo ? x.z : 0u, t);
+                w[k] = sad16(in && rel + 12u < lo ? x.w : 0u, t);
             } else if (g < T) {
-                chunk_masked(v[k], (int32_t)(pc[k] * 16u) - (int32_t)mo, (int32_t)lo, (int32_t)hole, want_odd, w, od);
+                chunk_masked(v[k], (int32_t)(pc[k] * 16u) - (int32_t)mo, (int32_t)lo, (int32_t)hole, want_odd, w[k],
+                             od[k]);
             }
-            const bool end = g < T && (pc[k] + 1u == no || lane == 63u || g + 1u == T);
-            const uint32_t sr = po[k] > W0 ? po[k] - W0 : 0u;   // the run's first lane in this window
-            const uint32_t X = wave_scan_incl(w);
-            const uint32_t Xp = bperm(X, sr ? sr - 1u : 0u);
-            if (end) atomicAdd(reinterpret_cast<unsigned long long*>(accW + o), (unsigned long long)(X - (sr ? Xp : 0u)));
-            if (want_odd) {
-                const uint32_t Y = wave_scan_incl(od);
-                const uint32_t Yp = bperm(Y, sr ? sr - 1u : 0u);
-                if (end) atomicAdd(reinterpret_cast<unsigned long long*>(accO + o), (unsigned long long)(Y - (sr ? Yp : 0u)));
+            end[k] = g < T && (pc[k] + 1u == no || lane == 63u || g + 1u == T);
+            sr[k] = po[k] > W0 ? po[k] - W0 : 0u;   // the run's first lane in this window
+        }
+        // the C windows' scans interleaved (their DPP steps fill each other's wait states)
+        wave_scan_incl_n<C>(w);
+#pragma unroll
+        for (int k = 0; k < C; ++k) {
+            const uint32_t Xp = bperm(w[k], sr[k] ? sr[k] - 1u : 0u);
+            if (end[k])
+                atomicAdd(reinterpret_cast<unsigned long long*>(accW + own[k]),
+                          (unsigned long long)(w[k] - (sr[k] ? Xp : 0u)));
+        }
+        if (want_odd) {   // wave-uniform
+            wave_scan_incl_n<C>(od);
+#pragma unroll
+            for (int k = 0; k < C; ++k) {
+                const uint32_t Yp = bperm(od[k], sr[k] ? sr[k] - 1u : 0u);
+                if (end[k])
+                    atomicAdd(reinterpret_cast<unsigned long long*>(accO + own[k]),
+                              (unsigned long long)(od[k] - (sr[k] ? Yp : 0u)));
             }
         }
     }
