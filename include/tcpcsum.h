@@ -217,7 +217,10 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t *ctx, const void *h_base, uint64_t 
 
 /* Wire layout in host memory: n packets at h_pkts + h_pkt_off[i] (offsets
  * within one host region of region_bytes). FILL patches check in place in
- * host memory. Synchronous. */
+ * host memory. Synchronous. A region that one page-locked allocation covers
+ * (tcpcsum_host_alloc, or a pool registered once with
+ * tcpcsum_ctx_register_host) is read in place over PCIe; otherwise it is
+ * copied to the device first. */
 int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t *ctx, void *h_pkts, size_t region_bytes,
                             const uint64_t *h_pkt_off, uint64_t n, uint32_t cap, int mode,
                             uint16_t *h_out, uint8_t *h_status);

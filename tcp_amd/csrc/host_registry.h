@@ -122,7 +122,11 @@ public:
     const std::vector<HostRange>& ranges() const { return regs_; }
 
 private:
-    // Lock the pages of [lo, hi) (page-aligned) that no known range covers.
+    // Lock the pages of [lo, hi) (page-aligned) that no known range covers. A
+    // page already locked by someone else — another context of this process, the
+    // application — is taken as theirs (recorded, never locked twice, never
+    // unlocked here): HIP keeps one registration per page, so a second lock and a
+    // second unlock would undo the first owner's.
     int lock_pages(uintptr_t lo, uintptr_t hi) {
         std::vector<std::pair<uintptr_t, uintptr_t>> gaps;
         uintptr_t cur = lo;
@@ -136,11 +140,26 @@ private:
         if (cur < hi) gaps.push_back({cur, hi});
         int rc = 0;
         for (const auto& g : gaps) {
-            intptr_t delta = 0;
-            rc = b_.lock(g.first, g.second - g.first, &delta);
+            uintptr_t pg = g.first;
+            while (pg < g.second && !rc) {
+                uintptr_t rs = 0, re = 0;
+                intptr_t delta = 0;
+                if (b_.pinned_extent(pg, &rs, &re, &delta) && rs <= pg && re > pg) {
+                    bool known = false;
+                    for (const auto& r : regs_) known = known || (r.lo == rs && r.hi == re);
+                    if (!known) regs_.push_back({rs, re, delta, false});   // someone else's pages
+                    pg = std::min<uintptr_t>((re + kHostPage - 1) & ~(kHostPage - 1), g.second);
+                    continue;
+                }
+                uintptr_t run = pg + kHostPage;   // the run of pages nobody has locked
+                while (run < g.second && !b_.pinned_extent(run, &rs, &re, &delta)) run += kHostPage;
+                rc = b_.lock(pg, run - pg, &delta);
+                if (rc) break;
+                regs_.push_back({pg, run, delta, true});
+                bytes_ += run - pg;
+                pg = run;
+            }
             if (rc) break;
-            regs_.push_back({g.first, g.second, delta, true});
-            bytes_ += g.second - g.first;
         }
         rebuild();
         return rc;

@@ -44,7 +44,9 @@ struct HipHostBackend {
         *delta = (intptr_t)d - (intptr_t)lo;
         return 0;
     }
-    void unlock(uintptr_t lo) { (void)hipHostUnregister((void*)lo); }
+    void unlock(uintptr_t lo) {
+        if (hipHostUnregister((void*)lo) != hipSuccess) (void)hipGetLastError();   // nothing to undo
+    }
     bool pinned_extent(uintptr_t p, uintptr_t* lo, uintptr_t* hi, intptr_t* delta) {
         hipPointerAttribute_t a;
         bool ok = hipPointerGetAttributes(&a, (const void*)p) == hipSuccess && a.type == hipMemoryTypeHost &&
@@ -308,6 +310,10 @@ struct tcpcsum_ctx {
     uint16_t* k_wip = nullptr;
     uint32_t* h_len = nullptr;   // scatter-gather batches: per-packet readable bytes
     uint32_t* k_len = nullptr;
+    // bounce buffer for host ranges that are only partly page-locked (HIP copies
+    // them as locked from their first page and fails)
+    uint8_t* h_bounce = nullptr;
+    size_t bounce_bytes = 0;
     size_t pkt_cap = 0;
     // launch shapes of this context's batches (tcpcsum_ctx_set_tuning)
     tcpcsum::Tuning tune;
@@ -406,6 +412,7 @@ void tcpcsum_ctx_destroy(tcpcsum_ctx_t* c) {
     if (c->h_wstat) hipHostFree(c->h_wstat);
     if (c->h_wip) hipHostFree(c->h_wip);
     if (c->h_len) hipHostFree(c->h_len);
+    if (c->h_bounce) hipHostFree(c->h_bounce);
     c->reg.release(0, 0);
     for (int i = 0; i < 2; ++i)
         if (c->st[i]) hipStreamDestroy(c->st[i]);
@@ -439,18 +446,79 @@ void tcpcsum_host_free(void* p) {
 namespace {
 
 // Device-visible address of page-locked (hipHostMalloc / hipHostRegister'ed)
-// host memory, or nullptr for pageable memory. Kernels read and write such
-// memory directly over PCIe ("zero-copy"): no staging copy, only the bytes the
-// kernel touches cross the link.
-void* pinned_dev_ptr(const void* p) {
+// host memory [p, p + bytes), or nullptr when any of it is pageable. Kernels
+// read and write such memory directly over PCIe ("zero-copy"): no staging copy,
+// only the bytes the kernel touches cross the link. The whole range must lie in
+// ONE page-locked allocation or registration — a region only partly locked
+// (its first page locked by a neighbouring registration, say) takes the copy
+// path instead of letting a kernel touch unlocked pages.
+void* pinned_dev_ptr(const void* p, size_t bytes = 1) {
     if (!p) return nullptr;
     hipPointerAttribute_t a;
     if (hipPointerGetAttributes(&a, p) != hipSuccess) {
         (void)hipGetLastError();   // pageable memory: not an error for us
         return nullptr;
     }
-    if (a.type == hipMemoryTypeHost && a.devicePointer) return a.devicePointer;
-    return nullptr;
+    if (a.type != hipMemoryTypeHost || !a.devicePointer) return nullptr;
+    uintptr_t rs = 0;
+    size_t rsz = 0;
+    if (hipPointerGetAttribute(&rs, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, (hipDeviceptr_t)p) != hipSuccess ||
+        hipPointerGetAttribute(&rsz, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, (hipDeviceptr_t)p) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    const uintptr_t b = (uintptr_t)p;
+    if (rs > b || b + (bytes ? bytes : 1) > rs + rsz) return nullptr;
+    return a.devicePointer;
+}
+
+// [p, p + bytes) starts in page-locked memory but runs past that allocation.
+bool partly_pinned(const void* p, size_t bytes) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost && a.devicePointer && !pinned_dev_ptr(p, bytes);
+}
+
+constexpr size_t kBounce = 4u << 20;
+
+// Host <-> device copies on st. A range only partly page-locked goes through the
+// context's pinned bounce buffer, synchronously (a rare, caller-made layout).
+hipError_t copy_h2d(tcpcsum_ctx* c, void* d, const void* h, size_t n, hipStream_t st) {
+    if (!partly_pinned(h, n)) return hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, st);
+    if (!c->h_bounce) {
+        hipError_t e = hipHostMalloc((void**)&c->h_bounce, kBounce, hipHostMallocDefault);
+        if (e != hipSuccess) return e;
+        c->bounce_bytes = kBounce;
+    }
+    for (size_t o = 0; o < n; o += kBounce) {
+        const size_t k = n - o < kBounce ? n - o : kBounce;
+        hipError_t e = hipStreamSynchronize(st);   // the bounce buffer is free again
+        if (e != hipSuccess) return e;
+        memcpy(c->h_bounce, (const uint8_t*)h + o, k);
+        e = hipMemcpyAsync((uint8_t*)d + o, c->h_bounce, k, hipMemcpyHostToDevice, st);
+        if (e != hipSuccess) return e;
+    }
+    return hipStreamSynchronize(st);
+}
+
+hipError_t copy_d2h(tcpcsum_ctx* c, void* h, const void* d, size_t n, hipStream_t st) {
+    if (!partly_pinned(h, n)) return hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, st);
+    if (!c->h_bounce) {
+        hipError_t e = hipHostMalloc((void**)&c->h_bounce, kBounce, hipHostMallocDefault);
+        if (e != hipSuccess) return e;
+        c->bounce_bytes = kBounce;
+    }
+    for (size_t o = 0; o < n; o += kBounce) {
+        const size_t k = n - o < kBounce ? n - o : kBounce;
+        hipError_t e = hipMemcpyAsync(c->h_bounce, (const uint8_t*)d + o, k, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) return e;
+        memcpy((uint8_t*)h + o, c->h_bounce, k);
+    }
+    return hipSuccess;
 }
 
 int ensure_pkt_staging(tcpcsum_ctx* c, uint64_t n, hipStream_t st) {
@@ -497,17 +565,18 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t st
     const tcpcsum::Tuning tu = c->tune;
     hipError_t e;
     int rc;
-    if (const uint8_t* zb = (const uint8_t*)pinned_dev_ptr(h_base)) {
+    const size_t span = (size_t)((n - 1) * stride + len);
+    if (const uint8_t* zb = (const uint8_t*)pinned_dev_ptr(h_base, span)) {
         hipStream_t st = c->st[0];
         const uint32_t* zss = nullptr;
-        if (h_sum_start) zss = (const uint32_t*)pinned_dev_ptr(h_sum_start);
-        uint16_t* zout = (uint16_t*)pinned_dev_ptr(h_out);
+        if (h_sum_start) zss = (const uint32_t*)pinned_dev_ptr(h_sum_start, n * sizeof(uint32_t));
+        uint16_t* zout = (uint16_t*)pinned_dev_ptr(h_out, n * sizeof(uint16_t));
         if ((h_sum_start && !zss) || !zout) {   // stage the small arrays
             rc = ctx_ensure(c, 16, (size_t)n);
             if (rc) return rc;
         }
         if (h_sum_start && !zss) {
-            e = hipMemcpyAsync(c->d_ss[0], h_sum_start, n * sizeof(uint32_t), hipMemcpyHostToDevice, st);
+            e = copy_h2d(c, c->d_ss[0], h_sum_start, n * sizeof(uint32_t), st);
             if (e != hipSuccess) return hip_fail(e);
             zss = c->d_ss[0];
         }
@@ -515,7 +584,7 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t st
         rc = check_launch();
         if (rc) return rc;
         if (!zout) {
-            e = hipMemcpyAsync(h_out, c->d_out[0], n * sizeof(uint16_t), hipMemcpyDeviceToHost, st);
+            e = copy_d2h(c, h_out, c->d_out[0], n * sizeof(uint16_t), st);
             if (e != hipSuccess) return hip_fail(e);
         }
         e = hipStreamSynchronize(st);
@@ -539,15 +608,15 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t st
         // keep the device-side start alignment mod 16 equal to the host's so the
         // kernel shape matches what the same batch gets on device memory
         const size_t mis = (uintptr_t)src & 15u;
-        e = hipMemcpyAsync(c->d_buf[slot] + mis, src, bytes, hipMemcpyHostToDevice, st);
+        e = copy_h2d(c, c->d_buf[slot] + mis, src, bytes, st);
         if (e == hipSuccess && h_sum_start)
-            e = hipMemcpyAsync(c->d_ss[slot], h_sum_start + s0, cnt * sizeof(uint32_t), hipMemcpyHostToDevice, st);
+            e = copy_h2d(c, c->d_ss[slot], h_sum_start + s0, cnt * sizeof(uint32_t), st);
         if (e != hipSuccess) return hip_fail(e);
         tcpcsum::launch_uniform(c->d_buf[slot] + mis, stride, len, h_sum_start ? c->d_ss[slot] : nullptr, sum_start,
                                 c->d_out[slot], cnt, st, tu);
         rc = check_launch();
         if (rc) return rc;
-        e = hipMemcpyAsync(h_out + s0, c->d_out[slot], cnt * sizeof(uint16_t), hipMemcpyDeviceToHost, st);
+        e = copy_d2h(c, h_out + s0, c->d_out[slot], cnt * sizeof(uint16_t), st);
         if (e != hipSuccess) return hip_fail(e);
         // before slot is reused two chunks later, its previous work must be done
         if (s0 + per < n) {
@@ -584,18 +653,18 @@ int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t* c, void* h_pkts, size_t region_bytes,
     hipStream_t st = c->st[0];
     int rc = ensure_pkt_staging(c, n, st);
     if (rc) return rc;
-    const uint64_t* koff = (const uint64_t*)pinned_dev_ptr(h_pkt_off);
+    const uint64_t* koff = (const uint64_t*)pinned_dev_ptr(h_pkt_off, n * sizeof(uint64_t));
     if (!koff) {
         memcpy(c->h_off, h_pkt_off, n * sizeof(uint64_t));
         koff = c->k_off;
     }
-    uint16_t* zout = h_out ? (uint16_t*)pinned_dev_ptr(h_out) : nullptr;
-    uint8_t* zst = h_status ? (uint8_t*)pinned_dev_ptr(h_status) : nullptr;
+    uint16_t* zout = h_out ? (uint16_t*)pinned_dev_ptr(h_out, n * sizeof(uint16_t)) : nullptr;
+    uint8_t* zst = h_status ? (uint8_t*)pinned_dev_ptr(h_status, n) : nullptr;
     uint16_t* kout = zout ? zout : c->k_wout;
     uint8_t* kst = zst ? zst : c->k_wstat;
     const bool fill = (mode & TCPCSUM_IPV4_VERIFY) == 0;
     hipError_t e;
-    if (uint8_t* zp = (uint8_t*)pinned_dev_ptr(h_pkts)) {
+    if (uint8_t* zp = (uint8_t*)pinned_dev_ptr(h_pkts, region_bytes)) {
         // zero-copy over PCIe: 16-lane groups, 512 B per round (more waves with
         // reads in flight) beat the HBM-tuned MTU shape — 1024 x 1500-B FILL
         // batch 49 vs 59 us on MI355X (tools/e2e.py --sweep)
@@ -619,7 +688,7 @@ int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t* c, void* h_pkts, size_t region_bytes,
             if (e != hipSuccess) { g_last_hip_error.store((int)e); return TCPCSUM_ENOMEM; }
             c->d_region_bytes = need;
         }
-        e = hipMemcpyAsync(c->d_region + mis, h_pkts, region_bytes, hipMemcpyHostToDevice, st);
+        e = copy_h2d(c, c->d_region + mis, h_pkts, region_bytes, st);
         if (e != hipSuccess) return hip_fail(e);
         const bool ipfill = fill && (mode & TCPCSUM_IPV4_IPHDR);
         tcpcsum::launch_ipv4(c->d_region + mis, koff, nullptr, n, cap, (uint64_t)region_bytes,
@@ -681,8 +750,8 @@ int tcpcsum_ipv4_batch_ptrs_host(tcpcsum_ctx_t* c, void* const* h_pkts, const ui
         foot += len;
         cap = len > cap ? len : cap;
     }
-    uint16_t* zout = h_out ? (uint16_t*)pinned_dev_ptr(h_out) : nullptr;
-    uint8_t* zst = h_status ? (uint8_t*)pinned_dev_ptr(h_status) : nullptr;
+    uint16_t* zout = h_out ? (uint16_t*)pinned_dev_ptr(h_out, n * sizeof(uint16_t)) : nullptr;
+    uint8_t* zst = h_status ? (uint8_t*)pinned_dev_ptr(h_status, n) : nullptr;
     // zero-copy over PCIe: the 16-lane group shape for latency-bound batches
     // (as tcpcsum_ipv4_batch_host on a pinned pool)
     tcpcsum::Tuning tu = c->tune;

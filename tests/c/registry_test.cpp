@@ -144,11 +144,41 @@ static void scenario(bool flat, uint64_t seed) {
     CHECK(h.locks.empty() && reg.owned_bytes() == 0 && reg.owned_ranges() == 0);
 }
 
+// Two contexts over one host (tcpcsum_ctx_t each has its own registry): pages
+// the first locked are never locked again by the second, and each unlocks only
+// what it locked.
+static void two_registries(uint64_t seed) {
+    FakeHost h;
+    std::mt19937_64 r(seed);
+    tcpcsum::HostRegistry<FakeHost> a(h), b(h);
+    std::vector<std::pair<uintptr_t, size_t>> bufs;
+    uintptr_t cur = 0x7e0000002010ull;
+    for (int i = 0; i < 300; ++i) {
+        const size_t n = 4096 + 16;
+        bufs.push_back({cur, n - 16});
+        cur += n;
+    }
+    uintptr_t dev;
+    for (int k = 0; k < 2000; ++k) {
+        const auto& x = bufs[r() % bufs.size()];
+        const size_t len = 20 + r() % 1400;
+        CHECK((k & 1 ? a : b).resolve(x.first, len, &dev) == 0);
+        check_mapping(h, x.first, len, dev);
+    }
+    const size_t before = h.locks.size(), a_owned = a.owned_ranges();
+    CHECK(before == a_owned + b.owned_ranges());   // every lock has exactly one owner
+    a.release(0, 0);
+    CHECK(h.locks.size() == before - a_owned);
+    b.release(0, 0);
+    CHECK(h.locks.empty());
+}
+
 int main(int argc, char** argv) {
     const uint64_t seed = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : 1;
     for (uint64_t s = seed; s < seed + 4; ++s) {
         scenario(true, s);
         scenario(false, s);
+        two_registries(s);
     }
     std::printf(fails ? "FAIL (%d)\n" : "OK\n", fails);
     return fails ? 1 : 0;

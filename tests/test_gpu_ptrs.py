@@ -235,3 +235,32 @@ def test_ipv4_ptrs_host_context_tuning(dev):
         finally:
             a.unregister_host()
             b.unregister_host()
+
+
+@pytest.mark.parametrize("register", ["none", "whole", "half"])
+def test_ipv4_region_host_registered_pool(dev, register):
+    """The region host path over a pageable pool: copied when pageable, read in place when the whole
+    region is registered with the context (tcpcsum_ctx_register_host, once), and copied again when
+    only part of it is — never a kernel on unlocked pages. Results identical in all three."""
+    import tcp_amd
+    from tests.packets import build_batch
+    rng = np.random.default_rng(21)
+    region, off, _ = build_batch(rng, 512, slot=32768, malformed=True)
+    ref = region.copy()
+    want_out, want_st = oracle.ipv4_batch(ref, off, 32768, tcp_amd.IPV4_FILL)
+    with tcp_amd.HostContext(0) as ctx:
+        try:
+            if register == "whole":
+                ctx.register_host(region.ctypes.data, region.nbytes)
+            elif register == "half":
+                ctx.register_host(region.ctypes.data, region.nbytes // 2)
+            out, st = ctx.ipv4_batch(region, off, 32768, tcp_amd.IPV4_FILL)
+            assert np.array_equal(st, want_st) and np.array_equal(out, want_out)
+            assert np.array_equal(region, ref)
+            v, vs = ctx.ipv4_batch(region, off, 32768, tcp_amd.IPV4_VERIFY)
+            assert np.all(v[vs == tcp_amd.PKT_OK] == 0)
+            # the uniform host path over the same (un/partly/fully registered) bytes, odd shapes
+            u = ctx.batch_uniform(region, 1501, 1499, (region.nbytes - 1499) // 1501, 777)
+            assert np.array_equal(u, oracle.batch_uniform(region, 1501, 1499, u.size, 777))
+        finally:
+            ctx.unregister_host()

@@ -86,7 +86,9 @@ def main():
         pin[:] = reg
         variants = ([(sh, fl) for sh in (-1, 0, 1, 3, 5) for fl in (0, tcp_amd.TUNE_WIN16)]
                     if "--sweep" in sys.argv else [(-1, 0)])
-        for name, r in (("pageable", reg), ("pinned_zero_copy", pin)):
+        for name, r in (("pageable", reg), ("pinned_zero_copy", pin), ("pageable_registered", reg)):
+            if name == "pageable_registered":   # the pool page-locked once (tcpcsum_ctx_register_host)
+                ctx.register_host(reg.ctypes.data, reg.nbytes)
             for sh, fl in variants:
                 ctx.set_tuning(0, 0, sh, fl)
                 ctx.ipv4_batch(r, offs, 32768, tcp_amd.IPV4_FILL)
@@ -98,6 +100,7 @@ def main():
                                   "GiB/s_packet_bytes_median": round(1024 * 1500 / tmed / 2**30, 2)}),
                       flush=True)
             ctx.set_tuning(0, 0, -1, 0)
+        ctx.unregister_host()
 
     # the loop's own layout: 1024 separate pageable buffers, in and out alternating
     bufs = []
