@@ -415,6 +415,35 @@ def test_tx_build_vs_oracle(dev, layout):
         tcp_amd.set_tuning(0, 0, -1, 0)
 
 
+def test_tx_build_length_limits(dev):
+    """The largest packet the IPv4 tot_len can describe (65491-B payload -> 65535 B) is built and
+    checked; longer payloads (65492..65535) are not written and report check 0, like the oracle's
+    restatement of context.c:150-213; without the DATA flag the length is ignored."""
+    import tcp_amd
+    from tests.test_oracle import make_txsegs
+    rng = np.random.default_rng(77)
+    payload = rng.integers(0, 256, 1 << 17, dtype=np.uint8)
+    segs, _ = make_txsegs(rng, 8, payload.size, max_len=100)
+    lens = [65491, 65492, 65535, 65490, 0, 1, 65491, 3]
+    pos = 0
+    for i, L in enumerate(lens):
+        segs[i]["len"] = L
+        segs[i]["payload_off"] = int(rng.integers(0, payload.size - L))
+        segs[i]["out_off"] = pos
+        segs[i]["flags"] = 16 | 1 if i != 6 else 1          # the last 65491: no DATA flag
+        pos += 44 + (L if L <= 65491 else 0) + 16
+    garbage = rng.integers(0, 256, pos + 64, dtype=np.uint8)
+    for mode in (0, tcp_amd.IPV4_IPHDR):
+        want = garbage.copy()
+        want_c = oracle.tx_build(payload, segs, want, iphdr=bool(mode))
+        dout = to_dev(garbage, dev)
+        chk = torch.empty(len(lens), dtype=torch.int16, device=dev)
+        tcp_amd.tx_build(to_dev(payload, dev), to_dev(segs.view(np.uint8), dev), len(lens), 65535, dout, mode, chk)
+        assert np.array_equal(u16(chk), want_c)
+        assert np.array_equal(dout.cpu().numpy(), want)
+        assert want_c[1] == 0 and want_c[2] == 0
+
+
 def test_ipv4_verify_flags_checksum_partial(dev):
     """New behaviour (no reference result — parity pinned to the oracle only): VERIFY marks
     CHECKSUM_PARTIAL segments (check = un-complemented pseudo sum) instead of plain failures."""
