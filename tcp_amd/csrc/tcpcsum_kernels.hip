@@ -1599,6 +1599,15 @@ UniformPlan plan_uniform(uintptr_t b, uint64_t stride, uint32_t len, uint64_t n,
     }
     p.unroll = tu.unroll ? tu.unroll : kShapeUnroll[p.shape];
     p.max_blocks = tu.max_blocks > 0 ? tu.max_blocks : kShapeBlocks[p.shape];
+    // Byte-granular batches (odd starts or lengths) spend ~3x the VALU per chunk
+    // on byte masks and odd-byte sums: more, shallower waves hide it better —
+    // 4096 workgroups, at most 4 segments in flight per group (swept on MI355X at
+    // 99, 577, 1499, 3001 and 8191 B: 6-25 % faster than the aligned shapes'
+    // defaults; profiles/r02_sweep_m1.jsonl)
+    if (p.mode == M1) {
+        if (!tu.unroll && p.shape != 9 && p.unroll > 4) p.unroll = 4;
+        if (tu.max_blocks <= 0) p.max_blocks = 4096;
+    }
     p.pipe = tu.flags & TCPCSUM_TUNE_PIPE_ON ? true : tu.flags & TCPCSUM_TUNE_PIPE_OFF ? false : kShapePipe[p.shape];
     p.nt = tu.flags & TCPCSUM_TUNE_NT_ON ? true : tu.flags & TCPCSUM_TUNE_NT_OFF ? false : kShapeNt[p.shape];
     p.blocked = (tu.flags & TCPCSUM_TUNE_BLOCKED) ? 1 : 0;
