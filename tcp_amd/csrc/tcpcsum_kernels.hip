@@ -1607,6 +1607,12 @@ UniformPlan plan_uniform(uintptr_t b, uint64_t stride, uint32_t len, uint64_t n,
     if (p.mode == M1) {
         if (!tu.unroll && p.shape != 9 && p.unroll > 4) p.unroll = 4;
         if (tu.max_blocks <= 0) p.max_blocks = 4096;
+    } else if (p.shape == 9 && tu.max_blocks <= 0 && (p.mode != M16 || len < 12288u)) {
+        // one wave per segment: segments of one round (jumbo frames, 8-12 KiB)
+        // and the dword-masked path want 4x the waves of the 64 KiB config's grid
+        // (9000 B: 0.356 -> 0.234 ms, 12300 B: 0.323 -> 0.242; 16-64 KiB aligned
+        // keep 256; profiles/r02_sweep_long.jsonl)
+        p.max_blocks = 1024;
     }
     p.pipe = tu.flags & TCPCSUM_TUNE_PIPE_ON ? true : tu.flags & TCPCSUM_TUNE_PIPE_OFF ? false : kShapePipe[p.shape];
     p.nt = tu.flags & TCPCSUM_TUNE_NT_ON ? true : tu.flags & TCPCSUM_TUNE_NT_OFF ? false : kShapeNt[p.shape];
