@@ -42,8 +42,26 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 enum : int { M16 = 0, M4 = 1, M1 = 2 };
 
+// Every pointer the kernels dereference is a global-memory address (HBM, or
+// page-locked host memory mapped into the device's address space), never LDS
+// or scratch: loads and stores go through address space 1, so the compiler
+// emits global_* rather than flat_* instructions. A flat load counts against
+// lgkmcnt as well as vmcnt, so the s_waitcnt lgkmcnt(0) of the next
+// ds_bpermute / LDS access would wait for it too and serialise the loads.
+template <class T>
+using gptr = __attribute__((address_space(1))) T*;
+
+template <class T>
+__device__ __forceinline__ T ldg(const void* p) {
+    return *(gptr<const T>)(p);
+}
+template <class T>
+__device__ __forceinline__ void stg(void* p, T v) {
+    *(gptr<T>)(p) = v;
+}
+
 __device__ __forceinline__ u32x4 ld16(const uint8_t* p) {
-    return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return __builtin_nontemporal_load((gptr<const u32x4>)(p));
 }
 
 // Zero-filled device memory: lanes with nothing to load read it instead of
@@ -149,7 +167,7 @@ __device__ __forceinline__ uint64_t combine(uint64_t start, uint64_t W, uint64_t
 template <bool NT>
 __device__ __forceinline__ u32x4 ldq(const uint8_t* p) {
     if constexpr (NT) return ld16(p);
-    else return *reinterpret_cast<const u32x4*>(p);
+    else return ldg<u32x4>(p);
 }
 
 template <int G, int C, int U, int MODE, bool NT>
@@ -430,7 +448,7 @@ __global__ __launch_bounds__(256) void k_desc(const uint8_t* __restrict__ base,
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint64_t seg = tile * SPT + (uint64_t)(u * GPW + q);
-            dst[u] = *reinterpret_cast<const u32x4*>(zsel(seg < n, reinterpret_cast<const uint8_t*>(desc + seg)));
+            dst[u] = ldg<u32x4>(zsel(seg < n, reinterpret_cast<const uint8_t*>(desc + seg)));
         }
     };
     u32x4 dn[U];
@@ -699,7 +717,7 @@ __global__ __launch_bounds__(256) void k_desc_lb(const uint8_t* __restrict__ bas
     const uint64_t ntiles = (n + 63) / 64;
     for (uint64_t t = (uint64_t)blockIdx.x * 4u + wv; t < ntiles; t += nwaves) {
         const uint64_t seg = t * 64 + lane;
-        const u32x4 d = *reinterpret_cast<const u32x4*>(zsel(seg < n, reinterpret_cast<const uint8_t*>(desc + seg)));
+        const u32x4 d = ldg<u32x4>(zsel(seg < n, reinterpret_cast<const uint8_t*>(desc + seg)));
         const uint8_t* p = base + ((uint64_t)d.x | ((uint64_t)d.y << 32));
         const uint32_t len = d.z;   // 0 past n
         const bool odd = ((uintptr_t)p & 1u) != 0;
@@ -749,10 +767,10 @@ struct IpPkt {
 // A native u16 at p: one 2-byte store when p is even, two byte stores otherwise.
 __device__ __forceinline__ void store_u16(uint8_t* p, uint16_t v) {
     if (((uintptr_t)p & 1u) == 0) {
-        *reinterpret_cast<uint16_t*>(p) = v;
+        stg<uint16_t>(p, v);
     } else {
-        p[0] = (uint8_t)(v & 0xffu);
-        p[1] = (uint8_t)(v >> 8);
+        stg<uint8_t>(p, (uint8_t)(v & 0xffu));
+        stg<uint8_t>(p + 1, (uint8_t)(v >> 8));
     }
 }
 
@@ -835,10 +853,10 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const 
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint64_t i = tile * SPT + (uint64_t)(u * GPW + q);
-            on[u] = *reinterpret_cast<const uint64_t*>(zsel(i < n, reinterpret_cast<const uint8_t*>(off + i)));
-            on1[u] = *reinterpret_cast<const uint64_t*>(zsel(i + 1 < n, reinterpret_cast<const uint8_t*>(off + i + 1)));
+            on[u] = ldg<uint64_t>(zsel(i < n, reinterpret_cast<const uint8_t*>(off + i)));
+            on1[u] = ldg<uint64_t>(zsel(i + 1 < n, reinterpret_cast<const uint8_t*>(off + i + 1)));
             if constexpr (PL)
-                pn[u] = *reinterpret_cast<const uint32_t*>(zsel(i < n, reinterpret_cast<const uint8_t*>(plen + i)));
+                pn[u] = ldg<uint32_t>(zsel(i < n, reinterpret_cast<const uint8_t*>(plen + i)));
             else
                 pn[u] = 0xffffffffu;
         }
@@ -1012,7 +1030,7 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const 
         if (d.fill) {
             uint8_t* cp = d.ip + d.th + 16;
             if (dword_store && ((uintptr_t)cp & 3u) == 0)   // check and the unchanged urg_ptr in one dword
-                *reinterpret_cast<uint32_t*>(cp) = d.urg | d.c;
+                stg<uint32_t>(cp, d.urg | d.c);
             else
                 store_u16(cp, d.c);   // native u16 store, as context.c:208
             if (iphdr) store_u16(d.ip + 10, d.ic);
@@ -1053,11 +1071,11 @@ __global__ __launch_bounds__(256) void k_ipv4_lb(uint8_t* __restrict__ pkts, con
     for (uint64_t t = (uint64_t)blockIdx.x * 4u + wv; t < ntiles; t += nwaves) {
         const uint64_t i = t * 64 + lane;
         const bool live = i < n;
-        const uint64_t o = *reinterpret_cast<const uint64_t*>(zsel(live, reinterpret_cast<const uint8_t*>(off + i)));
+        const uint64_t o = ldg<uint64_t>(zsel(live, reinterpret_cast<const uint8_t*>(off + i)));
         uint32_t room = 0;   // PL: readable bytes at the packet (region end, its own length)
         bool hdr;
         if constexpr (PL) {
-            const uint32_t pl = *reinterpret_cast<const uint32_t*>(zsel(live, reinterpret_cast<const uint8_t*>(plen + i)));
+            const uint32_t pl = ldg<uint32_t>(zsel(live, reinterpret_cast<const uint8_t*>(plen + i)));
             const uint64_t rr = live && o < limit ? limit - o : 0u;
             room = (uint32_t)(rr < (uint64_t)pl ? rr : (uint64_t)pl);
             hdr = room >= 20u;
@@ -1072,7 +1090,7 @@ __global__ __launch_bounds__(256) void k_ipv4_lb(uint8_t* __restrict__ pkts, con
         uint32_t D[6];
 #pragma unroll
         for (int k = 0; k < 6; ++k)
-            D[k] = *reinterpret_cast<const uint32_t*>(zsel(hdr && (k < 5 || sh != 0), d0 + 4 * k));
+            D[k] = ldg<uint32_t>(zsel(hdr && (k < 5 || sh != 0), d0 + 4 * k));
         auto rel4 = [&](int k) { return __builtin_amdgcn_alignbyte(D[k + 1], D[k], sh); };   // bytes [4k, 4k+4)
         const uint32_t h0 = rel4(0), h8 = rel4(2), sa = rel4(3), da = rel4(4);
         const uint32_t ver = (h0 >> 4) & 15u, ihl = h0 & 15u;
@@ -1098,11 +1116,11 @@ __global__ __launch_bounds__(256) void k_ipv4_lb(uint8_t* __restrict__ pkts, con
         uint64_t S = combine(ps, acc[wv][0][lane], any_odd ? acc[wv][1][lane] : 0, odd);
         // FILL sums with the check as zero (context.c:182): TCP+16 is an even offset,
         // so its native word (L2-hot: just summed) contributes exactly its value
-        if (!verify) S -= (uint32_t)tcp[16] | ((uint32_t)tcp[17] << 8);
+        if (!verify) S -= (uint32_t)ldg<uint8_t>(tcp + 16) | ((uint32_t)ldg<uint8_t>(tcp + 17) << 8);
         const uint16_t c = fold_ref(S);
         uint32_t st = TCPCSUM_PKT_OK;
         if (verify && c != 0) {   // rare: was the check left as the bare pseudo-header sum?
-            const uint32_t cw = (uint32_t)tcp[16] | ((uint32_t)tcp[17] << 8);
+            const uint32_t cw = (uint32_t)ldg<uint8_t>(tcp + 16) | ((uint32_t)ldg<uint8_t>(tcp + 17) << 8);
             if (cw == (uint32_t)(uint16_t)~fold_ref(ps)) st |= TCPCSUM_PKT_CSUM_PARTIAL;
         }
         if (iphdr) {
@@ -1112,8 +1130,8 @@ __global__ __launch_bounds__(256) void k_ipv4_lb(uint8_t* __restrict__ pkts, con
 #pragma unroll
             for (int k = 0; k < 5; ++k) w = sad16(rel4(k), w);
             for (uint32_t k = 5; k < ihl; ++k) {   // IP options
-                const uint32_t lo = *reinterpret_cast<const uint32_t*>(d0 + 4 * k);
-                const uint32_t hi = sh ? *reinterpret_cast<const uint32_t*>(d0 + 4 * k + 4) : 0u;
+                const uint32_t lo = ldg<uint32_t>(d0 + 4 * k);
+                const uint32_t hi = sh ? ldg<uint32_t>(d0 + 4 * k + 4) : 0u;
                 w = sad16(__builtin_amdgcn_alignbyte(hi, lo, sh), w);
             }
             const uint16_t ic = fold_ref((uint64_t)w - (verify ? 0u : (h8 >> 16)));

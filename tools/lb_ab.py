@@ -50,7 +50,11 @@ def main():
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / steps
 
+    only = os.environ.get("LB_ONLY")   # run just this workload (profiling)
+
     def ab(name, f_old, f_new, out, nbytes, rounds=7):
+        if only and only != name:
+            return
         f_old()
         a = out.clone()
         f_new()
@@ -124,6 +128,8 @@ def main():
             return new.tcpcsum_ipv4_batch_dev(reg.data_ptr(), R, offs.data_ptr(), m, 1536, 1, out.data_ptr(),
                                               sta.data_ptr(), h, ctypes.byref(t8))
         ab(name, f_old, f_new, out[:m], nbytes)
+        if only and only != name:
+            continue
         ok = bool((out[:m] == 0).all().item()) and bool((sta[:m] == 0).all().item())
         print(json.dumps({"measure": name, "verify_all_zero": ok}), flush=True)
     old.tcpcsum_set_tuning(0, 0, -1, 0)
