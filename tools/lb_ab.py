@@ -9,7 +9,7 @@ Workloads (device-resident, as tools/wirebench.py builds them):
     1536-B slots — forced balanced (shape 8).
 Results must agree between the two builds. JSON lines.
 
-  python tools/lb_ab.py [old.so]
+  python tools/lb_ab.py [old.so]     (round-1 ABI or ABI v2 builds; LB_ONLY=name runs one workload)
 """
 import ctypes
 import json
@@ -30,9 +30,15 @@ def main():
     new = tcp_amd.lib()
     old = ctypes.CDLL(old_path)
     vp, u64, u32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32
-    old.tcpcsum_ipv4_batch_dev.argtypes = [vp, u64, vp, u64, u32, ctypes.c_int, vp, vp, vp]
-    old.tcpcsum_batch_desc_dev.argtypes = [vp, vp, u64, u32, vp, vp]
-    old.tcpcsum_set_tuning.argtypes = [ctypes.c_int] * 4
+    v2 = hasattr(old, "tcpcsum_tuning_check")   # ABI v2: per-call tuning (an earlier round-2 build)
+    if v2:
+        old.tcpcsum_ipv4_batch_dev.argtypes = [vp, u64, vp, u64, u32, ctypes.c_int, vp, vp, vp, vp]
+        old.tcpcsum_batch_desc_dev.argtypes = [vp, vp, u64, u32, vp, vp, vp]
+    else:
+        old.tcpcsum_ipv4_batch_dev.argtypes = [vp, u64, vp, u64, u32, ctypes.c_int, vp, vp, vp]
+        old.tcpcsum_batch_desc_dev.argtypes = [vp, vp, u64, u32, vp, vp]
+        old.tcpcsum_set_tuning.argtypes = [ctypes.c_int] * 4
+    old_tag = os.path.basename(old_path).replace("libtcpcsum_", "").replace(".so", "")
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream()
     h = st.cuda_stream
@@ -59,9 +65,9 @@ def main():
         a = out.clone()
         f_new()
         same = bool(torch.equal(a, out))
-        res = {"r01": [], "head": []}
+        res = {old_tag: [], "head": []}
         for _ in range(rounds):
-            res["r01"].append(timeit(f_old))
+            res[old_tag].append(timeit(f_old))
             res["head"].append(timeit(f_new))
         for lib, ts in res.items():
             ms = statistics.median(ts)
@@ -88,6 +94,9 @@ def main():
         mx = int(lens.max())
 
         def f_old():
+            if v2:
+                return old.tcpcsum_batch_desc_dev(data.data_ptr(), dd.data_ptr(), n, mx, out.data_ptr(), h,
+                                                  ctypes.byref(t7))
             old.tcpcsum_set_tuning(0, 0, 7, 0)
             return old.tcpcsum_batch_desc_dev(data.data_ptr(), dd.data_ptr(), n, mx, out.data_ptr(), h)
 
@@ -120,6 +129,9 @@ def main():
         R = reg.numel()
 
         def f_old():
+            if v2:
+                return old.tcpcsum_ipv4_batch_dev(reg.data_ptr(), R, offs.data_ptr(), m, 1536, 1, out.data_ptr(),
+                                                  sta.data_ptr(), h, ctypes.byref(t8))
             old.tcpcsum_set_tuning(0, 0, 8, 0)
             return old.tcpcsum_ipv4_batch_dev(reg.data_ptr(), R, offs.data_ptr(), m, 1536, 1, out.data_ptr(),
                                               sta.data_ptr(), h)
@@ -132,7 +144,8 @@ def main():
             continue
         ok = bool((out[:m] == 0).all().item()) and bool((sta[:m] == 0).all().item())
         print(json.dumps({"measure": name, "verify_all_zero": ok}), flush=True)
-    old.tcpcsum_set_tuning(0, 0, -1, 0)
+    if not v2:
+        old.tcpcsum_set_tuning(0, 0, -1, 0)
 
 
 if __name__ == "__main__":
