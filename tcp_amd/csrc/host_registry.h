@@ -113,6 +113,21 @@ public:
         rebuild();
     }
 
+    // Forget the mappings of memory page-locked by someone else (kept, they could
+    // go stale: their owner may free or unregister them between two batches).
+    // Called at the start of every batch; the first packet of a batch in such
+    // memory looks its mapping up again.
+    void forget_foreign() {
+        bool any = false;
+        for (const auto& r : regs_) any = any || !r.owned;
+        if (!any) return;
+        std::vector<HostRange> keep;
+        for (const auto& r : regs_)
+            if (r.owned) keep.push_back(r);
+        regs_.swap(keep);
+        rebuild();
+    }
+
     uint64_t owned_ranges() const {
         uint64_t k = 0;
         for (const auto& r : regs_) k += r.owned ? 1u : 0u;

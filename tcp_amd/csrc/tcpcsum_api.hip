@@ -310,10 +310,15 @@ struct tcpcsum_ctx {
     uint16_t* k_wip = nullptr;
     uint32_t* h_len = nullptr;   // scatter-gather batches: per-packet readable bytes
     uint32_t* k_len = nullptr;
-    // bounce buffer for host ranges that are only partly page-locked (HIP copies
-    // them as locked from their first page and fails)
-    uint8_t* h_bounce = nullptr;
-    size_t bounce_bytes = 0;
+    // two pinned bounce buffers for every copy from / to host memory that is not
+    // page-locked as a whole: pageable memory never reaches a HIP copy (whose
+    // pageable path pins the user pages in place, under the same pages this
+    // context registers for scatter-gather batches), and ranges only partly
+    // page-locked would make HIP copy them as locked from their first page.
+    // bounce_ev[i]: the last copy through h_bounce[i] (recorded on its stream)
+    uint8_t* h_bounce[2] = {nullptr, nullptr};
+    hipEvent_t bounce_ev[2] = {nullptr, nullptr};
+    bool bounce_busy[2] = {false, false};
     size_t pkt_cap = 0;
     // launch shapes of this context's batches (tcpcsum_ctx_set_tuning)
     tcpcsum::Tuning tune;
@@ -412,7 +417,10 @@ void tcpcsum_ctx_destroy(tcpcsum_ctx_t* c) {
     if (c->h_wstat) hipHostFree(c->h_wstat);
     if (c->h_wip) hipHostFree(c->h_wip);
     if (c->h_len) hipHostFree(c->h_len);
-    if (c->h_bounce) hipHostFree(c->h_bounce);
+    for (int i = 0; i < 2; ++i) {
+        if (c->h_bounce[i]) hipHostFree(c->h_bounce[i]);
+        if (c->bounce_ev[i]) hipEventDestroy(c->bounce_ev[i]);
+    }
     c->reg.release(0, 0);
     for (int i = 0; i < 2; ++i)
         if (c->st[i]) hipStreamDestroy(c->st[i]);
@@ -472,54 +480,137 @@ void* pinned_dev_ptr(const void* p, size_t bytes = 1) {
     return a.devicePointer;
 }
 
-// [p, p + bytes) starts in page-locked memory but runs past that allocation.
-bool partly_pinned(const void* p, size_t bytes) {
-    hipPointerAttribute_t a;
-    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
-        (void)hipGetLastError();
-        return false;
-    }
-    return a.type == hipMemoryTypeHost && a.devicePointer && !pinned_dev_ptr(p, bytes);
-}
-
 constexpr size_t kBounce = 4u << 20;
 
-// Host <-> device copies on st. A range only partly page-locked goes through the
-// context's pinned bounce buffer, synchronously (a rare, caller-made layout).
-hipError_t copy_h2d(tcpcsum_ctx* c, void* d, const void* h, size_t n, hipStream_t st) {
-    if (!partly_pinned(h, n)) return hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, st);
-    if (!c->h_bounce) {
-        hipError_t e = hipHostMalloc((void**)&c->h_bounce, kBounce, hipHostMallocDefault);
-        if (e != hipSuccess) return e;
-        c->bounce_bytes = kBounce;
-    }
-    for (size_t o = 0; o < n; o += kBounce) {
-        const size_t k = n - o < kBounce ? n - o : kBounce;
-        hipError_t e = hipStreamSynchronize(st);   // the bounce buffer is free again
-        if (e != hipSuccess) return e;
-        memcpy(c->h_bounce, (const uint8_t*)h + o, k);
-        e = hipMemcpyAsync((uint8_t*)d + o, c->h_bounce, k, hipMemcpyHostToDevice, st);
-        if (e != hipSuccess) return e;
-    }
-    return hipStreamSynchronize(st);
-}
-
-hipError_t copy_d2h(tcpcsum_ctx* c, void* h, const void* d, size_t n, hipStream_t st) {
-    if (!partly_pinned(h, n)) return hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, st);
-    if (!c->h_bounce) {
-        hipError_t e = hipHostMalloc((void**)&c->h_bounce, kBounce, hipHostMallocDefault);
-        if (e != hipSuccess) return e;
-        c->bounce_bytes = kBounce;
-    }
-    for (size_t o = 0; o < n; o += kBounce) {
-        const size_t k = n - o < kBounce ? n - o : kBounce;
-        hipError_t e = hipMemcpyAsync(c->h_bounce, (const uint8_t*)d + o, k, hipMemcpyDeviceToHost, st);
-        if (e == hipSuccess) e = hipStreamSynchronize(st);
-        if (e != hipSuccess) return e;
-        memcpy((uint8_t*)h + o, c->h_bounce, k);
+hipError_t ensure_bounce(tcpcsum_ctx* c) {
+    for (int i = 0; i < 2; ++i) {
+        if (!c->h_bounce[i]) {
+            hipError_t e = hipHostMalloc((void**)&c->h_bounce[i], kBounce, hipHostMallocDefault);
+            if (e != hipSuccess) return e;
+        }
+        if (!c->bounce_ev[i]) {
+            hipError_t e = hipEventCreateWithFlags(&c->bounce_ev[i], hipEventDisableTiming);
+            if (e != hipSuccess) return e;
+        }
     }
     return hipSuccess;
 }
+
+// Bounce buffer i is free again (its last copy, on whatever stream, is done).
+hipError_t bounce_wait(tcpcsum_ctx* c, int i) {
+    if (!c->bounce_busy[i]) return hipSuccess;
+    c->bounce_busy[i] = false;
+    return hipEventSynchronize(c->bounce_ev[i]);
+}
+
+// Host -> device on st. Page-locked source: one async DMA. Otherwise chunks of
+// at most 4 MiB alternate between the two bounce buffers: the CPU copy of
+// chunk k+1 overlaps the DMA of chunk k. Returns with the DMAs queued on st.
+hipError_t copy_h2d(tcpcsum_ctx* c, void* d, const void* h, size_t n, hipStream_t st) {
+    if (pinned_dev_ptr(h, n)) return hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, st);
+    hipError_t e = ensure_bounce(c);
+    int i = 0;
+    for (size_t o = 0; o < n && e == hipSuccess; o += kBounce, i ^= 1) {
+        const size_t k = n - o < kBounce ? n - o : kBounce;
+        e = bounce_wait(c, i);
+        if (e != hipSuccess) break;
+        memcpy(c->h_bounce[i], (const uint8_t*)h + o, k);
+        e = hipMemcpyAsync((uint8_t*)d + o, c->h_bounce[i], k, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) e = hipEventRecord(c->bounce_ev[i], st);
+        if (e == hipSuccess) c->bounce_busy[i] = true;
+    }
+    return e;
+}
+
+// Device -> host on st. Page-locked destination: one async DMA, queued on st.
+// Otherwise through the bounce buffers, the DMA of chunk k+1 overlapping the
+// CPU copy-out of chunk k, and complete on return.
+hipError_t copy_d2h(tcpcsum_ctx* c, void* h, const void* d, size_t n, hipStream_t st) {
+    if (pinned_dev_ptr(h, n)) return hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, st);
+    hipError_t e = ensure_bounce(c);
+    size_t prev_o = 0, prev_k = 0;
+    int i = 0;
+    for (size_t o = 0; o < n && e == hipSuccess; o += kBounce, i ^= 1) {
+        const size_t k = n - o < kBounce ? n - o : kBounce;
+        e = bounce_wait(c, i);
+        if (e != hipSuccess) break;
+        e = hipMemcpyAsync(c->h_bounce[i], (const uint8_t*)d + o, k, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipEventRecord(c->bounce_ev[i], st);
+        if (e != hipSuccess) break;
+        c->bounce_busy[i] = true;
+        if (prev_k) {   // the previous chunk, while this one is in flight
+            e = bounce_wait(c, i ^ 1);
+            if (e == hipSuccess) memcpy((uint8_t*)h + prev_o, c->h_bounce[i ^ 1], prev_k);
+        }
+        prev_o = o;
+        prev_k = k;
+    }
+    if (e == hipSuccess && prev_k) {
+        e = bounce_wait(c, i ^ 1);
+        if (e == hipSuccess) memcpy((uint8_t*)h + prev_o, c->h_bounce[i ^ 1], prev_k);
+    }
+    return e;
+}
+
+// One call's page locks of pageable host ranges: the pages under each range
+// are registered for the call, the kernel reads (FILL: writes) them in place
+// over PCIe, and they are unregistered once the call's streams have drained —
+// never a HIP copy from pageable memory (whose pin-in-place is HIP's own,
+// under pages this library also registers) and no staging copy of the bytes.
+// Registering costs about 120 us for 32 MiB on MI355X hosts
+// (tools/pin_cache_probe.cpp). Ranges come in increasing address order (the
+// chunks of one batch): pages an earlier range already locked are not locked
+// again. Requires the mapping at the host address (as every registration on
+// MI355X hosts is), since a range may span two registrations. When a range
+// cannot be registered (some page locked by someone else, a mapping that
+// refuses it, a mapping elsewhere), pin() returns nullptr and the caller
+// copies through the bounce buffers instead.
+struct PinSet {
+    hipStream_t st[2];
+    std::vector<uintptr_t> los;
+    uintptr_t lo = 0, hi = 0;   // [lo, hi): pages locked so far, contiguous
+    PinSet(hipStream_t a, hipStream_t b) : st{a, b} {}
+    PinSet(const PinSet&) = delete;
+    PinSet& operator=(const PinSet&) = delete;
+    ~PinSet() { release(); }
+    const void* pin(const void* p, size_t n) {
+        uintptr_t a = (uintptr_t)p & ~(uintptr_t)4095;
+        const uintptr_t b = ((uintptr_t)p + n + 4095) & ~(uintptr_t)4095;
+        const bool joins = !los.empty() && a >= lo && a <= hi;   // continues the locked run
+        if (joins) a = hi;
+        if (a < b) {
+            void* d = nullptr;
+            if (hipHostRegister((void*)a, b - a, hipHostRegisterMapped) != hipSuccess) {
+                (void)hipGetLastError();
+                return nullptr;
+            }
+            if (hipHostGetDevicePointer(&d, (void*)a, 0) != hipSuccess || (uintptr_t)d != a) {
+                (void)hipGetLastError();
+                (void)hipHostUnregister((void*)a);
+                (void)hipGetLastError();
+                return nullptr;
+            }
+            los.push_back(a);
+            if (!joins) lo = a;
+            hi = b;
+        }
+        return p;   // mapped at its host address
+    }
+    // after every kernel that reads the pages (queued on st[0] / st[1]) is done
+    void release() {
+        if (los.empty()) return;
+        for (hipStream_t s : st)
+            if (s) (void)hipStreamSynchronize(s);
+        for (uintptr_t a : los)
+            if (hipHostUnregister((void*)a) != hipSuccess) (void)hipGetLastError();
+        los.clear();
+        lo = hi = 0;
+    }
+};
+
+// Pageable ranges at least this large are page-locked for the call rather than
+// copied through the bounce buffers.
+constexpr size_t kTempPinMin = 64u << 10;
 
 int ensure_pkt_staging(tcpcsum_ctx* c, uint64_t n, hipStream_t st) {
     if (n <= c->pkt_cap) return TCPCSUM_OK;
@@ -553,8 +644,9 @@ int ensure_pkt_staging(tcpcsum_ctx* c, uint64_t n, hipStream_t st) {
 
 // Pinned input: one launch reads the segments in host memory directly.
 // Pageable input: chunks of segments alternate between two slots (stream +
-// device buffers), so the H2D copy of chunk k+1 overlaps the kernel and D2H of
-// chunk k.
+// device buffers), each page-locked for the call and read in place (or copied
+// through the bounce buffers), so locking chunk k+1 overlaps the kernel of
+// chunk k and collecting chunk k's results overlaps the kernel of chunk k+1.
 int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t stride, uint32_t len,
                                const uint32_t* h_sum_start, uint32_t sum_start, uint16_t* h_out, uint64_t n) {
     if (!c) return TCPCSUM_EINVAL;
@@ -598,6 +690,13 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t st
     const uint64_t chunk_bytes = (per - 1) * stride + len;
     rc = ctx_ensure(c, (size_t)chunk_bytes + 16, (size_t)per);
     if (rc) return rc;
+    // Chunks alternate between two streams. Each chunk's bytes are page-locked
+    // for the call and read in place (else copied through the bounce buffers);
+    // locking chunk k and collecting chunk k-1's results overlap kernel k-1 / k.
+    uint16_t* zout = (uint16_t*)pinned_dev_ptr(h_out, n * sizeof(uint16_t));
+    PinSet pins(c->st[0], c->st[1]);
+    uint64_t prev_s0 = 0, prev_cnt = 0;
+    int prev_slot = -1;
     uint64_t k = 0;
     for (uint64_t s0 = 0; s0 < n; s0 += per, ++k) {
         const int slot = (int)(k & 1);
@@ -605,24 +704,35 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t st
         const uint64_t cnt = (n - s0) < per ? (n - s0) : per;
         const uint64_t bytes = (cnt - 1) * stride + len;
         const uint8_t* src = (const uint8_t*)h_base + s0 * stride;
-        // keep the device-side start alignment mod 16 equal to the host's so the
-        // kernel shape matches what the same batch gets on device memory
-        const size_t mis = (uintptr_t)src & 15u;
-        e = copy_h2d(c, c->d_buf[slot] + mis, src, bytes, st);
-        if (e == hipSuccess && h_sum_start)
+        // slot's previous chunk (k-2) finished when its results were collected
+        const uint8_t* in = bytes >= kTempPinMin ? (const uint8_t*)pins.pin(src, bytes) : nullptr;
+        if (!in) {
+            // keep the device-side start alignment mod 16 equal to the host's so
+            // the kernel shape matches what the same batch gets on device memory
+            const size_t mis = (uintptr_t)src & 15u;
+            e = copy_h2d(c, c->d_buf[slot] + mis, src, bytes, st);
+            if (e != hipSuccess) return hip_fail(e);
+            in = c->d_buf[slot] + mis;
+        }
+        if (h_sum_start) {
             e = copy_h2d(c, c->d_ss[slot], h_sum_start + s0, cnt * sizeof(uint32_t), st);
-        if (e != hipSuccess) return hip_fail(e);
-        tcpcsum::launch_uniform(c->d_buf[slot] + mis, stride, len, h_sum_start ? c->d_ss[slot] : nullptr, sum_start,
-                                c->d_out[slot], cnt, st, tu);
-        rc = check_launch();
-        if (rc) return rc;
-        e = copy_d2h(c, h_out + s0, c->d_out[slot], cnt * sizeof(uint16_t), st);
-        if (e != hipSuccess) return hip_fail(e);
-        // before slot is reused two chunks later, its previous work must be done
-        if (s0 + per < n) {
-            e = hipStreamSynchronize(c->st[slot ^ 1]);
             if (e != hipSuccess) return hip_fail(e);
         }
+        tcpcsum::launch_uniform(in, stride, len, h_sum_start ? c->d_ss[slot] : nullptr, sum_start,
+                                zout ? zout + s0 : c->d_out[slot], cnt, st, tu);
+        rc = check_launch();
+        if (rc) return rc;
+        if (prev_slot >= 0 && !zout) {   // chunk k-1's results, while chunk k runs
+            e = copy_d2h(c, h_out + prev_s0, c->d_out[prev_slot], prev_cnt * sizeof(uint16_t), c->st[prev_slot]);
+            if (e != hipSuccess) return hip_fail(e);
+        }
+        prev_s0 = s0;
+        prev_cnt = cnt;
+        prev_slot = slot;
+    }
+    if (prev_slot >= 0 && !zout) {
+        e = copy_d2h(c, h_out + prev_s0, c->d_out[prev_slot], prev_cnt * sizeof(uint16_t), c->st[prev_slot]);
+        if (e != hipSuccess) return hip_fail(e);
     }
     for (int i = 0; i < 2; ++i) {
         e = hipStreamSynchronize(c->st[i]);
@@ -633,8 +743,10 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t st
 
 // Pinned packet pool: the kernel reads each packet's bytes over PCIe and (FILL)
 // stores the check field in place in host memory — no staging of the packets.
-// Pageable pool: the region is copied H2D, checksummed, and the results are
-// stored at TCP+16 on the host. Either way the per-packet arrays (offsets in,
+// A pageable pool is page-locked for the call and read the same way; one that
+// cannot be (or a small one) is copied H2D through pinned bounce buffers,
+// checksummed, and the results are stored at TCP+16 on the host. Either way
+// the per-packet arrays (offsets in,
 // results and status out) go through the context's pinned staging when the
 // caller's are pageable: a CPU memcpy and zero-copy kernel access instead of a
 // pageable hipMemcpy (a staged, synchronous copy) per array per batch.
@@ -664,7 +776,10 @@ int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t* c, void* h_pkts, size_t region_bytes,
     uint8_t* kst = zst ? zst : c->k_wstat;
     const bool fill = (mode & TCPCSUM_IPV4_VERIFY) == 0;
     hipError_t e;
-    if (uint8_t* zp = (uint8_t*)pinned_dev_ptr(h_pkts, region_bytes)) {
+    PinSet tp(st, nullptr);
+    uint8_t* zp = (uint8_t*)pinned_dev_ptr(h_pkts, region_bytes);
+    if (!zp && region_bytes >= kTempPinMin) zp = (uint8_t*)const_cast<void*>(tp.pin(h_pkts, region_bytes));
+    if (zp) {
         // zero-copy over PCIe: 16-lane groups, 512 B per round (more waves with
         // reads in flight) beat the HBM-tuned MTU shape — 1024 x 1500-B FILL
         // batch 49 vs 59 us on MI355X (tools/e2e.py --sweep)
@@ -676,6 +791,7 @@ int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t* c, void* h_pkts, size_t region_bytes,
         if (rc) return rc;
         e = hipStreamSynchronize(st);
         if (e != hipSuccess) return hip_fail(e);
+        tp.release();
     } else {
         const size_t mis = (uintptr_t)h_pkts & 15u;
         const size_t need = region_bytes + mis + 16u;
@@ -731,7 +847,9 @@ int tcpcsum_ipv4_batch_ptrs_host(tcpcsum_ctx_t* c, void* const* h_pkts, const ui
     int rc = ensure_pkt_staging(c, n, st);
     if (rc) return rc;
     // per-packet device addresses and bounds, straight into the pinned staging
-    // the kernel reads (no copy of packet bytes anywhere)
+    // the kernel reads (no copy of packet bytes anywhere); memory pinned by
+    // someone else is looked up afresh each batch (its owner may have freed it)
+    c->reg.forget_foreign();
     uint64_t foot = 0;
     uint32_t cap = 20;
     for (uint64_t i = 0; i < n; ++i) {

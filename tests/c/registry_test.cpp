@@ -173,12 +173,41 @@ static void two_registries(uint64_t seed) {
     CHECK(h.locks.empty());
 }
 
+// Memory pinned by someone else is freed between two batches (and its pages
+// reused as pageable memory): after forget_foreign() the registry never hands
+// out its old mapping, it locks the pages itself.
+static void stale_foreign(uint64_t seed) {
+    FakeHost h;
+    h.flat = false;   // a stale mapping would show up as a wrong device address
+    h.rng.seed(seed);
+    tcpcsum::HostRegistry<FakeHost> reg(h);
+    const uintptr_t base = 0x7d0000000000ull;
+    h.foreign.push_back({base, base + 8 * kHostPage, (intptr_t)(77ull << 24)});
+    uintptr_t dev = 0;
+    CHECK(reg.resolve(base + 100, 1500, &dev) == 0);
+    check_mapping(h, base + 100, 1500, dev);
+    CHECK(reg.owned_ranges() == 0);
+    h.foreign.clear();   // the owner frees it
+    reg.forget_foreign();
+    CHECK(reg.resolve(base + 100, 1500, &dev) == 0);
+    check_mapping(h, base + 100, 1500, dev);   // through our own lock now
+    CHECK(reg.owned_ranges() == 1);
+    // pages we locked are kept across forget_foreign()
+    const uint64_t calls = h.lock_calls;
+    reg.forget_foreign();
+    CHECK(reg.resolve(base + 200, 1000, &dev) == 0);
+    CHECK(h.lock_calls == calls);
+    reg.release(0, 0);
+    CHECK(h.locks.empty());
+}
+
 int main(int argc, char** argv) {
     const uint64_t seed = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : 1;
     for (uint64_t s = seed; s < seed + 4; ++s) {
         scenario(true, s);
         scenario(false, s);
         two_registries(s);
+        stale_foreign(s);
     }
     std::printf(fails ? "FAIL (%d)\n" : "OK\n", fails);
     return fails ? 1 : 0;

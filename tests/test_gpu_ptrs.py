@@ -237,11 +237,12 @@ def test_ipv4_ptrs_host_context_tuning(dev):
             b.unregister_host()
 
 
-@pytest.mark.parametrize("register", ["none", "whole", "half"])
+@pytest.mark.parametrize("register", ["none", "whole", "half", "tail"])
 def test_ipv4_region_host_registered_pool(dev, register):
-    """The region host path over a pageable pool: copied when pageable, read in place when the whole
-    region is registered with the context (tcpcsum_ctx_register_host, once), and copied again when
-    only part of it is — never a kernel on unlocked pages. Results identical in all three."""
+    """The region host path over a pageable pool: page-locked for the call when pageable, read in
+    place when the whole region is registered with the context (tcpcsum_ctx_register_host, once),
+    and locked for the call or copied when only its first half / its second half is — never a kernel
+    on unlocked pages, and the context's own registrations survive the call. Results identical."""
     import tcp_amd
     from tests.packets import build_batch
     rng = np.random.default_rng(21)
@@ -254,6 +255,9 @@ def test_ipv4_region_host_registered_pool(dev, register):
                 ctx.register_host(region.ctypes.data, region.nbytes)
             elif register == "half":
                 ctx.register_host(region.ctypes.data, region.nbytes // 2)
+            elif register == "tail":
+                ctx.register_host(region.ctypes.data + region.nbytes // 2, region.nbytes // 2)
+            held = ctx.registered()
             out, st = ctx.ipv4_batch(region, off, 32768, tcp_amd.IPV4_FILL)
             assert np.array_equal(st, want_st) and np.array_equal(out, want_out)
             assert np.array_equal(region, ref)
@@ -262,5 +266,9 @@ def test_ipv4_region_host_registered_pool(dev, register):
             # the uniform host path over the same (un/partly/fully registered) bytes, odd shapes
             u = ctx.batch_uniform(region, 1501, 1499, (region.nbytes - 1499) // 1501, 777)
             assert np.array_equal(u, oracle.batch_uniform(region, 1501, 1499, u.size, 777))
+            assert ctx.registered() == held   # per-call locks are gone, the context's are intact
+            # and the context's registrations still work
+            out2, st2 = ctx.ipv4_batch(region, off, 32768, tcp_amd.IPV4_VERIFY)
+            assert np.all(out2[st2 == tcp_amd.PKT_OK] == 0)
         finally:
             ctx.unregister_host()
