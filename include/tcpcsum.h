@@ -203,14 +203,17 @@ void tcpcsum_ctx_destroy(tcpcsum_ctx_t *ctx);
  * this context is affected; other contexts and the device calls are not. */
 int tcpcsum_ctx_set_tuning(tcpcsum_ctx_t *ctx, const tcpcsum_tuning_t *tune);
 
-/* Page-locked host memory for packet pools: copies from it are plain DMA
- * (pageable memory is staged by the runtime). NULL on failure. */
+/* Page-locked host memory for packet pools: the host calls read it in place
+ * over PCIe with no per-call locking. NULL on failure. */
 void *tcpcsum_host_alloc(size_t bytes);
 void tcpcsum_host_free(void *p);
 
 /* Uniform layout in host memory; h_out[i] as tcpcsum_batch_uniform_dev.
  * h_sum_start may be NULL (then sum_start is used for every segment).
- * Synchronous: returns when h_out is complete. */
+ * Page-locked input is read in place over PCIe; pageable input is page-locked
+ * for the call, chunk by chunk, and read the same way (or, when it cannot be
+ * locked, copied through the context's pinned bounce buffers). Synchronous:
+ * returns when h_out is complete. */
 int tcpcsum_batch_uniform_host(tcpcsum_ctx_t *ctx, const void *h_base, uint64_t stride,
                                uint32_t len, const uint32_t *h_sum_start, uint32_t sum_start,
                                uint16_t *h_out, uint64_t n);
@@ -219,8 +222,9 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t *ctx, const void *h_base, uint64_t 
  * within one host region of region_bytes). FILL patches check in place in
  * host memory. Synchronous. A region that one page-locked allocation covers
  * (tcpcsum_host_alloc, or a pool registered once with
- * tcpcsum_ctx_register_host) is read in place over PCIe; otherwise it is
- * copied to the device first. */
+ * tcpcsum_ctx_register_host) is read in place over PCIe; a pageable region of
+ * 64 KiB or more is page-locked for the call and read in place the same way;
+ * otherwise it is copied to the device through pinned bounce buffers. */
 int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t *ctx, void *h_pkts, size_t region_bytes,
                             const uint64_t *h_pkt_off, uint64_t n, uint32_t cap, int mode,
                             uint16_t *h_out, uint8_t *h_status);
