@@ -1697,7 +1697,8 @@ void launch_desc(const uint8_t* base, const tcpcsum_desc_t* d, uint64_t n, uint3
     if (sh < 0)
         sh = nch <= 4 ? 0 : nch <= 8 ? 1 : nch <= 16 ? 2 : nch <= 32 ? 3 : nch <= 96 ? 4 : nch <= 256 ? 5 : 6;
     if (sh == 7 || sh == 8) {
-        const dim3 grid(grid_for((n + 63) / 64, max_blocks));
+        // one 64-segment tile per wave by default (4M x 84-B packets: -4 %)
+        const dim3 grid(grid_for((n + 63) / 64, tu.max_blocks > 0 ? tu.max_blocks : 1 << 24));
         if (sh == 7) hipLaunchKernelGGL(k_desc_lb<4>, grid, dim3(256), 0, s, base, d, n, out);
         else hipLaunchKernelGGL(k_desc_lb<8>, grid, dim3(256), 0, s, base, d, n, out);
         return;
@@ -1739,7 +1740,7 @@ static void launch_ipv4_t(uint8_t* pkts, const uint64_t* off, const uint32_t* pl
 void launch_ipv4(uint8_t* pkts, const uint64_t* off, const uint32_t* plen, uint64_t n, uint32_t cap, uint64_t limit,
                  uint64_t footprint, int mode, uint16_t* out, uint8_t* status, uint16_t* ipout, hipStream_t s,
                  const Tuning& tu) {
-    const int max_blocks = tu.max_blocks > 0 ? tu.max_blocks : 8192;
+    int max_blocks = tu.max_blocks > 0 ? tu.max_blocks : 8192;
     const int unroll = tu.unroll ? tu.unroll : 1;
     const bool nt = (tu.flags & TCPCSUM_TUNE_WIRE_CACHED) == 0;
     const uint32_t amask = (tu.flags & TCPCSUM_TUNE_WIN16) ? 15u : 127u;
@@ -1764,15 +1765,30 @@ void launch_ipv4(uint8_t* pkts, const uint64_t* off, const uint32_t* plen, uint6
     // forced: 0 (8,1), 1 (32,3), 2 (64,4), 3 (16,2), 4 (16,6), 5 (8,12), 6 (8,2), 7 (8,4),
     // 8 / 9: balanced chunk space (k_ipv4_lb) with 4 / 8 loads per lane in flight
     int sh = tu.shape;
-    // auto: large batches of small or mixed packets (mean footprint <= 1 KiB,
-    // e.g. packed IMIX) take the balanced kernel; MTU slots, jumbo packets and
-    // small batches (a releaseSend batch of <= 1024 packets: latency, not
-    // throughput — a balanced wave walks 64 packets in turn) the lane-group
-    // kernels, one speculative round trip per packet
-    if (sh < 0 || sh > 9)
-        sh = (n >= 65536u && mean <= 1024u) ? 8 : (nch <= 8 || mean <= 112u) ? 0 : nch <= 96 ? 5 : 1;
+    // auto: large batches of small or mixed packets (mean footprint < 960 B,
+    // e.g. packed IMIX, 576-896-B slots) take the balanced kernel; MTU-size
+    // slots, jumbo packets and small batches (a releaseSend batch of <= 1024
+    // packets: latency, not throughput — a balanced wave walks 64 packets in
+    // turn) the lane-group kernels, one speculative round trip per packet. Large
+    // batches of 1-1.5 KiB packets take 4-chunk rounds (fewer registers, more
+    // waves: 1024-B slots 0.226 -> 0.173 ms VERIFY, 1536-B 0.250 -> 0.242 than
+    // one 12-chunk round; tools/wire_mtu_sweep.sh)
+    if (sh < 0 || sh > 9) {
+        if (n >= 65536u && mean < 960u) {
+            sh = 8;
+        } else if (nch <= 8 || mean <= 112u) {
+            sh = 0;
+        } else if (nch <= 96 && n >= 65536u) {
+            sh = 7;
+            if (tu.max_blocks <= 0) max_blocks = 16384;
+        } else {
+            sh = nch <= 96 ? 5 : 1;
+        }
+    }
     if (sh == 8 || sh == 9) {
-        const dim3 grid(grid_for((n + 63) / 64, max_blocks));
+        // one 64-packet tile per wave by default (4M packed 84-B packets 0.116 ->
+        // 0.112 ms against 8192 blocks; tools/lb_sweep.sh)
+        const dim3 grid(grid_for((n + 63) / 64, tu.max_blocks > 0 ? tu.max_blocks : 1 << 24));
         if (sh == 8 && plen)
             hipLaunchKernelGGL((k_ipv4_lb<4, true>), grid, dim3(256), 0, s, pkts, off, plen, n, cap, limit, mode, out,
                                status, ipout);

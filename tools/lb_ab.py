@@ -81,6 +81,9 @@ def main():
     sta = torch.empty(1 << 22, dtype=torch.uint8, device=dev)
     t7 = tcp_amd.Tuning(0, 0, 7, 0)
     t8 = tcp_amd.Tuning(0, 0, 8, 0)
+    # LB_HEAD_DESC / LB_HEAD_WIRE="max_blocks,unroll,shape,flags": the head build's launch (the old build keeps 7 / 8)
+    h7 = tcp_amd.Tuning(*map(int, os.environ["LB_HEAD_DESC"].split(","))) if "LB_HEAD_DESC" in os.environ else t7
+    h8 = tcp_amd.Tuning(*map(int, os.environ["LB_HEAD_WIRE"].split(","))) if "LB_HEAD_WIRE" in os.environ else t8
 
     for name, lens in (("desc_lb_1M_imix", rng.choice(np.array([64, 576, 1500], np.uint32), n,
                                                        p=[7 / 12, 4 / 12, 1 / 12])),
@@ -102,7 +105,7 @@ def main():
 
         def f_new():
             return new.tcpcsum_batch_desc_dev(data.data_ptr(), dd.data_ptr(), n, mx, out.data_ptr(), h,
-                                              ctypes.byref(t7))
+                                              ctypes.byref(h7))
         ab(name, f_old, f_new, out[:n], int(lens.sum()))
 
     # wire workloads, built on device by the fused builder (context.c:169-206 framing)
@@ -138,7 +141,7 @@ def main():
 
         def f_new():
             return new.tcpcsum_ipv4_batch_dev(reg.data_ptr(), R, offs.data_ptr(), m, 1536, 1, out.data_ptr(),
-                                              sta.data_ptr(), h, ctypes.byref(t8))
+                                              sta.data_ptr(), h, ctypes.byref(h8))
         ab(name, f_old, f_new, out[:m], nbytes)
         if only and only != name:
             continue

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Launch-shape sweep of the lane-group wire kernel (k_ipv4) on 1M IPv4/TCP
-packets of 1500 B in 1536-B slots, device-resident, VERIFY and FILL.
+packets of 1500 B in 1536-B slots (SLOT / PAYLOAD env: other sizes),
+device-resident, VERIFY and FILL; SHAPES / BLOCKS / UNROLLS env: the grid.
 
 Rounds are interleaved (every configuration once per round, median over
 rounds) so box-level drift affects all shapes alike. JSON lines.
@@ -19,16 +20,17 @@ def main():
 
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream()
-    n, slot = 1 << 20, 1536
-    payload = torch.empty(n * 1456, dtype=torch.uint8, device=dev)
-    tcp_amd.synth_fill(payload, 0, n * 1456)
+    n, slot = 1 << 20, int(os.environ.get("SLOT", "1536"))
+    pay = int(os.environ.get("PAYLOAD", str(slot - 80)))   # TCP payload bytes (packet = pay + 44)
+    payload = torch.empty(n * pay, dtype=torch.uint8, device=dev)
+    tcp_amd.synth_fill(payload, 0, n * pay)
     data = torch.empty(n * slot, dtype=torch.uint8, device=dev)
     segs = np.zeros(n, tcp_amd.TXSEG_DTYPE)
-    segs["payload_off"] = np.arange(n, dtype=np.uint64) * 1456
+    segs["payload_off"] = np.arange(n, dtype=np.uint64) * pay
     segs["out_off"] = np.arange(n, dtype=np.uint64) * slot
     segs["saddr_be"], segs["daddr_be"] = 0x0100007F, np.arange(n, dtype=np.uint32)
-    segs["sport"], segs["dport"], segs["len"], segs["flags"] = 4000, 45001, 1456, 1 | 16
-    tcp_amd.tx_build(payload, torch.from_numpy(segs.view(np.uint8)).to(dev), n, 1456, data, 0, None)
+    segs["sport"], segs["dport"], segs["len"], segs["flags"] = 4000, 45001, pay, 1 | 16
+    tcp_amd.tx_build(payload, torch.from_numpy(segs.view(np.uint8)).to(dev), n, pay, data, 0, None)
     offs = torch.from_numpy((np.arange(n, dtype=np.uint64) * slot).view(np.int64)).to(dev)
     out = torch.empty(n, dtype=torch.int16, device=dev)
     stat = torch.empty(n, dtype=torch.uint8, device=dev)
@@ -65,8 +67,9 @@ def main():
     for c, ts in sorted(res.items(), key=lambda kv: (kv[0][0], sorted(kv[1])[2])):
         m, sh, mb, un = c
         ms = sorted(ts)[len(ts) // 2]
-        print(json.dumps({"measure": "ipv4_shape_sweep_1Mx1500", "mode": m, "shape": sh, "max_blocks": mb,
-                          "unroll": un, "ms": round(ms, 4), "GB/s_tcp_bytes": round(n * 1480 / (ms * 1e-3) / 1e9, 1),
+        print(json.dumps({"measure": f"ipv4_shape_sweep_1Mx{pay + 44}_slots{slot}", "mode": m, "shape": sh,
+                          "max_blocks": mb, "unroll": un, "ms": round(ms, 4),
+                          "GB/s_tcp_bytes": round(n * (pay + 24) / (ms * 1e-3) / 1e9, 1),
                           "verify_ok": checked[c]}), flush=True)
 
 
