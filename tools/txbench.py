@@ -53,9 +53,12 @@ def main():
         return e0.elapsed_time(e1) / steps * 1e-3
 
     if "--sweep" in sys.argv:
-        for sh in (0, 1, 2, 3, 4):
-          for mb in (1024, 2048, 4096, 8192):
-            for un in (1, 2):
+        shapes = [int(x) for x in os.environ.get("TX_SHAPES", "0,1,2,3,4").split(",")]
+        blocks = [int(x) for x in os.environ.get("TX_BLOCKS", "1024,4096,8192,16384,32768").split(",")]
+        unrolls = [int(x) for x in os.environ.get("TX_UNROLLS", "1,2").split(",")]
+        for sh in shapes:
+          for mb in blocks:
+            for un in unrolls:
                 tcp_amd.set_tuning(mb, un, sh, 0)
                 tt = timeit(lambda: tcp_amd.tx_build(payload, dsegs, n, L, out, 0, chk), 20)
                 print(json.dumps({"sweep": "tx_build", "shape": sh, "max_blocks": mb, "unroll": un,
