@@ -1625,6 +1625,11 @@ UniformPlan plan_uniform(uintptr_t b, uint64_t stride, uint32_t len, uint64_t n,
     if (p.mode == M1) {
         if (!tu.unroll && p.shape != 9 && p.unroll > 4) p.unroll = 4;
         if (tu.max_blocks <= 0) p.max_blocks = 4096;
+    } else if (p.shape <= 5 && tu.max_blocks <= 0) {
+        // segments of up to 1.5 KiB, 4-B aligned: one tile per wave, no grid-stride
+        // loop (1M x 1500 B 0.2248 -> 0.2186 ms = 7.19 TB/s, 256 B -3 %, 576 B -7 %;
+        // 4-8 KiB segments keep their grids; profiles/r02_grid_sweep.jsonl)
+        p.max_blocks = 1 << 24;
     } else if (p.shape == 9 && tu.max_blocks <= 0 && (p.mode != M16 || len < 12288u)) {
         // one wave per segment: segments of one round (jumbo frames, 8-12 KiB)
         // and the dword-masked path want 4x the waves of the 64 KiB config's grid
