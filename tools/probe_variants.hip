@@ -8,6 +8,8 @@
 //   lane64  — each lane reads 64 contiguous bytes (4 x 16 B), C/4 such runs
 //   glds    — global_load_lds_dwordx4 into LDS (no VGPR destination), C per
 //             wave in flight, then ds_read_b128 and sum
+// "_tile" variants launch one tile per wave (no grid-stride loop), as the
+// shipped uniform kernel does for segments up to 1.5 KiB since round 2.
 // Prints one JSON line per variant: GB/s (median of 5 x 10 launches).
 //   hipcc -O3 --offload-arch=gfx950 -o tools/probe_variants tools/probe_variants.hip
 #include <hip/hip_runtime.h>
@@ -50,7 +52,7 @@ __global__ __launch_bounds__(256) void k_wave(const uint8_t* __restrict__ src, u
         acc += w;
     }
     for (int s = 32; s >= 1; s >>= 1) acc += __shfl_xor(acc, s, 64);
-    if ((threadIdx.x & 63) == 0) atomicAdd(reinterpret_cast<unsigned long long*>(out + blockIdx.x), (unsigned long long)acc);
+    if ((threadIdx.x & 63) == 0) atomicAdd(reinterpret_cast<unsigned long long*>(out + (blockIdx.x & 8191u)), (unsigned long long)acc);
 }
 
 template <int C>
@@ -72,7 +74,7 @@ __global__ __launch_bounds__(256) void k_lane64(const uint8_t* __restrict__ src,
         acc += w;
     }
     for (int s = 32; s >= 1; s >>= 1) acc += __shfl_xor(acc, s, 64);
-    if ((threadIdx.x & 63) == 0) atomicAdd(reinterpret_cast<unsigned long long*>(out + blockIdx.x), (unsigned long long)acc);
+    if ((threadIdx.x & 63) == 0) atomicAdd(reinterpret_cast<unsigned long long*>(out + (blockIdx.x & 8191u)), (unsigned long long)acc);
 }
 
 template <int C>
@@ -99,7 +101,7 @@ __global__ __launch_bounds__(256) void k_glds(const uint8_t* __restrict__ src, u
         acc += w;
     }
     for (int s = 32; s >= 1; s >>= 1) acc += __shfl_xor(acc, s, 64);
-    if ((threadIdx.x & 63) == 0) atomicAdd(reinterpret_cast<unsigned long long*>(out + blockIdx.x), (unsigned long long)acc);
+    if ((threadIdx.x & 63) == 0) atomicAdd(reinterpret_cast<unsigned long long*>(out + (blockIdx.x & 8191u)), (unsigned long long)acc);
 }
 
 typedef void (*kfn)(const uint8_t*, uint64_t, uint64_t*);
@@ -122,6 +124,10 @@ int main() {
         {"lane64_C4_b2048", k_lane64<4>, 2048},       {"glds_C8_b1024", k_glds<8>, 1024},
         {"glds_C16_b512", k_glds<16>, 512},           {"glds_C16_b1024", k_glds<16>, 1024},
         {"glds_C32_b512", k_glds<32>, 512},
+        // one tile per wave (no grid-stride loop): 2 GiB / (1 KiB x C) waves
+        {"wave_C4_nt_tile", k_wave<4, true>, 131072},  {"wave_C8_nt_tile", k_wave<8, true>, 65536},
+        {"wave_C16_nt_tile", k_wave<16, true>, 32768}, {"wave_C24_nt_tile", k_wave<24, true>, 21846},
+        {"glds_C8_tile", k_glds<8>, 65536},            {"glds_C16_tile", k_glds<16>, 32768},
     };
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
@@ -141,8 +147,9 @@ int main() {
                 ms.push_back(t / 10);
             }
             std::sort(ms.begin(), ms.end());
-            std::vector<uint64_t> h(v.blocks);
-            CK(hipMemcpy(h.data(), out, v.blocks * sizeof(uint64_t), hipMemcpyDeviceToHost));
+            const int slots = v.blocks < 8192 ? v.blocks : 8192;   // blocks fold onto 8192 partials
+            std::vector<uint64_t> h(slots);
+            CK(hipMemcpy(h.data(), out, slots * sizeof(uint64_t), hipMemcpyDeviceToHost));
             uint64_t s = 0;
             for (auto x : h) s += x;
             if (rep)

@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--shapes", default="-1")
     ap.add_argument("--flags", default="0", help="TCPCSUM_TUNE_* bits: 1 pipe on, 2 pipe off, 4 nt on, 8 nt off")
     ap.add_argument("--probe", action="store_true")
+    ap.add_argument("--rot", type=int, default=0, help="rotating input buffers (0: enough for >= 1 GiB in total)")
     args = ap.parse_args()
     import torch
     import tcp_amd
@@ -40,6 +41,8 @@ def main():
         per, L, _ = CONFIGS[args.config]
     nbytes = per * L
     rot = max(1, math.ceil((1 << 30) / nbytes)) if nbytes < (1 << 30) else 1
+    if args.rot:
+        rot = args.rot
     dev = torch.device("cuda:0")
     bufs, sss = [], []
     for r in range(rot):
