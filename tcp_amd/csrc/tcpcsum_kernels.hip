@@ -1619,12 +1619,13 @@ UniformPlan plan_uniform(uintptr_t b, uint64_t stride, uint32_t len, uint64_t n,
     p.max_blocks = tu.max_blocks > 0 ? tu.max_blocks : kShapeBlocks[p.shape];
     // Byte-granular batches (odd starts or lengths) spend ~3x the VALU per chunk
     // on byte masks and odd-byte sums: more, shallower waves hide it better —
-    // 4096 workgroups, at most 4 segments in flight per group (swept on MI355X at
+    // 16384 workgroups, at most 4 segments in flight per group (swept on MI355X at
     // 99, 577, 1499, 3001 and 8191 B: 6-25 % faster than the aligned shapes'
-    // defaults; profiles/r02_sweep_m1.jsonl)
+    // defaults with 4096 workgroups, profiles/r02_sweep_m1.jsonl; 16384 a further
+    // 1-5 %, profiles/r02_grid_m1.jsonl)
     if (p.mode == M1) {
         if (!tu.unroll && p.shape != 9 && p.unroll > 4) p.unroll = 4;
-        if (tu.max_blocks <= 0) p.max_blocks = 4096;
+        if (tu.max_blocks <= 0) p.max_blocks = 16384;
     } else if (p.shape <= 5 && tu.max_blocks <= 0) {
         // segments of up to 1.5 KiB, 4-B aligned: one tile per wave, no grid-stride
         // loop (1M x 1500 B 0.2248 -> 0.2186 ms = 7.19 TB/s, 256 B -3 %, 576 B -7 %;
