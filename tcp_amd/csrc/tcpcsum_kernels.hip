@@ -589,9 +589,13 @@ __device__ __forceinline__ void chunk_masked(u32x4 v, int32_t rel, int32_t len, 
 // hole (the same segment-relative offset for every segment, kNoHole: none) as
 // above. On return accW[lane] / accO[lane] hold the lane's segment sums W and O
 // (O only when want_odd, wave-uniform). acc: the wave's 2 x 64 u64 LDS slots.
-template <int C>
-__device__ __forceinline__ void lb_sums(const uint8_t* a, uint32_t len, uint32_t hole, bool want_odd,
-                                        uint64_t* accW, uint64_t* accO) {
+// A4: every segment of the tile 4-B aligned in start and length (packed
+// IPv4/TCP packets of 4-B multiples, IMIX) — dword-granular masks, no byte
+// masks. A template parameter, not a branch in the sweep: a branch there joins
+// after the masks, and the join waits for every load of the round.
+template <int C, bool A4>
+__device__ __forceinline__ void lb_sums_t(const uint8_t* a, uint32_t len, uint32_t hole, bool want_odd,
+                                          uint64_t* accW, uint64_t* accO) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t m = (uint32_t)((uintptr_t)a & 15u);
     const uint32_t nj = len ? (m + len + 15u) >> 4 : 0u;   // chunks of the aligned hull
@@ -601,9 +605,6 @@ __device__ __forceinline__ void lb_sums(const uint8_t* a, uint32_t len, uint32_t
     const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     const uint64_t a0 = (uint64_t)(uintptr_t)a - m;
     const uint32_t a_lo = (uint32_t)a0, a_hi = (uint32_t)(a0 >> 32);
-    // every segment of the tile 4-B aligned in start and length (packed IPv4/TCP
-    // packets of 4-B multiples, IMIX): dword-granular masks, no byte masks
-    const bool a4 = __ballot(len != 0 && (((uint32_t)(uintptr_t)a | len) & 3u) != 0) == 0 && hole == kNoHole;
     accW[lane] = 0;
     if (want_odd) accO[lane] = 0;
     uint32_t carry = 0;   // segment owning the next window's first chunk
@@ -642,15 +643,15 @@ __device__ __forceinline__ void lb_sums(const uint8_t* a, uint32_t len, uint32_t
             const uint32_t no = (mo + lo + 15u) >> 4;
             w[k] = 0;
             od[k] = 0;
-            if (a4) {   // wave-uniform
+            // lanes past the chunk space (g >= T) loaded the zero buffer: they sum 0
+            if constexpr (A4) {
                 const uint32_t rel = pc[k] * 16u - mo;   // dwords at rel + 4j: inside iff < lo (unsigned)
                 const u32x4 x = v[k];
-                const bool in = g < T;
-                uint32_t t = sad16(in && rel < lo ? x.x : 0u, 0u);
-                t = sad16(in && rel + 4u < lo ? x.y : 0u, t);
-                t = sad16(in && rel + 8u < lo ? x.z : 0u, t);
-                w[k] = sad16(in && rel + 12u < lo ? x.w : 0u, t);
-            } else if (g < T) {
+                uint32_t t = sad16(rel < lo ? x.x : 0u, 0u);
+                t = sad16(rel + 4u < lo ? x.y : 0u, t);
+                t = sad16(rel + 8u < lo ? x.z : 0u, t);
+                w[k] = sad16(rel + 12u < lo ? x.w : 0u, t);
+            } else {
                 chunk_masked(v[k], (int32_t)(pc[k] * 16u) - (int32_t)mo, (int32_t)lo, (int32_t)hole, want_odd, w[k],
                              od[k]);
             }
@@ -678,6 +679,16 @@ __device__ __forceinline__ void lb_sums(const uint8_t* a, uint32_t len, uint32_t
         }
     }
     __builtin_amdgcn_wave_barrier();
+}
+
+template <int C>
+__device__ __forceinline__ void lb_sums(const uint8_t* a, uint32_t len, uint32_t hole, bool want_odd,
+                                        uint64_t* accW, uint64_t* accO) {
+    const bool a4 = __ballot(len != 0 && (((uint32_t)(uintptr_t)a | len) & 3u) != 0) == 0 && hole == kNoHole;
+    if (a4)
+        lb_sums_t<C, true>(a, len, hole, want_odd, accW, accO);
+    else
+        lb_sums_t<C, false>(a, len, hole, want_odd, accW, accO);
 }
 
 // One segment summed by the whole wave (wave-uniform a, len): 64 chunks per
@@ -1633,10 +1644,12 @@ UniformPlan plan_uniform(uintptr_t b, uint64_t stride, uint32_t len, uint64_t n,
         p.max_blocks = 1 << 24;
     } else if (p.shape == 9 && tu.max_blocks <= 0 && (p.mode != M16 || len < 12288u)) {
         // one wave per segment: segments of one round (jumbo frames, 8-12 KiB)
-        // and the dword-masked path want 4x the waves of the 64 KiB config's grid
-        // (9000 B: 0.356 -> 0.234 ms, 12300 B: 0.323 -> 0.242; 16-64 KiB aligned
-        // keep 256; profiles/r02_sweep_long.jsonl)
-        p.max_blocks = 1024;
+        // and the dword-masked path want more waves than the 64 KiB config's
+        // grid — one segment per wave, no loop (9000 B: 0.356 -> 0.234 ms at 1024
+        // workgroups, 0.225 uncapped; 12300 B: 0.323 -> 0.242 -> 0.224; 20004 B
+        // 0.239 -> 0.228; 16-64 KiB aligned keep 256; profiles/r02_sweep_long.jsonl,
+        // r02_grid_long.jsonl)
+        p.max_blocks = 1 << 24;
     }
     p.pipe = tu.flags & TCPCSUM_TUNE_PIPE_ON ? true : tu.flags & TCPCSUM_TUNE_PIPE_OFF ? false : kShapePipe[p.shape];
     p.nt = tu.flags & TCPCSUM_TUNE_NT_ON ? true : tu.flags & TCPCSUM_TUNE_NT_OFF ? false : kShapeNt[p.shape];
