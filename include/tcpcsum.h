@@ -52,7 +52,7 @@ extern "C" {
 /* Launch-shape override, passed per call (NULL = the built-in shapes measured
  * on MI355X). Fields: max_blocks (0 = per-shape default, else
  * the resident grid), unroll in {0,1,2,4,8} (0 = default; segments in flight
- * per lane group), shape in {-1, 0..12} (-1 = auto; meaning per entry point,
+ * per lane group), shape in {-1, 0..13} (-1 = auto; meaning per entry point,
  * see TCPCSUM_TUNE_* below), flags = TCPCSUM_TUNE_* bits (0 = defaults).
  * Every entry point taking one returns TCPCSUM_EINVAL for an invalid value. */
 typedef struct tcpcsum_tuning {
@@ -281,12 +281,13 @@ int tcpcsum_stream_probe_dev(const void *d_src, uint64_t nbytes, uint64_t *d_par
  * 4,8,16,32,64,96,128,256,512 chunks, 9 = one wave per long segment,
  * 10 / 11 = one / two lanes per segment (up to 5 / 8 chunks), 12 = flat
  * tiles (contiguous 1 KiB per load instruction; 1-32 KiB segments, 4-B
- * aligned, stride >= len);
+ * aligned, stride >= len), 13 = split segments (a workgroup of four waves
+ * per segment, 4*unroll chunk loads per thread per round);
  * unroll: segments in flight per lane group; max_blocks: resident grid. */
 int tcpcsum_plan_uniform(uint64_t base, uint64_t stride, uint32_t len, uint64_t n,
                          const tcpcsum_tuning_t *tune, int *mode, int *shape, int *unroll, int *max_blocks);
 
-/* tcpcsum_tuning_t.shape, read per entry point: uniform 0..12 (a forced shape
+/* tcpcsum_tuning_t.shape, read per entry point: uniform 0..13 (a forced shape
  * that cannot cover the segments is ignored), ragged 0..6 = (G,C) (4,1) (8,1) (16,1) (32,1) (32,3) (64,4) (64,8)
  * and 7..8 = balanced chunk space (4 / 8 loads per lane in flight),
  * wire 0..7 = (8,1) (32,3) (64,4) (16,2) (16,6) (8,12) (8,2) (8,4) and 8..9 =

@@ -348,6 +348,62 @@ __global__ __launch_bounds__(256) void k_uniform_long(const uint8_t* __restrict_
     }
 }
 
+// Split segments (long segments, shape 13): one workgroup of four waves per
+// segment, one segment per workgroup (grid-stride only past 2^24 segments).
+// Round r, load k of thread t reads chunk r*256*C + k*256 + t, so each wave
+// instruction is one contiguous 1 KiB and the workgroup's instruction 4 KiB;
+// all C loads of a round are unconditional (zsel) and in flight together.
+// Lane partials are u32 per round (C*8 words of <= 0xffff), flushed to u64;
+// the four wave totals meet in LDS.
+template <int C, int MODE>
+__global__ __launch_bounds__(256) void k_uniform_split(const uint8_t* __restrict__ base, uint64_t stride,
+                                                       uint32_t len, uint32_t rounds,
+                                                       const uint32_t* __restrict__ ss, uint32_t ss_scalar,
+                                                       uint16_t* __restrict__ out, uint64_t n) {
+    __shared__ uint64_t part[4][2];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    for (uint64_t seg = blockIdx.x; seg < n; seg += gridDim.x) {
+        const uint8_t* p = base + seg * stride;
+        const uint32_t m = (uint32_t)((uintptr_t)p & 15u);
+        const uint8_t* a0 = p - m;
+        const uint32_t nch = (uint32_t)(((uint64_t)m + len + 15u) >> 4);
+        const bool odd = (MODE == M1) && ((uintptr_t)p & 1u);
+        uint64_t W = 0, O = 0;
+        for (uint32_t r = 0; r < rounds; ++r) {
+            u32x4 v[C];
+#pragma unroll
+            for (int k = 0; k < C; ++k) {
+                const uint32_t idx = r * (256u * C) + (uint32_t)(k * 256 + tid);
+                v[k] = ld16(zsel(idx < nch, a0 + (uint64_t)idx * 16u));
+            }
+            uint32_t w = 0, o = 0;
+#pragma unroll
+            for (int k = 0; k < C; ++k) {
+                const uint32_t idx = r * (256u * C) + (uint32_t)(k * 256 + tid);
+                if constexpr (MODE == M1)
+                    chunk_wo_bytes(v[k], (int64_t)idx * 16 - (int64_t)m, (int64_t)len, odd, w, o);
+                else
+                    w += chunk_w<MODE>(v[k], idx * 16u - m, len);
+            }
+            W += w;
+            O += o;
+        }
+        W = group_sum64<64>(W);
+        if constexpr (MODE == M1) O = group_sum64<64>(O);
+        if (lane == 0) {
+            part[wv][0] = W;
+            part[wv][1] = O;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            const uint64_t Wt = part[0][0] + part[1][0] + part[2][0] + part[3][0];
+            const uint64_t Ot = part[0][1] + part[1][1] + part[2][1] + part[3][1];
+            out[seg] = fold_ref(combine(ss ? ss[seg] : ss_scalar, Wt, Ot, odd));
+        }
+        __syncthreads();
+    }
+}
+
 // Flat tiles (segments of >= 1 KiB, 4-byte aligned): a wave takes SPT
 // consecutive segments and reads their byte span as one contiguous stream —
 // lane l loads chunk c0 + 64k + l, so every load instruction is one contiguous
@@ -1529,6 +1585,31 @@ void launch_long_t(const uint8_t* base, uint64_t stride, uint32_t len, const uin
                        stride, len, rounds, ss, ss0, out, n);
 }
 
+// split segments: unroll selects C = 4 * unroll chunk loads per thread per round,
+// halved while half of it still covers the segment in one round
+template <int MODE>
+void launch_split(const uint8_t* base, uint64_t stride, uint32_t len, const uint32_t* ss, uint32_t ss0,
+                  uint16_t* out, uint64_t n, hipStream_t s, int max_blocks, int unroll) {
+    uint64_t nch = 0;
+    for (uint64_t i = 0; i < 16 && i < n; ++i) {
+        const uint64_t c = ((((uintptr_t)base + i * stride) & 15u) + len + 15u) >> 4;
+        if (c > nch) nch = c;
+    }
+    if (nch == 0) return;
+    int C = unroll <= 1 ? 4 : unroll == 2 ? 8 : unroll == 4 ? 16 : 32;
+    while (C > 4 && 256u * (uint64_t)(C / 2) >= nch) C /= 2;
+    const uint32_t rounds = (uint32_t)((nch + 256u * C - 1) / (256u * C));
+    const unsigned g = (unsigned)(n < (uint64_t)max_blocks ? n : (uint64_t)max_blocks);
+#define TC_S(CC)                                                                                             \
+    hipLaunchKernelGGL((k_uniform_split<CC, MODE>), dim3(g), dim3(256), 0, s, base, stride, len, rounds, ss, \
+                       ss0, out, n)
+    if (C == 4) TC_S(4);
+    else if (C == 8) TC_S(8);
+    else if (C == 16) TC_S(16);
+    else TC_S(32);
+#undef TC_S
+}
+
 // flat tiles: unroll selects C (8 * unroll chunks per lane, 8 KiB * unroll per wave tile)
 inline void launch_flat(const uint8_t* base, uint64_t stride, uint32_t len, const uint32_t* ss, uint32_t ss0,
                         uint16_t* out, uint64_t n, hipStream_t s, int max_blocks, int unroll) {
@@ -1571,6 +1652,7 @@ void launch_uniform_mode(int shape, int unroll, const uint8_t* base, uint64_t st
         case 7: TC_U4(64, 4); break;   // <= 256
         case 8: TC_U4(64, 8); break;   // <= 512
         case 12: launch_flat(base, stride, len, ss, ss0, out, n, s, max_blocks, unroll); break;
+        case 13: launch_split<MODE>(base, stride, len, ss, ss0, out, n, s, max_blocks, unroll); break;
         case 10: TC_U4(1, 5); break;   // <= 5: one lane per segment, no cross-lane reduction
         case 11: TC_U4(2, 4); break;   // <= 8: two lanes per segment
         default:                       // one wave per segment, 8*unroll chunks per lane per round
@@ -1594,12 +1676,13 @@ namespace tcpcsum {
 // segments; shape 9 (one wave per segment) has no chunk limit.
 // Shape 12 is the flat tile (segments of 1 KiB .. 32 KiB, 4-byte aligned, stride
 // >= len), only used when forced or when kFlatAuto says so.
-static const uint32_t kShapeChunks[13] = {4, 8, 16, 32, 64, 96, 128, 256, 512, 0xffffffffu, 5, 8, 2048};
-static const int kShapeUnroll[13] = {4, 8, 8, 8, 8, 8, 8, 8, 4, 2, 2, 2, 2};
-static const int kShapeBlocks[13] = {4096, 512, 4096, 4096, 4096, 512, 4096, 1024, 2048, 256, 2048, 2048, 512};
-static const bool kShapePipe[13] = {false, false, false, false, false, false, false, false, false, false, false, false,
-                                    false};
-static const bool kShapeNt[13] = {true, true, true, true, true, true, true, true, true, true, true, true, true};
+// Shape 13 is the split segment (a workgroup of four waves per segment, no chunk limit).
+static const uint32_t kShapeChunks[14] = {4, 8, 16, 32, 64, 96, 128, 256, 512, 0xffffffffu, 5, 8, 2048, 0xffffffffu};
+static const int kShapeUnroll[14] = {4, 8, 8, 8, 8, 8, 8, 8, 4, 2, 2, 2, 2, 2};
+static const int kShapeBlocks[14] = {4096, 512, 4096, 4096, 4096, 512, 4096, 1024, 2048, 256, 2048, 2048, 512, 1 << 24};
+static const bool kShapePipe[14] = {false, false, false, false, false, false, false, false, false, false, false, false,
+                                    false, false};
+static const bool kShapeNt[14] = {true, true, true, true, true, true, true, true, true, true, true, true, true, true};
 
 static bool flat_ok(uintptr_t b, uint64_t stride, uint32_t len, int mode) {
     return mode != M1 && stride >= 1024 && stride >= len && stride + 46u <= 32u * 1024u && len >= 1024 &&
@@ -1620,10 +1703,16 @@ UniformPlan plan_uniform(uintptr_t b, uint64_t stride, uint32_t len, uint64_t n,
     p.shape = 9;
     for (int k = 0; k < 9; ++k)
         if (nch <= kShapeChunks[k]) { p.shape = k; break; }
+    // Segments past 8 KiB, dword or chunk aligned: four waves per segment
+    // (split) beat one wave per segment on MI355X — 9000 B -2 %, 12300 B -4 %,
+    // 20004 B -6 %, 24 KiB -7 %, 48-128 KiB -2..-7 %, the 64 KiB config even
+    // (profiles/r02_split_sweep.jsonl). Byte-granular segments keep one wave per
+    // segment: their byte masks make the split VALU-bound (12301 B +30 %).
+    if (p.shape == 9 && p.mode != M1) p.shape = 13;
     // a forced shape is honoured only if it covers the segment
     if (tu.shape == 12) {
         if (flat_ok(b, stride, len, p.mode)) p.shape = 12;
-    } else if (tu.shape >= 0 && tu.shape <= 11 && nch <= kShapeChunks[tu.shape]) {
+    } else if (tu.shape >= 0 && tu.shape <= 13 && nch <= kShapeChunks[tu.shape]) {
         p.shape = tu.shape;
     }
     p.unroll = tu.unroll ? tu.unroll : kShapeUnroll[p.shape];

@@ -18,6 +18,18 @@ def pytest_configure(config):
         subprocess.run(["make", "-C", REPO, "-j8"], check=True)
 
 
+@pytest.fixture(autouse=True)
+def _gpu_drained(request):
+    """After every GPU test, wait for the device and surface any HIP error there,
+    so an asynchronous fault is charged to the test whose work caused it."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    torch = sys.modules.get("torch")
+    if torch is not None and torch.cuda.is_available() and torch.cuda.is_initialized():
+        torch.cuda.synchronize()
+
+
 @pytest.fixture(scope="session")
 def golden():
     with open(os.path.join(REPO, "tests", "golden", "reference_vectors.json")) as f:

@@ -104,7 +104,7 @@ def test_argument_errors_need_no_device():
     ng = ctypes.c_int()
     assert L.tcpcsum_stream_probe_dev(1 << 20, 17, 1 << 20, ctypes.byref(ng), None, None) == api.EINVAL
     T = api.Tuning
-    for bad in (T(-1, 0, -1, 0), T(0, 3, -1, 0), T(0, 0, 13, 0), T(0, 0, -2, 0),
+    for bad in (T(-1, 0, -1, 0), T(0, 3, -1, 0), T(0, 0, 14, 0), T(0, 0, -2, 0),
                 T(0, 0, -1, 3),      # PIPE_ON | PIPE_OFF
                 T(0, 0, -1, 12),     # NT_ON | NT_OFF
                 T(0, 0, -1, 512)):
@@ -135,17 +135,19 @@ def test_no_device_is_reported_not_faked():
 @pytest.mark.parametrize("base,stride,length,n,expect", [
     (0, 1500, 1500, 1 << 20, (1, 5)),       # 1M x 1500: 4-B aligned, 95 chunks -> 32 lanes x 3
     (0, 64, 64, 1 << 20, (0, 0)),           # 1M x 64: 16-B aligned, 4 lanes
-    (0, 65536, 65536, 1 << 18, (0, 9)),     # 64 KiB: one wave per segment
+    (0, 65536, 65536, 1 << 18, (0, 13)),    # 64 KiB: four waves per segment (split)
+    (0, 9000, 9000, 1 << 17, (1, 13)),      # jumbo, dword aligned: split
     (3, 1501, 1501, 100, (2, 5)),           # byte-granular
     (0, 1500, 1500, 1, (1, 5)),
     (12, 64, 64, 8, (1, 1)),                # misaligned 64 B touches 5 chunks
     (0, 8192, 8192, 10, (0, 8)),
-    (0, 8208, 8193, 10, (2, 9)),            # 514 chunks -> long kernel
+    (0, 8208, 8193, 10, (2, 9)),            # 514 chunks, byte-granular -> one wave per segment
 ])
 def test_plan_uniform(base, stride, length, n, expect):
     mode, shape, unroll, blocks = api.plan_uniform(base, stride, length, n)
     assert (mode, shape) == expect
-    assert unroll in (1, 2, 4, 8) and 1 <= blocks <= 8192
+    # small tiles launch one tile per wave: the grid cap is then 1 << 24 (uncapped)
+    assert unroll in (1, 2, 4, 8) and (1 <= blocks <= 32768 or blocks == 1 << 24)
 
 
 def test_plan_respects_overrides():

@@ -20,6 +20,8 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
+from tests.devcopy import host, to_dev, u16  # noqa: E402  pinned copies only
+
 
 @pytest.fixture(scope="module")
 def dev():
@@ -76,16 +78,16 @@ def test_wire_fuzz_vs_oracle(dev, seed):
         cap = int(rng.choice([64, 1536, 9216, 65535]))
         ref = region.copy()
         want_out, want_st = oracle.ipv4_batch(ref, off, cap, mode)
-        doff = torch.from_numpy(off.view(np.int64)).to(dev)
+        doff = to_dev(off.view(np.int64), dev)
         for shape in (-1,) + tuple(range(10)):
-            dreg = torch.from_numpy(region.copy()).to(dev)
+            dreg = to_dev(region, dev)
             out = torch.empty(off.size, dtype=torch.int16, device=dev)
             st = torch.empty(off.size, dtype=torch.uint8, device=dev)
             tcp_amd.ipv4_batch(dreg, doff, off.size, cap, mode, out, st, tune=tcp_amd.make_tuning(0, 0, shape, 0))
             ctx = (seed, mode, shape, cap)
-            assert np.array_equal(st.cpu().numpy(), want_st), ctx
-            assert np.array_equal(out.cpu().numpy().view(np.uint16), want_out), ctx
-            assert np.array_equal(dreg.cpu().numpy(), ref), ctx
+            assert np.array_equal(host(st), want_st), ctx
+            assert np.array_equal(host(out).view(np.uint16), want_out), ctx
+            assert np.array_equal(host(dreg), ref), ctx
 
 
 @pytest.mark.parametrize("seed", range(4))
@@ -111,16 +113,16 @@ def test_wire_ptrs_fuzz_vs_oracle(dev, seed):
         if ok.any():
             o2, s2 = oracle.ipv4_batch(ref, off[ok], cap, mode)
             want_out[ok], want_st[ok] = o2, s2
-        dreg = torch.from_numpy(region.copy()).to(dev)
-        ptrs = torch.from_numpy((off + np.uint64(dreg.data_ptr())).view(np.int64)).to(dev)
-        dl = torch.from_numpy(lens.view(np.int32)).to(dev)
+        dreg = to_dev(region, dev)
+        ptrs = to_dev((off + np.uint64(dreg.data_ptr())).view(np.int64), dev)
+        dl = to_dev(lens.view(np.int32), dev)
         for shape in (-1, 0, 1, 3, 5, 8, 9):
             if not verify and shape != -1:
-                dreg.copy_(torch.from_numpy(region))
+                dreg.copy_(to_dev(region, dev))
             out = torch.empty(off.size, dtype=torch.int16, device=dev)
             st = torch.empty(off.size, dtype=torch.uint8, device=dev)
             tcp_amd.ipv4_batch_ptrs(ptrs, dl, off.size, cap, mode, out, st, tune=tcp_amd.make_tuning(0, 0, shape, 0))
             ctx = (seed, mode, shape, cap)
-            assert np.array_equal(st.cpu().numpy(), want_st), ctx
-            assert np.array_equal(out.cpu().numpy().view(np.uint16), want_out), ctx
-            assert np.array_equal(dreg.cpu().numpy(), ref), ctx
+            assert np.array_equal(host(st), want_st), ctx
+            assert np.array_equal(host(out).view(np.uint16), want_out), ctx
+            assert np.array_equal(host(dreg), ref), ctx

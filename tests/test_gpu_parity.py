@@ -15,6 +15,8 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
+from tests.devcopy import host, to_dev, u16  # noqa: E402  pinned copies only
+
 
 @pytest.fixture(scope="module")
 def dev():
@@ -24,14 +26,6 @@ def dev():
     rc, arch = tcp_amd.device_check()
     assert rc == 0, f"tcpcsum_device_check -> {rc} ({arch}); the HIP path must run on gfx950"
     return torch.device("cuda:0")
-
-
-def to_dev(a: np.ndarray, dev):
-    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
-
-
-def u16(t) -> np.ndarray:
-    return t.cpu().numpy().view(np.uint16)
 
 
 def test_native_library_is_loaded(dev):
@@ -101,7 +95,7 @@ def test_forced_shapes(dev):
     host = rng.integers(0, 256, 1 << 21, dtype=np.uint8)
     d = to_dev(host, dev)
     try:
-        for shape in range(13):
+        for shape in range(14):
             for unroll, flags in ((1, 0), (8, 0), (2, 1 | 8), (8, 1 | 4), (4, 2 | 8), (8, 16), (1, 16 | 8)):
                 tcp_amd.set_tuning(0, unroll, shape, flags)
                 for length, off in ((1500, 0), (1499, 1), (64, 4), (3000, 2), (64, 0), (60, 3), (100, 0),
@@ -112,6 +106,34 @@ def test_forced_shapes(dev):
                     assert np.array_equal(got, want), (shape, unroll, flags, length, off)
     finally:
         tcp_amd.set_tuning(0, 0, -1, 0)
+
+
+def test_split_segments_round_edges(dev):
+    """Shape 13 (four waves per segment): lengths at the edges of its rounds (256*C chunks per
+    round, C = 4..32), every start alignment mod 16, a capped grid (grid-stride over segments)."""
+    import tcp_amd
+    rng = np.random.default_rng(23)
+    host = rng.integers(0, 256, 6 << 20, dtype=np.uint8)
+    d = to_dev(host, dev)
+    ss = rng.integers(0, 2**32, 4096, dtype=np.uint32)
+    dss = to_dev(ss.view(np.int32), dev)
+    try:
+        for unroll in (1, 2, 4, 8):
+            for max_blocks in (0, 3):
+                tcp_amd.set_tuning(max_blocks, unroll, 13, 0)
+                for length in (8204, 16384, 16380, 16400, 32768, 32772, 65536, 131072 + 4, 262144):
+                    for off in (0, 4, 12):
+                        n = min(4096, ((6 << 20) - 16) // (length + 16))
+                        stride = length + 16
+                        got = u16(tcp_amd.batch_uniform(d, stride, length, n, dss[:n], offset=off))
+                        want = oracle.batch_uniform(host, stride, length, n, ss[:n], offset=off)
+                        assert np.array_equal(got, want), (unroll, max_blocks, length, off)
+    finally:
+        tcp_amd.set_tuning(0, 0, -1, 0)
+    # the default plan takes the split for aligned long segments and matches too
+    assert tcp_amd.api.plan_uniform(0, 65536, 65536, 64)[1] == 13
+    got = u16(tcp_amd.batch_uniform(d, 65536, 65536, 64, 7))
+    assert np.array_equal(got, oracle.batch_uniform(host, 65536, 65536, 64, 7))
 
 
 def test_two_fold_semantics_above_4g(dev):
@@ -182,13 +204,13 @@ def test_ipv4_fill_and_verify(dev, odd):
     out = torch.empty(off.size, dtype=torch.int16, device=dev)
     st = torch.empty(off.size, dtype=torch.uint8, device=dev)
     tcp_amd.ipv4_batch(dreg, doff, off.size, 32768, tcp_amd.IPV4_FILL, out, st)
-    assert np.array_equal(st.cpu().numpy(), want_st)
+    assert np.array_equal(host(st), want_st)
     assert np.array_equal(u16(out), want_out)
-    assert np.array_equal(dreg.cpu().numpy(), ref_region)     # checks patched in place, nothing else touched
+    assert np.array_equal(host(dreg), ref_region)     # checks patched in place, nothing else touched
     # rx side: every filled segment verifies to zero (loop.c:314-399 has no verify; new behaviour)
     tcp_amd.ipv4_batch(dreg, doff, off.size, 32768, tcp_amd.IPV4_VERIFY, out, st)
     v = u16(out)
-    ok = st.cpu().numpy() == tcp_amd.PKT_OK
+    ok = host(st) == tcp_amd.PKT_OK
     assert np.all(v[ok] == 0)
     want_v, _ = oracle.ipv4_batch(ref_region.copy(), off, 32768, tcp_amd.IPV4_VERIFY)
     assert np.array_equal(v, want_v)
@@ -216,7 +238,7 @@ def test_baseline_configs_match_reference_digests(dev, golden, name):
     assert oracle.digest(out) == (g["fnv1a64"], g["sum"], g["xor"])
     assert [f"{v:04x}" for v in out[:4]] == g["first4"] and f"{out[-1]:04x}" == g["last"]
     # the device generator equals the oracle's generator
-    assert np.array_equal(data[:4096].cpu().numpy(), oracle.gen_stream(g["seg0"] * L, 4096))
+    assert np.array_equal(host(data[:4096]), oracle.gen_stream(g["seg0"] * L, 4096))
     del data
 
 
@@ -247,7 +269,7 @@ def test_synth_fill_unaligned(dev):
     for off, nb, dst in [(3, 100, 1), (8, 64, 0), (13, 4000, 7)]:
         buf.zero_()
         tcp_amd.synth_fill(buf, off, nb, dst_offset=dst)
-        h = buf.cpu().numpy()
+        h = host(buf)
         assert np.array_equal(h[dst:dst + nb], oracle.gen_stream(off, nb))
         assert not h[:dst].any() and not h[dst + nb:].any()
 
@@ -343,7 +365,7 @@ def test_ipv4_iphdr_mode(dev, memory):
         out = torch.empty(off.size, dtype=torch.int16, device=dev)
         st = torch.empty(off.size, dtype=torch.uint8, device=dev)
         tcp_amd.ipv4_batch(dreg, doff, off.size, 32768, mode, out, st)
-        got_out, got_st, got_reg = u16(out), st.cpu().numpy(), dreg.cpu().numpy()
+        got_out, got_st, got_reg = u16(out), host(st), host(dreg)
     else:
         buf = region if memory == "pageable" else tcp_amd.pinned_empty(region.size)
         buf[:] = region
@@ -362,7 +384,7 @@ def test_ipv4_iphdr_mode(dev, memory):
     st = torch.empty(off.size, dtype=torch.uint8, device=dev)
     tcp_amd.ipv4_batch(dbad, to_dev(off.view(np.int64), dev), off.size, 32768,
                        tcp_amd.IPV4_VERIFY | tcp_amd.IPV4_IPHDR, out, st)
-    assert np.array_equal(st.cpu().numpy(), want_vs) and np.array_equal(u16(out), want_v)
+    assert np.array_equal(host(st), want_vs) and np.array_equal(u16(out), want_v)
     assert want_vs[okidx[0]] == tcp_amd.PKT_IPHDR_BAD
 
 
@@ -395,7 +417,7 @@ def test_tx_build_vs_oracle(dev, layout):
         dseg = to_dev(segs.view(np.uint8), dev)
         chk = torch.empty(n, dtype=torch.int16, device=dev)
         tcp_amd.tx_build(to_dev(payload, dev), dseg, n, max_len, dout, mode, chk)
-        got = dout.cpu().numpy()
+        got = host(dout)
         assert np.array_equal(u16(chk), want_c), layout
         if not np.array_equal(got, want):
             bad = np.flatnonzero(got != want)
@@ -410,7 +432,7 @@ def test_tx_build_vs_oracle(dev, layout):
             tcp_amd.set_tuning(0, unroll, shape, fl)   # 128: non-temporal payload stores
             dout = to_dev(garbage, dev)
             tcp_amd.tx_build(dpay, dseg, n, hint, dout, 0, None)
-            assert np.array_equal(dout.cpu().numpy(), want), (shape, unroll, hint, fl)
+            assert np.array_equal(host(dout), want), (shape, unroll, hint, fl)
     finally:
         tcp_amd.set_tuning(0, 0, -1, 0)
 
@@ -440,7 +462,7 @@ def test_tx_build_length_limits(dev):
         chk = torch.empty(len(lens), dtype=torch.int16, device=dev)
         tcp_amd.tx_build(to_dev(payload, dev), to_dev(segs.view(np.uint8), dev), len(lens), 65535, dout, mode, chk)
         assert np.array_equal(u16(chk), want_c)
-        assert np.array_equal(dout.cpu().numpy(), want)
+        assert np.array_equal(host(dout), want)
         assert want_c[1] == 0 and want_c[2] == 0
 
 
@@ -455,7 +477,7 @@ def test_ipv4_verify_flags_checksum_partial(dev):
     st = torch.empty(off.size, dtype=torch.uint8, device=dev)
     tcp_amd.ipv4_batch(to_dev(region, dev), to_dev(off.view(np.int64), dev), off.size, 32768,
                        tcp_amd.IPV4_VERIFY, out, st)
-    assert np.array_equal(u16(out), want_out) and np.array_equal(st.cpu().numpy(), want_st)
+    assert np.array_equal(u16(out), want_out) and np.array_equal(host(st), want_st)
     assert (want_st == tcp_amd.api.PKT_CSUM_PARTIAL).sum() > 300
 
 
@@ -515,7 +537,7 @@ def test_ipv4_region_bounds(dev, shape):
         tcp_amd.ipv4_batch(dreg, to_dev(off.view(np.int64), dev), off.size, 32768, tcp_amd.IPV4_FILL, out, st)
     finally:
         tcp_amd.set_tuning(0, 0, -1, 0)
-    assert np.array_equal(st.cpu().numpy(), want_st)
+    assert np.array_equal(host(st), want_st)
     assert np.array_equal(u16(out)[:-3], want_out[:-3])
 
 
@@ -540,9 +562,9 @@ def test_ipv4_forced_shapes(dev, shape):
                     tcp_amd.ipv4_batch(dreg, to_dev(off.view(np.int64), dev), off.size, 32768, mode, out, st)
                 finally:
                     tcp_amd.set_tuning(0, 0, -1, 0)
-                assert np.array_equal(st.cpu().numpy(), want_st), (mode, un, mb, fl)
+                assert np.array_equal(host(st), want_st), (mode, un, mb, fl)
                 assert np.array_equal(u16(out), want_out), (mode, un, mb, fl)
-                assert np.array_equal(dreg.cpu().numpy(), ref), (mode, un, mb, fl)
+                assert np.array_equal(host(dreg), ref), (mode, un, mb, fl)
         region = ref   # VERIFY runs over the filled packets
 
 
@@ -623,9 +645,9 @@ def test_ipv4_balanced_dword_tiles(dev, shape):
         st = torch.empty(off.size, dtype=torch.uint8, device=dev)
         tcp_amd.ipv4_batch(dreg, to_dev(off.view(np.int64), dev), off.size, 1536, mode, out, st,
                            tune=tcp_amd.make_tuning(0, 0, shape, 0))
-        assert np.array_equal(st.cpu().numpy(), want_st), mode
+        assert np.array_equal(host(st), want_st), mode
         assert np.array_equal(u16(out), want_out), mode
-        assert np.array_equal(dreg.cpu().numpy(), ref), mode
+        assert np.array_equal(host(dreg), ref), mode
         region = ref
 
 
@@ -656,9 +678,9 @@ def test_ipv4_span_hint_mispredicted(dev, shape):
                 tcp_amd.ipv4_batch(dreg, to_dev(offs.view(np.int64), dev), offs.size, 32768, mode, out, st)
             finally:
                 tcp_amd.set_tuning(0, 0, -1, 0)
-            assert np.array_equal(st.cpu().numpy(), want_st), name
+            assert np.array_equal(host(st), want_st), name
             assert np.array_equal(u16(out), want_out), name
-            assert np.array_equal(dreg.cpu().numpy(), ref), name
+            assert np.array_equal(host(dreg), ref), name
             reg = ref
 
 
@@ -700,9 +722,9 @@ def test_ipv4_window_and_store_variants(dev, shape, flags, layout):
                                1536 if layout not in ("odd", "jumbo") else 32768, mode, out, st)
         finally:
             tcp_amd.set_tuning(0, 0, -1, 0)
-        assert np.array_equal(st.cpu().numpy(), want_st), mode
+        assert np.array_equal(host(st), want_st), mode
         assert np.array_equal(u16(out), want_out), mode
-        assert np.array_equal(dreg.cpu().numpy(), ref), mode
+        assert np.array_equal(host(dreg), ref), mode
         region = ref   # the VERIFY pass runs over filled packets
 
 

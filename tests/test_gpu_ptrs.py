@@ -16,6 +16,8 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
+from tests.devcopy import host, to_dev, u16  # noqa: E402  pinned copies only
+
 
 @pytest.fixture(scope="module")
 def dev():
@@ -25,14 +27,6 @@ def dev():
     rc, arch = tcp_amd.device_check()
     assert rc == 0, f"tcpcsum_device_check -> {rc} ({arch}); the HIP path must run on gfx950"
     return torch.device("cuda:0")
-
-
-def to_dev(a: np.ndarray, dev):
-    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
-
-
-def u16(t) -> np.ndarray:
-    return t.cpu().numpy().view(np.uint16)
 
 
 def tot_len(buf: np.ndarray, o: int) -> int:
@@ -78,15 +72,15 @@ def test_ipv4_ptrs_dev_vs_oracle(dev, shape):
     st = torch.empty(n, dtype=torch.uint8, device=dev)
     tcp_amd.ipv4_batch_ptrs(ptrs, dl, n, 65535, tcp_amd.IPV4_FILL, out, st,
                             tune=tcp_amd.make_tuning(0, 0, shape, 0))
-    assert np.array_equal(st.cpu().numpy(), want_st)
+    assert np.array_equal(host(st), want_st)
     assert np.array_equal(u16(out), want_out)
-    assert np.array_equal(dreg.cpu().numpy(), ref)
+    assert np.array_equal(host(dreg), ref)
     # verify round trip: every filled packet verifies to 0
     tcp_amd.ipv4_batch_ptrs(ptrs, dl, n, 65535, tcp_amd.IPV4_VERIFY, out, st,
                             tune=tcp_amd.make_tuning(0, 0, shape, 0))
     want_v, want_vs = expected(ref.copy(), off, lens, tcp_amd.IPV4_VERIFY)
     assert np.array_equal(u16(out), want_v)
-    assert np.array_equal(st.cpu().numpy(), want_vs)
+    assert np.array_equal(host(st), want_vs)
     assert np.all(want_v[want_vs == tcp_amd.PKT_OK] == 0)
 
 
@@ -115,12 +109,12 @@ def test_ipv4_ptrs_dev_iphdr_and_tail(dev):
     out = torch.empty(off.size, dtype=torch.int16, device=dev)
     st = torch.empty(off.size, dtype=torch.uint8, device=dev)
     tcp_amd.ipv4_batch_ptrs(ptrs, to_dev(lens.view(np.int32), dev), off.size, 65535, mode, out, st)
-    assert np.array_equal(st.cpu().numpy(), want_st)
+    assert np.array_equal(host(st), want_st)
     assert np.array_equal(u16(out), want_out)
-    assert np.array_equal(dreg.cpu().numpy(), ref)
+    assert np.array_equal(host(dreg), ref)
     tcp_amd.ipv4_batch_ptrs(ptrs, to_dev(lens.view(np.int32), dev), off.size, 65535,
                             tcp_amd.IPV4_VERIFY | tcp_amd.IPV4_IPHDR, out, st)
-    assert np.all(u16(out) == 0) and np.all(st.cpu().numpy() == tcp_amd.PKT_OK)
+    assert np.all(u16(out) == 0) and np.all(host(st) == tcp_amd.PKT_OK)
 
 
 def _loop_pool(rng, n, slot=32768, payload=None):
