@@ -1708,7 +1708,11 @@ UniformPlan plan_uniform(uintptr_t b, uint64_t stride, uint32_t len, uint64_t n,
     // 20004 B -6 %, 24 KiB -7 %, 48-128 KiB -2..-7 %, the 64 KiB config even
     // (profiles/r02_split_sweep.jsonl). Byte-granular segments keep one wave per
     // segment: their byte masks make the split VALU-bound (12301 B +30 %).
-    if (p.shape == 9 && p.mode != M1) p.shape = 13;
+    // Multi-GiB batches of 64 KiB+ chunk-aligned segments keep the resident
+    // one-wave-per-segment grid: 256K x 64 KiB 2.392-2.398 vs 2.405-2.408 ms
+    // split, three same-process runs (profiles/r02_k64_check.jsonl).
+    const bool huge = p.mode == M16 && len >= 65536u && (double)n * len >= 4.0 * (1u << 30);
+    if (p.shape == 9 && p.mode != M1 && !huge) p.shape = 13;
     // a forced shape is honoured only if it covers the segment
     if (tu.shape == 12) {
         if (flat_ok(b, stride, len, p.mode)) p.shape = 12;

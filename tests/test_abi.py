@@ -135,7 +135,8 @@ def test_no_device_is_reported_not_faked():
 @pytest.mark.parametrize("base,stride,length,n,expect", [
     (0, 1500, 1500, 1 << 20, (1, 5)),       # 1M x 1500: 4-B aligned, 95 chunks -> 32 lanes x 3
     (0, 64, 64, 1 << 20, (0, 0)),           # 1M x 64: 16-B aligned, 4 lanes
-    (0, 65536, 65536, 1 << 18, (0, 13)),    # 64 KiB: four waves per segment (split)
+    (0, 65536, 65536, 1 << 18, (0, 9)),     # 16 GiB of 64 KiB: resident one-wave-per-segment grid
+    (0, 65536, 65536, 1 << 14, (0, 13)),    # 1 GiB of 64 KiB: four waves per segment (split)
     (0, 9000, 9000, 1 << 17, (1, 13)),      # jumbo, dword aligned: split
     (3, 1501, 1501, 100, (2, 5)),           # byte-granular
     (0, 1500, 1500, 1, (1, 5)),
