@@ -409,7 +409,10 @@ def main(argv=None) -> int:
     extra = {}
     if world == 1 and not args.no_other_configs:
         tcp_amd.set_tuning(0, 0, -1, 0)   # built-in launch shapes for the other configs
-        for cfg in sorted(CONFIGS):
+        # largest batch first: a 16 GiB batch allocated after smaller batches were freed runs
+        # 2.43-2.47 ms per launch, 2.40 on memory no earlier batch used (tools/order_check.py,
+        # profiles/r02_order_check.jsonl) — a property of the allocation, not of the kernel
+        for cfg in sorted(CONFIGS, key=lambda c: -CONFIGS[c][0] * CONFIGS[c][1]):
             if cfg == args.config:
                 continue
             steps = max(10, min(args.steps, 200 if CONFIGS[cfg][1] < 4096 else 40))
