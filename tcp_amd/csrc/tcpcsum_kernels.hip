@@ -1551,10 +1551,15 @@ using namespace tcpcsum;
 
 namespace {
 
+// HIP bounds a launch at gridDim.x * blockDim.x < 2^32 threads: with 256-thread
+// workgroups at most 2^24 - 1 of them (the kernels grid-stride past that).
+constexpr uint64_t kMaxGrid = (1u << 24) - 1u;
+
 inline unsigned grid_for(uint64_t waves_needed, int max_blocks) {
     uint64_t blocks = (waves_needed + 3) / 4;
     if (blocks < 1) blocks = 1;
     if (blocks > (uint64_t)max_blocks) blocks = (uint64_t)max_blocks;
+    if (blocks > kMaxGrid) blocks = kMaxGrid;
     return (unsigned)blocks;
 }
 
@@ -1599,7 +1604,9 @@ void launch_split(const uint8_t* base, uint64_t stride, uint32_t len, const uint
     int C = unroll <= 1 ? 4 : unroll == 2 ? 8 : unroll == 4 ? 16 : 32;
     while (C > 4 && 256u * (uint64_t)(C / 2) >= nch) C /= 2;
     const uint32_t rounds = (uint32_t)((nch + 256u * C - 1) / (256u * C));
-    const unsigned g = (unsigned)(n < (uint64_t)max_blocks ? n : (uint64_t)max_blocks);
+    uint64_t gb = n < (uint64_t)max_blocks ? n : (uint64_t)max_blocks;
+    if (gb > kMaxGrid) gb = kMaxGrid;
+    const unsigned g = (unsigned)gb;
 #define TC_S(CC)                                                                                             \
     hipLaunchKernelGGL((k_uniform_split<CC, MODE>), dim3(g), dim3(256), 0, s, base, stride, len, rounds, ss, \
                        ss0, out, n)
