@@ -1895,13 +1895,22 @@ void launch_ipv4(uint8_t* pkts, const uint64_t* off, const uint32_t* plen, uint6
     // batches of 1-1.5 KiB packets take 4-chunk rounds (fewer registers, more
     // waves: 1024-B slots 0.226 -> 0.173 ms VERIFY, 1536-B 0.250 -> 0.242 than
     // one 12-chunk round; tools/wire_mtu_sweep.sh)
+    // Large batches of 1.5-5 KiB packets (the cap, or the mean footprint when
+    // smaller, sizes them) keep 4- or 6-chunk rounds: 2 KiB slots VERIFY 0.549 ->
+    // 0.314 ms and FILL 0.578 -> 0.402 against one 96-chunk round per lane group
+    // (32,3); 3 KiB -19 % / -11 %, 4.5 KiB -7 % / -7 % with (16,6); 9 KiB jumbo
+    // slots alike across shapes and keep (32,3) (tools/wire_big_sweep.sh,
+    // profiles/r02_wire_big_sweep.jsonl)
+    const uint64_t nsz = mean && ((mean + 15u) >> 4) < nch ? (mean + 15u) >> 4 : nch;
     if (sh < 0 || sh > 9) {
         if (n >= 65536u && mean < 960u) {
             sh = 8;
         } else if (nch <= 8 || mean <= 112u) {
             sh = 0;
-        } else if (nch <= 96 && n >= 65536u) {
+        } else if (nsz <= 192 && n >= 65536u) {
             sh = 7;
+        } else if (nsz <= 320 && n >= 65536u) {
+            sh = 4;
         } else {
             sh = nch <= 96 ? 5 : 1;
         }
