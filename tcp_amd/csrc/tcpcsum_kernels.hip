@@ -777,14 +777,17 @@ __device__ __forceinline__ void wave_seg_sums(const uint8_t* a, uint32_t len, bo
 template <int C>
 __global__ __launch_bounds__(256) void k_desc_lb(const uint8_t* __restrict__ base,
                                                  const tcpcsum_desc_t* __restrict__ desc, uint64_t n,
-                                                 uint16_t* __restrict__ out) {
+                                                 uint16_t* __restrict__ out, uint32_t spw) {
+    // spw: segments per wave tile (1..64; lanes >= spw hold no segment) — fewer
+    // for long segments, so a batch of them still spreads over enough waves
     __shared__ uint64_t acc[4][2][64];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
-    const uint64_t ntiles = (n + 63) / 64;
+    const uint64_t ntiles = (n + spw - 1) / spw;
     for (uint64_t t = (uint64_t)blockIdx.x * 4u + wv; t < ntiles; t += nwaves) {
-        const uint64_t seg = t * 64 + lane;
-        const u32x4 d = ldg<u32x4>(zsel(seg < n, reinterpret_cast<const uint8_t*>(desc + seg)));
+        const uint64_t seg = t * spw + (uint64_t)lane;
+        const bool mine = (uint32_t)lane < spw && seg < n;
+        const u32x4 d = ldg<u32x4>(zsel(mine, reinterpret_cast<const uint8_t*>(desc + seg)));
         const uint8_t* p = base + ((uint64_t)d.x | ((uint64_t)d.y << 32));
         const uint32_t len = d.z;   // 0 past n
         const bool odd = ((uintptr_t)p & 1u) != 0;
@@ -803,7 +806,7 @@ __global__ __launch_bounds__(256) void k_desc_lb(const uint8_t* __restrict__ bas
         lb_sums<C>(p, big ? 0u : len, kNoHole, any_odd, acc[wv][0], acc[wv][1]);
         const uint64_t W = big ? bw : acc[wv][0][lane];
         const uint64_t O = !any_odd ? 0 : big ? bo : acc[wv][1][lane];
-        if (seg < n) out[seg] = fold_ref(combine((uint64_t)d.w, W, O, odd));
+        if (mine) out[seg] = fold_ref(combine((uint64_t)d.w, W, O, odd));
     }
 }
 
@@ -1816,10 +1819,17 @@ void launch_desc(const uint8_t* base, const tcpcsum_desc_t* d, uint64_t n, uint3
     if (sh < 0)
         sh = nch <= 4 ? 0 : nch <= 8 ? 1 : nch <= 16 ? 2 : nch <= 32 ? 3 : nch <= 96 ? 4 : nch <= 256 ? 5 : 6;
     if (sh == 7 || sh == 8) {
-        // one 64-segment tile per wave by default (4M x 84-B packets: -4 %)
-        const dim3 grid(grid_for((n + 63) / 64, tu.max_blocks > 0 ? tu.max_blocks : 1 << 24));
-        if (sh == 7) hipLaunchKernelGGL(k_desc_lb<4>, grid, dim3(256), 0, s, base, d, n, out);
-        else hipLaunchKernelGGL(k_desc_lb<8>, grid, dim3(256), 0, s, base, d, n, out);
+        // Segments per wave tile: 64, or for long segments as many as make about
+        // 8192 chunks (128 KiB) of work per wave at max_len — a tile of 64 long
+        // segments leaves too few waves: 64K x 64 KiB 1.385 ms with 64 per tile
+        // against 0.635 for lane groups (tools/desc_sweep.py,
+        // profiles/r02_desc_sweep.jsonl)
+        uint32_t spw = 64;
+        while (spw > 1 && (uint64_t)spw * nch > 8192u) spw >>= 1;
+        // one tile per wave by default (4M x 84-B packets: -4 %)
+        const dim3 grid(grid_for((n + spw - 1) / spw, tu.max_blocks > 0 ? tu.max_blocks : 1 << 24));
+        if (sh == 7) hipLaunchKernelGGL(k_desc_lb<4>, grid, dim3(256), 0, s, base, d, n, out, spw);
+        else hipLaunchKernelGGL(k_desc_lb<8>, grid, dim3(256), 0, s, base, d, n, out, spw);
         return;
     }
     switch (sh) {

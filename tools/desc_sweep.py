@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""Launch-shape sweep of the ragged-descriptor kernels (k_desc lane groups, k_desc_lb
+balanced) on equal-length descriptor batches of several sizes, device-resident.
+
+Each size: n descriptors of L bytes at stride L rounded up to 16 (>= 65536 of them,
+>= ~1.5 GB), every start value from synth_pseudo. Interleaved rounds (every shape
+once per round, median over rounds); every shape's results must equal the auto
+choice's. JSON lines.
+
+  python tools/desc_sweep.py            (SIZES / SHAPES env: comma lists)
+"""
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    import numpy as np
+    import torch
+    import tcp_amd
+    from tests.devcopy import to_dev
+    dev = torch.device("cuda:0")
+    st = torch.cuda.current_stream()
+    sizes = [int(x) for x in os.environ.get("SIZES", "64,1500,4096,9000,32768,65536").split(",")]
+    shapes = [int(x) for x in os.environ.get("SHAPES", "-1,3,4,5,6,7,8").split(",")]
+    rounds = int(os.environ.get("ROUNDS", "5"))
+    for L in sizes:
+        stride = (L + 15) & ~15
+        n = max(65536, (3 << 29) // stride)
+        data = torch.empty(n * stride, dtype=torch.uint8, device=dev)
+        tcp_amd.synth_fill(data, 0, n * stride)
+        d = np.zeros(n, tcp_amd.DESC_DTYPE)
+        d["offset"] = np.arange(n, dtype=np.uint64) * stride
+        d["len"] = L
+        d["sum_start"] = np.arange(n, dtype=np.uint32) * 7
+        dd = to_dev(d.view(np.uint8), dev)
+        outs = {sh: torch.empty(n, dtype=torch.int16, device=dev) for sh in shapes}
+        times = {sh: [] for sh in shapes}
+        for _ in range(rounds):
+            for sh in shapes:
+                t = tcp_amd.make_tuning(0, 0, sh, 0)
+                for _ in range(2):
+                    tcp_amd.batch_desc(data, dd, n, L, out=outs[sh], tune=t)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(st)
+                for _ in range(10):
+                    tcp_amd.batch_desc(data, dd, n, L, out=outs[sh], tune=t)
+                e1.record(st)
+                torch.cuda.synchronize()
+                times[sh].append(e0.elapsed_time(e1) / 10)
+        ref = outs[shapes[0]]
+        for sh in shapes:
+            ms = statistics.median(times[sh])
+            print(json.dumps({"measure": "desc_shape_sweep", "len": L, "n": n, "shape": sh, "ms": round(ms, 4),
+                              "GB/s": round(n * L / (ms * 1e-3) / 1e9, 1),
+                              "equal_to_auto": bool(torch.equal(outs[sh], ref))}), flush=True)
+        del data, dd, outs
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
