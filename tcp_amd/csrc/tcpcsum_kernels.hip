@@ -1980,7 +1980,11 @@ void launch_tx_build(const uint8_t* payload, const tcpcsum_txseg_t* segs, uint64
         else if (unroll == 2) launch_tx_t<G, C, 2>(payload, segs, n, outp, mode, checks, s, max_blocks, nts); \
         else launch_tx_t<G, C, 4>(payload, segs, n, outp, mode, checks, s, max_blocks, nts);    \
     } while (0)
-    int shape = nfull <= 8 ? 0 : nfull <= 96 ? 2 : 4;
+    // payloads of 129 B .. 1.25 KiB: 16-lane groups, two chunks per lane per round
+    // (256 B 1.76 -> 1.05 ms, 536 B 1.40 -> 1.07, 1024 B 0.92 -> 0.82, 1200 B -1 %;
+    // 1456 B keeps (32,3): 0.778 vs 0.839; tools/tx_size_sweep*.sh,
+    // profiles/r02_tx_size_sweep.jsonl)
+    int shape = nfull <= 8 ? 0 : nfull <= 80 ? 1 : nfull <= 96 ? 2 : 4;
     if (tu.shape >= 0 && tu.shape <= 4) shape = tu.shape;   // any shape is correct (extra rounds)
     switch (shape) {
         case 0: TX_U(8, 1); break;

@@ -8,7 +8,7 @@ and writes each packet once: algorithmic bytes = payload read + packet write
 of the payloads into place (torch copy_) plus the checksum kernel over the
 built segments.
 
-  python tools/txbench.py -> JSON lines
+  python tools/txbench.py -> JSON lines   (--sweep: launch shapes; TX_LEN=payload bytes)
 """
 import json
 import os
@@ -22,7 +22,9 @@ def main():
     import torch
     import tcp_amd
 
-    n, L = 1 << 20, 1456
+    # TX_LEN: payload bytes (default the MTU's 1456); n keeps ~1.5 GB of payload (>= 64K packets)
+    L = int(os.environ.get("TX_LEN", "1456"))
+    n = 1 << 20 if L == 1456 else max(1 << 16, min(1 << 22, (3 << 29) // max(L + 44, 1)))
     dev = torch.device("cuda:0")
     payload = torch.empty(n * L, dtype=torch.uint8, device=dev)
     tcp_amd.synth_fill(payload, 0, n * L)
@@ -61,7 +63,7 @@ def main():
             for un in unrolls:
                 tcp_amd.set_tuning(mb, un, sh, 0)
                 tt = timeit(lambda: tcp_amd.tx_build(payload, dsegs, n, L, out, 0, chk), 20)
-                print(json.dumps({"sweep": "tx_build", "shape": sh, "max_blocks": mb, "unroll": un,
+                print(json.dumps({"sweep": "tx_build", "len": L, "n": n, "shape": sh, "max_blocks": mb, "unroll": un,
                                   "ms": round(tt * 1e3, 4),
                                   "GB/s": round((n * L + n * (L + 44) + n * 48) / tt / 1e9, 1)}), flush=True)
         tcp_amd.set_tuning(0, 0, -1, 0)
