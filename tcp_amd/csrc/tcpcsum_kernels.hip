@@ -1723,6 +1723,10 @@ UniformPlan plan_uniform(uintptr_t b, uint64_t stride, uint32_t len, uint64_t n,
     // split, three same-process runs (profiles/r02_k64_check.jsonl).
     const bool huge = p.mode == M16 && len >= 65536u && (double)n * len >= 4.0 * (1u << 30);
     if (p.shape == 9 && p.mode != M1 && !huge) p.shape = 13;
+    // 8 KiB chunk-aligned segments (exactly 512 chunks): the split is 9 % ahead of
+    // (64,8) (0.208 vs 0.228 ms per 1.5 GB); 6.4-8 KiB otherwise within 2 % of the
+    // best shape (tools/uniform_size_sweep*.sh, profiles/r02_uniform_size_sweep.jsonl)
+    if (p.shape == 8 && p.mode == M16 && nch == 512) p.shape = 13;
     // a forced shape is honoured only if it covers the segment
     if (tu.shape == 12) {
         if (flat_ok(b, stride, len, p.mode)) p.shape = 12;

@@ -141,7 +141,7 @@ def test_no_device_is_reported_not_faked():
     (3, 1501, 1501, 100, (2, 5)),           # byte-granular
     (0, 1500, 1500, 1, (1, 5)),
     (12, 64, 64, 8, (1, 1)),                # misaligned 64 B touches 5 chunks
-    (0, 8192, 8192, 10, (0, 8)),
+    (0, 8192, 8192, 10, (0, 13)),            # exactly 512 chunks: split
     (0, 8208, 8193, 10, (2, 9)),            # 514 chunks, byte-granular -> one wave per segment
 ])
 def test_plan_uniform(base, stride, length, n, expect):
