@@ -810,3 +810,27 @@ def test_desc_balanced_tile_edges(dev, shape):
         finally:
             tcp_amd.set_tuning(0, 0, -1, 0)
         assert np.array_equal(got, oracle.batch_desc(host, off, lens, ss)), n
+
+
+@pytest.mark.parametrize("shape", [7, 8])
+@pytest.mark.parametrize("max_len", [1500, 4096, 9000, 40000, 65536])
+def test_desc_balanced_segments_per_wave(dev, shape, max_len):
+    """The balanced kernel's wave tile holds fewer segments as max_len grows (64 at 1.5 KiB down
+    to 1 at 64 KiB): tiles of every size, ragged lengths up to max_len, odd offsets, batches that
+    end mid-tile — exact against the oracle."""
+    import tcp_amd
+    rng = np.random.default_rng(max_len + shape)
+    size = 24 << 20
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    d = to_dev(host, dev)
+    n = int(min(3001, (size // max_len) * 2 + 3))
+    lens = rng.integers(0, max_len + 1, n).astype(np.uint32)
+    lens[::5] = max_len
+    off = np.array([rng.integers(0, size - l) for l in lens], np.uint64)
+    ss = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    tcp_amd.set_tuning(0, 0, shape, 0)
+    try:
+        got = u16(tcp_amd.batch_desc(d, to_dev(_desc(off, lens, ss), dev), n, max_len))
+    finally:
+        tcp_amd.set_tuning(0, 0, -1, 0)
+    assert np.array_equal(got, oracle.batch_desc(host, off, lens, ss))
