@@ -834,3 +834,27 @@ def test_desc_balanced_segments_per_wave(dev, shape, max_len):
     finally:
         tcp_amd.set_tuning(0, 0, -1, 0)
     assert np.array_equal(got, oracle.batch_desc(host, off, lens, ss))
+
+
+@pytest.mark.parametrize("slot,max_payload", [(2048, 1990), (4608, 4500)])
+def test_ipv4_large_batch_size_classes(dev, slot, max_payload):
+    """Large wire batches of 2-4.5 KiB packets take the 4- / 6-chunk-round shapes by size class
+    (auto); FILL then VERIFY, every result and every byte of the region against the oracle."""
+    import tcp_amd
+    from tests.packets import build_batch
+    rng = np.random.default_rng(slot)
+    n = 65536
+    region, off, _ = build_batch(rng, n, slot=slot, malformed=True, max_payload=max_payload)
+    ref = region.copy()
+    want_out, want_st = oracle.ipv4_batch(ref, off, slot, tcp_amd.IPV4_FILL)
+    dreg = to_dev(region, dev)
+    doff = to_dev(off.view(np.int64), dev)
+    out = torch.empty(n, dtype=torch.int16, device=dev)
+    st = torch.empty(n, dtype=torch.uint8, device=dev)
+    tcp_amd.ipv4_batch(dreg, doff, n, slot, tcp_amd.IPV4_FILL, out, st)
+    assert np.array_equal(host(st), want_st)
+    assert np.array_equal(u16(out), want_out)
+    assert np.array_equal(host(dreg), ref)
+    tcp_amd.ipv4_batch(dreg, doff, n, slot, tcp_amd.IPV4_VERIFY, out, st)
+    ok = want_st == tcp_amd.PKT_OK
+    assert np.all(u16(out)[ok] == 0) and np.array_equal(host(st), want_st)
