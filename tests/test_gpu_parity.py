@@ -398,14 +398,15 @@ def test_c_client_on_gpu(dev):
     assert "host-batch mismatches: 0 /" in r.stdout and "pointer-batch mismatches: 0 /" in r.stdout
 
 
-@pytest.mark.parametrize("layout", ["packed", "packed_odd", "slots", "jumbo"])
+@pytest.mark.parametrize("layout", ["packed", "packed_odd", "slots", "jumbo", "small"])
 def test_tx_build_vs_oracle(dev, layout):
-    """Device-side segment assembly + checksum == the oracle's context.c:150-213, byte for byte."""
+    """Device-side segment assembly + checksum == the oracle's context.c:150-213, byte for byte.
+    "small": payloads up to 536 B (the 16-lane default shape)."""
     import tcp_amd
     from tests.test_oracle import make_txsegs
-    rng = np.random.default_rng({"packed": 1, "packed_odd": 2, "slots": 3, "jumbo": 4}[layout])
+    rng = np.random.default_rng({"packed": 1, "packed_odd": 2, "slots": 3, "jumbo": 4, "small": 5}[layout])
     payload = rng.integers(0, 256, 1 << 20, dtype=np.uint8)
-    max_len = 9000 if layout == "jumbo" else 1456
+    max_len = {"jumbo": 9000, "small": 536}.get(layout, 1456)
     n = 400 if layout == "jumbo" else 3000
     segs, size = make_txsegs(rng, n, payload.size, max_len=max_len, odd=layout == "packed_odd",
                              slot=32768 if layout == "slots" else None)
