@@ -20,7 +20,7 @@ def main():
 
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream()
-    n, slot = 1 << 20, int(os.environ.get("SLOT", "1536"))
+    n, slot = int(os.environ.get("N", str(1 << 20))), int(os.environ.get("SLOT", "1536"))
     pay = int(os.environ.get("PAYLOAD", str(slot - 80)))   # TCP payload bytes (packet = pay + 44)
     payload = torch.empty(n * pay, dtype=torch.uint8, device=dev)
     tcp_amd.synth_fill(payload, 0, n * pay)
