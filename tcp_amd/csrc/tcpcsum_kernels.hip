@@ -1816,6 +1816,7 @@ void launch_desc(const uint8_t* base, const tcpcsum_desc_t* d, uint64_t n, uint3
     // 7 / 8: balanced chunk space with 4 / 8 loads per lane in flight)
     int sh = tu.shape;
     if (sh > 8) sh = -1;
+    const bool auto_shape = sh < 0;
     // auto: a large ragged batch takes the balanced kernel (a ragged batch has mixed
     // lengths by nature; uniform lengths belong to tcpcsum_batch_uniform_dev); small
     // batches and very long segments the lane groups by max_len
@@ -1830,6 +1831,11 @@ void launch_desc(const uint8_t* base, const tcpcsum_desc_t* d, uint64_t n, uint3
         // profiles/r02_desc_sweep.jsonl)
         uint32_t spw = 64;
         while (spw > 1 && (uint64_t)spw * nch > 8192u) spw >>= 1;
+        // and, chosen automatically, at least 4096 wave tiles where the batch allows
+        // (16 waves per CU: 16K x 1500-B descriptors 0.0361 -> 0.0082 ms; a forced
+        // shape keeps the max_len tile, which is what the tile-edge tests exercise)
+        if (auto_shape)
+            while (spw > 1 && (n + spw - 1) / spw < 4096u) spw >>= 1;
         // one tile per wave by default (4M x 84-B packets: -4 %)
         const dim3 grid(grid_for((n + spw - 1) / spw, tu.max_blocks > 0 ? tu.max_blocks : 1 << 24));
         if (sh == 7) hipLaunchKernelGGL(k_desc_lb<4>, grid, dim3(256), 0, s, base, d, n, out, spw);

@@ -7,7 +7,7 @@ Each size: n descriptors of L bytes at stride L rounded up to 16 (>= 65536 of th
 once per round, median over rounds); every shape's results must equal the auto
 choice's. JSON lines.
 
-  python tools/desc_sweep.py            (SIZES / SHAPES env: comma lists)
+  python tools/desc_sweep.py            (SIZES / SHAPES env: comma lists; N: descriptors per batch)
 """
 import json
 import os
@@ -29,7 +29,7 @@ def main():
     rounds = int(os.environ.get("ROUNDS", "5"))
     for L in sizes:
         stride = (L + 15) & ~15
-        n = max(65536, (3 << 29) // stride)
+        n = int(os.environ["N"]) if os.environ.get("N") else max(65536, (3 << 29) // stride)
         data = torch.empty(n * stride, dtype=torch.uint8, device=dev)
         tcp_amd.synth_fill(data, 0, n * stride)
         d = np.zeros(n, tcp_amd.DESC_DTYPE)
