@@ -1131,16 +1131,17 @@ __global__ __launch_bounds__(256) void k_ipv4_lb(uint8_t* __restrict__ pkts, con
                                                  const uint32_t* __restrict__ plen,
                                                  uint64_t n, uint32_t cap, uint64_t limit, int mode,
                                                  uint16_t* __restrict__ out, uint8_t* __restrict__ status,
-                                                 uint16_t* __restrict__ ipout) {
+                                                 uint16_t* __restrict__ ipout, uint32_t spw) {
+    // spw: packets per wave tile (1..64; lanes >= spw hold none), as in k_desc_lb
     __shared__ uint64_t acc[4][2][64];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
-    const uint64_t ntiles = (n + 63) / 64;
+    const uint64_t ntiles = (n + spw - 1) / spw;
     const bool verify = (mode & TCPCSUM_IPV4_VERIFY) != 0;
     const bool iphdr = (mode & TCPCSUM_IPV4_IPHDR) != 0;
     for (uint64_t t = (uint64_t)blockIdx.x * 4u + wv; t < ntiles; t += nwaves) {
-        const uint64_t i = t * 64 + lane;
-        const bool live = i < n;
+        const uint64_t i = t * spw + (uint64_t)lane;
+        const bool live = (uint32_t)lane < spw && i < n;
         const uint64_t o = ldg<uint64_t>(zsel(live, reinterpret_cast<const uint8_t*>(off + i)));
         uint32_t room = 0;   // PL: readable bytes at the packet (region end, its own length)
         bool hdr;
@@ -1907,6 +1908,7 @@ void launch_ipv4(uint8_t* pkts, const uint64_t* off, const uint32_t* plen, uint6
     // forced: 0 (8,1), 1 (32,3), 2 (64,4), 3 (16,2), 4 (16,6), 5 (8,12), 6 (8,2), 7 (8,4),
     // 8 / 9: balanced chunk space (k_ipv4_lb) with 4 / 8 loads per lane in flight
     int sh = tu.shape;
+    const bool auto_shape = sh < 0 || sh > 9;
     // auto: large batches of small or mixed packets (mean footprint < 960 B,
     // e.g. packed IMIX, 576-896-B slots) take the balanced kernel; MTU-size
     // slots, jumbo packets and small batches (a releaseSend batch of <= 1024
@@ -1939,21 +1941,26 @@ void launch_ipv4(uint8_t* pkts, const uint64_t* off, const uint32_t* plen, uint6
         }
     }
     if (sh == 8 || sh == 9) {
-        // one 64-packet tile per wave by default (4M packed 84-B packets 0.116 ->
-        // 0.112 ms against 8192 blocks; tools/lb_sweep.sh)
-        const dim3 grid(grid_for((n + 63) / 64, tu.max_blocks > 0 ? tu.max_blocks : 1 << 24));
+        // 64 packets per wave tile; chosen automatically, at least 4096 tiles where
+        // the batch allows (16 waves per CU; profiles/r02_wire_lb_small_batches.jsonl)
+        uint32_t spw = 64;
+        if (auto_shape)
+            while (spw > 1 && (n + spw - 1) / spw < 4096u) spw >>= 1;
+        // one tile per wave by default (4M packed 84-B packets 0.116 -> 0.112 ms
+        // against 8192 blocks; tools/lb_sweep.sh)
+        const dim3 grid(grid_for((n + spw - 1) / spw, tu.max_blocks > 0 ? tu.max_blocks : 1 << 24));
         if (sh == 8 && plen)
             hipLaunchKernelGGL((k_ipv4_lb<4, true>), grid, dim3(256), 0, s, pkts, off, plen, n, cap, limit, mode, out,
-                               status, ipout);
+                               status, ipout, spw);
         else if (sh == 8)
             hipLaunchKernelGGL((k_ipv4_lb<4, false>), grid, dim3(256), 0, s, pkts, off, plen, n, cap, limit, mode, out,
-                               status, ipout);
+                               status, ipout, spw);
         else if (plen)
             hipLaunchKernelGGL((k_ipv4_lb<8, true>), grid, dim3(256), 0, s, pkts, off, plen, n, cap, limit, mode, out,
-                               status, ipout);
+                               status, ipout, spw);
         else
             hipLaunchKernelGGL((k_ipv4_lb<8, false>), grid, dim3(256), 0, s, pkts, off, plen, n, cap, limit, mode, out,
-                               status, ipout);
+                               status, ipout, spw);
         return;
     }
     switch (sh) {
