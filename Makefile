@@ -16,7 +16,7 @@ HIPFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Wno-unused-parame
 CFLAGS_LIB ?= -O2 -fPIC -Wall -Wextra
 
 LIB := tcp_amd/libtcpcsum.so
-HIP_SRCS := tcp_amd/csrc/tcpcsum_kernels.hip tcp_amd/csrc/tcpcsum_api.hip
+HIP_SRCS := tcp_amd/csrc/tcpcsum_kernels.hip tcp_amd/csrc/tcpcsum_api.hip tcp_amd/csrc/tcpcsum_host.hip
 HDRS := include/tcpcsum.h tcp_amd/csrc/tcpcsum_internal.h tcp_amd/csrc/host_registry.h
 OBJDIR := build/obj
 
@@ -32,8 +32,8 @@ $(OBJDIR)/scalar_dropin.o: tcp_amd/csrc/scalar_dropin.c include/tcpcsum.h
 	@mkdir -p $(OBJDIR)
 	$(CC) $(CFLAGS_LIB) -Iinclude -c $< -o $@
 
-$(LIB): $(OBJDIR)/tcpcsum_kernels.o $(OBJDIR)/tcpcsum_api.o $(OBJDIR)/scalar_dropin.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@.tmp $^ -Wl,-soname,libtcpcsum.so
+$(LIB): $(OBJDIR)/tcpcsum_kernels.o $(OBJDIR)/tcpcsum_api.o $(OBJDIR)/tcpcsum_host.o $(OBJDIR)/scalar_dropin.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@.tmp $^ -Wl,-soname,libtcpcsum.so -lpthread
 	mv $@.tmp $@
 
 # LD_PRELOAD seam library (sendmmsg / recvmmsg interposer) over the C ABI

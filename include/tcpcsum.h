@@ -25,7 +25,12 @@
  *     (NULL = built-in defaults) or from the tcpcsum_ctx_t they run in; no
  *     call keeps a pointer after it returns (async calls: until the stream
  *     reaches that point), except the host-buffer registrations a context
- *     holds (tcpcsum_ipv4_batch_ptrs_host).
+ *     holds when asked to (tcpcsum_ctx_register_host, or
+ *     TCPCSUM_CTX_AUTO_REGISTER).
+ *   - The library never page-locks (hipHostRegister) memory on its own: only
+ *     ranges its caller hands to tcpcsum_ctx_register_host, or packet buffers
+ *     under the opt-in TCPCSUM_CTX_AUTO_REGISTER. Pageable host memory is
+ *     copied by CPU threads into the context's pinned staging instead.
  *   - The caller owns every buffer.
  *   - The batch API covers sum_start < 2^32 (getPseudoHeaderSum returns at
  *     most 6 * 0xFFFF) and segment lengths <= INT32_MAX (csum_continue's
@@ -47,7 +52,7 @@ extern "C" {
 #define TCPCSUM_EHIP (-3)     /* a HIP call failed (tcpcsum_last_hip_error) */
 #define TCPCSUM_ENOMEM (-4)   /* allocation failed */
 
-#define TCPCSUM_ABI_VERSION 2
+#define TCPCSUM_ABI_VERSION 3
 
 /* Launch-shape override, passed per call (NULL = the built-in shapes measured
  * on MI355X). Fields: max_blocks (0 = per-shape default, else
@@ -191,11 +196,22 @@ int tcpcsum_tx_build_dev(const void *d_payload, const tcpcsum_txseg_t *d_segs, u
 
 /* ------------------------------------------------------ host-memory batches
  * The path as the reference sees it: segments start and end in host memory
- * (raw-socket buffers). A context owns one device, pinned staging and device
- * scratch, and pipelines H2D copy, checksum and D2H copy in chunks. */
+ * (raw-socket buffers). A context owns one device, two streams, pinned
+ * staging and a few host copy threads (TCPCSUM_HOST_THREADS, default half the
+ * CPUs the process may use, at most 8). Host memory is used one of two ways:
+ *   - page-locked memory (tcpcsum_host_alloc / hipHostMalloc, a caller's own
+ *     hipHostRegister, tcpcsum_ctx_register_host) is read — FILL: written —
+ *     in place by the kernel over PCIe;
+ *   - pageable memory is copied by the CPU threads into the context's pinned
+ *     staging (uniform batches chunk by chunk, overlapped with the kernel on
+ *     the previous chunk; wire batches only the packets' bytes), the kernel
+ *     reads the staging, and FILL's checks are stored back into the caller's
+ *     packets by the CPU. Nothing is page-locked behind the caller's back.
+ * All host calls are synchronous: they return when every result is in place. */
 typedef struct tcpcsum_ctx tcpcsum_ctx_t;
 
-/* scratch_bytes: device staging size per pipeline slot (0 = 64 MiB). */
+/* scratch_bytes: pinned staging per pipeline slot for pageable uniform
+ * batches (0 = 16 MiB). */
 int tcpcsum_ctx_create(int device, size_t scratch_bytes, tcpcsum_ctx_t **out);
 void tcpcsum_ctx_destroy(tcpcsum_ctx_t *ctx);
 
@@ -203,28 +219,49 @@ void tcpcsum_ctx_destroy(tcpcsum_ctx_t *ctx);
  * this context is affected; other contexts and the device calls are not. */
 int tcpcsum_ctx_set_tuning(tcpcsum_ctx_t *ctx, const tcpcsum_tuning_t *tune);
 
+/* Context flags (0 = default). */
+/* tcpcsum_ipv4_batch_ptrs_host: page-lock each pageable packet buffer on first
+ * use (whole pages, hipHostRegister) and keep it registered — later batches
+ * over the same buffers read and write them in place with no copy — up to
+ * 256 MiB of registrations, past which new buffers are copied. Opt-in: the
+ * caller promises that the pages under those buffers are neither freed nor
+ * page-locked / unlocked by anyone else (including HIP copies of other data
+ * sharing those pages) until tcpcsum_ctx_unregister_host / _destroy. The
+ * reference's buffers qualify (allocated once, never freed, loop.c:180-183). */
+#define TCPCSUM_CTX_AUTO_REGISTER 1u
+int tcpcsum_ctx_set_flags(tcpcsum_ctx_t *ctx, uint32_t flags);
+
+/* Counters of what the context did (cumulative since creation). */
+typedef struct tcpcsum_ctx_stats {
+    uint64_t batches;            /* host batch calls */
+    uint64_t pkts_in_place;      /* wire packets read / written in page-locked memory */
+    uint64_t pkts_staged;        /* wire packets copied through pinned staging */
+    uint64_t bytes_staged;       /* bytes copied into pinned staging (all host paths) */
+    uint64_t registered_ranges;  /* current registrations of this context */
+    uint64_t registered_bytes;
+    uint64_t copy_threads;       /* host threads used for staging copies (incl. the caller's) */
+    uint64_t reserved;
+} tcpcsum_ctx_stats_t;
+int tcpcsum_ctx_get_stats(tcpcsum_ctx_t *ctx, tcpcsum_ctx_stats_t *out);
+
 /* Page-locked host memory for packet pools: the host calls read it in place
- * over PCIe with no per-call locking. NULL on failure. */
+ * over PCIe. NULL on failure. */
 void *tcpcsum_host_alloc(size_t bytes);
 void tcpcsum_host_free(void *p);
 
 /* Uniform layout in host memory; h_out[i] as tcpcsum_batch_uniform_dev.
  * h_sum_start may be NULL (then sum_start is used for every segment).
- * Page-locked input is read in place over PCIe; pageable input is page-locked
- * for the call, chunk by chunk, and read the same way (or, when it cannot be
- * locked, copied through the context's pinned bounce buffers). Synchronous:
- * returns when h_out is complete. */
+ * Page-locked input is read in place; pageable input is staged (above). */
 int tcpcsum_batch_uniform_host(tcpcsum_ctx_t *ctx, const void *h_base, uint64_t stride,
                                uint32_t len, const uint32_t *h_sum_start, uint32_t sum_start,
                                uint16_t *h_out, uint64_t n);
 
 /* Wire layout in host memory: n packets at h_pkts + h_pkt_off[i] (offsets
- * within one host region of region_bytes). FILL patches check in place in
- * host memory. Synchronous. A region that one page-locked allocation covers
- * (tcpcsum_host_alloc, or a pool registered once with
- * tcpcsum_ctx_register_host) is read in place over PCIe; a pageable region of
- * 64 KiB or more is page-locked for the call and read in place the same way;
- * otherwise it is copied to the device through pinned bounce buffers. */
+ * within one host region of region_bytes; each header must lie inside it).
+ * FILL patches check in place in host memory. A region that one page-locked
+ * allocation covers (tcpcsum_host_alloc, or a pool registered once with
+ * tcpcsum_ctx_register_host) is read in place; otherwise only the packets are
+ * copied into staging. Results exactly as tcpcsum_ipv4_batch_dev. */
 int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t *ctx, void *h_pkts, size_t region_bytes,
                             const uint64_t *h_pkt_off, uint64_t n, uint32_t cap, int mode,
                             uint16_t *h_out, uint8_t *h_status);
@@ -232,19 +269,18 @@ int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t *ctx, void *h_pkts, size_t region_byte
 /* Wire batch over the caller's own per-packet buffers (the reference's
  * layout: 1024 separately malloc'd 32 KiB out-buffers, loop.c:180-183, one
  * iov_base per message, loop.c:53-54): packet i at h_pkts[i] with h_lens[i]
- * readable bytes. Pageable buffers are page-locked with hipHostRegister on
- * first use and stay registered with the context (cached; later batches over
- * the same buffers cost no registration) until tcpcsum_ctx_unregister_host or
- * tcpcsum_ctx_destroy: the caller must not release those pages to the OS
- * (free() of a registered buffer) before then. The kernel reads the packets in
- * host memory over PCIe and FILL stores each check in place — no CPU pass over
- * packet bytes and no staging copy. Synchronous. */
+ * readable bytes (results and status as tcpcsum_ipv4_batch_ptrs_dev). A
+ * packet inside one page-locked mapping (this context's registrations, or
+ * memory someone else page-locked) is read and FILLed in place; any other is
+ * copied into staging and its check stored back — unless the context has
+ * TCPCSUM_CTX_AUTO_REGISTER, which page-locks its buffer now and keeps it. */
 int tcpcsum_ipv4_batch_ptrs_host(tcpcsum_ctx_t *ctx, void *const *h_pkts, const uint32_t *h_lens, uint64_t n,
                                  int mode, uint16_t *h_out, uint8_t *h_status);
 
-/* Page-lock [p, p+bytes) for this context ahead of time (what the first
- * tcpcsum_ipv4_batch_ptrs_host over it would do), e.g. once per pool buffer at
- * loop.c:180-183. */
+/* Page-lock [p, p+bytes) (whole pages) for this context, e.g. once per pool
+ * at loop.c:180-183; later host batches over it run in place. The contract
+ * is hipHostRegister's: the caller keeps those pages mapped, and does not
+ * page-lock or unlock them elsewhere, until it unregisters them. */
 int tcpcsum_ctx_register_host(tcpcsum_ctx_t *ctx, void *p, size_t bytes);
 /* Drop every registration of this context that overlaps [p, p+bytes)
  * (p = NULL: all of them). Call before freeing registered buffers. */

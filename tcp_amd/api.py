@@ -22,7 +22,7 @@ except Exception:  # pragma: no cover - torch is always present in this image
 
 __all__ = [
     "DESC_DTYPE", "TXSEG_DTYPE", "IPV4_FILL", "IPV4_VERIFY", "IPV4_IPHDR", "PKT_OK", "PKT_SKIPPED",
-    "PKT_IPHDR_BAD", "PKT_CSUM_PARTIAL", "TUNE_WIRE_CACHED", "TUNE_WIN16", "TUNE_TX_NT_STORE", "TUNE_FILL_DWORD",
+    "PKT_IPHDR_BAD", "PKT_CSUM_PARTIAL", "CTX_AUTO_REGISTER", "TUNE_WIRE_CACHED", "TUNE_WIN16", "TUNE_TX_NT_STORE", "TUNE_FILL_DWORD",
     "TcpCsumError", "Tuning", "HostContext", "lib", "lib_path", "device_check", "make_tuning", "set_tuning",
     "get_tuning", "plan_uniform", "getPseudoHeaderSum", "csum_continue", "batch_uniform", "batch_desc",
     "ipv4_batch", "ipv4_batch_ptrs", "tx_build", "synth_fill", "synth_pseudo", "stream_probe", "pinned_empty",
@@ -43,6 +43,7 @@ PKT_OK = 0
 PKT_SKIPPED = 1
 PKT_IPHDR_BAD = 2
 PKT_CSUM_PARTIAL = 4
+CTX_AUTO_REGISTER = 1
 
 # tcpcsum_desc_t {u64 offset; u32 len; u32 sum_start}
 DESC_DTYPE = np.dtype([("offset", "<u8"), ("len", "<u4"), ("sum_start", "<u4")])
@@ -88,6 +89,14 @@ class Tuning(ctypes.Structure):
 
 tunep = ctypes.POINTER(Tuning)
 
+
+class CtxStats(ctypes.Structure):
+    """tcpcsum_ctx_stats_t."""
+    _fields_ = [("batches", ctypes.c_uint64), ("pkts_in_place", ctypes.c_uint64), ("pkts_staged", ctypes.c_uint64),
+                ("bytes_staged", ctypes.c_uint64), ("registered_ranges", ctypes.c_uint64),
+                ("registered_bytes", ctypes.c_uint64), ("copy_threads", ctypes.c_uint64),
+                ("reserved", ctypes.c_uint64)]
+
 # name -> (restype, argtypes); must cover every function in include/tcpcsum.h
 SIGNATURES = {
     "tcpcsum_abi_version": (ctypes.c_int, []),
@@ -103,6 +112,8 @@ SIGNATURES = {
     "tcpcsum_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_size_t, ctypes.POINTER(vp)]),
     "tcpcsum_ctx_destroy": (None, [vp]),
     "tcpcsum_ctx_set_tuning": (ctypes.c_int, [vp, tunep]),
+    "tcpcsum_ctx_set_flags": (ctypes.c_int, [vp, u32]),
+    "tcpcsum_ctx_get_stats": (ctypes.c_int, [vp, vp]),
     "tcpcsum_host_alloc": (vp, [ctypes.c_size_t]),
     "tcpcsum_host_free": (None, [vp]),
     "tcpcsum_batch_uniform_host": (ctypes.c_int, [vp, vp, u64, u32, vp, u32, vp, u64]),
@@ -364,12 +375,24 @@ def pinned_empty(nbytes: int, dtype=np.uint8) -> np.ndarray:
 
 
 class HostContext:
-    """tcpcsum_ctx_t: host-memory batches (H2D -> kernel -> D2H), synchronous."""
+    """tcpcsum_ctx_t: host-memory batches, synchronous. Page-locked memory is read in place; pageable
+    memory is copied into the context's pinned staging (never page-locked behind the caller's back),
+    unless ``auto_register`` (TCPCSUM_CTX_AUTO_REGISTER) lets ipv4_batch_ptrs lock packet buffers."""
 
-    def __init__(self, device: int = 0, scratch_bytes: int = 0):
+    def __init__(self, device: int = 0, scratch_bytes: int = 0, auto_register: bool = False):
         h = vp()
         _check(lib().tcpcsum_ctx_create(device, scratch_bytes, ctypes.byref(h)), "tcpcsum_ctx_create")
         self._h = h
+        if auto_register:
+            self.set_flags(CTX_AUTO_REGISTER)
+
+    def set_flags(self, flags: int) -> None:
+        _check(lib().tcpcsum_ctx_set_flags(self._h, flags), "tcpcsum_ctx_set_flags")
+
+    def stats(self) -> dict:
+        st = CtxStats()
+        _check(lib().tcpcsum_ctx_get_stats(self._h, ctypes.byref(st)), "tcpcsum_ctx_get_stats")
+        return {k: int(getattr(st, k)) for k, _ in CtxStats._fields_ if k != "reserved"}
 
     def close(self) -> None:
         if self._h:
@@ -423,8 +446,8 @@ class HostContext:
 
     def ipv4_batch_ptrs(self, ptrs, lens, mode: int):
         """Scatter-gather wire batch over host buffers: ``ptrs`` host addresses (ints), ``lens`` readable
-        bytes per packet. Pageable buffers are page-locked on first use and stay registered with this
-        context (FILL patches the checks in place)."""
+        bytes per packet. Page-locked buffers are used in place; pageable ones are copied into staging
+        (or, with auto_register, page-locked on first use and kept). FILL patches the checks in place."""
         p = np.ascontiguousarray(np.asarray(ptrs, dtype=np.uint64))
         ln = np.ascontiguousarray(np.asarray(lens, dtype=np.uint32))
         if p.size != ln.size:

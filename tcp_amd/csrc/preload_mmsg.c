@@ -17,25 +17,41 @@
  *   recvmmsg  TCPCSUM_PRELOAD_RX=verify verify every received batch on the GPU
  *                                       (the reference verifies nothing,
  *                                       loop.c:314-399); failures are counted
+ *             TCPCSUM_PRELOAD_RX=drop   verify, and return only the segments
+ *                                       that pass: the vector is reordered (a
+ *                                       permutation of the caller's entries, so
+ *                                       every buffer stays referenced) with the
+ *                                       passing segments first, and the count
+ *                                       returned is theirs
  *             TCPCSUM_PRELOAD_RX=off    (default)
  *   TCPCSUM_PRELOAD_IPHDR=1      also fill / verify the IPv4 header checksum
  *   TCPCSUM_PRELOAD_ANY_SOCKET=1 act on every socket, not only SOCK_RAW ones
  *                                (tests run it over UDP loopback, no root)
  *   TCPCSUM_PRELOAD_STATS=1      print counters to stderr at exit
- *   TCPCSUM_PRELOAD_COPY=1       gather packets into a page-locked staging
- *                                area instead (for applications that free()
- *                                their packet buffers; see below)
+ *   TCPCSUM_PRELOAD_INPLACE=1    page-lock each packet buffer on first use and
+ *                                keep it (TCPCSUM_CTX_AUTO_REGISTER): the
+ *                                kernel then reads the caller's buffers in
+ *                                place and stores the checks there, with no
+ *                                CPU copy. Only for applications that never
+ *                                free their packet buffers and do not
+ *                                page-lock them themselves — the reference
+ *                                qualifies (loop.c:180-183).
  *
- * Default: the kernel works on the caller's own buffers — one iov_base per
- * message, each buffer page-locked on first use and kept registered for the
- * life of the process (tcpcsum_ipv4_batch_ptrs_host) — reading the packets
- * over PCIe and storing the checks in place: no CPU pass over packet bytes.
- * This suits the reference, which allocates its 2 x 1024 packet buffers once
- * and never frees them (loop.c:180-183). With TCPCSUM_PRELOAD_COPY=1 packets
- * are copied into pinned staging and only the 2-byte check fields are
- * written back. If the GPU path cannot run, the call fails with errno = ENXIO
- * rather than sending packets with unchecked checksums: there is no silent
+ * Default: every message's bytes are copied by the library's host threads
+ * into pinned staging (tcpcsum_ipv4_batch_ptrs_host), checksummed there, and
+ * FILL's 2-byte checks are written back into the caller's buffers. Nothing
+ * is page-locked behind the application's back. Buffers the application
+ * page-locked itself (hipHostMalloc, hipHostRegister) are read in place.
+ * If the GPU path cannot run, the call fails with errno = ENXIO rather than
+ * sending (or accepting) packets with unchecked checksums: there is no silent
  * CPU fallback.
+ *
+ * A segment passes RX verification when its TCP checksum verifies to 0, or it
+ * is CHECKSUM_PARTIAL (checksum left to offload — Linux loopback does this for
+ * the kernel's own segments), and (with IPHDR) its IPv4 header
+ * checksum verifies. Messages that are not IPv4/TCP, or are truncated, are
+ * not TCP segments the library can verify: they are passed through untouched
+ * (the reference filters them itself, loop.c:319).
  */
 #define _GNU_SOURCE
 #include <dlfcn.h>
@@ -53,11 +69,11 @@
 typedef int (*sendmmsg_fn)(int, struct mmsghdr *, unsigned int, int);
 typedef int (*recvmmsg_fn)(int, struct mmsghdr *, unsigned int, int, struct timespec *);
 
-enum { MODE_OFF = 0, MODE_FILL = 1, MODE_VERIFY = 2 };
+enum { MODE_OFF = 0, MODE_FILL = 1, MODE_VERIFY = 2, MODE_DROP = 3 };
 
 struct tcpcsum_preload_stats {
     unsigned long long tx_batches, tx_packets, tx_filled, tx_verified, tx_verify_failed, tx_skipped;
-    unsigned long long rx_batches, rx_packets, rx_verified, rx_verify_failed, rx_skipped, rx_partial;
+    unsigned long long rx_batches, rx_packets, rx_verified, rx_verify_failed, rx_skipped, rx_partial, rx_dropped;
     unsigned long long errors;
 };
 
@@ -65,15 +81,11 @@ static pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;
 static pthread_once_t g_once = PTHREAD_ONCE_INIT;
 static sendmmsg_fn real_sendmmsg;
 static recvmmsg_fn real_recvmmsg;
-static int g_tx = MODE_FILL, g_rx = MODE_OFF, g_iphdr, g_any, g_stats, g_copy;
+static int g_tx = MODE_FILL, g_rx = MODE_OFF, g_iphdr, g_any, g_stats, g_inplace;
 static tcpcsum_ctx_t *g_ctx;
 static int g_ctx_failed;
-static uint8_t *g_stage;   /* pinned */
-static size_t g_stage_bytes;
-static uint64_t *g_off;
-static uint16_t *g_out;
+static uint16_t *g_out;     /* pinned: the kernel writes results straight here */
 static uint8_t *g_status;
-static size_t g_cap_pkts;
 static struct tcpcsum_preload_stats g_st;
 
 static int env_mode(const char *name, int dflt) {
@@ -81,8 +93,14 @@ static int env_mode(const char *name, int dflt) {
     if (!v) return dflt;
     if (!strcmp(v, "fill")) return MODE_FILL;
     if (!strcmp(v, "verify")) return MODE_VERIFY;
+    if (!strcmp(v, "drop")) return MODE_DROP;
     if (!strcmp(v, "off") || !strcmp(v, "0")) return MODE_OFF;
     return dflt;
+}
+
+static int env_flag(const char *name) {
+    const char *v = getenv(name);
+    return v && atoi(v);
 }
 
 static void print_stats(void) {
@@ -90,21 +108,23 @@ static void print_stats(void) {
     fprintf(stderr,
             "tcpcsum_preload: tx batches=%llu packets=%llu filled=%llu verified=%llu verify_failed=%llu "
             "skipped=%llu | rx batches=%llu packets=%llu verified=%llu verify_failed=%llu skipped=%llu "
-            "partial=%llu | errors=%llu\n",
+            "partial=%llu dropped=%llu | errors=%llu\n",
             g_st.tx_batches, g_st.tx_packets, g_st.tx_filled, g_st.tx_verified, g_st.tx_verify_failed,
             g_st.tx_skipped, g_st.rx_batches, g_st.rx_packets, g_st.rx_verified, g_st.rx_verify_failed,
-            g_st.rx_skipped, g_st.rx_partial, g_st.errors);
+            g_st.rx_skipped, g_st.rx_partial, g_st.rx_dropped, g_st.errors);
 }
 
 static void init_once(void) {
     real_sendmmsg = (sendmmsg_fn) dlsym(RTLD_NEXT, "sendmmsg");
     real_recvmmsg = (recvmmsg_fn) dlsym(RTLD_NEXT, "recvmmsg");
     g_tx = env_mode("TCPCSUM_PRELOAD_TX", MODE_FILL);
+    if (g_tx == MODE_DROP) g_tx = MODE_VERIFY;   /* never drop what the application sends */
     g_rx = env_mode("TCPCSUM_PRELOAD_RX", MODE_OFF);
-    g_iphdr = getenv("TCPCSUM_PRELOAD_IPHDR") && atoi(getenv("TCPCSUM_PRELOAD_IPHDR"));
-    g_any = getenv("TCPCSUM_PRELOAD_ANY_SOCKET") && atoi(getenv("TCPCSUM_PRELOAD_ANY_SOCKET"));
-    g_stats = getenv("TCPCSUM_PRELOAD_STATS") && atoi(getenv("TCPCSUM_PRELOAD_STATS"));
-    g_copy = getenv("TCPCSUM_PRELOAD_COPY") && atoi(getenv("TCPCSUM_PRELOAD_COPY"));
+    g_iphdr = env_flag("TCPCSUM_PRELOAD_IPHDR");
+    g_any = env_flag("TCPCSUM_PRELOAD_ANY_SOCKET");
+    g_stats = env_flag("TCPCSUM_PRELOAD_STATS");
+    /* TCPCSUM_PRELOAD_COPY=1 (round 2) named what is now the default */
+    g_inplace = env_flag("TCPCSUM_PRELOAD_INPLACE") && !env_flag("TCPCSUM_PRELOAD_COPY");
     atexit(print_stats);
 }
 
@@ -124,65 +144,56 @@ static int wants_fd(int fd) {
 }
 
 /* g_mu held. */
-static int ensure_ctx(size_t bytes, size_t npkts) {
+static int ensure_ctx(void) {
     if (g_ctx_failed) return -1;
     if (!g_ctx) {
         int rc = tcpcsum_ctx_create(0, 0, &g_ctx);
+        if (!rc && g_inplace) rc = tcpcsum_ctx_set_flags(g_ctx, TCPCSUM_CTX_AUTO_REGISTER);
+        if (!rc) {
+            g_out = (uint16_t *) tcpcsum_host_alloc(1024 * sizeof(uint16_t));
+            g_status = (uint8_t *) tcpcsum_host_alloc(1024);
+            if (!g_out || !g_status) rc = TCPCSUM_ENOMEM;
+        }
         if (rc) {
             fprintf(stderr, "tcpcsum_preload: GPU checksum path unavailable (%s); refusing to send/accept "
                             "packets with unchecked checksums\n", tcpcsum_strerror(rc));
             g_ctx_failed = 1;
+            tcpcsum_ctx_destroy(g_ctx);
             g_ctx = NULL;
             return -1;
         }
     }
-    if (bytes > g_stage_bytes) {
-        size_t nb = g_stage_bytes ? g_stage_bytes : (size_t) 1 << 21;
-        while (nb < bytes) nb *= 2;
-        uint8_t *p = (uint8_t *) tcpcsum_host_alloc(nb);
-        if (!p) return -1;
-        tcpcsum_host_free(g_stage);
-        g_stage = p;
-        g_stage_bytes = nb;
-    }
-    if (npkts > g_cap_pkts) {
-        size_t np = g_cap_pkts ? g_cap_pkts : 1024;
-        while (np < npkts) np *= 2;
-        uint64_t *o = (uint64_t *) tcpcsum_host_alloc(np * sizeof(uint64_t));
-        uint16_t *u = (uint16_t *) tcpcsum_host_alloc(np * sizeof(uint16_t));
-        uint8_t *s = (uint8_t *) tcpcsum_host_alloc(np);
-        if (!o || !u || !s) {
-            tcpcsum_host_free(o); tcpcsum_host_free(u); tcpcsum_host_free(s);
-            return -1;
-        }
-        tcpcsum_host_free(g_off); tcpcsum_host_free(g_out); tcpcsum_host_free(g_status);
-        g_off = o; g_out = u; g_status = s;
-        g_cap_pkts = np;
-    }
     return 0;
 }
 
-/* g_mu held. Count one message of a finished batch (k: its slot in the
- * batch arrays). */
-static void account(int k, int fill, int is_tx) {
+/* g_mu held. Whether message k of a finished batch is kept (rx drop), and its
+ * accounting. */
+static int account(int k, int fill, int is_tx) {
     const int skipped = (g_status[k] & TCPCSUM_PKT_SKIPPED) != 0;
     if (skipped) {
         if (is_tx) g_st.tx_skipped++; else g_st.rx_skipped++;
-    } else if (fill) {
-        g_st.tx_filled++;
-    } else {
-        /* CHECKSUM_PARTIAL segments (checksum left to offload, e.g. Linux
-         * loopback) are counted apart, not as corrupt */
-        const int partial = (g_status[k] & TCPCSUM_PKT_CSUM_PARTIAL) != 0;
-        const int bad = (g_out[k] != 0 && !partial) || (g_status[k] & TCPCSUM_PKT_IPHDR_BAD);
-        if (is_tx) { g_st.tx_verified++; if (bad) g_st.tx_verify_failed++; }
-        else { g_st.rx_verified++; if (bad) g_st.rx_verify_failed++; if (partial) g_st.rx_partial++; }
+        return 1;
     }
+    if (fill) {
+        g_st.tx_filled++;
+        return 1;
+    }
+    /* CHECKSUM_PARTIAL segments (checksum left to offload, e.g. Linux
+     * loopback) are counted apart, not as corrupt */
+    const int partial = (g_status[k] & TCPCSUM_PKT_CSUM_PARTIAL) != 0;
+    const int bad = (g_out[k] != 0 && !partial) || (g_status[k] & TCPCSUM_PKT_IPHDR_BAD);
+    if (is_tx) { g_st.tx_verified++; if (bad) g_st.tx_verify_failed++; }
+    else { g_st.rx_verified++; if (bad) g_st.rx_verify_failed++; if (partial) g_st.rx_partial++; }
+    return !bad;
 }
 
-/* Default path: the GPU reads the caller's buffers in place (scatter-gather,
- * each buffer page-locked once) and FILL stores the checks there. */
-static int gpu_batch_inplace(struct mmsghdr *vec, unsigned int vlen, const unsigned int *lens, int fill, int is_tx) {
+/* Checksum a batch of <= 1024 messages on the GPU (one iov_base per message:
+ * the reference's layout, loop.c:53-54; other messages are SKIPPED). lens:
+ * each message's byte count (iov_len for tx, msg_len for rx). fill: store the
+ * checks in the caller's buffers. keep (nullable): per message, whether it
+ * passed. Returns 0, or -1 with errno set. */
+static int gpu_batch(struct mmsghdr *vec, unsigned int vlen, const unsigned int *lens, int fill, int is_tx,
+                     unsigned char *keep) {
     void *ptrs[1024];
     uint32_t plen[1024];
     for (unsigned int i = 0; i < vlen; ++i) {
@@ -191,7 +202,7 @@ static int gpu_batch_inplace(struct mmsghdr *vec, unsigned int vlen, const unsig
         plen[i] = one ? lens[i] : 0;   /* < 20 bytes: SKIPPED, nothing read */
     }
     pthread_mutex_lock(&g_mu);
-    if (ensure_ctx(0, vlen)) {
+    if (ensure_ctx()) {
         g_st.errors++;
         pthread_mutex_unlock(&g_mu);
         errno = ENXIO;
@@ -206,68 +217,9 @@ static int gpu_batch_inplace(struct mmsghdr *vec, unsigned int vlen, const unsig
         errno = ENXIO;
         return -1;
     }
-    for (unsigned int i = 0; i < vlen; ++i) account((int) i, fill, is_tx);
-    pthread_mutex_unlock(&g_mu);
-    return 0;
-}
-
-/* Checksum a batch of single-iovec messages on the GPU. fill: write the check
- * fields back into the caller's buffers. Returns 0, or -1 (errno set). lens
- * gives each message's byte count (iov_len for tx, msg_len for rx). */
-static int gpu_batch(struct mmsghdr *vec, unsigned int vlen, const unsigned int *lens, int fill, int is_tx) {
-    if (!g_copy) return gpu_batch_inplace(vec, vlen, lens, fill, is_tx);
-    size_t total = 0;
-    unsigned int m = 0;
     for (unsigned int i = 0; i < vlen; ++i) {
-        if (vec[i].msg_hdr.msg_iovlen != 1 || lens[i] < 20) continue;
-        total += ((size_t) lens[i] + 16 + 15) & ~(size_t) 15;
-        ++m;
-    }
-    if (!m) return 0;
-    pthread_mutex_lock(&g_mu);
-    if (ensure_ctx(total, vlen)) {
-        g_st.errors++;
-        pthread_mutex_unlock(&g_mu);
-        errno = ENXIO;
-        return -1;
-    }
-    /* gather: each packet at a 16-B aligned offset, 16 zero bytes of slack after it */
-    size_t pos = 0;
-    unsigned int k = 0;
-    for (unsigned int i = 0; i < vlen; ++i) {
-        if (vec[i].msg_hdr.msg_iovlen != 1 || lens[i] < 20) continue;
-        memcpy(g_stage + pos, vec[i].msg_hdr.msg_iov[0].iov_base, lens[i]);
-        memset(g_stage + pos + lens[i], 0, 16);
-        g_off[k++] = pos;
-        pos += ((size_t) lens[i] + 16 + 15) & ~(size_t) 15;
-    }
-    int mode = (fill ? TCPCSUM_IPV4_FILL : TCPCSUM_IPV4_VERIFY) | (g_iphdr ? TCPCSUM_IPV4_IPHDR : 0);
-    /* cap: a packet may not claim more bytes than were handed to the socket */
-    int rc = tcpcsum_ipv4_batch_host(g_ctx, g_stage, pos, g_off, m, 65535u, mode, g_out, g_status);
-    if (rc) {
-        g_st.errors++;
-        pthread_mutex_unlock(&g_mu);
-        fprintf(stderr, "tcpcsum_preload: batch failed: %s\n", tcpcsum_strerror(rc));
-        errno = ENXIO;
-        return -1;
-    }
-    k = 0;
-    for (unsigned int i = 0; i < vlen; ++i) {
-        if (vec[i].msg_hdr.msg_iovlen != 1 || lens[i] < 20) {
-            if (is_tx) g_st.tx_skipped++; else g_st.rx_skipped++;
-            continue;
-        }
-        const uint8_t *sp = g_stage + g_off[k];
-        uint8_t *dp = (uint8_t *) vec[i].msg_hdr.msg_iov[0].iov_base;
-        const unsigned int tot = ((unsigned) sp[2] << 8) | sp[3];
-        if (tot > lens[i]) g_status[k] |= TCPCSUM_PKT_SKIPPED;   /* claims more than was handed over */
-        if (fill && !(g_status[k] & TCPCSUM_PKT_SKIPPED)) {
-            const unsigned int tcp = (sp[0] & 15u) * 4u;
-            memcpy(dp + tcp + 16, sp + tcp + 16, 2);
-            if (g_iphdr) memcpy(dp + 10, sp + 10, 2);
-        }
-        account((int) k, fill, is_tx);
-        ++k;
+        const int ok = account((int) i, fill, is_tx);
+        if (keep) keep[i] = (unsigned char) ok;
     }
     pthread_mutex_unlock(&g_mu);
     return 0;
@@ -284,7 +236,7 @@ int sendmmsg(int fd, struct mmsghdr *vec, unsigned int vlen, int flags) {
                 const struct msghdr *h = &vec[done + i].msg_hdr;
                 lens[i] = h->msg_iovlen == 1 ? (unsigned int) h->msg_iov[0].iov_len : 0;
             }
-            if (gpu_batch(vec + done, cnt, lens, g_tx == MODE_FILL, 1)) return -1;
+            if (gpu_batch(vec + done, cnt, lens, g_tx == MODE_FILL, 1, NULL)) return -1;
             pthread_mutex_lock(&g_mu);
             g_st.tx_batches++;
             g_st.tx_packets += cnt;
@@ -298,18 +250,41 @@ int sendmmsg(int fd, struct mmsghdr *vec, unsigned int vlen, int flags) {
 int recvmmsg(int fd, struct mmsghdr *vec, unsigned int vlen, int flags, struct timespec *timeout) {
     pthread_once(&g_once, init_once);
     int r = real_recvmmsg(fd, vec, vlen, flags, timeout);
-    if (r > 0 && g_rx == MODE_VERIFY && wants_fd(fd)) {
+    if (r > 0 && g_rx != MODE_OFF && wants_fd(fd)) {
         unsigned int lens[1024];
-        unsigned int done = 0;
+        unsigned char keep[1024];
+        unsigned int done = 0, kept = 0;
         while (done < (unsigned int) r) {
             unsigned int cnt = (unsigned int) r - done < 1024 ? (unsigned int) r - done : 1024;
             for (unsigned int i = 0; i < cnt; ++i) lens[i] = vec[done + i].msg_len;
-            if (gpu_batch(vec + done, cnt, lens, 0, 0)) return -1;
+            if (gpu_batch(vec + done, cnt, lens, 0, 0, keep)) return -1;
+            if (g_rx == MODE_DROP) {
+                /* stable partition by swaps: passing messages move to the front in
+                 * arrival order; failing ones end up behind them, still in the
+                 * vector (the caller's buffers all stay referenced) */
+                for (unsigned int i = 0; i < cnt; ++i) {
+                    if (!keep[i]) continue;
+                    if (kept != done + i) {
+                        struct mmsghdr t = vec[kept];
+                        vec[kept] = vec[done + i];
+                        vec[done + i] = t;
+                    }
+                    ++kept;
+                }
+            } else {
+                kept += cnt;
+            }
             pthread_mutex_lock(&g_mu);
             g_st.rx_batches++;
             g_st.rx_packets += cnt;
             pthread_mutex_unlock(&g_mu);
             done += cnt;
+        }
+        if (g_rx == MODE_DROP) {
+            pthread_mutex_lock(&g_mu);
+            g_st.rx_dropped += (unsigned int) r - kept;
+            pthread_mutex_unlock(&g_mu);
+            r = (int) kept;
         }
     }
     return r;

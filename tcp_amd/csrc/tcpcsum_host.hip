@@ -1,0 +1,761 @@
+// tcpcsum_host.hip — the host-memory half of the C ABI (tcpcsum_ctx_*, *_host).
+//
+// The path as the reference runs it starts and ends in host memory: finished
+// packets sit in the loop's out-buffers (loop.c:107-116, 1024 separately
+// malloc'd 32 KiB buffers, loop.c:180-183) until releaseSend flushes them
+// (loop.c:27-94). A context turns such batches into kernel launches.
+//
+// Which host memory a kernel touches, and how:
+//   * memory the caller page-locked — tcpcsum_host_alloc / hipHostMalloc, a
+//     hipHostRegister of its own, or tcpcsum_ctx_register_host — is read in
+//     place by the kernel over PCIe (zero-copy), and FILL stores the checks
+//     there;
+//   * pageable memory is never page-locked behind the caller's back and never
+//     handed to a HIP copy. CPU threads copy its bytes into the context's own
+//     pinned staging — uniform batches chunk by chunk, wire batches packet by
+//     packet (only the packets, not the slack between them) — which the kernel
+//     reads over PCIe; FILL results go back as 2-byte CPU stores at TCP+16
+//     (and IP+10), exactly where context.c:208 puts them.
+//   * opt-in only (TCPCSUM_CTX_AUTO_REGISTER): tcpcsum_ipv4_batch_ptrs_host
+//     page-locks each pageable packet buffer on first use and keeps it, which
+//     suits the reference's buffers (allocated once, never freed).
+//
+// Why no per-call page-locking (round 2 did that): a registration is visible
+// to the whole process and HIP keeps page-lock state per page, shared with
+// its own pin-in-place of pageable copy sources, which it caches and which
+// hipPointerGetAttributes does not report (tools/pin_cache_probe.cpp). A
+// hipHostRegister / hipHostUnregister of a pageable range's page hull — pages
+// that can also hold other heap objects — can therefore undo a page lock HIP
+// still counts on; a later pageable hipMemcpy through that cached pin then
+// reads an unmapped page (hipErrorIllegalAddress, seen three times in round 2
+// on exactly such copies after host-path calls). A context now locks only
+// what its caller asked it to, and unlocks only that, on request.
+//
+// All checksum arithmetic runs in the gfx950 kernels of tcpcsum_kernels.hip;
+// this file reads header fields (IHL, tot_len) only to size the copies.
+
+#include <hip/hip_runtime.h>
+#include <sched.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <climits>
+#include <condition_variable>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <new>
+#include <thread>
+#include <vector>
+
+#include "host_registry.h"
+#include "tcpcsum.h"
+#include "tcpcsum_internal.h"
+
+namespace tcpcsum {
+
+// HostRegistry backend over HIP: hipHostRegister'ed pages are mapped for the
+// device (on MI355X hosts at their host address: tools/hostreg_probe.py).
+struct HipHostBackend {
+    int lock(uintptr_t lo, size_t bytes, intptr_t* delta) {
+        hipError_t e = hipHostRegister((void*)lo, bytes, hipHostRegisterMapped);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            return (int)e;
+        }
+        void* d = nullptr;
+        e = hipHostGetDevicePointer(&d, (void*)lo, 0);
+        if (e != hipSuccess || !d) {
+            (void)hipGetLastError();
+            (void)hipHostUnregister((void*)lo);
+            (void)hipGetLastError();
+            return (int)(e != hipSuccess ? e : hipErrorInvalidValue);
+        }
+        *delta = (intptr_t)d - (intptr_t)lo;
+        return 0;
+    }
+    void unlock(uintptr_t lo) {
+        if (hipHostUnregister((void*)lo) != hipSuccess) (void)hipGetLastError();   // nothing to undo
+    }
+    bool pinned_extent(uintptr_t p, uintptr_t* lo, uintptr_t* hi, intptr_t* delta) {
+        hipPointerAttribute_t a;
+        bool ok = hipPointerGetAttributes(&a, (const void*)p) == hipSuccess && a.type == hipMemoryTypeHost &&
+                  a.devicePointer;
+        uintptr_t rs = 0;
+        size_t rsz = 0;
+        ok = ok && hipPointerGetAttribute(&rs, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, (hipDeviceptr_t)p) == hipSuccess &&
+             hipPointerGetAttribute(&rsz, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, (hipDeviceptr_t)p) == hipSuccess;
+        (void)hipGetLastError();   // pageable memory: not an error for us
+        if (!ok) return false;
+        *lo = rs;
+        *hi = rs + rsz;
+        *delta = (intptr_t)a.devicePointer - (intptr_t)p;
+        return true;
+    }
+};
+
+// A few host threads for the copies into pinned staging: one core's memcpy
+// (≈10-20 GB/s) is below the PCIe rate the kernel reads staging at
+// (≈50 GiB/s), and the copy of chunk k+1 must keep pace with the kernel on
+// chunk k. The calling thread works too; workers that wake late find the job
+// done and go back to sleep (nobody waits for a sleeper to wake).
+class CopyPool {
+public:
+    explicit CopyPool(int workers) : nw_(workers < 0 ? 0 : workers) {}
+    CopyPool(const CopyPool&) = delete;
+    CopyPool& operator=(const CopyPool&) = delete;
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            quit_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    int threads() const { return nw_ + 1; }
+
+    // body(lo, hi) over [0, n) in pieces of `grain`; returns when every piece is done.
+    void run(size_t n, size_t grain, const std::function<void(size_t, size_t)>& body) {
+        if (n == 0) return;
+        if (grain == 0) grain = 1;
+        if (nw_ == 0 || n <= grain) {
+            body(0, n);
+            return;
+        }
+        start();
+        auto job = std::make_shared<Job>(&body, n, grain);
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            cur_ = job;
+            ++gen_;
+        }
+        cv_.notify_all();
+        job->drain();
+        while (job->done.load(std::memory_order_acquire) < n) std::this_thread::yield();
+        std::lock_guard<std::mutex> lk(m_);
+        if (cur_ == job) cur_.reset();
+    }
+
+private:
+    struct Job {
+        Job(const std::function<void(size_t, size_t)>* b, size_t n_, size_t g) : body(b), n(n_), grain(g) {}
+        const std::function<void(size_t, size_t)>* body;   // valid while done < n
+        size_t n, grain;
+        std::atomic<size_t> next{0}, done{0};
+        void drain() {
+            for (;;) {
+                const size_t i = next.fetch_add(grain, std::memory_order_relaxed);
+                if (i >= n) return;
+                const size_t e = std::min(n, i + grain);
+                (*body)(i, e);
+                done.fetch_add(e - i, std::memory_order_release);
+            }
+        }
+    };
+    void start() {
+        if (started_) return;
+        started_ = true;
+        try {
+            for (int i = 0; i < nw_; ++i) th_.emplace_back([this] { loop(); });
+        } catch (...) {   // fewer threads than asked: the caller still does all the work it must
+        }
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            std::shared_ptr<Job> job;
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return quit_ || gen_ != seen; });
+                if (quit_) return;
+                seen = gen_;
+                job = cur_;
+            }
+            if (job) job->drain();
+        }
+    }
+    int nw_;
+    bool started_ = false;
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_;
+    std::shared_ptr<Job> cur_;
+    uint64_t gen_ = 0;
+    bool quit_ = false;
+};
+
+// Host threads for staging copies: TCPCSUM_HOST_THREADS, else half the CPUs
+// this process may use (the affinity mask, capped by a cgroup CPU quota), 1..8.
+int default_copy_threads() {
+    if (const char* e = getenv("TCPCSUM_HOST_THREADS")) {
+        const int v = atoi(e);
+        if (v >= 1) return std::min(v, 64);
+    }
+    int cpus = 1;
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof set, &set) == 0) cpus = std::max(1, CPU_COUNT(&set));
+    if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+        char q[32] = {0};
+        long long per = 0;
+        if (fscanf(f, "%31s %lld", q, &per) == 2 && strcmp(q, "max") != 0 && per > 0) {
+            const long long quota = atoll(q);
+            if (quota > 0) cpus = std::min<long long>(cpus, std::max<long long>(1, (quota + per - 1) / per));
+        }
+        fclose(f);
+    }
+    return std::max(1, std::min(8, cpus / 2));
+}
+
+// Page-locked host memory owned by a context, with its device view.
+struct Pinned {
+    uint8_t* h = nullptr;
+    uint8_t* d = nullptr;
+    size_t bytes = 0;
+    Pinned() = default;
+    Pinned(const Pinned&) = delete;
+    Pinned& operator=(const Pinned&) = delete;
+    ~Pinned() { release(); }
+    // grow to at least `need` bytes; the caller knows no kernel is using it
+    hipError_t ensure(size_t need) {
+        if (need <= bytes) return hipSuccess;
+        size_t nb = bytes ? bytes : 4096;
+        while (nb < need) nb *= 2;
+        release();
+        void* p = nullptr;
+        hipError_t e = hipHostMalloc(&p, nb, hipHostMallocDefault);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            return e;
+        }
+        void* dp = nullptr;
+        e = hipHostGetDevicePointer(&dp, p, 0);
+        if (e != hipSuccess || !dp) {
+            (void)hipGetLastError();
+            (void)hipHostFree(p);
+            return e != hipSuccess ? e : hipErrorInvalidValue;
+        }
+        h = (uint8_t*)p;
+        d = (uint8_t*)dp;
+        bytes = nb;
+        return hipSuccess;
+    }
+    void release() {
+        if (h) (void)hipHostFree(h);
+        h = d = nullptr;
+        bytes = 0;
+    }
+};
+
+}  // namespace tcpcsum
+
+using tcpcsum::check_launch;
+using tcpcsum::get_tuning;
+using tcpcsum::hip_fail;
+using tcpcsum::require_device;
+
+// Auto-registration budget (TCPCSUM_CTX_AUTO_REGISTER): the reference's two
+// pools are 2 x 1024 x 32 KiB = 64 MiB (loop.c:180-183); past this much, new
+// buffers are copied instead of page-locked.
+constexpr uint64_t kAutoRegisterBudget = 256ull << 20;
+// Staging chunk per pipeline slot for pageable uniform batches (0 = default).
+constexpr size_t kDefaultChunk = 16u << 20;
+
+struct tcpcsum_ctx {
+    int device = 0;
+    size_t chunk = 0;
+    uint32_t flags = 0;
+    hipStream_t st[2] = {nullptr, nullptr};
+    hipEvent_t slot_ev[2] = {nullptr, nullptr};
+    bool slot_busy[2] = {false, false};
+    tcpcsum::Pinned slot[2];   // uniform batches: one staged chunk per stream
+    tcpcsum::Pinned gath;      // wire batches: packets copied out of pageable memory
+    tcpcsum::Pinned ss, res;   // per-segment start values / results, when the caller's are pageable
+    // per-packet arrays the wire kernels read (addresses, bounds) and write
+    // (results, status), kept in pinned memory so a pageable caller array costs
+    // a CPU memcpy rather than a HIP copy
+    tcpcsum::Pinned p_off, p_len, p_out, p_stat;
+    // gathered packets of the current batch: index, source, staging offset, bytes
+    std::vector<uint64_t> g_idx, g_off;
+    std::vector<uint8_t*> g_src;
+    std::vector<uint32_t> g_len;
+    tcpcsum::Tuning tune;
+    tcpcsum::HipHostBackend backend;
+    tcpcsum::HostRegistry<tcpcsum::HipHostBackend> reg{backend};
+    std::unique_ptr<tcpcsum::CopyPool> pool;
+    tcpcsum_ctx_stats_t stats{};
+    std::mutex mu;
+};
+
+namespace {
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) hipSetDevice(prev);
+    }
+};
+
+// Device-visible address of page-locked (hipHostMalloc / hipHostRegister'ed)
+// host memory [p, p + bytes), or nullptr when any of it is pageable. Kernels
+// read and write such memory directly over PCIe. The whole range must lie in
+// ONE page-locked allocation or registration: a range locked only in part
+// (its first page locked by a neighbouring registration, say) is staged.
+void* pinned_dev_ptr(const void* p, size_t bytes = 1) {
+    if (!p) return nullptr;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();   // pageable memory: not an error for us
+        return nullptr;
+    }
+    if (a.type != hipMemoryTypeHost || !a.devicePointer) return nullptr;
+    uintptr_t rs = 0;
+    size_t rsz = 0;
+    if (hipPointerGetAttribute(&rs, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, (hipDeviceptr_t)p) != hipSuccess ||
+        hipPointerGetAttribute(&rsz, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, (hipDeviceptr_t)p) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    const uintptr_t b = (uintptr_t)p;
+    if (rs > b || b + (bytes ? bytes : 1) > rs + rsz) return nullptr;
+    return a.devicePointer;
+}
+
+// memcpy on the context's copy threads (pieces of 256 KiB).
+void par_copy(tcpcsum_ctx* c, void* dst, const void* src, size_t n) {
+    constexpr size_t kGrain = 256u << 10;
+    uint8_t* d = (uint8_t*)dst;
+    const uint8_t* s = (const uint8_t*)src;
+    c->pool->run(n, kGrain, [&](size_t lo, size_t hi) { memcpy(d + lo, s + lo, hi - lo); });
+}
+
+int ensure_pkt_arrays(tcpcsum_ctx* c, uint64_t n) {
+    hipError_t e = c->p_off.ensure(n * sizeof(uint64_t));
+    if (e == hipSuccess) e = c->p_len.ensure(n * sizeof(uint32_t));
+    if (e == hipSuccess) e = c->p_out.ensure(n * sizeof(uint16_t));
+    if (e == hipSuccess) e = c->p_stat.ensure(n);
+    if (e != hipSuccess) {
+        tcpcsum::note_hip_error((int)e);
+        return TCPCSUM_ENOMEM;
+    }
+    return TCPCSUM_OK;
+}
+
+// Copy the packets listed in g_* into c->gath (each at a 16-B aligned offset)
+// and point their kernel addresses there. Packets are few KiB each: pieces of
+// 16 packets per thread.
+int gather_packets(tcpcsum_ctx* c, uint64_t* k_off, size_t total) {
+    const size_t m = c->g_idx.size();
+    if (!m) return TCPCSUM_OK;
+    hipError_t e = c->gath.ensure(total ? total : 16);
+    if (e != hipSuccess) {
+        tcpcsum::note_hip_error((int)e);
+        return TCPCSUM_ENOMEM;
+    }
+    uint8_t* gh = c->gath.h;
+    c->pool->run(m, 16, [&](size_t lo, size_t hi) {
+        for (size_t k = lo; k < hi; ++k) memcpy(gh + c->g_off[k], c->g_src[k], c->g_len[k]);
+    });
+    for (size_t k = 0; k < m; ++k) k_off[c->g_idx[k]] = (uint64_t)(uintptr_t)(c->gath.d + c->g_off[k]);
+    c->stats.pkts_staged += m;
+    c->stats.bytes_staged += total;
+    return TCPCSUM_OK;
+}
+
+// FILL on staged packets: the kernel stored each check in the staging copy;
+// put it (and the IPv4 header checksum, with IPHDR) into the caller's packet.
+void write_back_checks(tcpcsum_ctx* c, const uint8_t* status, bool iphdr) {
+    const size_t m = c->g_idx.size();
+    for (size_t k = 0; k < m; ++k) {
+        if (status[c->g_idx[k]] != TCPCSUM_PKT_OK) continue;
+        const uint8_t* sp = c->gath.h + c->g_off[k];
+        uint8_t* dp = c->g_src[k];
+        const unsigned tcp = (sp[0] & 15u) * 4u;
+        memcpy(dp + tcp + 16, sp + tcp + 16, 2);   // context.c:208: native u16 at TCP+16
+        if (iphdr) memcpy(dp + 10, sp + 10, 2);
+    }
+}
+
+// Bytes of a wire packet worth copying: its tot_len (at least the 20-byte IP
+// header), never more than `bound` readable bytes. A packet whose tot_len
+// exceeds the bound keeps tot_len > copied bytes and is SKIPPED by the
+// kernel exactly as when it is read in place.
+inline uint32_t copy_len(const uint8_t* ip, uint64_t bound) {
+    const uint32_t tot = ((uint32_t)ip[2] << 8) | ip[3];
+    const uint64_t want = tot < 20u ? 20u : tot;
+    return (uint32_t)std::min<uint64_t>(want, bound);
+}
+
+}  // namespace
+
+extern "C" {
+
+int tcpcsum_ctx_create(int device, size_t scratch_bytes, tcpcsum_ctx_t** out) {
+    if (!out) return TCPCSUM_EINVAL;
+    *out = nullptr;
+    int count = 0;
+    hipError_t e = hipGetDeviceCount(&count);
+    if (e != hipSuccess || device < 0 || device >= count) {
+        tcpcsum::note_hip_error((int)e);
+        return TCPCSUM_ENODEV;
+    }
+    DeviceGuard g(device);
+    int rc = require_device(nullptr, 0);
+    if (rc) return rc;
+    tcpcsum_ctx* c = new (std::nothrow) tcpcsum_ctx();
+    if (!c) return TCPCSUM_ENOMEM;
+    c->device = device;
+    c->chunk = scratch_bytes ? scratch_bytes : kDefaultChunk;
+    c->pool.reset(new (std::nothrow) tcpcsum::CopyPool(tcpcsum::default_copy_threads() - 1));
+    if (!c->pool) {
+        delete c;
+        return TCPCSUM_ENOMEM;
+    }
+    c->stats.copy_threads = (uint64_t)c->pool->threads();
+    for (int i = 0; i < 2; ++i) {
+        e = hipStreamCreateWithFlags(&c->st[i], hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&c->slot_ev[i], hipEventDisableTiming);
+        if (e != hipSuccess) {
+            tcpcsum_ctx_destroy(c);
+            return hip_fail(e);
+        }
+    }
+    *out = c;
+    return TCPCSUM_OK;
+}
+
+void tcpcsum_ctx_destroy(tcpcsum_ctx_t* c) {
+    if (!c) return;
+    DeviceGuard g(c->device);
+    for (int i = 0; i < 2; ++i)
+        if (c->st[i]) hipStreamSynchronize(c->st[i]);
+    c->reg.release(0, 0);
+    for (int i = 0; i < 2; ++i) {
+        if (c->slot_ev[i]) hipEventDestroy(c->slot_ev[i]);
+        if (c->st[i]) hipStreamDestroy(c->st[i]);
+    }
+    delete c;   // pinned buffers and copy threads go with it
+}
+
+int tcpcsum_ctx_set_tuning(tcpcsum_ctx_t* c, const tcpcsum_tuning_t* tune) {
+    if (!c) return TCPCSUM_EINVAL;
+    tcpcsum::Tuning tu;
+    if (get_tuning(tune, &tu)) return TCPCSUM_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->tune = tu;
+    return TCPCSUM_OK;
+}
+
+int tcpcsum_ctx_set_flags(tcpcsum_ctx_t* c, uint32_t flags) {
+    if (!c || (flags & ~(uint32_t)TCPCSUM_CTX_AUTO_REGISTER)) return TCPCSUM_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->flags = flags;
+    return TCPCSUM_OK;
+}
+
+int tcpcsum_ctx_get_stats(tcpcsum_ctx_t* c, tcpcsum_ctx_stats_t* out) {
+    if (!c || !out) return TCPCSUM_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->stats.registered_ranges = c->reg.owned_ranges();
+    c->stats.registered_bytes = c->reg.owned_bytes();
+    *out = c->stats;
+    return TCPCSUM_OK;
+}
+
+void* tcpcsum_host_alloc(size_t bytes) {
+    void* p = nullptr;
+    if (!bytes) return nullptr;
+    hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        tcpcsum::note_hip_error((int)e);
+        return nullptr;
+    }
+    return p;
+}
+
+void tcpcsum_host_free(void* p) {
+    if (p) hipHostFree(p);
+}
+
+// Page-locked input: one launch reads the segments in place. Pageable input:
+// chunks alternate between two streams and two pinned staging slots; the copy
+// threads fill slot k&1 with chunk k while the kernel reads chunk k-1 from the
+// other slot. Start values and results use the caller's arrays when those are
+// page-locked, else pinned staging (copied in / out by the CPU).
+int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t stride, uint32_t len,
+                               const uint32_t* h_sum_start, uint32_t sum_start, uint16_t* h_out, uint64_t n) {
+    if (!c) return TCPCSUM_EINVAL;
+    if (n == 0) return TCPCSUM_OK;
+    if (!h_base || !h_out || len > (uint32_t)INT_MAX) return TCPCSUM_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    const tcpcsum::Tuning tu = c->tune;
+    c->stats.batches++;
+    hipError_t e;
+    int rc;
+    const uint32_t* kss = nullptr;
+    if (h_sum_start) {
+        kss = (const uint32_t*)pinned_dev_ptr(h_sum_start, n * sizeof(uint32_t));
+        if (!kss) {
+            e = c->ss.ensure(n * sizeof(uint32_t));
+            if (e != hipSuccess) return hip_fail(e);
+            par_copy(c, c->ss.h, h_sum_start, n * sizeof(uint32_t));
+            kss = (const uint32_t*)c->ss.d;
+        }
+    }
+    uint16_t* kout = (uint16_t*)pinned_dev_ptr(h_out, n * sizeof(uint16_t));
+    const bool out_staged = kout == nullptr;
+    if (out_staged) {
+        e = c->res.ensure(n * sizeof(uint16_t));
+        if (e != hipSuccess) return hip_fail(e);
+        kout = (uint16_t*)c->res.d;
+    }
+    const size_t span = (size_t)((n - 1) * stride + len);
+    if (const uint8_t* zb = (const uint8_t*)pinned_dev_ptr(h_base, span)) {
+        tcpcsum::launch_uniform(zb, stride, len, kss, sum_start, kout, n, c->st[0], tu);
+        rc = check_launch();
+        if (rc) return rc;
+        e = hipStreamSynchronize(c->st[0]);
+        if (e != hipSuccess) return hip_fail(e);
+    } else {
+        // segments per chunk: (cnt-1)*stride + len <= chunk (at least one segment)
+        uint64_t per = 1;
+        if (stride == 0) per = n;
+        else if (c->chunk > len) per = (c->chunk - len) / stride + 1;
+        if (per > n) per = n;
+        const size_t slot_bytes = (size_t)((per - 1) * stride + len) + 16;
+        for (int i = 0; i < 2; ++i) {
+            e = c->slot[i].ensure(slot_bytes);
+            if (e != hipSuccess) return hip_fail(e);
+        }
+        uint64_t k = 0;
+        for (uint64_t s0 = 0; s0 < n; s0 += per, ++k) {
+            const int s = (int)(k & 1);
+            const uint64_t cnt = (n - s0) < per ? (n - s0) : per;
+            const size_t bytes = (size_t)((cnt - 1) * stride + len);
+            const uint8_t* src = (const uint8_t*)h_base + s0 * stride;
+            if (c->slot_busy[s]) {   // the kernel that last read this slot (chunk k-2)
+                c->slot_busy[s] = false;
+                e = hipEventSynchronize(c->slot_ev[s]);
+                if (e != hipSuccess) return hip_fail(e);
+            }
+            // keep the start's alignment mod 16, so the kernel shape matches what the
+            // same batch gets in place
+            const size_t mis = (uintptr_t)src & 15u;
+            par_copy(c, c->slot[s].h + mis, src, bytes);
+            c->stats.bytes_staged += bytes;
+            tcpcsum::launch_uniform(c->slot[s].d + mis, stride, len, kss ? kss + s0 : nullptr, sum_start,
+                                    kout + s0, cnt, c->st[s], tu);
+            rc = check_launch();
+            if (rc) return rc;
+            e = hipEventRecord(c->slot_ev[s], c->st[s]);
+            if (e != hipSuccess) return hip_fail(e);
+            c->slot_busy[s] = true;
+        }
+        for (int i = 0; i < 2; ++i) {
+            c->slot_busy[i] = false;
+            e = hipStreamSynchronize(c->st[i]);
+            if (e != hipSuccess) return hip_fail(e);
+        }
+    }
+    if (out_staged) par_copy(c, h_out, c->res.h, n * sizeof(uint16_t));
+    return TCPCSUM_OK;
+}
+
+// Wire batch in one host region. A region that one page-locked allocation
+// covers is read (FILL: written) in place over PCIe. A pageable region: the
+// packets — not the slack between them — are copied into pinned staging, the
+// kernel runs over the copies, and FILL's checks are stored back into the
+// caller's packets. Per-packet arrays go through pinned staging when the
+// caller's are pageable.
+int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t* c, void* h_pkts, size_t region_bytes, const uint64_t* h_pkt_off,
+                            uint64_t n, uint32_t cap, int mode, uint16_t* h_out, uint8_t* h_status) {
+    if (!c) return TCPCSUM_EINVAL;
+    if (n == 0) return TCPCSUM_OK;
+    if (!h_pkts || !h_pkt_off || !region_bytes || (mode & ~3)) return TCPCSUM_EINVAL;
+    if (cap > 65535u) cap = 65535u;
+    // every packet header must lie inside the region; packets whose tot_len
+    // runs past its end are SKIPPED by the kernel (limit = region_bytes)
+    for (uint64_t i = 0; i < n; ++i)
+        if (h_pkt_off[i] > region_bytes || region_bytes - h_pkt_off[i] < 20u) return TCPCSUM_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    hipStream_t st = c->st[0];
+    c->stats.batches++;
+    int rc = ensure_pkt_arrays(c, n);
+    if (rc) return rc;
+    uint16_t* zout = h_out ? (uint16_t*)pinned_dev_ptr(h_out, n * sizeof(uint16_t)) : nullptr;
+    uint8_t* zst = h_status ? (uint8_t*)pinned_dev_ptr(h_status, n) : nullptr;
+    uint16_t* kout = zout ? zout : (uint16_t*)c->p_out.d;
+    uint8_t* kst = zst ? zst : c->p_stat.d;
+    const bool fill = (mode & TCPCSUM_IPV4_VERIFY) == 0;
+    // zero-copy over PCIe: 16-lane groups, 512 B per round (more waves with
+    // reads in flight) beat the HBM-tuned MTU shape — 1024 x 1500-B FILL
+    // batch 49 vs 59 us on MI355X (tools/e2e.py --sweep)
+    tcpcsum::Tuning tu = c->tune;
+    if (tu.shape < 0 && n < 65536u) tu.shape = 3;
+    hipError_t e;
+    uint8_t* zp = (uint8_t*)pinned_dev_ptr(h_pkts, region_bytes);
+    c->g_idx.clear();
+    if (zp) {
+        const uint64_t* koff = (const uint64_t*)pinned_dev_ptr(h_pkt_off, n * sizeof(uint64_t));
+        if (!koff) {
+            memcpy(c->p_off.h, h_pkt_off, n * sizeof(uint64_t));
+            koff = (const uint64_t*)c->p_off.d;
+        }
+        c->stats.pkts_in_place += n;
+        tcpcsum::launch_ipv4(zp, koff, nullptr, n, cap, (uint64_t)region_bytes, (uint64_t)region_bytes, mode, kout,
+                             kst, nullptr, st, tu);
+    } else {
+        // the region's packets, copied into staging and addressed one by one
+        // (the scatter-gather kernel, bounded per packet by the bytes copied)
+        uint64_t* k_off = (uint64_t*)c->p_off.h;
+        uint32_t* k_len = (uint32_t*)c->p_len.h;
+        uint8_t* base = (uint8_t*)h_pkts;
+        size_t total = 0;
+        uint32_t maxl = 20;
+        c->g_off.resize(n);
+        c->g_src.resize(n);
+        c->g_len.resize(n);
+        c->g_idx.resize(n);
+        for (uint64_t i = 0; i < n; ++i) {
+            uint8_t* ip = base + h_pkt_off[i];
+            const uint32_t cl = copy_len(ip, std::min<uint64_t>(cap, region_bytes - h_pkt_off[i]));
+            c->g_idx[i] = i;
+            c->g_src[i] = ip;
+            c->g_len[i] = cl;
+            c->g_off[i] = total;
+            total += ((size_t)cl + 15u) & ~(size_t)15u;
+            k_len[i] = cl;
+            maxl = std::max(maxl, cl);
+        }
+        rc = gather_packets(c, k_off, total);
+        if (rc) return rc;
+        tcpcsum::launch_ipv4(nullptr, (const uint64_t*)c->p_off.d, (const uint32_t*)c->p_len.d, n, maxl, ~0ull,
+                             total, mode, kout, kst, nullptr, st, tu);
+    }
+    rc = check_launch();
+    if (rc) return rc;
+    e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return hip_fail(e);
+    if (fill && !c->g_idx.empty())
+        write_back_checks(c, zst ? h_status : c->p_stat.h, (mode & TCPCSUM_IPV4_IPHDR) != 0);
+    if (h_out && !zout) memcpy(h_out, c->p_out.h, n * sizeof(uint16_t));
+    if (h_status && !zst) memcpy(h_status, c->p_stat.h, n);
+    return TCPCSUM_OK;
+}
+
+// Wire batch over the caller's own per-packet buffers (the loop's layout).
+// Each packet is read in place when one page-locked mapping covers it (the
+// context's registrations, or memory someone else page-locked), else copied
+// into pinned staging — or, with TCPCSUM_CTX_AUTO_REGISTER, its pages are
+// locked now and kept (within kAutoRegisterBudget).
+int tcpcsum_ipv4_batch_ptrs_host(tcpcsum_ctx_t* c, void* const* h_pkts, const uint32_t* h_lens, uint64_t n, int mode,
+                                 uint16_t* h_out, uint8_t* h_status) {
+    if (!c) return TCPCSUM_EINVAL;
+    if (n == 0) return TCPCSUM_OK;
+    if (!h_pkts || !h_lens || (mode & ~3)) return TCPCSUM_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    hipStream_t st = c->st[0];
+    c->stats.batches++;
+    int rc = ensure_pkt_arrays(c, n);
+    if (rc) return rc;
+    const bool may_lock = (c->flags & TCPCSUM_CTX_AUTO_REGISTER) != 0;
+    // memory page-locked by someone else is looked up afresh each batch (its
+    // owner may have freed it)
+    c->reg.forget_foreign();
+    uint64_t* k_off = (uint64_t*)c->p_off.h;
+    uint32_t* k_len = (uint32_t*)c->p_len.h;
+    c->g_idx.clear();
+    c->g_off.clear();
+    c->g_src.clear();
+    c->g_len.clear();
+    uint64_t foot = 0;
+    size_t total = 0;
+    uint32_t cap = 20;
+    uint64_t in_place = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        uint32_t len = h_lens[i] > 65535u ? 65535u : h_lens[i];   // tot_len is a u16
+        uint8_t* p = (uint8_t*)h_pkts[i];
+        k_off[i] = 0;
+        if (len < 20u || !p) {   // too short for an IP header: SKIPPED, nothing is read
+            k_len[i] = 0;
+            continue;
+        }
+        uintptr_t dev = 0;
+        if (c->reg.resolve((uintptr_t)p, len, may_lock, kAutoRegisterBudget, &dev) == 0) {
+            k_off[i] = dev;
+            ++in_place;
+        } else {
+            len = copy_len(p, len);
+            c->g_idx.push_back(i);
+            c->g_src.push_back(p);
+            c->g_len.push_back(len);
+            c->g_off.push_back(total);
+            total += ((size_t)len + 15u) & ~(size_t)15u;
+        }
+        k_len[i] = len;
+        foot += len;
+        cap = len > cap ? len : cap;
+    }
+    if (c->reg.last_lock_error()) tcpcsum::note_hip_error(c->reg.last_lock_error());
+    c->stats.pkts_in_place += in_place;
+    rc = gather_packets(c, k_off, total);
+    if (rc) return rc;
+    uint16_t* zout = h_out ? (uint16_t*)pinned_dev_ptr(h_out, n * sizeof(uint16_t)) : nullptr;
+    uint8_t* zst = h_status ? (uint8_t*)pinned_dev_ptr(h_status, n) : nullptr;
+    // zero-copy over PCIe: the 16-lane group shape for latency-bound batches
+    // (as tcpcsum_ipv4_batch_host on a pinned pool)
+    tcpcsum::Tuning tu = c->tune;
+    if (tu.shape < 0 && n < 65536u) tu.shape = 3;
+    tcpcsum::launch_ipv4(nullptr, (const uint64_t*)c->p_off.d, (const uint32_t*)c->p_len.d, n, cap, ~0ull, foot,
+                         mode, zout ? zout : (uint16_t*)c->p_out.d, zst ? zst : c->p_stat.d, nullptr, st, tu);
+    rc = check_launch();
+    if (rc) return rc;
+    hipError_t e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return hip_fail(e);
+    if ((mode & TCPCSUM_IPV4_VERIFY) == 0 && !c->g_idx.empty())
+        write_back_checks(c, zst ? h_status : c->p_stat.h, (mode & TCPCSUM_IPV4_IPHDR) != 0);
+    if (h_out && !zout) memcpy(h_out, c->p_out.h, n * sizeof(uint16_t));
+    if (h_status && !zst) memcpy(h_status, c->p_stat.h, n);
+    return TCPCSUM_OK;
+}
+
+int tcpcsum_ctx_register_host(tcpcsum_ctx_t* c, void* p, size_t bytes) {
+    if (!c || !p || !bytes) return TCPCSUM_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    const int rc = c->reg.lock_range((uintptr_t)p, bytes);
+    if (rc) {
+        tcpcsum::note_hip_error(rc);
+        return TCPCSUM_EHIP;
+    }
+    return TCPCSUM_OK;
+}
+
+int tcpcsum_ctx_unregister_host(tcpcsum_ctx_t* c, void* p, size_t bytes) {
+    if (!c) return TCPCSUM_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    for (int i = 0; i < 2; ++i) (void)hipStreamSynchronize(c->st[i]);
+    c->reg.release((uintptr_t)p, bytes);
+    return TCPCSUM_OK;
+}
+
+int tcpcsum_ctx_registered(tcpcsum_ctx_t* c, uint64_t* ranges, uint64_t* bytes) {
+    if (!c) return TCPCSUM_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (ranges) *ranges = c->reg.owned_ranges();
+    if (bytes) *bytes = c->reg.owned_bytes();
+    return TCPCSUM_OK;
+}
+
+}  // extern "C"

@@ -51,4 +51,11 @@ void launch_synth_pseudo(uint32_t* ss, uint64_t seg0, uint64_t n, uint32_t seg_l
 // returns the grid size (= partials written)
 int launch_probe(const uint8_t* src, uint64_t nbytes, uint64_t* partials, hipStream_t s, const Tuning& tu);
 
+// Shared by the two C-ABI translation units (tcpcsum_api.hip, tcpcsum_host.hip).
+void note_hip_error(int e);                              // diagnostics: tcpcsum_last_hip_error
+int hip_fail(hipError_t e);                              // note e, return TCPCSUM_EHIP
+int get_tuning(const tcpcsum_tuning_t* t, Tuning* out);  // validate; NULL = defaults
+int require_device(char* arch, size_t arch_len);         // current device is a gfx950
+int check_launch();                                      // hipGetLastError -> status
+
 }  // namespace tcpcsum

@@ -3,17 +3,20 @@
  * does (loop.c:27-94 releaseSend, loop.c:22-25 fetchPackageBatch), over UDP
  * loopback so no root is needed. Run under LD_PRELOAD=libtcpcsum_preload.so.
  *
- *   mmsg_loop <npkts> <out-file> [cpu-checks]
+ *   mmsg_loop <npkts> <out-file> [cpu-checks | corrupt]
  *
  * Builds npkts IPv4/TCP packets in separate 32 KiB malloc'd buffers (as
  * loop.c:180-183 allocates them) with the reference's framing
  * (context.c:169-206): check = 0, or — with "cpu-checks" — the check the
  * reference's CPU path would store (tcpcsum_continue == csum_continue,
- * context.c:208). Sends them with sendmmsg in batches of <= 1024 and
- * receives them with recvmmsg. Writes to <out-file>: for every packet
- * u32 length + the bytes as built, then u32 length + the bytes as received.
- * Exit 0 on success; 3 if sendmmsg failed (errno printed); 4 if recvmmsg
- * failed; 5 if a packet went missing.
+ * context.c:208). "corrupt": CPU checks, then one TCP header byte (the
+ * window's low byte) of every 7th packet flipped after the check was taken,
+ * so those no longer verify; the receiver then expects only the others (the
+ * interposer's TCPCSUM_PRELOAD_RX=drop). Sends them with sendmmsg in batches
+ * of <= 1024 and receives them with recvmmsg. Writes to <out-file>: for every
+ * packet u32 length + the bytes as built, then u32 length + the bytes as
+ * received (length 0: never received). Exit 0 on success; 3 if sendmmsg
+ * failed (errno printed); 4 if recvmmsg failed; 5 if a packet went missing.
  */
 #define _GNU_SOURCE
 #include <arpa/inet.h>
@@ -24,6 +27,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/socket.h>
+#include <time.h>
 #include <unistd.h>
 
 #include "tcpcsum.h"
@@ -34,7 +38,7 @@ static uint32_t next32(void) {
     return (uint32_t) (rng >> 16);
 }
 
-static size_t build(uint8_t *b, int i, int cpu_checks) {
+static size_t build(uint8_t *b, int i, int cpu_checks, int corrupt) {
     size_t payload = (size_t) (next32() % 1457);            /* 0 .. 1456 (1500-B MTU) */
     size_t tot = 20 + 24 + payload;
     memset(b, 0, 44);
@@ -57,13 +61,15 @@ static size_t build(uint8_t *b, int i, int cpu_checks) {
                                       (const char *) t, (int) (24 + payload));
         memcpy(t + 16, &c, 2);
     }
+    if (corrupt && i % 7 == 3) t[15] ^= 0x5a;
     return tot;
 }
 
 int main(int argc, char **argv) {
     if (argc < 3) { fprintf(stderr, "usage: %s npkts out [cpu-checks]\n", argv[0]); return 2; }
     int n = atoi(argv[1]);
-    int cpu_checks = argc > 3 && !strcmp(argv[3], "cpu-checks");
+    int corrupt = argc > 3 && !strcmp(argv[3], "corrupt");
+    int cpu_checks = corrupt || (argc > 3 && !strcmp(argv[3], "cpu-checks"));
     FILE *f = fopen(argv[2], "wb");
     if (!f || n <= 0) return 2;
     int rx = socket(AF_INET, SOCK_DGRAM, 0), tx = socket(AF_INET, SOCK_DGRAM, 0);
@@ -77,10 +83,11 @@ int main(int argc, char **argv) {
     uint8_t **orig = calloc((size_t) n, sizeof *orig);
     for (int i = 0; i < n; ++i) {
         out[i] = malloc(32768); in[i] = malloc(32768);
-        olen[i] = build(out[i], i, cpu_checks);
+        olen[i] = build(out[i], i, cpu_checks, corrupt);
         orig[i] = malloc(olen[i]);
         memcpy(orig[i], out[i], olen[i]);
     }
+    int drops_only = 0;
     enum { B = 64 };   /* stay below the default socket receive buffer per burst */
     struct mmsghdr mv[B];
     struct iovec iv[B];
@@ -98,19 +105,35 @@ int main(int argc, char **argv) {
             if (r < 0) { fprintf(stderr, "sendmmsg: %s\n", strerror(errno)); return 3; }
             sent += r;
         }
+        int want = cnt;   /* corrupt: the 7th-packet corruptions are dropped on receipt */
+        if (corrupt)
+            for (int k = 0; k < cnt; ++k) want -= (s0 + k) % 7 == 3;
+        static uint8_t scratch[B][32768];
         int got = 0;
-        while (got < cnt) {
+        while (got < want) {
             memset(mv, 0, sizeof mv);
             for (int k = 0; k < cnt - got; ++k) {
-                iv[k].iov_base = in[s0 + got + k]; iv[k].iov_len = 32768;
+                iv[k].iov_base = scratch[k]; iv[k].iov_len = 32768;
                 mv[k].msg_hdr.msg_iov = &iv[k]; mv[k].msg_hdr.msg_iovlen = 1;
             }
             struct timespec to = {5, 0};
             int r = recvmmsg(rx, mv, (unsigned) (cnt - got), MSG_WAITFORONE, &to);
             if (r < 0) { fprintf(stderr, "recvmmsg: %s\n", strerror(errno)); return 4; }
-            if (r == 0) return 5;
-            for (int k = 0; k < r; ++k) ilen[s0 + got + k] = mv[k].msg_len;
+            if (r == 0 && !corrupt) return 5;
+            for (int k = 0; k < r; ++k) {
+                /* which packet: daddr = 10.x.y.z carries its index */
+                const uint8_t *b = (const uint8_t *) mv[k].msg_hdr.msg_iov[0].iov_base;
+                const int idx = mv[k].msg_len >= 20 ? (b[17] << 16) | (b[18] << 8) | b[19] : -1;
+                if (idx < s0 || idx >= s0 + cnt || ilen[idx]) { fprintf(stderr, "unexpected message\n"); return 5; }
+                memcpy(in[idx], b, mv[k].msg_len);
+                ilen[idx] = mv[k].msg_len;
+            }
             got += r;
+            if (r == 0) {   /* every message of this receive was dropped: wait for the rest */
+                struct timespec ts = {0, 1000000};
+                nanosleep(&ts, NULL);
+                if (++drops_only > 5000) return 5;
+            }
         }
     }
     for (int i = 0; i < n; ++i) {

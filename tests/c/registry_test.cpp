@@ -1,8 +1,9 @@
 // registry_test.cpp — CPU unit test of tcp_amd/csrc/host_registry.h (the page
-// locking behind tcpcsum_ipv4_batch_ptrs_host) against a fake backend that
+// lookup behind tcpcsum_ipv4_batch_ptrs_host) against a fake backend that
 // models a host: every resolved packet must lie entirely in locked pages
 // (ours or someone else's) under ONE device mapping, pages are never locked
-// twice, and release() unlocks exactly what was locked.
+// twice, nothing is locked unless the caller allows it, nothing is ever
+// unlocked during a lookup, and release() unlocks exactly what was locked.
 //
 //   registry_test [seed]   exit 0 when every check holds
 #include <cstdio>
@@ -34,7 +35,7 @@ struct FakeHost {
     std::map<uintptr_t, Lock> locks;   // ours, by start
     std::vector<Lock> foreign;         // page-locked by someone else (tcpcsum_host_alloc)
     std::mt19937_64 rng{1};
-    uint64_t lock_calls = 0;
+    uint64_t lock_calls = 0, unlock_calls = 0, extent_calls = 0;
 
     int lock(uintptr_t lo, size_t bytes, intptr_t* delta) {
         CHECK(lo % kHostPage == 0 && bytes % kHostPage == 0 && bytes > 0);
@@ -48,8 +49,10 @@ struct FakeHost {
     void unlock(uintptr_t lo) {
         CHECK(locks.count(lo) == 1);
         locks.erase(lo);
+        ++unlock_calls;
     }
     bool pinned_extent(uintptr_t p, uintptr_t* lo, uintptr_t* hi, intptr_t* delta) {
+        ++extent_calls;
         for (const auto& f : foreign)
             if (f.lo <= p && p < f.hi) { *lo = f.lo; *hi = f.hi; *delta = f.delta; return true; }
         for (const auto& kv : locks)
@@ -59,12 +62,16 @@ struct FakeHost {
         return false;
     }
     // the mapping that holds byte a, or nullptr
+    // (device mappings are page granular: the rest of a foreign allocation's last page is mapped too)
     const Lock* holder(uintptr_t a) const {
-        for (const auto& f : foreign) if (f.lo <= a && a < f.hi) return &f;
+        for (const auto& f : foreign)
+            if ((f.lo & ~(kHostPage - 1)) <= a && a < ((f.hi + kHostPage - 1) & ~(kHostPage - 1))) return &f;
         for (const auto& kv : locks) if (kv.second.lo <= a && a < kv.second.hi) return &kv.second;
         return nullptr;
     }
 };
+
+using Reg = tcpcsum::HostRegistry<FakeHost>;
 
 // [p, p+len) -> dev is safe: every byte's page is mapped, and dev + k is where byte p + k lives.
 static void check_mapping(const FakeHost& h, uintptr_t p, size_t len, uintptr_t dev) {
@@ -83,7 +90,7 @@ static void scenario(bool flat, uint64_t seed) {
     h.flat = flat;
     h.rng.seed(seed);
     std::mt19937_64 r(seed * 7 + 3);
-    tcpcsum::HostRegistry<FakeHost> reg(h);
+    Reg reg(h);
     // a heap: buffers laid end to end with 16-B headers, like malloc; some are
     // "pinned" allocations (page-aligned, locked by someone else)
     struct Buf { uintptr_t p; size_t n; };
@@ -109,8 +116,12 @@ static void scenario(bool flat, uint64_t seed) {
             const size_t len = 20 + r() % (b.n - 20 < 1500 ? b.n - 20 : 1500);
             const size_t off = r() % (b.n - len + 1);
             uintptr_t dev = 0;
-            const int rc = reg.resolve(b.p + off, len, &dev);
-            CHECK(rc == 0);
+            const uint64_t unlocks = h.unlock_calls;
+            const int rc = reg.resolve(b.p + off, len, true, UINT64_MAX, &dev);
+            CHECK(h.unlock_calls == unlocks);   // a lookup never unlocks anything
+            // flat hosts: every packet maps; otherwise a packet across two locks mapped
+            // at unrelated offsets is refused (the caller copies it) rather than re-locked
+            CHECK(rc == 0 || (!flat && rc == Reg::kUnmappable));
             if (rc == 0) check_mapping(h, b.p + off, len, dev);
         }
         // what the registry owns is what the backend has locked
@@ -131,10 +142,10 @@ static void scenario(bool flat, uint64_t seed) {
             pk.push_back({b.p, 20 + r() % (b.n - 20 < 1500 ? b.n - 20 : 1500)});
         }
         uintptr_t dev;
-        for (auto& x : pk) CHECK(reg.resolve(x.first, x.second, &dev) == 0);
+        for (auto& x : pk) CHECK(reg.resolve(x.first, x.second, true, UINT64_MAX, &dev) == 0);
         const uint64_t calls = h.lock_calls;
         for (auto& x : pk) {
-            CHECK(reg.resolve(x.first, x.second, &dev) == 0);
+            CHECK(reg.resolve(x.first, x.second, false, 0, &dev) == 0);
             CHECK(dev == x.first);
         }
         CHECK(h.lock_calls == calls);
@@ -150,7 +161,7 @@ static void scenario(bool flat, uint64_t seed) {
 static void two_registries(uint64_t seed) {
     FakeHost h;
     std::mt19937_64 r(seed);
-    tcpcsum::HostRegistry<FakeHost> a(h), b(h);
+    Reg a(h), b(h);
     std::vector<std::pair<uintptr_t, size_t>> bufs;
     uintptr_t cur = 0x7e0000002010ull;
     for (int i = 0; i < 300; ++i) {
@@ -162,7 +173,7 @@ static void two_registries(uint64_t seed) {
     for (int k = 0; k < 2000; ++k) {
         const auto& x = bufs[r() % bufs.size()];
         const size_t len = 20 + r() % 1400;
-        CHECK((k & 1 ? a : b).resolve(x.first, len, &dev) == 0);
+        CHECK((k & 1 ? a : b).resolve(x.first, len, true, UINT64_MAX, &dev) == 0);
         check_mapping(h, x.first, len, dev);
     }
     const size_t before = h.locks.size(), a_owned = a.owned_ranges();
@@ -180,25 +191,100 @@ static void stale_foreign(uint64_t seed) {
     FakeHost h;
     h.flat = false;   // a stale mapping would show up as a wrong device address
     h.rng.seed(seed);
-    tcpcsum::HostRegistry<FakeHost> reg(h);
+    Reg reg(h);
     const uintptr_t base = 0x7d0000000000ull;
     h.foreign.push_back({base, base + 8 * kHostPage, (intptr_t)(77ull << 24)});
     uintptr_t dev = 0;
-    CHECK(reg.resolve(base + 100, 1500, &dev) == 0);
+    CHECK(reg.resolve(base + 100, 1500, false, 0, &dev) == 0);
     check_mapping(h, base + 100, 1500, dev);
     CHECK(reg.owned_ranges() == 0);
     h.foreign.clear();   // the owner frees it
     reg.forget_foreign();
-    CHECK(reg.resolve(base + 100, 1500, &dev) == 0);
+    // without auto-registration the stale mapping is not used: the packet is refused (copied)
+    CHECK(reg.resolve(base + 100, 1500, false, 0, &dev) == Reg::kUnmappable);
+    CHECK(reg.resolve(base + 100, 1500, true, UINT64_MAX, &dev) == 0);
     check_mapping(h, base + 100, 1500, dev);   // through our own lock now
     CHECK(reg.owned_ranges() == 1);
     // pages we locked are kept across forget_foreign()
     const uint64_t calls = h.lock_calls;
     reg.forget_foreign();
-    CHECK(reg.resolve(base + 200, 1000, &dev) == 0);
+    CHECK(reg.resolve(base + 200, 1000, true, UINT64_MAX, &dev) == 0);
     CHECK(h.lock_calls == calls);
     reg.release(0, 0);
     CHECK(h.locks.empty());
+}
+
+
+// Default mode (no auto-registration): pageable packets are refused (the caller
+// copies them), nothing is locked, someone else's page-locked memory and the
+// context's explicit registrations are used in place, and a pageable page is
+// asked about once, not once per packet per batch.
+static void no_lock_mode(uint64_t seed) {
+    FakeHost h;
+    std::mt19937_64 r(seed);
+    Reg reg(h);
+    const uintptr_t heap = 0x7c0000001010ull, pinned = 0x7c0100000000ull, mine = 0x7c0200000000ull;
+    h.foreign.push_back({pinned, pinned + 64 * kHostPage, 0});
+    CHECK(reg.lock_range(mine, 16 * kHostPage) == 0);
+    const uint64_t locks = h.lock_calls;
+    uintptr_t dev = 0;
+    for (int batch = 0; batch < 5; ++batch) {
+        reg.forget_foreign();
+        const uint64_t extent_before = h.extent_calls;
+        for (int k = 0; k < 1024; ++k) {
+            const uintptr_t p = heap + (uintptr_t)k * (32768 + 16);
+            CHECK(reg.resolve(p, 1500, false, 0, &dev) == Reg::kUnmappable);
+        }
+        // first batch: one lookup per buffer; later batches: none (the pageable memo)
+        CHECK(h.extent_calls - extent_before == (batch == 0 ? 1024u : 0u));
+        for (int k = 0; k < 64; ++k) {
+            const uintptr_t p = pinned + (uintptr_t)k * kHostPage + r() % 2000;
+            CHECK(reg.resolve(p, 1500, false, 0, &dev) == 0 && dev == p);
+            const uintptr_t q = mine + (uintptr_t)(k % 15) * kHostPage + r() % 2000;
+            CHECK(reg.resolve(q, 1500, false, 0, &dev) == 0 && dev == q);
+        }
+        // a packet running off the end of someone else's allocation is refused (copied)
+        CHECK(reg.resolve(pinned + 64 * kHostPage - 100, 1500, false, 0, &dev) == Reg::kUnmappable);
+    }
+    CHECK(h.lock_calls == locks && h.unlock_calls == 0);
+    reg.release(0, 0);
+    CHECK(h.locks.empty());
+}
+
+// A foreign allocation whose reported size is not a page multiple:
+// its last page is mapped whole, so a packet crossing the allocation's last byte
+// into that page resolves through it, and one running on into pages the
+// registry locks itself resolves through the merged view — no re-lock.
+static void unaligned_foreign() {
+    FakeHost h;
+    Reg reg(h);
+    const uintptr_t base = 0x7b0000000000ull;
+    h.foreign.push_back({base, base + 5000, 0});   // HIP reports the unaligned extent
+    uintptr_t dev = 0;
+    CHECK(reg.resolve(base + 4900, 200, false, 0, &dev) == 0 && dev == base + 4900);
+    CHECK(reg.resolve(base + 8000, 1000, true, UINT64_MAX, &dev) == 0 && dev == base + 8000);
+    check_mapping(h, base + 8000, 1000, dev);
+    CHECK(h.unlock_calls == 0);
+    for (const auto& kv : h.locks) CHECK(kv.second.lo >= base + 2 * kHostPage);   // never the foreign pages
+    reg.release(0, 0);
+    CHECK(h.locks.empty());
+}
+
+// Auto-registration stays within its byte budget; past it packets are refused.
+static void bounded(uint64_t seed) {
+    FakeHost h;
+    Reg reg(h);
+    const uintptr_t heap = 0x7a0000000010ull;
+    uintptr_t dev = 0;
+    int mapped = 0, refused = 0;
+    for (int k = 0; k < 200; ++k) {
+        const int rc = reg.resolve(heap + (uintptr_t)k * 32784, 1500, true, 64 * kHostPage, &dev);
+        CHECK(rc == 0 || rc == Reg::kUnmappable);
+        (rc == 0 ? mapped : refused)++;
+    }
+    CHECK(reg.owned_bytes() <= 64 * kHostPage && mapped > 0 && refused > 0);
+    (void)seed;
+    reg.release(0, 0);
 }
 
 int main(int argc, char** argv) {
@@ -208,7 +294,10 @@ int main(int argc, char** argv) {
         scenario(false, s);
         two_registries(s);
         stale_foreign(s);
+        no_lock_mode(s);
+        bounded(s);
     }
+    unaligned_foreign();
     std::printf(fails ? "FAIL (%d)\n" : "OK\n", fails);
     return fails ? 1 : 0;
 }

@@ -101,6 +101,8 @@ def test_argument_errors_need_no_device():
     assert L.tcpcsum_ctx_unregister_host(None, None, 0) == api.EINVAL
     assert L.tcpcsum_ctx_registered(None, None, None) == api.EINVAL
     assert L.tcpcsum_ctx_set_tuning(None, None) == api.EINVAL
+    assert L.tcpcsum_ctx_set_flags(None, 0) == api.EINVAL
+    assert L.tcpcsum_ctx_get_stats(None, None) == api.EINVAL
     ng = ctypes.c_int()
     assert L.tcpcsum_stream_probe_dev(1 << 20, 17, 1 << 20, ctypes.byref(ng), None, None) == api.EINVAL
     T = api.Tuning

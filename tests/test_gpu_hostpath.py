@@ -1,0 +1,120 @@
+"""Host-memory paths next to HIP's own pageable copies (the round-2 fault).
+
+In round 2 the library page-locked the page hull of every pageable range for
+the length of a call (hipHostRegister ... hipHostUnregister). Those pages can
+hold other heap data, and HIP's pageable copies pin their sources in place and
+cache those pins; a later pageable hipMemcpy (a torch ``.to(device)``) raised
+hipErrorIllegalAddress. The library now copies pageable memory into its own
+pinned staging and never page-locks what it was not asked to. These tests run
+exactly the sequence that faulted — host batches on a pageable numpy region,
+then pageable torch copies of the memory around it — and two contexts working
+on one pageable buffer from two threads at once.
+"""
+import threading
+
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    import tcp_amd
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rc, arch = tcp_amd.device_check()
+    assert rc == 0, f"tcpcsum_device_check -> {rc} ({arch})"
+    return torch.device("cuda:0")
+
+
+def _wire_region(rng, n, slot):
+    from tests.packets import build_batch
+    region, off, _ = build_batch(rng, n, slot=slot, malformed=True)
+    return region, off
+
+
+def test_pageable_torch_copies_around_host_batches(dev):
+    """One pageable allocation split at a non-page boundary: the front holds a wire pool the host
+    paths work on (region, uniform and per-packet pointers), the back is a neighbouring array that
+    torch copies to the device before, between and after them (HIP's pageable path, pin-in-place
+    for copies this large). Every copy lands intact, every batch matches the oracle, and the
+    context ends up holding no registration."""
+    import tcp_amd
+    rng = np.random.default_rng(2024)
+    front = 512 * 32768 + 1000                        # the boundary falls inside a page
+    buf = rng.integers(0, 256, front + (24 << 20), dtype=np.uint8)
+    region, off = _wire_region(rng, 512, 32768)
+    buf[:region.size] = region
+    pool = buf[:front]
+    neighbour = buf[front:]
+    want_nb = neighbour.copy()
+    ref = pool.copy()
+    want_out, want_st = oracle.ipv4_batch(ref, off, 32768, tcp_amd.IPV4_FILL)
+    want_u = oracle.batch_uniform(ref, 1500, 1500, 4000, 4242)
+    with tcp_amd.HostContext(0) as ctx:
+        for rep in range(3):
+            d_nb = torch.from_numpy(neighbour).to(dev)        # pageable H2D of the neighbour
+            out, st = ctx.ipv4_batch(pool, off, 32768, tcp_amd.IPV4_FILL)
+            assert np.array_equal(out, want_out) and np.array_equal(st, want_st)
+            assert np.array_equal(pool, ref)
+            d_pool = torch.from_numpy(pool).to(dev)           # the pool itself, after the host batch
+            u = ctx.batch_uniform(pool, 1500, 1500, 4000, 4242)
+            assert np.array_equal(u, want_u)
+            ptrs = [pool.ctypes.data + int(o) for o in off]
+            lens = [min(32768, pool.size - int(o)) for o in off]
+            v, vs = ctx.ipv4_batch_ptrs(ptrs, lens, tcp_amd.IPV4_VERIFY)
+            assert np.all(v[vs == tcp_amd.PKT_OK] == 0)
+            d_nb2 = torch.from_numpy(neighbour).to(dev)       # the sequence that faulted in round 2
+            back = d_nb2.cpu().numpy()                         # pageable D2H
+            torch.cuda.synchronize()
+            assert np.array_equal(back, want_nb)
+            assert np.array_equal(d_nb.cpu().numpy(), want_nb)
+            assert np.array_equal(d_pool.cpu().numpy(), ref)
+            assert ctx.registered() == (0, 0), rep
+        stats = ctx.stats()
+        assert stats["pkts_in_place"] == 0 and stats["pkts_staged"] == 3 * 2 * 512
+        assert stats["bytes_staged"] > 0
+
+
+def test_two_threads_one_pageable_buffer(dev):
+    """Two contexts on two threads VERIFY and checksum the same pageable pool at the same time
+    (legitimate use: nothing either does is visible to the other), while the main thread keeps
+    copying the pool to the device with torch."""
+    import tcp_amd
+    rng = np.random.default_rng(99)
+    region, off = _wire_region(rng, 700, 4096)
+    oracle.ipv4_batch(region, off, 4096, tcp_amd.IPV4_FILL)   # valid checks everywhere
+    want_v, want_vs = oracle.ipv4_batch(region.copy(), off, 4096, tcp_amd.IPV4_VERIFY)
+    want_u = oracle.batch_uniform(region, 1024, 1000, 2000, 9)
+    errors = []
+
+    def worker(seed):
+        try:
+            with tcp_amd.HostContext(0) as ctx:
+                for _ in range(20):
+                    v, vs = ctx.ipv4_batch(region, off, 4096, tcp_amd.IPV4_VERIFY)
+                    assert np.array_equal(v, want_v) and np.array_equal(vs, want_vs)
+                    u = ctx.batch_uniform(region, 1024, 1000, 2000, 9)
+                    assert np.array_equal(u, want_u)
+                    ptrs = [region.ctypes.data + int(o) for o in off]
+                    v2, vs2 = ctx.ipv4_batch_ptrs(ptrs, [4096] * off.size, tcp_amd.IPV4_VERIFY)
+                    assert np.array_equal(v2, want_v) and np.array_equal(vs2, want_vs)
+                assert ctx.registered() == (0, 0)
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(repr(e))
+
+    ts = [threading.Thread(target=worker, args=(s,)) for s in range(2)]
+    for t in ts:
+        t.start()
+    for _ in range(10):
+        d = torch.from_numpy(region).to(dev)
+        assert np.array_equal(d.cpu().numpy(), region)
+    for t in ts:
+        t.join()
+    torch.cuda.synchronize()
+    assert not errors, errors

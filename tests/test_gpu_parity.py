@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
-from tests.devcopy import host, to_dev, u16  # noqa: E402  pinned copies only
+from tests.tensors import host, to_dev, u16  # noqa: E402
 
 
 @pytest.fixture(scope="module")

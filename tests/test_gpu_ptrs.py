@@ -2,8 +2,9 @@
 
 The reference keeps every outgoing packet in its own malloc'd 32 KiB buffer
 (/root/reference/loop.c:180-183) and hands sendmmsg one iov_base per message
-(loop.c:53-54). tcpcsum_ipv4_batch_ptrs_dev / _host checksum such batches in
-place, with a per-packet byte bound (iov_len / msg_len). Every result is
+(loop.c:53-54). tcpcsum_ipv4_batch_ptrs_dev / _host checksum such batches with
+a per-packet byte bound (iov_len / msg_len): in place where the memory is
+page-locked, through the context's pinned staging where it is pageable. Every result is
 compared with the oracle's FILL / VERIFY of the same packet bytes
 (context.c:104-145 framing of context.c:169-209), bit for bit.
 """
@@ -16,7 +17,7 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
-from tests.devcopy import host, to_dev, u16  # noqa: E402  pinned copies only
+from tests.tensors import host, to_dev, u16  # noqa: E402
 
 
 @pytest.fixture(scope="module")
@@ -133,9 +134,13 @@ def _loop_pool(rng, n, slot=32768, payload=None):
     return bufs, np.array(lens, np.uint32)
 
 
-def test_ipv4_ptrs_host_loop_layout(dev):
-    """1024 separate pageable buffers: FILL in place, then VERIFY; registrations are cached across
-    batches and released on request; bytes outside the check fields never change."""
+@pytest.mark.parametrize("auto_register", [False, True])
+def test_ipv4_ptrs_host_loop_layout(dev, auto_register):
+    """1024 separate pageable buffers: FILL, then VERIFY, then a shuffled sub-batch with short bounds.
+    Default: every packet is copied into the context's pinned staging and its check stored back —
+    nothing is page-locked. auto_register (TCPCSUM_CTX_AUTO_REGISTER): each buffer is page-locked on
+    first use, later batches run in place with no new registration, and the registrations go on
+    request. Either way bytes outside the check fields never change."""
     import tcp_amd
     rng = np.random.default_rng(11)
     bufs, lens = _loop_pool(rng, 1024)
@@ -145,14 +150,20 @@ def test_ipv4_ptrs_host_loop_layout(dev):
         o, s = expected(r, np.array([0], np.uint64), np.array([l], np.uint32), tcp_amd.IPV4_FILL)
         want.append((o[0], s[0]))
     ptrs = [b.ctypes.data for b in bufs]
-    with tcp_amd.HostContext(0) as ctx:
+    with tcp_amd.HostContext(0, auto_register=auto_register) as ctx:
         try:
             out, st = ctx.ipv4_batch_ptrs(ptrs, lens, tcp_amd.IPV4_FILL)
             assert [(int(a), int(b)) for a, b in zip(out, st)] == [(int(a), int(b)) for a, b in want]
             for b, r in zip(bufs, refs):
                 assert np.array_equal(b, r)
             nreg, nbytes = ctx.registered()
-            assert nreg >= 1 and nbytes >= 1024 * 4096
+            stats = ctx.stats()
+            if auto_register:
+                assert nreg >= 1 and nbytes >= 1024 * 4096
+                assert stats["pkts_in_place"] == 1024 and stats["pkts_staged"] == 0
+            else:
+                assert (nreg, nbytes) == (0, 0)
+                assert stats["pkts_in_place"] == 0 and stats["pkts_staged"] == 1024
             # same buffers again (a second releaseSend): no new registrations, same results
             out2, _ = ctx.ipv4_batch_ptrs(ptrs, lens, tcp_amd.IPV4_FILL)
             assert np.array_equal(out2, out)
@@ -168,6 +179,8 @@ def test_ipv4_ptrs_host_loop_layout(dev):
             short[::5] = True
             assert np.all(vs[short] == tcp_amd.PKT_SKIPPED) and np.all(v[short] == 0)
             assert np.all(vs[~short] == tcp_amd.PKT_OK) and np.all(v[~short] == 0)
+            for b, r in zip(bufs, refs):
+                assert np.array_equal(b, r)
         finally:
             ctx.unregister_host()
         assert ctx.registered() == (0, 0)
@@ -175,7 +188,8 @@ def test_ipv4_ptrs_host_loop_layout(dev):
 
 def test_ipv4_ptrs_host_pinned_and_mixed(dev):
     """Packets in page-locked memory (tcpcsum_host_alloc) are used through their existing mapping
-    (no registration); mixed with pageable buffers and NULL / short messages in one batch."""
+    (no registration, no copy); pageable buffers in the same batch are staged; NULL and short
+    messages are SKIPPED."""
     import tcp_amd
     rng = np.random.default_rng(12)
     pinned = tcp_amd.pinned_empty(64 * 2048)
@@ -194,22 +208,20 @@ def test_ipv4_ptrs_host_pinned_and_mixed(dev):
     lens += [1500, 10]
     ref_page = [b.copy() for b in pageable]
     with tcp_amd.HostContext(0) as ctx:
-        try:
-            out, st = ctx.ipv4_batch_ptrs(ptrs, np.array(lens, np.uint32), tcp_amd.IPV4_FILL)
-            w1, s1 = expected(ref_pinned, np.arange(64, dtype=np.uint64) * 2048,
-                              np.array(lens[0:128:2], np.uint32), tcp_amd.IPV4_FILL)
-            assert np.array_equal(out[0:128:2], w1) and np.array_equal(st[0:128:2], s1)
-            for i in range(64):
-                w2, s2 = expected(ref_page[i], np.array([0], np.uint64), np.array([lens[2 * i + 1]], np.uint32),
-                                  tcp_amd.IPV4_FILL)
-                assert out[2 * i + 1] == w2[0] and st[2 * i + 1] == s2[0]
-                assert np.array_equal(pageable[i], ref_page[i])
-            assert np.array_equal(pinned, ref_pinned)
-            assert list(st[-2:]) == [tcp_amd.PKT_SKIPPED] * 2 and list(out[-2:]) == [0, 0]
-            nreg, nbytes = ctx.registered()
-            assert nreg >= 1 and nbytes <= 64 * 2 * 4096     # only the pageable buffers were page-locked
-        finally:
-            ctx.unregister_host()
+        out, st = ctx.ipv4_batch_ptrs(ptrs, np.array(lens, np.uint32), tcp_amd.IPV4_FILL)
+        w1, s1 = expected(ref_pinned, np.arange(64, dtype=np.uint64) * 2048,
+                          np.array(lens[0:128:2], np.uint32), tcp_amd.IPV4_FILL)
+        assert np.array_equal(out[0:128:2], w1) and np.array_equal(st[0:128:2], s1)
+        for i in range(64):
+            w2, s2 = expected(ref_page[i], np.array([0], np.uint64), np.array([lens[2 * i + 1]], np.uint32),
+                              tcp_amd.IPV4_FILL)
+            assert out[2 * i + 1] == w2[0] and st[2 * i + 1] == s2[0]
+            assert np.array_equal(pageable[i], ref_page[i])
+        assert np.array_equal(pinned, ref_pinned)
+        assert list(st[-2:]) == [tcp_amd.PKT_SKIPPED] * 2 and list(out[-2:]) == [0, 0]
+        assert ctx.registered() == (0, 0)
+        stats = ctx.stats()
+        assert stats["pkts_in_place"] == 64 and stats["pkts_staged"] == 64
 
 
 def test_ipv4_ptrs_host_context_tuning(dev):
@@ -219,24 +231,20 @@ def test_ipv4_ptrs_host_context_tuning(dev):
     bufs, lens = _loop_pool(rng, 200, slot=4096)
     ptrs = [b.ctypes.data for b in bufs]
     with tcp_amd.HostContext(0) as a, tcp_amd.HostContext(0) as b:
-        try:
-            b.set_tuning(0, 0, 5, tcp_amd.TUNE_WIN16)
-            va, sa = a.ipv4_batch_ptrs(ptrs, lens, tcp_amd.IPV4_VERIFY)
-            vb, sb = b.ipv4_batch_ptrs(ptrs, lens, tcp_amd.IPV4_VERIFY)
-            assert np.array_equal(va, vb) and np.array_equal(sa, sb)
-            with pytest.raises(tcp_amd.TcpCsumError):
-                b.set_tuning(0, 3)
-        finally:
-            a.unregister_host()
-            b.unregister_host()
+        b.set_tuning(0, 0, 5, tcp_amd.TUNE_WIN16)
+        va, sa = a.ipv4_batch_ptrs(ptrs, lens, tcp_amd.IPV4_VERIFY)
+        vb, sb = b.ipv4_batch_ptrs(ptrs, lens, tcp_amd.IPV4_VERIFY)
+        assert np.array_equal(va, vb) and np.array_equal(sa, sb)
+        with pytest.raises(tcp_amd.TcpCsumError):
+            b.set_tuning(0, 3)
 
 
 @pytest.mark.parametrize("register", ["none", "whole", "half", "tail"])
 def test_ipv4_region_host_registered_pool(dev, register):
-    """The region host path over a pageable pool: page-locked for the call when pageable, read in
-    place when the whole region is registered with the context (tcpcsum_ctx_register_host, once),
-    and locked for the call or copied when only its first half / its second half is — never a kernel
-    on unlocked pages, and the context's own registrations survive the call. Results identical."""
+    """The region host path over a pageable pool: its packets staged when the pool is pageable or only
+    partly registered (first half / second half), read in place when the whole pool is registered
+    with the context (tcpcsum_ctx_register_host, once). The call never adds or drops a registration.
+    Results identical."""
     import tcp_amd
     from tests.packets import build_batch
     rng = np.random.default_rng(21)
@@ -255,13 +263,14 @@ def test_ipv4_region_host_registered_pool(dev, register):
             out, st = ctx.ipv4_batch(region, off, 32768, tcp_amd.IPV4_FILL)
             assert np.array_equal(st, want_st) and np.array_equal(out, want_out)
             assert np.array_equal(region, ref)
+            stats = ctx.stats()
+            assert (stats["pkts_in_place"], stats["pkts_staged"]) == ((512, 0) if register == "whole" else (0, 512))
             v, vs = ctx.ipv4_batch(region, off, 32768, tcp_amd.IPV4_VERIFY)
             assert np.all(v[vs == tcp_amd.PKT_OK] == 0)
             # the uniform host path over the same (un/partly/fully registered) bytes, odd shapes
             u = ctx.batch_uniform(region, 1501, 1499, (region.nbytes - 1499) // 1501, 777)
             assert np.array_equal(u, oracle.batch_uniform(region, 1501, 1499, u.size, 777))
-            assert ctx.registered() == held   # per-call locks are gone, the context's are intact
-            # and the context's registrations still work
+            assert ctx.registered() == held
             out2, st2 = ctx.ipv4_batch(region, off, 32768, tcp_amd.IPV4_VERIFY)
             assert np.all(out2[st2 == tcp_amd.PKT_OK] == 0)
         finally:

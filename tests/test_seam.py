@@ -27,13 +27,13 @@ def _ensure_built():
         subprocess.run(["make", "-C", REPO, "tests/c/mmsg_loop", "tcp_amd/libtcpcsum_preload.so"], check=True)
 
 
-def run_loop(tmp_path, n, env_extra, cpu_checks=False):
+def run_loop(tmp_path, n, env_extra, cpu_checks=False, corrupt=False):
     _ensure_built()
     out = tmp_path / "mm.bin"
-    env = dict(os.environ)
+    env = {k: v for k, v in os.environ.items() if not k.startswith("TCPCSUM_PRELOAD")}
     env.update({"LD_PRELOAD": PRELOAD, "TCPCSUM_PRELOAD_ANY_SOCKET": "1", "TCPCSUM_PRELOAD_STATS": "1"})
     env.update(env_extra)
-    args = [EXE, str(n), str(out)] + (["cpu-checks"] if cpu_checks else [])
+    args = [EXE, str(n), str(out)] + (["corrupt"] if corrupt else ["cpu-checks"] if cpu_checks else [])
     r = subprocess.run(args, env=env, capture_output=True, text=True, timeout=120)
     pkts = []
     if r.returncode == 0:
@@ -50,7 +50,7 @@ def run_loop(tmp_path, n, env_extra, cpu_checks=False):
     stats = {}
     m = re.search(r"tcpcsum_preload: (.*)", r.stderr)
     if m:
-        for side, body in zip(("tx", "rx"), m.group(1).split("|")[:2]):
+        for side, body in zip(("tx", "rx", "all"), m.group(1).split("|")[:3]):
             for k, v in re.findall(r"(\w+)=(\d+)", body):
                 stats[f"{side}_{k}"] = int(v)
     return r, pkts, stats
@@ -79,11 +79,12 @@ def test_fails_loudly_without_gpu(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("copy", ["0", "1"])
-def test_tx_fill_on_gpu(tmp_path, copy):
-    """Default: in place on the caller's 32 KiB buffers (scatter-gather); COPY=1: gather into staging."""
+@pytest.mark.parametrize("inplace", ["0", "1"])
+def test_tx_fill_on_gpu(tmp_path, inplace):
+    """Default: the caller's 32 KiB buffers are copied into pinned staging and the checks stored back;
+    INPLACE=1: each buffer page-locked on first use and filled in place (scatter-gather)."""
     r, pkts, stats = run_loop(tmp_path, 3000, {"TCPCSUM_PRELOAD_TX": "fill", "TCPCSUM_PRELOAD_RX": "verify",
-                                               "TCPCSUM_PRELOAD_COPY": copy})
+                                               "TCPCSUM_PRELOAD_INPLACE": inplace})
     assert r.returncode == 0, r.stderr
     assert len(pkts) == 3000
     for built, got in pkts:
@@ -105,14 +106,39 @@ def test_tx_verify_live_parity_with_cpu_checks(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("copy", ["0", "1"])
-def test_tx_fill_with_ip_header(tmp_path, copy):
+@pytest.mark.parametrize("inplace", ["0", "1"])
+def test_tx_fill_with_ip_header(tmp_path, inplace):
     r, pkts, stats = run_loop(tmp_path, 700, {"TCPCSUM_PRELOAD_TX": "fill", "TCPCSUM_PRELOAD_IPHDR": "1",
-                                              "TCPCSUM_PRELOAD_RX": "verify", "TCPCSUM_PRELOAD_COPY": copy})
+                                              "TCPCSUM_PRELOAD_RX": "verify", "TCPCSUM_PRELOAD_INPLACE": inplace})
     assert r.returncode == 0, r.stderr
     for built, got in pkts:
         assert got == oracle_fill(built, 2)
     assert stats["rx_verify_failed"] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("inplace", ["0", "1"])
+def test_rx_drop_on_gpu(tmp_path, inplace):
+    """TCPCSUM_PRELOAD_RX=drop: segments whose checksum does not verify (one TCP header byte of every
+    7th packet flipped after the CPU computed its check) never reach the caller; every other segment
+    arrives byte-identical, and which ones were dropped is exactly what the oracle's VERIFY says."""
+    n = 2100
+    r, pkts, stats = run_loop(tmp_path, n, {"TCPCSUM_PRELOAD_TX": "off", "TCPCSUM_PRELOAD_RX": "drop",
+                                            "TCPCSUM_PRELOAD_INPLACE": inplace}, corrupt=True)
+    assert r.returncode == 0, r.stderr
+    assert len(pkts) == n
+    bad = 0
+    for built, got in pkts:
+        region = np.frombuffer(built + b"\0" * 16, np.uint8).copy()
+        v, st = oracle.ipv4_batch(region, np.array([0], np.uint64), 65535, 1)
+        ok = st[0] == 0 and v[0] == 0
+        bad += not ok
+        if ok:
+            assert got == built                      # delivered untouched
+        else:
+            assert got == b""                        # never delivered
+    assert bad == n // 7
+    assert stats["rx_verified"] == n and stats["rx_verify_failed"] == bad and stats["rx_dropped"] == bad
 
 
 # ----------------------------------------------------------------- raw sockets

@@ -21,7 +21,7 @@ def main():
     import numpy as np
     import torch
     import tcp_amd
-    from tests.devcopy import to_dev
+    from tests.tensors import to_dev
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream()
     sizes = [int(x) for x in os.environ.get("SIZES", "64,1500,4096,9000,32768,65536").split(",")]
