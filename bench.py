@@ -136,51 +136,56 @@ def host_cpu_info() -> dict:
             "hw_threads": os.cpu_count(), "threads_in_affinity": avail, "cgroup_cpu_quota": quota}
 
 
-def cpu_baseline(seg_len: int, seconds: float) -> dict:
-    """The reference's scalar checksum (C restatement of context.c:104-145, oracle/) on this host,
-    as BASELINE.md plans it: gcc -O0 -g (the reference Makefile sets no CFLAGS, Makefile:3) and
-    -O2, on 1 thread and on every hardware thread of the affinity mask (nproc), best of >= 5 passes
-    over the same host-resident batch (bounded sample). Persistent threads, contiguous shards."""
-    import oracle
-    # the same batch as the GPU step when it fits in 1.5 GiB (1M x 1500 B: exactly it), so the
-    # sample streams from host DRAM like the GPU's does from HBM
-    nseg = max(1, min(1 << 20, (3 << 29) // seg_len))
-    info = host_cpu_info()
-    nproc = max(1, info["threads_in_affinity"])
-    # where a cgroup quota grants fewer CPUs than the affinity mask shows (the GPU
-    # pool: 16 of 256), also time that many threads — what this job may sustain
-    quota = info["cgroup_cpu_quota"]
-    qthreads = int(quota) if quota and 1 < int(quota) < nproc else None
-    res = {}
-    plan = [("O2", nproc, 0.15), ("O2", 1, 0.2), ("O0", 1, 0.4), ("O0", nproc, 0.1)]
-    if qthreads:
-        plan.append(("O2", qthreads, 0.15))
-    for opt, th, share in plan:
-        gibs, digest, passes, mean = oracle.cpu_bench(th, seg_len, nseg, seconds * share, opt, mean=True)
-        res[(opt, th)] = {"GiB/s": round(gibs, 3), "passes": passes, "digest": digest, "mean": round(mean, 3)}
-    # value: the most favourable -O2 figure (nproc, or the quota's thread count if a
-    # throttled nproc run came out slower)
-    vth = nproc if not qthreads or res[("O2", nproc)]["GiB/s"] >= res[("O2", qthreads)]["GiB/s"] else qthreads
-    best = res[("O2", vth)]
+def usable_cpus(info: dict) -> int:
+    """Threads this job can run at once: the affinity mask, capped by a cgroup CPU quota (the GPU
+    pool grants 16 CPUs of quota while the mask shows all 256 hardware threads)."""
+    n = max(1, info["threads_in_affinity"] or 1)
+    q = info["cgroup_cpu_quota"]
+    if q:
+        n = min(n, max(1, math.ceil(q)))
+    return n
 
-    def name(o, t):
-        return f"{o}_{'1thread' if t == 1 else 'nproc' if t == nproc else f'{t}threads'}"
-    out = {
-        "value": best["GiB/s"], "unit": "GiB/s", "cores": vth, "kind": "port",
-        "sample": f"{nseg} x {seg_len}-byte segments (Appendix B stream, host DRAM), gcc -O2, {vth} threads, "
-                  f"best of >= {best['passes']} passes (persistent threads, contiguous shards)",
-        "threads": vth,
-        "O2_nproc": res[("O2", nproc)]["GiB/s"], "O2_1thread": res[("O2", 1)]["GiB/s"],
-        "O0_nproc": res[("O0", nproc)]["GiB/s"], "O0_1thread": res[("O0", 1)]["GiB/s"],
-        "passes": {name(o, t): r["passes"] for (o, t), r in res.items()},
-        # mean over all passes: below the best pass where a cgroup CPU quota throttles the threads
-        "mean_over_passes": {name(o, t): r["mean"] for (o, t), r in res.items()},
-        "digests_agree": len({r["digest"] for r in res.values()}) == 1,
+
+def cpu_baseline(seconds: float) -> dict:
+    """The reference's scalar checksum (C restatement of context.c:104-145, oracle/) on this host, as
+    BASELINE.md plans it, for each single-GPU config's segment size: gcc -O2 and -O0 -g (the
+    reference Makefile sets no CFLAGS, Makefile:3), on 1 thread and on every CPU this job may use
+    (usable_cpus). Each figure is >= 5 passes over the same host-resident batch, timed from before
+    the workers are released to after the last one finishes; best and median pass reported, and
+    `value` is the median at -O2 on the usable CPUs for the 1500-B config — a rate this job can
+    sustain, not a lucky pass. Bounded sample: the 1500-B and 64-KiB batches are 1.5 GB (the
+    1500-B one is exactly the GPU's batch) — a quarter of that on one thread — and the 64-B one is the
+    GPU's 64 MiB batch."""
+    import oracle
+    info = host_cpu_info()
+    T = usable_cpus(info)
+    # (segment bytes, opt, threads, share of `seconds`)
+    plan = [(1500, "O2", T, 0.25), (1500, "O2", 1, 0.15), (1500, "O0", 1, 0.1), (1500, "O0", T, 0.1),
+            (64, "O2", T, 0.1), (64, "O2", 1, 0.05), (64, "O0", 1, 0.05),
+            (65536, "O2", T, 0.1), (65536, "O2", 1, 0.05), (65536, "O0", 1, 0.05)]
+    figures = {}
+    digests = {}
+    for L, opt, th, share in plan:
+        # one thread gets a quarter of the batch (384 MB: still far past the host's caches)
+        nseg = (1 << 20) if L <= 1500 else (3 << 29) // L
+        if th == 1 and L > 64:
+            nseg //= 4
+        r = oracle.cpu_bench(th, L, nseg, seconds * share, opt)
+        key = f"{L}B_{opt}_{'1thread' if th == 1 else f'{th}threads'}"
+        figures[key] = {"best": round(r["best"], 3), "median": round(r["median"], 3), "passes": r["passes"],
+                        "sample": f"{nseg} x {L} B"}
+        digests.setdefault(L, set()).add(r["digest"])
+    head = figures[f"1500B_O2_{'1thread' if T == 1 else f'{T}threads'}"]
+    return {
+        "value": head["median"], "unit": "GiB/s", "cores": T, "kind": "port",
+        "sample": (f"1M x 1500-byte segments (Appendix B stream, 1.5 GB in host DRAM, first touched by the "
+                   f"thread that reads it), gcc -O2, {T} threads = the CPUs this job may use; median of "
+                   f"{head['passes']} passes (best {head['best']})"),
+        "threads": T,
+        "figures": figures,
+        "digests_agree": all(len(v) == 1 for v in digests.values()),
         **info,
     }
-    if qthreads:
-        out[f"O2_{qthreads}threads_quota"] = res[("O2", qthreads)]["GiB/s"]
-    return out
 
 
 def run_config(config: str, steps: int, warmup: int, rank: int, world: int, dist, device, rotate: int = 0,
@@ -323,7 +328,7 @@ def main(argv=None) -> int:
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", choices=sorted(CONFIGS), default="1500")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=16.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-other-configs", action="store_true",
                     help="skip the other BASELINE configs (64 B, 64 KiB) reported beside the headline at N=1")
@@ -478,7 +483,7 @@ def main(argv=None) -> int:
         if extra:
             line["other_configs"] = extra
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(L, args.cpu_seconds)
+            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -40,7 +40,8 @@ _SIGS = {
     "oracle_tx_build": (None, [vp, vp, u64, vp, ctypes.c_int, vp]),
     "oracle_digest": (None, [vp, u64, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_uint16)]),
     "oracle_cpu_bench": (ctypes.c_double, [ctypes.c_int, u32, u64, ctypes.c_double, ctypes.POINTER(u64),
-                                           ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_double)]),
+                                           ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_double),
+                                           ctypes.POINTER(ctypes.c_double)]),
 }
 
 
@@ -129,18 +130,18 @@ def digest(out: np.ndarray) -> tuple[str, int, str]:
     return f"{f.value:016x}", int(s.value), f"{x.value:04x}"
 
 
-def cpu_bench(threads: int, seg_len: int, nseg: int, min_seconds: float, opt: str = "O2", mean: bool = False):
-    """Best-pass GiB/s of the restatement over a host-resident synthetic batch, the outputs' digest
-    and the pass count (mean=True: also the mean GiB/s over all passes)."""
+def cpu_bench(threads: int, seg_len: int, nseg: int, min_seconds: float, opt: str = "O2") -> dict:
+    """Time the restatement over a host-resident synthetic batch (>= 5 passes and min_seconds):
+    best and median pass in GiB/s, mean over all passes, the outputs' digest and the pass count."""
     d = u64()
     p = ctypes.c_int()
     tot = ctypes.c_double()
-    gibs = lib(opt).oracle_cpu_bench(threads, seg_len, nseg, min_seconds, ctypes.byref(d), ctypes.byref(p),
-                                     ctypes.byref(tot))
-    if mean:
-        m = nseg * seg_len * p.value / tot.value / 2**30 if tot.value > 0 else 0.0
-        return float(gibs), f"{d.value:016x}", int(p.value), float(m)
-    return float(gibs), f"{d.value:016x}", int(p.value)
+    med = ctypes.c_double()
+    best = lib(opt).oracle_cpu_bench(threads, seg_len, nseg, min_seconds, ctypes.byref(d), ctypes.byref(p),
+                                     ctypes.byref(tot), ctypes.byref(med))
+    mean = nseg * seg_len * p.value / tot.value / 2**30 if tot.value > 0 else 0.0
+    return {"best": float(best), "median": float(med.value), "mean": float(mean), "digest": f"{d.value:016x}",
+            "passes": int(p.value)}
 
 
 def tx_build(payload: np.ndarray, segs: np.ndarray, out: np.ndarray, iphdr: bool = False) -> np.ndarray:

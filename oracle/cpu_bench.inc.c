@@ -26,17 +26,17 @@ static uint64_t cb_mix(uint64_t z) {
     return z ^ (z >> 31);
 }
 
-static void cb_fill(uint8_t *dst, uint64_t nbytes) {
-    /* stream offset 0, nbytes multiple of 8 handled bytewise at the tail */
-    uint64_t w = 0;
-    for (; (w + 1) * 8 <= nbytes; ++w) {
-        uint64_t v = cb_mix(0x5EEDC0DEull + (w + 1) * 0x9E3779B97F4A7C15ull);
-        memcpy(dst + w * 8, &v, 8);
+/* bytes [b0, b1) of the stream, written at dst + b0 */
+static void cb_fill_range(uint8_t *dst, uint64_t b0, uint64_t b1) {
+    uint64_t b = b0;
+    for (; b < b1 && (b & 7); ++b)
+        dst[b] = (uint8_t) (cb_mix(0x5EEDC0DEull + (b / 8 + 1) * 0x9E3779B97F4A7C15ull) >> (8 * (b & 7)));
+    for (; b + 8 <= b1; b += 8) {
+        uint64_t v = cb_mix(0x5EEDC0DEull + (b / 8 + 1) * 0x9E3779B97F4A7C15ull);
+        memcpy(dst + b, &v, 8);
     }
-    if (w * 8 < nbytes) {
-        uint64_t v = cb_mix(0x5EEDC0DEull + (w + 1) * 0x9E3779B97F4A7C15ull);
-        memcpy(dst + w * 8, &v, nbytes - w * 8);
-    }
+    for (; b < b1; ++b)
+        dst[b] = (uint8_t) (cb_mix(0x5EEDC0DEull + (b / 8 + 1) * 0x9E3779B97F4A7C15ull) >> (8 * (b & 7)));
 }
 
 struct cb_job {
@@ -62,6 +62,7 @@ static void cb_work(const struct cb_job *j) {
 struct cb_pool {
     pthread_barrier_t start, done;
     volatile int stop;
+    volatile int fill;   /* this round writes the thread's shard of the input instead */
 };
 
 struct cb_arg {
@@ -69,12 +70,22 @@ struct cb_arg {
     struct cb_job job;
 };
 
+/* One round of thread a: its shard of the checksums, or (fill round) its shard
+ * of the input bytes — so every page is first touched by the thread that
+ * later reads it (NUMA-local on a multi-socket host). */
+static void cb_round(const struct cb_arg *a) {
+    if (a->pool->fill)
+        cb_fill_range((uint8_t *) a->job.buf, a->job.s0 * a->job.seg_len, a->job.s1 * a->job.seg_len);
+    else
+        cb_work(&a->job);
+}
+
 static void *cb_worker(void *arg) {
     struct cb_arg *a = (struct cb_arg *) arg;
     for (;;) {
         pthread_barrier_wait(&a->pool->start);
         if (a->pool->stop) break;
-        cb_work(&a->job);
+        cb_round(a);
         pthread_barrier_wait(&a->pool->done);
     }
     return 0;
@@ -87,10 +98,21 @@ static double cb_now(void) {
 }
 
 #define CB_MAX_THREADS 1024
+#define CB_MAX_PASSES 4096
 
-/* Best pass (GiB/s) over at least 5 passes and min_seconds of passes. */
+static int cb_cmp_double(const void *a, const void *b) {
+    const double x = *(const double *) a, y = *(const double *) b;
+    return x < y ? -1 : x > y;
+}
+
+/* Passes over the batch: at least 5 and min_seconds of them (at most
+ * CB_MAX_PASSES). A pass is timed from just BEFORE thread 0 releases the
+ * start barrier to just after the last thread reaches the done barrier, so a
+ * worker that starts early (thread 0 preempted after the release) or late (a
+ * cgroup quota throttling it) is inside the pass, never outside it. Returns
+ * the best pass in GiB/s; *median_out = the median pass in GiB/s. */
 double CB_BENCH_NAME(int nthreads, uint32_t seg_len, uint64_t nseg, double min_seconds,
-                     uint64_t *digest_out, int *passes_out, double *total_out) {
+                     uint64_t *digest_out, int *passes_out, double *total_out, double *median_out) {
     if (nthreads < 1) nthreads = 1;
     if (nthreads > CB_MAX_THREADS) nthreads = CB_MAX_THREADS;
     uint64_t bytes = nseg * (uint64_t) seg_len;
@@ -98,12 +120,16 @@ double CB_BENCH_NAME(int nthreads, uint32_t seg_len, uint64_t nseg, double min_s
     uint16_t *out = (uint16_t *) calloc(nseg ? nseg : 1, sizeof(uint16_t));
     pthread_t *th = (pthread_t *) calloc((size_t) nthreads, sizeof(pthread_t));
     struct cb_arg *args = (struct cb_arg *) calloc((size_t) nthreads, sizeof(struct cb_arg));
-    if (!buf || !out || !th || !args) { free(buf); free(out); free(th); free(args); return -1.0; }
-    cb_fill(buf, bytes);
+    double *times = (double *) calloc(CB_MAX_PASSES, sizeof(double));
+    if (!buf || !out || !th || !args || !times) {
+        free(buf); free(out); free(th); free(args); free(times);
+        return -1.0;
+    }
     memset(out, 0, nseg * sizeof(uint16_t));   /* first-touch the output */
 
     struct cb_pool pool;
     pool.stop = 0;
+    pool.fill = 1;
     pthread_barrier_init(&pool.start, 0, (unsigned) nthreads);
     pthread_barrier_init(&pool.done, 0, (unsigned) nthreads);
     for (int t = 0; t < nthreads; ++t) {
@@ -113,18 +139,23 @@ double CB_BENCH_NAME(int nthreads, uint32_t seg_len, uint64_t nseg, double min_s
         args[t].job.s1 = nseg * (uint64_t) (t + 1) / (uint64_t) nthreads;
         if (t) pthread_create(&th[t], 0, cb_worker, &args[t]);
     }
-    double best = 1e300, total = 0.0;
-    int passes = 0;
-    while (passes < 5 || total < min_seconds) {
+    /* untimed: the fill round, then one warm pass */
+    for (int r = 0; r < 2; ++r) {
         pthread_barrier_wait(&pool.start);
+        cb_round(&args[0]);
+        pthread_barrier_wait(&pool.done);
+        pool.fill = 0;
+    }
+    double total = 0.0;
+    int passes = 0;
+    while ((passes < 5 || total < min_seconds) && passes < CB_MAX_PASSES) {
         double t0 = cb_now();
-        cb_work(&args[0].job);
+        pthread_barrier_wait(&pool.start);
+        cb_round(&args[0]);
         pthread_barrier_wait(&pool.done);
         double dt = cb_now() - t0;
+        times[passes++] = dt;
         total += dt;
-        if (dt < best) best = dt;
-        ++passes;
-        if (passes > 100000) break;
     }
     pool.stop = 1;
     pthread_barrier_wait(&pool.start);
@@ -139,11 +170,16 @@ double CB_BENCH_NAME(int nthreads, uint32_t seg_len, uint64_t nseg, double min_s
         }
         *digest_out = h;
     }
+    qsort(times, (size_t) passes, sizeof(double), cb_cmp_double);
+    const double best = times[0];
+    const double med = passes & 1 ? times[passes / 2] : 0.5 * (times[passes / 2 - 1] + times[passes / 2]);
     if (passes_out) *passes_out = passes;
     if (total_out) *total_out = total;
+    if (median_out) *median_out = (double) bytes / med / (double) (1ull << 30);
     free(buf);
     free(out);
     free(th);
     free(args);
+    free(times);
     return (double) bytes / best / (double) (1ull << 30);
 }

@@ -71,11 +71,13 @@ void oracle_digest(const uint16_t *out, uint64_t n, uint64_t *fnv, uint64_t *sum
 /* CPU throughput harness (CLOCK_MONOTONIC, pthreads, contiguous shards).
  * Times the checksum of nseg synthetic segments of seg_len bytes held in
  * host memory, pseudo-header sum computed per segment as context.c:208 does.
- * Repeats passes until min_seconds elapsed (>= 5 passes, persistent threads);
- * returns the best pass in GiB/s, the fnv1a64 digest of the outputs and the
- * summed duration of all passes (mean rate = passes * bytes / total). */
+ * Repeats passes until min_seconds elapsed (>= 5 passes, persistent threads,
+ * each pass timed from before the start barrier releases the workers to
+ * after the last one finishes); returns the best pass in GiB/s, the fnv1a64
+ * digest of the outputs, the summed duration of all passes (mean rate =
+ * passes * bytes / total) and the median pass in GiB/s. */
 double oracle_cpu_bench(int nthreads, uint32_t seg_len, uint64_t nseg, double min_seconds,
-                        uint64_t *digest_out, int *passes_out, double *total_out);
+                        uint64_t *digest_out, int *passes_out, double *total_out, double *median_out);
 
 #ifdef __cplusplus
 }
