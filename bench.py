@@ -188,10 +188,26 @@ def cpu_baseline(seconds: float) -> dict:
     }
 
 
+def digest_matches(res, config: str, world: int, rank: int, per_gpu: int):
+    """Rank `rank`'s results of rotation 0 vs the reference's Appendix B digest (None: no digest)."""
+    import numpy as np
+    gold = json.load(open(os.path.join(REPO, "tests", "golden", "reference_vectors.json")))["digests"]
+    key = {("1500", 1): "1Mx1500", ("64", 1): "1Mx64", ("64k", 1): "256Kx64KiB"}.get((config, world))
+    if config == "1500" and world > 1 and per_gpu == 1 << 20:
+        key = f"8Mx1500_shard{rank}" if rank < 8 else None
+    if not key:
+        return None
+    g = gold[key]
+    return bool(int(res.astype(np.uint64).sum()) == g["sum"]
+                and f"{int(np.bitwise_xor.reduce(res)):04x}" == g["xor"]
+                and [f"{v:04x}" for v in res[:4]] == g["first4"] and f"{res[-1]:04x}" == g["last"])
+
+
 def run_config(config: str, steps: int, warmup: int, rank: int, world: int, dist, device, rotate: int = 0,
-               streams: int = 1):
+               streams: int = 1, multi: int = 0):
     """Generate this rank's shard of `config` in HBM, check rotation 0 against the reference's
-    digest, then time `steps` launches (after `warmup`) between barriers.
+    digest, then time `steps` launches (after `warmup`) between barriers. multi = K > 0: each step
+    is ONE launch over K distinct batches (tcpcsum_batch_uniform_multi_dev).
     Returns (result dict, rank's buffers for the probe)."""
     import numpy as np
     import torch
@@ -207,6 +223,8 @@ def run_config(config: str, steps: int, warmup: int, rank: int, world: int, dist
     rot = max(1, math.ceil((2 << 30) / batch_bytes))
     if rotate:
         rot = rotate
+    if multi:
+        rot = max(rot, multi)
     stream = torch.cuda.current_stream()
     bufs, sss = [], []
     for r in range(rot):
@@ -225,19 +243,8 @@ def run_config(config: str, steps: int, warmup: int, rank: int, world: int, dist
     tcp_amd.batch_uniform(bufs[0], L, L, cnt, sss[0], out=out)
     torch.cuda.synchronize()
     res = out.cpu().numpy().view(np.uint16)
-    check = None
     try:
-        gold = json.load(open(os.path.join(REPO, "tests", "golden", "reference_vectors.json")))["digests"]
-        key = {("1500", 1): "1Mx1500", ("64", 1): "1Mx64", ("64k", 1): "256Kx64KiB"}.get((config, world))
-        if config == "1500" and world == 8:
-            key = f"8Mx1500_shard{rank}"
-        elif config == "1500" and world > 1 and per_gpu == 1 << 20:
-            key = f"8Mx1500_shard{rank}" if rank < 8 else None
-        if key:
-            g = gold[key]
-            check = bool(int(res.astype(np.uint64).sum()) == g["sum"]
-                         and f"{int(np.bitwise_xor.reduce(res)):04x}" == g["xor"]
-                         and [f"{v:04x}" for v in res[:4]] == g["first4"] and f"{res[-1]:04x}" == g["last"])
+        check = digest_matches(res, config, world, rank, per_gpu)
     except Exception:
         check = None
 
@@ -253,11 +260,19 @@ def run_config(config: str, steps: int, warmup: int, rank: int, world: int, dist
     sts = [stream] + [torch.cuda.Stream(device=device) for _ in range(streams - 1)]
     outs = [out] + [torch.empty(cnt, dtype=torch.int16, device=device) for _ in range(streams - 1)]
 
+    if multi:   # K batches per launch, each its own rotation and result array
+        mouts = [out] + [torch.empty(cnt, dtype=torch.int16, device=device) for _ in range(multi - 1)]
+        marr = [tcp_amd.ubatches([(bufs[(g * multi + j) % rot], L, L, cnt, sss[(g * multi + j) % rot], mouts[j])
+                                  for j in range(multi)]) for g in range(max(1, rot // multi))]
+
     def step():
         r = k[0] % rot
         j = k[0] % streams
         k[0] += 1
-        tcp_amd.batch_uniform(bufs[r], L, L, cnt, sss[r], out=outs[j], stream=sts[j])
+        if multi:
+            tcp_amd.batch_uniform_multi(marr[(k[0] - 1) % len(marr)], stream=sts[0])
+        else:
+            tcp_amd.batch_uniform(bufs[r], L, L, cnt, sss[r], out=outs[j], stream=sts[j])
 
     # HIP events on the launch stream(s) bracket the kernels of the timed region
     ev0 = [torch.cuda.Event(enable_timing=True) for _ in sts]
@@ -271,34 +286,50 @@ def run_config(config: str, steps: int, warmup: int, rank: int, world: int, dist
     kernel_ms = max(ev0[0].elapsed_time(e) for e in ev1) / steps
     wall_max = max_over_ranks(wall, dist, device)
     kernel_ms_max = max_over_ranks(kernel_ms, dist, device)
+    if multi:   # batch 0 of group 0 is rotation 0 = the Appendix B batch
+        tcp_amd.batch_uniform_multi(marr[0], stream=sts[0])
+        torch.cuda.synchronize()
+        try:
+            mcheck = digest_matches(mouts[0].cpu().numpy().view(np.uint16), config, world, rank, per_gpu)
+        except Exception:
+            mcheck = None
+        check = check and mcheck
     r = {"config": config, "desc": desc, "L": L, "cnt": cnt, "rot": rot, "batch_bytes": batch_bytes,
          "check": check, "wall_max": wall_max, "kernel_ms": kernel_ms, "kernel_ms_max": kernel_ms_max,
-         "streams": streams}
+         "streams": streams, "multi": multi}
     return r, bufs, rot
 
 
 def spawn_ranks(args, argv, script=None) -> int:
     """`bench.py --gpus N` with no launcher: start ranks 0..N-1 as child processes (this process
     has made no GPU call), rendezvous on 127.0.0.1, relay rank 0's JSON line, return the worst
-    exit code. If a rank fails the others are stopped (by PID) instead of waiting in a barrier."""
+    exit code. If a rank fails the others are stopped (by PID) instead of waiting in a barrier, and
+    every failed rank's exit code and the tail of its stderr are written to this process's stderr
+    (rank 0's stderr is relayed in any case)."""
     import socket
     import subprocess
+    import tempfile
     with socket.socket() as so:
         so.bind(("127.0.0.1", 0))
         port = so.getsockname()[1]
     cmd = [sys.executable, script or os.path.abspath(__file__)] + list(argv if argv is not None else sys.argv[1:])
-    procs = []
+    procs, errs = [], []
     for r in range(args.gpus):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
                    LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+        err = tempfile.TemporaryFile()
+        errs.append(err)
+        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL,
+                                      stderr=err))
     rc = 0
+    first_failed = None
+    out0 = b""
     try:
         while True:
             codes = [p.poll() for p in procs]
-            failed = [c for c in codes if c not in (None, 0)]
+            failed = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
             if failed:   # a rank died: the others would wait in a barrier for ever
-                rc = failed[0]
+                first_failed, rc = failed[0]
                 for p in procs:
                     if p.poll() is None:
                         p.terminate()
@@ -312,11 +343,26 @@ def spawn_ranks(args, argv, script=None) -> int:
             except subprocess.TimeoutExpired:
                 p.kill()
                 p.wait()
+        out0 = procs[0].stdout.read() if procs[0].stdout else b""
     finally:
         for p in procs:
             if p.poll() is None:
                 p.kill()
-    out0 = procs[0].stdout.read() if procs[0].stdout else b""
+        for r, (p, err) in enumerate(zip(procs, errs)):
+            err.seek(0)
+            text = err.read().decode(errors="replace")
+            err.close()
+            if r == 0 and text:
+                sys.stderr.write(text)
+            if p.returncode not in (0, None) and (r != 0 or not text):
+                tail = "\n".join(text.splitlines()[-30:])
+                cause = " (first to fail)" if r == first_failed else " (stopped after another rank failed)" \
+                    if first_failed is not None else ""
+                sys.stderr.write(f"bench.py: rank {r} exited with code {p.returncode}{cause}; stderr tail:\n"
+                                 f"{tail}\n")
+            elif r == 0 and p.returncode not in (0, None):
+                sys.stderr.write(f"bench.py: rank 0 exited with code {p.returncode}\n")
+        sys.stderr.flush()
     sys.stdout.write(out0.decode())
     sys.stdout.flush()
     return rc
@@ -441,6 +487,21 @@ def main(argv=None) -> int:
                     "GiB/s": round(e2["batch_bytes"] * steps / e2["wall_max"] / (1 << 30), 2),
                     "ms_per_launch_effective": round(e2["kernel_ms"], 5), "effective_GB/s": round(gbs2, 1),
                     "roofline_frac_effective": round(gbs2 / HBM_PEAK_GBS, 4), "digest_check": e2["check"]}
+                torch.cuda.empty_cache()
+                # the caller-facing form: K = 16 distinct batches in ONE launch
+                # (tcpcsum_batch_uniform_multi_dev), the ramp and drain paid once per launch
+                K = 16
+                e3, ebufs, _ = run_config(cfg, max(5, steps // 8), min(args.warmup, 3), rank, world, dist, device,
+                                          multi=K)
+                del ebufs
+                per_batch_ms = e3["kernel_ms"] / K
+                gbs3 = e3["batch_bytes"] / (per_batch_ms * 1e-3) / 1e9
+                extra[cfg]["multi_batch"] = {
+                    "batches_per_launch": K, "api": "tcpcsum_batch_uniform_multi_dev",
+                    "kernel_avg_ms_per_launch": round(e3["kernel_ms"], 5), "ms_per_batch": round(per_batch_ms, 5),
+                    "GiB/s": round(e3["batch_bytes"] * K * max(5, steps // 8) / e3["wall_max"] / (1 << 30), 2),
+                    "achieved_GB/s": round(gbs3, 1), "roofline_frac": round(gbs3 / HBM_PEAK_GBS, 4),
+                    "digest_check": e3["check"], "traffic": load_traffic(cfg + "_multi")}
                 torch.cuda.empty_cache()
 
     if rank == 0:

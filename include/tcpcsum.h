@@ -122,6 +122,27 @@ int tcpcsum_batch_uniform_dev(const void *d_base, uint64_t stride, uint32_t len,
                               const uint32_t *d_sum_start, uint32_t sum_start,
                               uint16_t *d_out, uint64_t n, void *stream, const tcpcsum_tuning_t *tune);
 
+/* Several independent uniform batches in ONE launch — e.g. the small-segment
+ * batches a loop flushes one after another (releaseSend, loop.c:27-94): the
+ * launch's ramp and drain, which dominate a single batch of 64-B segments, are
+ * paid once. Batch j is exactly tcpcsum_batch_uniform_dev(b[j].d_base,
+ * b[j].stride, b[j].len, b[j].d_sum_start, b[j].sum_start, b[j].d_out, b[j].n).
+ * batches is a HOST array of k entries (passed to the kernel by value,
+ * TCPCSUM_MULTI_MAX per launch). Batches whose segments fit one lane-group
+ * shape (up to 8 KiB) share a launch; longer ones are launched one by one. */
+#define TCPCSUM_MULTI_MAX 16
+typedef struct tcpcsum_ubatch {
+    const void *d_base;
+    uint64_t stride;
+    const uint32_t *d_sum_start;   /* NULL: sum_start for every segment */
+    uint16_t *d_out;
+    uint64_t n;
+    uint32_t len;
+    uint32_t sum_start;
+} tcpcsum_ubatch_t;
+int tcpcsum_batch_uniform_multi_dev(const tcpcsum_ubatch_t *batches, uint32_t k, void *stream,
+                                    const tcpcsum_tuning_t *tune);
+
 /* Ragged layout: segment i = d_base[d_desc[i].offset .. +d_desc[i].len).
  * max_len: an upper bound on every d_desc[i].len (picks the kernel shape;
  * segments longer than max_len are still summed correctly, only slower).

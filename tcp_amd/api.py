@@ -24,7 +24,8 @@ __all__ = [
     "DESC_DTYPE", "TXSEG_DTYPE", "IPV4_FILL", "IPV4_VERIFY", "IPV4_IPHDR", "PKT_OK", "PKT_SKIPPED",
     "PKT_IPHDR_BAD", "PKT_CSUM_PARTIAL", "CTX_AUTO_REGISTER", "TUNE_WIRE_CACHED", "TUNE_WIN16", "TUNE_TX_NT_STORE", "TUNE_FILL_DWORD",
     "TcpCsumError", "Tuning", "HostContext", "lib", "lib_path", "device_check", "make_tuning", "set_tuning",
-    "get_tuning", "plan_uniform", "getPseudoHeaderSum", "csum_continue", "batch_uniform", "batch_desc",
+    "get_tuning", "plan_uniform", "getPseudoHeaderSum", "csum_continue", "batch_uniform", "batch_uniform_multi",
+    "ubatches", "batch_desc",
     "ipv4_batch", "ipv4_batch_ptrs", "tx_build", "synth_fill", "synth_pseudo", "stream_probe", "pinned_empty",
 ]
 
@@ -90,6 +91,16 @@ class Tuning(ctypes.Structure):
 tunep = ctypes.POINTER(Tuning)
 
 
+class UBatch(ctypes.Structure):
+    """tcpcsum_ubatch_t: one batch of a multi-batch uniform launch."""
+    _fields_ = [("d_base", ctypes.c_void_p), ("stride", ctypes.c_uint64), ("d_sum_start", ctypes.c_void_p),
+                ("d_out", ctypes.c_void_p), ("n", ctypes.c_uint64), ("len", ctypes.c_uint32),
+                ("sum_start", ctypes.c_uint32)]
+
+
+MULTI_MAX = 16
+
+
 class CtxStats(ctypes.Structure):
     """tcpcsum_ctx_stats_t."""
     _fields_ = [("batches", ctypes.c_uint64), ("pkts_in_place", ctypes.c_uint64), ("pkts_staged", ctypes.c_uint64),
@@ -107,6 +118,7 @@ SIGNATURES = {
     "tcpcsum_continue": (ctypes.c_ushort, [ctypes.c_ulong, ctypes.c_char_p, ctypes.c_int]),
     "tcpcsum_batch_uniform_dev": (ctypes.c_int, [vp, u64, u32, vp, u32, vp, u64, vp, tunep]),
     "tcpcsum_batch_desc_dev": (ctypes.c_int, [vp, vp, u64, u32, vp, vp, tunep]),
+    "tcpcsum_batch_uniform_multi_dev": (ctypes.c_int, [vp, u32, vp, tunep]),
     "tcpcsum_ipv4_batch_dev": (ctypes.c_int, [vp, u64, vp, u64, u32, ctypes.c_int, vp, vp, vp, tunep]),
     "tcpcsum_ipv4_batch_ptrs_dev": (ctypes.c_int, [vp, vp, u64, u32, ctypes.c_int, vp, vp, vp, tunep]),
     "tcpcsum_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_size_t, ctypes.POINTER(vp)]),
@@ -274,6 +286,38 @@ def batch_uniform(data, stride: int, length: int, n: int, sum_start=0, out=None,
                                          _dev_ptr(out, "out"), n, _stream_handle(stream), _tune(tune))
     _check(rc, "tcpcsum_batch_uniform_dev")
     return out
+
+
+def ubatches(batches) -> ctypes.Array:
+    """A host tcpcsum_ubatch_t array from (data, stride, length, n, sum_start, out[, offset]) tuples:
+    ``data`` a device uint8 tensor, ``sum_start`` an int or a device int32 tensor, ``out`` a device
+    int16 tensor of >= n entries."""
+    arr = (UBatch * len(batches))()
+    for j, b in enumerate(batches):
+        data, stride, length, n, ss, out = b[:6]
+        offset = b[6] if len(b) > 6 else 0
+        if n and offset + (n - 1) * stride + length > data.numel() * data.element_size():
+            raise ValueError(f"batch {j} runs past the end of its data")
+        if out.numel() < n:
+            raise ValueError(f"batch {j}: out too short")
+        if isinstance(ss, int):
+            ss_ptr, ss0 = 0, ss
+        else:
+            if ss.numel() < n:
+                raise ValueError(f"batch {j}: sum_start too short")
+            ss_ptr, ss0 = _dev_ptr(ss, "sum_start"), 0
+        arr[j] = UBatch(_dev_ptr(data, "data") + offset, stride, ss_ptr or None, _dev_ptr(out, "out"), n, length,
+                        ss0 & 0xFFFFFFFF)
+    return arr
+
+
+def batch_uniform_multi(batches, stream=None, tune=None) -> None:
+    """Several uniform batches in one launch (tcpcsum_batch_uniform_multi_dev). ``batches``: a list of
+    (data, stride, length, n, sum_start, out[, offset]) tuples or a ready ``ubatches()`` array."""
+    arr = batches if isinstance(batches, ctypes.Array) else ubatches(batches)
+    rc = lib().tcpcsum_batch_uniform_multi_dev(ctypes.cast(arr, ctypes.c_void_p), len(arr),
+                                               _stream_handle(stream), _tune(tune))
+    _check(rc, "tcpcsum_batch_uniform_multi_dev")
 
 
 def batch_desc(data, desc, n: int, max_len: int, out=None, stream=None, tune=None):

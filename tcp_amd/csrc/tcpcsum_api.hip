@@ -19,6 +19,7 @@
 
 static_assert(sizeof(tcpcsum_desc_t) == 16, "descriptor is read as one 16-B load");
 static_assert(sizeof(tcpcsum_txseg_t) == 48, "tx descriptor is read as three 16-B loads");
+static_assert(sizeof(tcpcsum_ubatch_t) == 48 && sizeof(tcpcsum::UniformMultiEntry) == 48, "batch descriptor layout");
 
 namespace {
 
@@ -155,6 +156,24 @@ int tcpcsum_batch_uniform_dev(const void* d_base, uint64_t stride, uint32_t len,
     tcpcsum::launch_uniform((const uint8_t*)d_base, stride, len, d_sum_start, sum_start, d_out, n,
                             (hipStream_t)stream, tu);
     return check_launch();
+}
+
+int tcpcsum_batch_uniform_multi_dev(const tcpcsum_ubatch_t* b, uint32_t k, void* stream,
+                                    const tcpcsum_tuning_t* tune) {
+    tcpcsum::Tuning tu;
+    if (get_tuning(tune, &tu)) return TCPCSUM_EINVAL;
+    if (k == 0) return TCPCSUM_OK;
+    if (!b) return TCPCSUM_EINVAL;
+    for (uint32_t i = 0; i < k; ++i)
+        if (b[i].n && (!b[i].d_base || !b[i].d_out || b[i].len > (uint32_t)INT_MAX)) return TCPCSUM_EINVAL;
+    int rc = require_device(nullptr, 0);
+    if (rc) return rc;
+    for (uint32_t i = 0; i < k; i += TCPCSUM_MULTI_MAX) {
+        tcpcsum::launch_uniform_multi(b + i, std::min<uint32_t>(TCPCSUM_MULTI_MAX, k - i), (hipStream_t)stream, tu);
+        rc = check_launch();
+        if (rc) return rc;
+    }
+    return TCPCSUM_OK;
 }
 
 int tcpcsum_batch_desc_dev(const void* d_base, const tcpcsum_desc_t* d_desc, uint64_t n, uint32_t max_len,

@@ -33,6 +33,23 @@ struct UniformPlan {
 };
 UniformPlan plan_uniform(uintptr_t base, uint64_t stride, uint32_t len, uint64_t n, const Tuning& tu);
 
+// One batch of a multi-batch uniform launch (kernel-argument layout).
+struct UniformMultiEntry {
+    const uint8_t* base;
+    const uint32_t* ss;   // nullable: ss0 for every segment
+    uint16_t* out;
+    uint64_t stride;
+    uint64_t n;
+    uint32_t len;
+    uint32_t ss0;
+};
+struct UniformMultiArgs {
+    UniformMultiEntry e[TCPCSUM_MULTI_MAX];
+};
+// k <= TCPCSUM_MULTI_MAX batches: one launch when they share a lane-group
+// shape, else one launch per batch.
+void launch_uniform_multi(const tcpcsum_ubatch_t* b, uint32_t k, hipStream_t s, const Tuning& tu);
+
 void launch_uniform(const uint8_t* base, uint64_t stride, uint32_t len, const uint32_t* ss, uint32_t ss0,
                     uint16_t* out, uint64_t n, hipStream_t s, const Tuning& tu);
 void launch_desc(const uint8_t* base, const tcpcsum_desc_t* d, uint64_t n, uint32_t max_len, uint16_t* out,

@@ -29,6 +29,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "tcpcsum.h"
 #include "tcpcsum_internal.h"
 
@@ -266,6 +268,34 @@ __global__ __launch_bounds__(256) void k_uniform(const uint8_t* __restrict__ bas
             b.finish(t2, base, stride, len, out, n, q, gl);
             t = t3;
         }
+    }
+}
+
+// Several independent uniform batches in one launch (tcpcsum_batch_uniform_multi_dev):
+// batch b is grid row blockIdx.y, so the batch index is a scalar from the
+// dispatcher — no search — and its descriptor is read straight out of the
+// kernel-argument segment with scalar loads. A 64 MiB batch of 64-B segments
+// streams in ~8.4 us at peak; launched alone it takes ~13 us, the rest being
+// the grid's ramp and drain, which one launch over K batches
+// pays once. Rows are dispatched in order, so batch b+1's first waves fill the
+// CUs batch b's last waves leave.
+template <int G, int C, int U, int MODE>
+__global__ __launch_bounds__(256) void k_uniform_multi(UniformMultiArgs args) {
+    using Tile = UniformTile<G, C, U, MODE, true>;
+    const __attribute__((address_space(4))) UniformMultiArgs* A =
+        (const __attribute__((address_space(4))) UniformMultiArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    const __attribute__((address_space(4))) UniformMultiEntry& e = A->e[blockIdx.y];
+    const uint8_t* base = e.base;
+    const uint64_t stride = e.stride, n = e.n;
+    const uint32_t len = e.len;
+    const int lane = threadIdx.x & 63;
+    const int q = lane / G, gl = lane % G;
+    const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
+    const uint64_t ntiles = (n + Tile::SPT - 1) / Tile::SPT;
+    for (uint64_t t = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6); t < ntiles; t += nwaves) {
+        Tile a;
+        a.load(t, base, stride, len, e.ss, e.ss0, n, q, gl);
+        a.finish(t, base, stride, len, e.out, n, q, gl);
     }
 }
 
@@ -1792,6 +1822,85 @@ void launch_uniform(const uint8_t* base, uint64_t stride, uint32_t len, const ui
 #else
     launch_uniform_pn<false, true>(p, base, stride, len, ss, ss0, out, n, s);
 #endif
+}
+
+template <int G, int C, int U, int MODE>
+static void launch_multi_t(const UniformMultiArgs& a, uint32_t k, hipStream_t s, int max_blocks) {
+    constexpr int UE = (C * U > 32) ? (32 / C > 0 ? 32 / C : 1) : U;   // VGPR budget, as launch_uniform_t
+    constexpr int SPT = (64 / G) * UE;
+    uint64_t tiles = 0;
+    for (uint32_t i = 0; i < k; ++i) tiles = std::max<uint64_t>(tiles, (a.e[i].n + SPT - 1) / SPT);
+    hipLaunchKernelGGL((k_uniform_multi<G, C, UE, MODE>), dim3(grid_for(tiles, max_blocks), k), dim3(256), 0, s, a);
+}
+
+template <int MODE>
+static void launch_multi_mode(int shape, int unroll, const UniformMultiArgs& a, uint32_t k, hipStream_t s,
+                              int max_blocks) {
+#define TM(G, C, U) launch_multi_t<G, C, U, MODE>(a, k, s, max_blocks)
+#define TM48(G, C)                 \
+    do {                           \
+        if (unroll <= 4) TM(G, C, 4); \
+        else TM(G, C, 8);          \
+    } while (0)
+    switch (shape) {
+        case 0: TM(4, 1, 4); break;
+        case 1: TM48(8, 1); break;
+        case 2: TM48(16, 1); break;
+        case 3: TM48(32, 1); break;
+        case 4: TM48(64, 1); break;
+        case 5: TM48(32, 3); break;
+        case 6: TM48(64, 2); break;
+        case 7: TM48(64, 4); break;
+        case 8: TM(64, 8, 4); break;
+        case 10: TM(1, 5, 2); break;
+        default: TM(2, 4, 2); break;   // 11
+    }
+#undef TM48
+#undef TM
+}
+
+// Batches that share a lane-group shape (segments up to 8 KiB) go out as one
+// launch, in the most general alignment mode any of them needs and the widest
+// shape any of them needs (a shape covers every shorter segment). Anything
+// else — long segments, split or flat shapes — is launched batch by batch, where
+// a launch's ramp is a small share of its time anyway.
+void launch_uniform_multi(const tcpcsum_ubatch_t* b, uint32_t k, hipStream_t s, const Tuning& tu) {
+    UniformMultiArgs a;
+    uint32_t m = 0;
+    int mode = M16, shape = -1;
+    bool one = true;
+    for (uint32_t i = 0; i < k; ++i) {
+        if (b[i].n == 0) continue;
+        const UniformPlan p = plan_uniform((uintptr_t)b[i].d_base, b[i].stride, b[i].len, b[i].n, tu);
+        const bool lane_group = p.shape <= 8 || p.shape == 10 || p.shape == 11;
+        if (!lane_group || (shape >= 0 && (shape > 8 || p.shape > 8) && shape != p.shape)) one = false;
+        mode = std::max(mode, p.mode);
+        shape = std::max(shape, p.shape);
+        a.e[m++] = UniformMultiEntry{(const uint8_t*)b[i].d_base, b[i].d_sum_start, b[i].d_out, b[i].stride,
+                                     b[i].n, b[i].len, b[i].sum_start};
+    }
+    if (m == 0) return;
+    if (!one) {
+        for (uint32_t i = 0; i < k; ++i)
+            if (b[i].n)
+                launch_uniform((const uint8_t*)b[i].d_base, b[i].stride, b[i].len, b[i].d_sum_start, b[i].sum_start,
+                               b[i].d_out, b[i].n, s, tu);
+        return;
+    }
+    // the single-batch defaults for this shape and mode (plan_uniform)
+    int unroll = kShapeUnroll[shape];
+    int max_blocks = kShapeBlocks[shape];
+    if (mode == M1) {
+        unroll = std::min(unroll, 4);
+        max_blocks = 16384;
+    } else if (shape <= 5) {
+        max_blocks = 1 << 24;   // one tile per wave
+    }
+    if (tu.unroll) unroll = tu.unroll;
+    if (tu.max_blocks > 0) max_blocks = tu.max_blocks;
+    if (mode == M16) launch_multi_mode<M16>(shape, unroll, a, m, s, max_blocks);
+    else if (mode == M4) launch_multi_mode<M4>(shape, unroll, a, m, s, max_blocks);
+    else launch_multi_mode<M1>(shape, unroll, a, m, s, max_blocks);
 }
 
 template <int G, int C, int U>

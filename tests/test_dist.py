@@ -91,6 +91,7 @@ import bench
 rank, world, _ = bench.dist_env()
 dist.init_process_group("gloo")
 if os.environ.get("STUB_FAIL_RANK") == str(rank):
+    print(f"stub rank {{rank}}: simulated failure", file=sys.stderr)
     sys.exit(7)
 wall = bench.timed_region(lambda: time.sleep(0.001 * (rank + 1)), 3, 1, dist, lambda: None)
 wmax = bench.max_over_ranks(wall, dist, torch.device("cpu"))
@@ -131,3 +132,6 @@ def test_spawn_ranks_stops_the_others_when_one_fails(tmp_path):
     env["STUB_FAIL_RANK"] = "1"
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode == 7
+    # the failing rank's exit code and the tail of its stderr reach the launcher's stderr
+    assert "rank 1 exited with code 7 (first to fail)" in r.stderr
+    assert "stub rank 1: simulated failure" in r.stderr
