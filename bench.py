@@ -174,7 +174,7 @@ def cpu_baseline(seconds: float) -> dict:
         key = f"{L}B_{opt}_{'1thread' if th == 1 else f'{th}threads'}"
         figures[key] = {"best": round(r["best"], 3), "median": round(r["median"], 3), "passes": r["passes"],
                         "sample": f"{nseg} x {L} B"}
-        digests.setdefault(L, set()).add(r["digest"])
+        digests.setdefault((L, nseg), set()).add(r["digest"])   # same batch -> same results at any -O / threads
     head = figures[f"1500B_O2_{'1thread' if T == 1 else f'{T}threads'}"]
     return {
         "value": head["median"], "unit": "GiB/s", "cores": T, "kind": "port",

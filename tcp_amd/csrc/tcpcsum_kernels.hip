@@ -1843,7 +1843,7 @@ static void launch_multi_mode(int shape, int unroll, const UniformMultiArgs& a, 
         else TM(G, C, 8);          \
     } while (0)
     switch (shape) {
-        case 0: TM(4, 1, 4); break;
+        case 0: TM48(4, 1); break;
         case 1: TM48(8, 1); break;
         case 2: TM48(16, 1); break;
         case 3: TM48(32, 1); break;

@@ -80,23 +80,34 @@ int main(int argc, char **argv) {
         }
         uint16_t pout[P];
         uint8_t pst[P];
-        CHECK(tcpcsum_ipv4_batch_ptrs_host(ctx, pkt, plen, P, TCPCSUM_IPV4_FILL, pout, pst) == TCPCSUM_OK);
-        int pbad = 0;
-        for (int i = 0; i < P; ++i) {
-            uint8_t *b = (uint8_t *) pkt[i];
-            uint16_t got, want;
-            uint32_t sa, da;
-            memcpy(&got, b + 36, 2);
-            memset(b + 36, 0, 2);
-            memcpy(&sa, b + 12, 4); memcpy(&da, b + 16, 4);
-            want = tcpcsum_continue(tcpcsum_pseudo(sa, da, htons((uint16_t) (plen[i] - 20))), (const char *) b + 20,
-                                    (int) plen[i] - 20);
-            pbad += got != want || pout[i] != want || pst[i] != TCPCSUM_PKT_OK;
+        /* pass 0: default (packets copied through the context's pinned staging,
+         * nothing page-locked); pass 1: TCPCSUM_CTX_AUTO_REGISTER (each buffer
+         * page-locked on first use and filled in place) */
+        for (int pass = 0; pass < 2; ++pass) {
+            CHECK(tcpcsum_ctx_set_flags(ctx, pass ? TCPCSUM_CTX_AUTO_REGISTER : 0u) == TCPCSUM_OK);
+            CHECK(tcpcsum_ipv4_batch_ptrs_host(ctx, pkt, plen, P, TCPCSUM_IPV4_FILL, pout, pst) == TCPCSUM_OK);
+            int pbad = 0;
+            for (int i = 0; i < P; ++i) {
+                uint8_t *b = (uint8_t *) pkt[i];
+                uint16_t got, want;
+                uint32_t sa, da;
+                memcpy(&got, b + 36, 2);
+                memset(b + 36, 0, 2);
+                memcpy(&sa, b + 12, 4); memcpy(&da, b + 16, 4);
+                want = tcpcsum_continue(tcpcsum_pseudo(sa, da, htons((uint16_t) (plen[i] - 20))),
+                                        (const char *) b + 20, (int) plen[i] - 20);
+                pbad += got != want || pout[i] != want || pst[i] != TCPCSUM_PKT_OK;
+            }
+            uint64_t nreg = 0, nbytes = 0;
+            tcpcsum_ctx_stats_t st;
+            CHECK(tcpcsum_ctx_registered(ctx, &nreg, &nbytes) == TCPCSUM_OK);
+            CHECK(tcpcsum_ctx_get_stats(ctx, &st) == TCPCSUM_OK);
+            if (pass == 0) CHECK(nreg == 0 && nbytes == 0 && st.pkts_staged == P && st.pkts_in_place == 0);
+            else CHECK(nreg > 0 && nbytes >= P * 4096u && st.pkts_in_place == P);
+            CHECK(pbad == 0);
+            printf("gpu pointer-batch (%s) mismatches: %d / %d (%llu registrations)\n", pass ? "in place" : "staged",
+                   pbad, P, (unsigned long long) nreg);
         }
-        uint64_t nreg = 0, nbytes = 0;
-        CHECK(tcpcsum_ctx_registered(ctx, &nreg, &nbytes) == TCPCSUM_OK && nreg > 0 && nbytes >= P * 4096u);
-        CHECK(pbad == 0);
-        printf("gpu pointer-batch mismatches: %d / %d (%llu registrations)\n", pbad, P, (unsigned long long) nreg);
         CHECK(tcpcsum_ctx_unregister_host(ctx, NULL, 0) == TCPCSUM_OK);
         for (int i = 0; i < P; ++i) free(pkt[i]);
         tcpcsum_ctx_destroy(ctx);

@@ -395,7 +395,9 @@ def test_c_client_on_gpu(dev):
     exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "c", "abi_smoke")
     r = subprocess.run([exe, "--gpu"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "host-batch mismatches: 0 /" in r.stdout and "pointer-batch mismatches: 0 /" in r.stdout
+    assert "host-batch mismatches: 0 /" in r.stdout
+    assert "pointer-batch (staged) mismatches: 0 /" in r.stdout
+    assert "pointer-batch (in place) mismatches: 0 /" in r.stdout
 
 
 @pytest.mark.parametrize("layout", ["packed", "packed_odd", "slots", "jumbo", "small"])
