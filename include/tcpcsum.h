@@ -174,9 +174,14 @@ int tcpcsum_ipv4_batch_dev(void *d_pkts, uint64_t region_bytes, const uint64_t *
  * packet with tot_len > d_lens[i] or d_lens[i] < 20 is SKIPPED). cap, modes,
  * results and status exactly as tcpcsum_ipv4_batch_dev. This is the
  * loop's own layout — one separate out-buffer per packet (loop.c:180-183,
- * iov_base per message at loop.c:53-54) — with no gather copy. */
-int tcpcsum_ipv4_batch_ptrs_dev(void *const *d_pkt_ptrs, const uint32_t *d_lens, uint64_t n, uint32_t cap, int mode,
-                                uint16_t *d_out, uint8_t *d_status, void *stream, const tcpcsum_tuning_t *tune);
+ * iov_base per message at loop.c:53-54) — with no gather copy.
+ * bytes_hint: the sum of d_lens[i] if the caller knows it (0 = unknown, taken
+ * as n * cap). Only the kernel shape depends on it — as the region's size
+ * does for tcpcsum_ipv4_batch_dev: large batches of small or mixed packets go
+ * to the balanced kernel, MTU-size packets to the lane groups. */
+int tcpcsum_ipv4_batch_ptrs_dev(void *const *d_pkt_ptrs, const uint32_t *d_lens, uint64_t n, uint32_t cap,
+                                uint64_t bytes_hint, int mode, uint16_t *d_out, uint8_t *d_status, void *stream,
+                                const tcpcsum_tuning_t *tune);
 
 /* Segment assembly + checksum in one pass (device-side
  * us_internal_socket_context_send_packet, context.c:150-213, minus its 10 %

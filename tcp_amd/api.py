@@ -120,7 +120,7 @@ SIGNATURES = {
     "tcpcsum_batch_desc_dev": (ctypes.c_int, [vp, vp, u64, u32, vp, vp, tunep]),
     "tcpcsum_batch_uniform_multi_dev": (ctypes.c_int, [vp, u32, vp, tunep]),
     "tcpcsum_ipv4_batch_dev": (ctypes.c_int, [vp, u64, vp, u64, u32, ctypes.c_int, vp, vp, vp, tunep]),
-    "tcpcsum_ipv4_batch_ptrs_dev": (ctypes.c_int, [vp, vp, u64, u32, ctypes.c_int, vp, vp, vp, tunep]),
+    "tcpcsum_ipv4_batch_ptrs_dev": (ctypes.c_int, [vp, vp, u64, u32, u64, ctypes.c_int, vp, vp, vp, tunep]),
     "tcpcsum_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_size_t, ctypes.POINTER(vp)]),
     "tcpcsum_ctx_destroy": (None, [vp]),
     "tcpcsum_ctx_set_tuning": (ctypes.c_int, [vp, tunep]),
@@ -340,10 +340,12 @@ def ipv4_batch(pkts, pkt_off, n: int, cap: int, mode: int, out=None, status=None
     return out, status
 
 
-def ipv4_batch_ptrs(pkt_ptrs, lens, n: int, cap: int, mode: int, out=None, status=None, stream=None, tune=None):
+def ipv4_batch_ptrs(pkt_ptrs, lens, n: int, cap: int, mode: int, out=None, status=None, stream=None, tune=None,
+                    bytes_hint: int = 0):
     """Scatter-gather wire batch: ``pkt_ptrs`` a device int64 tensor of packet addresses (device-accessible),
-    ``lens`` a device int32 tensor of per-packet readable bytes."""
-    rc = lib().tcpcsum_ipv4_batch_ptrs_dev(_dev_ptr(pkt_ptrs, "pkt_ptrs"), _dev_ptr(lens, "lens"), n, cap, mode,
+    ``lens`` a device int32 tensor of per-packet readable bytes; ``bytes_hint`` their sum if known (shape only)."""
+    rc = lib().tcpcsum_ipv4_batch_ptrs_dev(_dev_ptr(pkt_ptrs, "pkt_ptrs"), _dev_ptr(lens, "lens"), n, cap,
+                                           bytes_hint, mode,
                                            _dev_ptr(out, "out"), _dev_ptr(status, "status"), _stream_handle(stream),
                                            _tune(tune))
     _check(rc, "tcpcsum_ipv4_batch_ptrs_dev")

@@ -203,8 +203,9 @@ int tcpcsum_ipv4_batch_dev(void* d_pkts, uint64_t region_bytes, const uint64_t* 
     return check_launch();
 }
 
-int tcpcsum_ipv4_batch_ptrs_dev(void* const* d_pkt_ptrs, const uint32_t* d_lens, uint64_t n, uint32_t cap, int mode,
-                                uint16_t* d_out, uint8_t* d_status, void* stream, const tcpcsum_tuning_t* tune) {
+int tcpcsum_ipv4_batch_ptrs_dev(void* const* d_pkt_ptrs, const uint32_t* d_lens, uint64_t n, uint32_t cap,
+                                uint64_t bytes_hint, int mode, uint16_t* d_out, uint8_t* d_status, void* stream,
+                                const tcpcsum_tuning_t* tune) {
     tcpcsum::Tuning tu;
     if (get_tuning(tune, &tu)) return TCPCSUM_EINVAL;
     if (n == 0) return TCPCSUM_OK;
@@ -214,8 +215,9 @@ int tcpcsum_ipv4_batch_ptrs_dev(void* const* d_pkt_ptrs, const uint32_t* d_lens,
     int rc = require_device(nullptr, 0);
     if (rc) return rc;
     // addresses as offsets from 0, bounded per packet by d_lens
-    tcpcsum::launch_ipv4(nullptr, (const uint64_t*)d_pkt_ptrs, d_lens, n, cap, ~0ull, n * (uint64_t)cap, mode, d_out,
-                         d_status, nullptr, (hipStream_t)stream, tu);
+    tcpcsum::launch_ipv4(nullptr, (const uint64_t*)d_pkt_ptrs, d_lens, n, cap, ~0ull,
+                         bytes_hint ? bytes_hint : n * (uint64_t)cap, mode, d_out, d_status, nullptr,
+                         (hipStream_t)stream, tu);
     return check_launch();
 }
 

@@ -93,9 +93,9 @@ def test_argument_errors_need_no_device():
     assert L.tcpcsum_ipv4_batch_dev(1 << 20, 1 << 20, 1 << 20, 5, 1500, 7, None, None, None, None) == api.EINVAL
     assert L.tcpcsum_ipv4_batch_dev(1 << 20, 1 << 20, 1 << 20, 5, 1500, 4, None, None, None, None) == api.EINVAL
     assert L.tcpcsum_ipv4_batch_dev(1 << 20, 0, 1 << 20, 5, 1500, 0, None, None, None, None) == api.EINVAL
-    assert L.tcpcsum_ipv4_batch_ptrs_dev(None, 1 << 20, 5, 1500, 0, None, None, None, None) == api.EINVAL
-    assert L.tcpcsum_ipv4_batch_ptrs_dev((1 << 20) + 4, 1 << 20, 5, 1500, 0, None, None, None, None) == api.EINVAL
-    assert L.tcpcsum_ipv4_batch_ptrs_dev(1 << 20, 1 << 20, 5, 1500, 8, None, None, None, None) == api.EINVAL
+    assert L.tcpcsum_ipv4_batch_ptrs_dev(None, 1 << 20, 5, 1500, 0, 0, None, None, None, None) == api.EINVAL
+    assert L.tcpcsum_ipv4_batch_ptrs_dev((1 << 20) + 4, 1 << 20, 5, 1500, 0, 0, None, None, None, None) == api.EINVAL
+    assert L.tcpcsum_ipv4_batch_ptrs_dev(1 << 20, 1 << 20, 5, 1500, 0, 8, None, None, None, None) == api.EINVAL
     assert L.tcpcsum_ipv4_batch_ptrs_host(None, 1 << 20, 1 << 20, 5, 0, None, None) == api.EINVAL
     assert L.tcpcsum_ctx_register_host(None, 1 << 20, 4096) == api.EINVAL
     assert L.tcpcsum_ctx_unregister_host(None, None, 0) == api.EINVAL

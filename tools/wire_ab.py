@@ -61,7 +61,7 @@ def main():
                                                   out.data_ptr(), sta.data_ptr(), h, None)
 
     def f_ptrs(mode):
-        return lambda: new.tcpcsum_ipv4_batch_ptrs_dev(ptrs.data_ptr(), lens.data_ptr(), n, 1536, mode,
+        return lambda: new.tcpcsum_ipv4_batch_ptrs_dev(ptrs.data_ptr(), lens.data_ptr(), n, 1536, 0, mode,
                                                        out.data_ptr(), sta.data_ptr(), h, None)
 
     def timeit(fn, steps=30):
