@@ -266,6 +266,8 @@ typedef struct tcpcsum_ctx_stats {
     uint64_t registered_ranges;  /* current registrations of this context */
     uint64_t registered_bytes;
     uint64_t copy_threads;       /* host threads used for staging copies (incl. the caller's) */
+    uint64_t ns_copy;            /* wall time spent copying into / out of staging (CPU) */
+    uint64_t ns_wait;            /* wall time spent waiting for the device after the last launch */
     uint64_t reserved;
 } tcpcsum_ctx_stats_t;
 int tcpcsum_ctx_get_stats(tcpcsum_ctx_t *ctx, tcpcsum_ctx_stats_t *out);

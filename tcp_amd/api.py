@@ -106,7 +106,7 @@ class CtxStats(ctypes.Structure):
     _fields_ = [("batches", ctypes.c_uint64), ("pkts_in_place", ctypes.c_uint64), ("pkts_staged", ctypes.c_uint64),
                 ("bytes_staged", ctypes.c_uint64), ("registered_ranges", ctypes.c_uint64),
                 ("registered_bytes", ctypes.c_uint64), ("copy_threads", ctypes.c_uint64),
-                ("reserved", ctypes.c_uint64)]
+                ("ns_copy", ctypes.c_uint64), ("ns_wait", ctypes.c_uint64), ("reserved", ctypes.c_uint64)]
 
 # name -> (restype, argtypes); must cover every function in include/tcpcsum.h
 SIGNATURES = {

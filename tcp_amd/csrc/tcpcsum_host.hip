@@ -34,6 +34,7 @@
 // All checksum arithmetic runs in the gfx950 kernels of tcpcsum_kernels.hip;
 // this file reads header fields (IHL, tot_len) only to size the copies.
 
+#include <emmintrin.h>
 #include <hip/hip_runtime.h>
 #include <sched.h>
 #include <stdint.h>
@@ -49,6 +50,7 @@
 #include <memory>
 #include <mutex>
 #include <new>
+#include <chrono>
 #include <thread>
 #include <vector>
 
@@ -97,6 +99,11 @@ struct HipHostBackend {
         return true;
     }
 };
+
+inline uint64_t now_ns() {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 // A few host threads for the copies into pinned staging: one core's memcpy
 // (≈10-20 GB/s) is below the PCIe rate the kernel reads staging at
@@ -164,28 +171,36 @@ private:
         } catch (...) {   // fewer threads than asked: the caller still does all the work it must
         }
     }
+    // A worker spins briefly after each job before it sleeps: a wire batch
+    // hands the pool one job per launch block, microseconds apart, and a
+    // condition-variable wake-up costs about as long as a block's copy.
     void loop() {
         uint64_t seen = 0;
         for (;;) {
+            const uint64_t t0 = now_ns();
+            while (gen_.load(std::memory_order_acquire) == seen && !quit_.load(std::memory_order_relaxed) &&
+                   now_ns() - t0 < kSpinNs)
+                _mm_pause();
             std::shared_ptr<Job> job;
             {
                 std::unique_lock<std::mutex> lk(m_);
-                cv_.wait(lk, [&] { return quit_ || gen_ != seen; });
+                cv_.wait(lk, [&] { return quit_.load() || gen_.load() != seen; });
                 if (quit_) return;
-                seen = gen_;
+                seen = gen_.load();
                 job = cur_;
             }
             if (job) job->drain();
         }
     }
+    static constexpr uint64_t kSpinNs = 50000;
     int nw_;
     bool started_ = false;
     std::vector<std::thread> th_;
     std::mutex m_;
     std::condition_variable cv_;
     std::shared_ptr<Job> cur_;
-    uint64_t gen_ = 0;
-    bool quit_ = false;
+    std::atomic<uint64_t> gen_{0};
+    std::atomic<bool> quit_{false};
 };
 
 // Host threads for staging copies: TCPCSUM_HOST_THREADS, else half the CPUs
@@ -208,6 +223,38 @@ int default_copy_threads() {
         fclose(f);
     }
     return std::max(1, std::min(8, cpus / 2));
+}
+
+// memcpy into staging with non-temporal (streaming) stores: the kernel reads
+// the staging over PCIe, not the CPU, so the copy should not first read the
+// destination lines into the cache (read-for-ownership) nor evict the source
+// stream's own working set. Ends with sfence: streaming stores are weakly
+// ordered, and the piece must be globally visible before the launch.
+inline void copy_nt(uint8_t* d, const uint8_t* s, size_t n) {
+    size_t h = (16u - ((uintptr_t)d & 15u)) & 15u;
+    if (h > n) h = n;
+    memcpy(d, s, h);
+    d += h;
+    s += h;
+    n -= h;
+    const size_t k = n & ~(size_t)63;
+    for (size_t i = 0; i < k; i += 64) {
+        const __m128i a = _mm_loadu_si128((const __m128i*)(s + i));
+        const __m128i b = _mm_loadu_si128((const __m128i*)(s + i + 16));
+        const __m128i c = _mm_loadu_si128((const __m128i*)(s + i + 32));
+        const __m128i e = _mm_loadu_si128((const __m128i*)(s + i + 48));
+        _mm_stream_si128((__m128i*)(d + i), a);
+        _mm_stream_si128((__m128i*)(d + i + 16), b);
+        _mm_stream_si128((__m128i*)(d + i + 32), c);
+        _mm_stream_si128((__m128i*)(d + i + 48), e);
+    }
+    memcpy(d + k, s + k, n - k);
+    _mm_sfence();
+}
+
+inline int env_int(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return e && *e ? atoi(e) : dflt;
 }
 
 // Page-locked host memory owned by a context, with its device view.
@@ -286,6 +333,8 @@ struct tcpcsum_ctx {
     tcpcsum::HipHostBackend backend;
     tcpcsum::HostRegistry<tcpcsum::HipHostBackend> reg{backend};
     std::unique_ptr<tcpcsum::CopyPool> pool;
+    bool nt_copy = true;   // streaming stores for the uniform chunks (TCPCSUM_HOST_NT=0: plain memcpy)
+    int wire_blocks = 4;   // wire batches: launches per batch, each after its packets are staged
     tcpcsum_ctx_stats_t stats{};
     std::mutex mu;
 };
@@ -328,12 +377,25 @@ void* pinned_dev_ptr(const void* p, size_t bytes = 1) {
     return a.devicePointer;
 }
 
-// memcpy on the context's copy threads (pieces of 256 KiB).
-void par_copy(tcpcsum_ctx* c, void* dst, const void* src, size_t n) {
+// memcpy on the context's copy threads (pieces of 256 KiB); nt: streaming stores.
+void par_copy(tcpcsum_ctx* c, void* dst, const void* src, size_t n, bool nt = false) {
     constexpr size_t kGrain = 256u << 10;
     uint8_t* d = (uint8_t*)dst;
     const uint8_t* s = (const uint8_t*)src;
-    c->pool->run(n, kGrain, [&](size_t lo, size_t hi) { memcpy(d + lo, s + lo, hi - lo); });
+    const uint64_t t0 = tcpcsum::now_ns();
+    if (nt)
+        c->pool->run(n, kGrain, [&](size_t lo, size_t hi) { tcpcsum::copy_nt(d + lo, s + lo, hi - lo); });
+    else
+        c->pool->run(n, kGrain, [&](size_t lo, size_t hi) { memcpy(d + lo, s + lo, hi - lo); });
+    c->stats.ns_copy += tcpcsum::now_ns() - t0;
+}
+
+// hipStreamSynchronize, timed into stats.ns_wait.
+hipError_t wait_stream(tcpcsum_ctx* c, hipStream_t st) {
+    const uint64_t t0 = tcpcsum::now_ns();
+    const hipError_t e = hipStreamSynchronize(st);
+    c->stats.ns_wait += tcpcsum::now_ns() - t0;
+    return e;
 }
 
 int ensure_pkt_arrays(tcpcsum_ctx* c, uint64_t n) {
@@ -348,10 +410,9 @@ int ensure_pkt_arrays(tcpcsum_ctx* c, uint64_t n) {
     return TCPCSUM_OK;
 }
 
-// Copy the packets listed in g_* into c->gath (each at a 16-B aligned offset)
-// and point their kernel addresses there. Packets are few KiB each: pieces of
-// 16 packets per thread.
-int gather_packets(tcpcsum_ctx* c, uint64_t* k_off, size_t total) {
+// Make room for `total` bytes of staged packets and point every listed
+// packet's kernel address into it (the copies themselves: copy_staged).
+int stage_packets(tcpcsum_ctx* c, uint64_t* k_off, size_t total) {
     const size_t m = c->g_idx.size();
     if (!m) return TCPCSUM_OK;
     hipError_t e = c->gath.ensure(total ? total : 16);
@@ -359,13 +420,42 @@ int gather_packets(tcpcsum_ctx* c, uint64_t* k_off, size_t total) {
         tcpcsum::note_hip_error((int)e);
         return TCPCSUM_ENOMEM;
     }
-    uint8_t* gh = c->gath.h;
-    c->pool->run(m, 16, [&](size_t lo, size_t hi) {
-        for (size_t k = lo; k < hi; ++k) memcpy(gh + c->g_off[k], c->g_src[k], c->g_len[k]);
-    });
     for (size_t k = 0; k < m; ++k) k_off[c->g_idx[k]] = (uint64_t)(uintptr_t)(c->gath.d + c->g_off[k]);
     c->stats.pkts_staged += m;
     c->stats.bytes_staged += total;
+    return TCPCSUM_OK;
+}
+
+// Copy staged packets [g0, g1) of the list into c->gath (16 packets a piece).
+void copy_staged(tcpcsum_ctx* c, size_t g0, size_t g1) {
+    if (g1 <= g0) return;
+    const uint64_t t0 = tcpcsum::now_ns();
+    uint8_t* gh = c->gath.h;
+    c->pool->run(g1 - g0, 16, [&](size_t lo, size_t hi) {
+        for (size_t k = g0 + lo; k < g0 + hi; ++k) memcpy(gh + c->g_off[k], c->g_src[k], c->g_len[k]);
+    });
+    c->stats.ns_copy += tcpcsum::now_ns() - t0;
+}
+
+// The scatter-gather wire kernel over packets [0, n) whose addresses / bounds
+// are in c->p_off / c->p_len, in up to c->wire_blocks launches on st: the CPU
+// copies block j+1's staged packets while the kernel runs on block j.
+int launch_wire_blocks(tcpcsum_ctx* c, uint64_t n, uint32_t cap, uint64_t foot, int mode, uint16_t* kout,
+                       uint8_t* kst, hipStream_t st, const tcpcsum::Tuning& tu) {
+    const uint64_t blocks = c->g_idx.empty() || n < 256u ? 1u : (uint64_t)std::max(1, c->wire_blocks);
+    const uint64_t per = (n + blocks - 1) / blocks;
+    size_t g = 0;
+    for (uint64_t i0 = 0; i0 < n; i0 += per) {
+        const uint64_t cnt = std::min<uint64_t>(per, n - i0);
+        size_t g1 = g;
+        while (g1 < c->g_idx.size() && c->g_idx[g1] < i0 + cnt) ++g1;
+        copy_staged(c, g, g1);
+        g = g1;
+        tcpcsum::launch_ipv4(nullptr, (const uint64_t*)c->p_off.d + i0, (const uint32_t*)c->p_len.d + i0, cnt, cap,
+                             ~0ull, foot / n * cnt, mode, kout + i0, kst + i0, nullptr, st, tu);
+        const int rc = check_launch();
+        if (rc) return rc;
+    }
     return TCPCSUM_OK;
 }
 
@@ -419,6 +509,8 @@ int tcpcsum_ctx_create(int device, size_t scratch_bytes, tcpcsum_ctx_t** out) {
         return TCPCSUM_ENOMEM;
     }
     c->stats.copy_threads = (uint64_t)c->pool->threads();
+    c->nt_copy = tcpcsum::env_int("TCPCSUM_HOST_NT", 1) != 0;
+    c->wire_blocks = std::max(1, std::min(64, tcpcsum::env_int("TCPCSUM_HOST_WIRE_BLOCKS", 4)));
     for (int i = 0; i < 2; ++i) {
         e = hipStreamCreateWithFlags(&c->st[i], hipStreamNonBlocking);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->slot_ev[i], hipEventDisableTiming);
@@ -506,7 +598,7 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t st
         if (!kss) {
             e = c->ss.ensure(n * sizeof(uint32_t));
             if (e != hipSuccess) return hip_fail(e);
-            par_copy(c, c->ss.h, h_sum_start, n * sizeof(uint32_t));
+            par_copy(c, c->ss.h, h_sum_start, n * sizeof(uint32_t), c->nt_copy);
             kss = (const uint32_t*)c->ss.d;
         }
     }
@@ -522,7 +614,7 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t st
         tcpcsum::launch_uniform(zb, stride, len, kss, sum_start, kout, n, c->st[0], tu);
         rc = check_launch();
         if (rc) return rc;
-        e = hipStreamSynchronize(c->st[0]);
+        e = wait_stream(c, c->st[0]);
         if (e != hipSuccess) return hip_fail(e);
     } else {
         // segments per chunk: (cnt-1)*stride + len <= chunk (at least one segment)
@@ -543,13 +635,15 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t st
             const uint8_t* src = (const uint8_t*)h_base + s0 * stride;
             if (c->slot_busy[s]) {   // the kernel that last read this slot (chunk k-2)
                 c->slot_busy[s] = false;
+                const uint64_t t0 = tcpcsum::now_ns();
                 e = hipEventSynchronize(c->slot_ev[s]);
+                c->stats.ns_wait += tcpcsum::now_ns() - t0;
                 if (e != hipSuccess) return hip_fail(e);
             }
             // keep the start's alignment mod 16, so the kernel shape matches what the
             // same batch gets in place
             const size_t mis = (uintptr_t)src & 15u;
-            par_copy(c, c->slot[s].h + mis, src, bytes);
+            par_copy(c, c->slot[s].h + mis, src, bytes, c->nt_copy);
             c->stats.bytes_staged += bytes;
             tcpcsum::launch_uniform(c->slot[s].d + mis, stride, len, kss ? kss + s0 : nullptr, sum_start,
                                     kout + s0, cnt, c->st[s], tu);
@@ -561,7 +655,7 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t st
         }
         for (int i = 0; i < 2; ++i) {
             c->slot_busy[i] = false;
-            e = hipStreamSynchronize(c->st[i]);
+            e = wait_stream(c, c->st[i]);
             if (e != hipSuccess) return hip_fail(e);
         }
     }
@@ -636,14 +730,14 @@ int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t* c, void* h_pkts, size_t region_bytes,
             k_len[i] = cl;
             maxl = std::max(maxl, cl);
         }
-        rc = gather_packets(c, k_off, total);
+        rc = stage_packets(c, k_off, total);
         if (rc) return rc;
-        tcpcsum::launch_ipv4(nullptr, (const uint64_t*)c->p_off.d, (const uint32_t*)c->p_len.d, n, maxl, ~0ull,
-                             total, mode, kout, kst, nullptr, st, tu);
+        rc = launch_wire_blocks(c, n, maxl, total, mode, kout, kst, st, tu);
+        if (rc) return rc;
     }
     rc = check_launch();
     if (rc) return rc;
-    e = hipStreamSynchronize(st);
+    e = wait_stream(c, st);
     if (e != hipSuccess) return hip_fail(e);
     if (fill && !c->g_idx.empty())
         write_back_checks(c, zst ? h_status : c->p_stat.h, (mode & TCPCSUM_IPV4_IPHDR) != 0);
@@ -708,7 +802,7 @@ int tcpcsum_ipv4_batch_ptrs_host(tcpcsum_ctx_t* c, void* const* h_pkts, const ui
     }
     if (c->reg.last_lock_error()) tcpcsum::note_hip_error(c->reg.last_lock_error());
     c->stats.pkts_in_place += in_place;
-    rc = gather_packets(c, k_off, total);
+    rc = stage_packets(c, k_off, total);
     if (rc) return rc;
     uint16_t* zout = h_out ? (uint16_t*)pinned_dev_ptr(h_out, n * sizeof(uint16_t)) : nullptr;
     uint8_t* zst = h_status ? (uint8_t*)pinned_dev_ptr(h_status, n) : nullptr;
@@ -716,11 +810,10 @@ int tcpcsum_ipv4_batch_ptrs_host(tcpcsum_ctx_t* c, void* const* h_pkts, const ui
     // (as tcpcsum_ipv4_batch_host on a pinned pool)
     tcpcsum::Tuning tu = c->tune;
     if (tu.shape < 0 && n < 65536u) tu.shape = 3;
-    tcpcsum::launch_ipv4(nullptr, (const uint64_t*)c->p_off.d, (const uint32_t*)c->p_len.d, n, cap, ~0ull, foot,
-                         mode, zout ? zout : (uint16_t*)c->p_out.d, zst ? zst : c->p_stat.d, nullptr, st, tu);
-    rc = check_launch();
+    rc = launch_wire_blocks(c, n, cap, foot, mode, zout ? zout : (uint16_t*)c->p_out.d, zst ? zst : c->p_stat.d, st,
+                            tu);
     if (rc) return rc;
-    hipError_t e = hipStreamSynchronize(st);
+    hipError_t e = wait_stream(c, st);
     if (e != hipSuccess) return hip_fail(e);
     if ((mode & TCPCSUM_IPV4_VERIFY) == 0 && !c->g_idx.empty())
         write_back_checks(c, zst ? h_status : c->p_stat.h, (mode & TCPCSUM_IPV4_IPHDR) != 0);

@@ -3,19 +3,21 @@
 
 The reference's packets start and end in host memory (raw-socket buffers).
 This measures the library's host entry points on MI355X:
-  * tcpcsum_batch_uniform_host over 1M x 1500 B in pageable memory
-    (pipelined H2D -> kernel -> D2H) and in pinned memory (zero-copy: the
+  * tcpcsum_batch_uniform_host over 1M x 1500 B in pageable memory (copied
+    by the context's host threads into pinned staging, chunk k+1 while the
+    kernel reads chunk k over PCIe) and in pinned memory (zero-copy: the
     kernel reads host memory over PCIe);
   * tcpcsum_ipv4_batch_host FILL on one releaseSend-sized batch (1024 packets
     of 1500 B, loop.c:27-94) in the reference's pool layout (32 KiB slots) and
     packed, pageable vs pinned — per-batch latency (--sweep: per wire kernel
     shape / window flag);
   * tcpcsum_ipv4_batch_ptrs_host FILL over 1024 separately allocated pageable
-    buffers (the loop's own layout, loop.c:180-183): first batch (page-locks
-    the buffers) and steady state;
+    buffers (the loop's own layout, loop.c:180-183): default (packets copied
+    into pinned staging) and TCPCSUM_CTX_AUTO_REGISTER (buffers page-locked
+    on first use, then read in place): first batch and steady state;
   * the sendmmsg seam itself (tools/mmsg_bench under libtcpcsum_preload.so,
-    in place and with TCPCSUM_PRELOAD_COPY=1) beside the reference's CPU path
-    for the same batch (one csum_continue per packet, -O2, one core).
+    default = staged, and TCPCSUM_PRELOAD_INPLACE=1) beside the reference's
+    CPU path for the same batch (one csum_continue per packet, -O2, one core).
 
   python tools/e2e.py  -> one JSON line per measurement
 """
@@ -113,24 +115,30 @@ def main():
     outb = bufs[1::2]
     ptrs = [b.ctypes.data for b in outb]
     lens = np.full(1024, 1500, np.uint32)
-    t0 = time.perf_counter()
-    ctx.ipv4_batch_ptrs(ptrs, lens, tcp_amd.IPV4_FILL)
-    first = time.perf_counter() - t0
-    tmin, tmed = best_of(lambda: ctx.ipv4_batch_ptrs(ptrs, lens, tcp_amd.IPV4_FILL), 200)
-    nreg, nbytes = ctx.registered()
-    print(json.dumps({"measure": "ipv4_fill_ptrs_host_1024x1500", "layout": "1024 separate 32 KiB buffers (pageable)",
-                      "first_batch_us": round(first * 1e6, 1), "us_best": round(tmin * 1e6, 1),
-                      "us_median": round(tmed * 1e6, 1), "registrations": nreg, "registered_bytes": nbytes,
-                      "GiB/s_packet_bytes_median": round(1024 * 1500 / tmed / 2**30, 2)}), flush=True)
-    if "--sweep" in sys.argv:
-        for sh in (0, 1, 3, 4, 5, 6, 7, 8):
-            for fl in (0, tcp_amd.TUNE_WIN16, tcp_amd.TUNE_WIRE_CACHED):
-                ctx.set_tuning(0, 0, sh, fl)
-                tmin, tmed = best_of(lambda: ctx.ipv4_batch_ptrs(ptrs, lens, tcp_amd.IPV4_FILL), 100)
-                print(json.dumps({"measure": "ipv4_fill_ptrs_host_1024x1500", "shape": sh, "flags": fl,
-                                  "us_best": round(tmin * 1e6, 1), "us_median": round(tmed * 1e6, 1)}), flush=True)
-        ctx.set_tuning(0, 0, -1, 0)
-    ctx.unregister_host()
+    ctx.close()
+    for mode in ("staged", "auto_register"):
+        ctx = tcp_amd.HostContext(0, auto_register=(mode == "auto_register"))
+        t0 = time.perf_counter()
+        ctx.ipv4_batch_ptrs(ptrs, lens, tcp_amd.IPV4_FILL)
+        first = time.perf_counter() - t0
+        tmin, tmed = best_of(lambda: ctx.ipv4_batch_ptrs(ptrs, lens, tcp_amd.IPV4_FILL), 200)
+        nreg, nbytes = ctx.registered()
+        print(json.dumps({"measure": "ipv4_fill_ptrs_host_1024x1500", "mode": mode,
+                          "layout": "1024 separate 32 KiB buffers (pageable)",
+                          "first_batch_us": round(first * 1e6, 1), "us_best": round(tmin * 1e6, 1),
+                          "us_median": round(tmed * 1e6, 1), "registrations": nreg, "registered_bytes": nbytes,
+                          "GiB/s_packet_bytes_median": round(1024 * 1500 / tmed / 2**30, 2),
+                          "ctx": ctx.stats()}), flush=True)
+        if "--sweep" in sys.argv:
+            for sh in (0, 1, 3, 4, 5, 6, 7, 8):
+                for fl in (0, tcp_amd.TUNE_WIN16, tcp_amd.TUNE_WIRE_CACHED):
+                    ctx.set_tuning(0, 0, sh, fl)
+                    tmin, tmed = best_of(lambda: ctx.ipv4_batch_ptrs(ptrs, lens, tcp_amd.IPV4_FILL), 100)
+                    print(json.dumps({"measure": "ipv4_fill_ptrs_host_1024x1500", "mode": mode, "shape": sh,
+                                      "flags": fl, "us_best": round(tmin * 1e6, 1), "us_median": round(tmed * 1e6, 1)}),
+                          flush=True)
+            ctx.set_tuning(0, 0, -1, 0)
+        ctx.unregister_host()
     ctx.close()
 
     # the seam itself: the interposer's per-batch latency vs the reference's CPU path
@@ -140,10 +148,10 @@ def main():
     import subprocess
     for label, mode, env_extra in (("cpu_reference_O2", "cpu", {}),
                                    ("preload_off", "gpu", {"TCPCSUM_PRELOAD_TX": "off"}),
-                                   ("preload_fill_inplace", "gpu", {"TCPCSUM_PRELOAD_TX": "fill"}),
-                                   ("preload_fill_copy", "gpu", {"TCPCSUM_PRELOAD_TX": "fill",
-                                                                 "TCPCSUM_PRELOAD_COPY": "1"})):
-        env = dict(os.environ)
+                                   ("preload_fill_staged", "gpu", {"TCPCSUM_PRELOAD_TX": "fill"}),
+                                   ("preload_fill_inplace", "gpu", {"TCPCSUM_PRELOAD_TX": "fill",
+                                                                    "TCPCSUM_PRELOAD_INPLACE": "1"})):
+        env = {k: v for k, v in os.environ.items() if not k.startswith("TCPCSUM_PRELOAD")}
         if mode == "gpu":
             env.update({"LD_PRELOAD": pre, "TCPCSUM_PRELOAD_ANY_SOCKET": "1"})
         env.update(env_extra)
