@@ -319,6 +319,8 @@ struct tcpcsum_ctx {
     hipEvent_t slot_ev[2] = {nullptr, nullptr};
     bool slot_busy[2] = {false, false};
     tcpcsum::Pinned slot[2];   // uniform batches: one staged chunk per stream
+    uint8_t* d_slot[2] = {nullptr, nullptr};   // ... and its device copy (uniform_dma)
+    size_t d_slot_bytes = 0;
     tcpcsum::Pinned gath;      // wire batches: packets copied out of pageable memory
     tcpcsum::Pinned ss, res;   // per-segment start values / results, when the caller's are pageable
     // per-packet arrays the wire kernels read (addresses, bounds) and write
@@ -334,6 +336,7 @@ struct tcpcsum_ctx {
     tcpcsum::HostRegistry<tcpcsum::HipHostBackend> reg{backend};
     std::unique_ptr<tcpcsum::CopyPool> pool;
     bool nt_copy = true;   // streaming stores for the uniform chunks (TCPCSUM_HOST_NT=0: plain memcpy)
+    bool uniform_dma = true;   // staged uniform chunks go to HBM by DMA (TCPCSUM_HOST_DMA=0: kernel reads them over PCIe)
     int wire_blocks = 4;   // wire batches: launches per batch, each after its packets are staged
     tcpcsum_ctx_stats_t stats{};
     std::mutex mu;
@@ -510,6 +513,7 @@ int tcpcsum_ctx_create(int device, size_t scratch_bytes, tcpcsum_ctx_t** out) {
     }
     c->stats.copy_threads = (uint64_t)c->pool->threads();
     c->nt_copy = tcpcsum::env_int("TCPCSUM_HOST_NT", 1) != 0;
+    c->uniform_dma = tcpcsum::env_int("TCPCSUM_HOST_DMA", 1) != 0;
     c->wire_blocks = std::max(1, std::min(64, tcpcsum::env_int("TCPCSUM_HOST_WIRE_BLOCKS", 4)));
     for (int i = 0; i < 2; ++i) {
         e = hipStreamCreateWithFlags(&c->st[i], hipStreamNonBlocking);
@@ -530,6 +534,7 @@ void tcpcsum_ctx_destroy(tcpcsum_ctx_t* c) {
         if (c->st[i]) hipStreamSynchronize(c->st[i]);
     c->reg.release(0, 0);
     for (int i = 0; i < 2; ++i) {
+        if (c->d_slot[i]) hipFree(c->d_slot[i]);
         if (c->slot_ev[i]) hipEventDestroy(c->slot_ev[i]);
         if (c->st[i]) hipStreamDestroy(c->st[i]);
     }
@@ -627,13 +632,25 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t st
             e = c->slot[i].ensure(slot_bytes);
             if (e != hipSuccess) return hip_fail(e);
         }
+        if (c->uniform_dma && slot_bytes > c->d_slot_bytes) {
+            for (int i = 0; i < 2; ++i) {
+                if (c->d_slot[i]) (void)hipFree(c->d_slot[i]);
+                c->d_slot[i] = nullptr;
+            }
+            c->d_slot_bytes = 0;
+            for (int i = 0; i < 2; ++i) {
+                e = hipMalloc(&c->d_slot[i], slot_bytes);
+                if (e != hipSuccess) return hip_fail(e);
+            }
+            c->d_slot_bytes = slot_bytes;
+        }
         uint64_t k = 0;
         for (uint64_t s0 = 0; s0 < n; s0 += per, ++k) {
             const int s = (int)(k & 1);
             const uint64_t cnt = (n - s0) < per ? (n - s0) : per;
             const size_t bytes = (size_t)((cnt - 1) * stride + len);
             const uint8_t* src = (const uint8_t*)h_base + s0 * stride;
-            if (c->slot_busy[s]) {   // the kernel that last read this slot (chunk k-2)
+            if (c->slot_busy[s]) {   // the DMA (or kernel) that last read this slot: chunk k-2
                 c->slot_busy[s] = false;
                 const uint64_t t0 = tcpcsum::now_ns();
                 e = hipEventSynchronize(c->slot_ev[s]);
@@ -645,12 +662,22 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t st
             const size_t mis = (uintptr_t)src & 15u;
             par_copy(c, c->slot[s].h + mis, src, bytes, c->nt_copy);
             c->stats.bytes_staged += bytes;
-            tcpcsum::launch_uniform(c->slot[s].d + mis, stride, len, kss ? kss + s0 : nullptr, sum_start,
-                                    kout + s0, cnt, c->st[s], tu);
+            const uint8_t* kin = c->slot[s].d + mis;
+            if (c->uniform_dma) {   // pinned -> HBM by the DMA engines, then the kernel reads HBM
+                e = hipMemcpyAsync(c->d_slot[s] + mis, c->slot[s].h + mis, bytes, hipMemcpyHostToDevice, c->st[s]);
+                if (e != hipSuccess) return hip_fail(e);
+                e = hipEventRecord(c->slot_ev[s], c->st[s]);
+                if (e != hipSuccess) return hip_fail(e);
+                kin = c->d_slot[s] + mis;
+            }
+            tcpcsum::launch_uniform(kin, stride, len, kss ? kss + s0 : nullptr, sum_start, kout + s0, cnt, c->st[s],
+                                    tu);
             rc = check_launch();
             if (rc) return rc;
-            e = hipEventRecord(c->slot_ev[s], c->st[s]);
-            if (e != hipSuccess) return hip_fail(e);
+            if (!c->uniform_dma) {
+                e = hipEventRecord(c->slot_ev[s], c->st[s]);
+                if (e != hipSuccess) return hip_fail(e);
+            }
             c->slot_busy[s] = true;
         }
         for (int i = 0; i < 2; ++i) {

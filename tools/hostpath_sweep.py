@@ -4,6 +4,8 @@ context's copy knobs, read at tcpcsum_ctx_create:
   TCPCSUM_HOST_THREADS       copy threads (incl. the caller's)
   TCPCSUM_HOST_NT            streaming stores for the uniform chunks
   TCPCSUM_HOST_WIRE_BLOCKS   launches per wire batch (copy block j+1 while block j runs)
+  TCPCSUM_HOST_DMA           uniform chunks: DMA to HBM then the kernel (0: kernel reads staging over PCIe)
+--configs: threads:nt:wire_blocks:dma,...
 Measures tcpcsum_batch_uniform_host over 1M x 1500 B pageable, and one
 releaseSend batch (1024 x 1500-B packets) FILLed through
 tcpcsum_ipv4_batch_host (pageable 32 KiB-slot pool) and
@@ -35,7 +37,7 @@ def timed(fn, reps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=2)
-    ap.add_argument("--configs", default="8:1:4,12:1:4,16:1:4,8:0:4,8:1:1,8:1:2,8:1:8,12:1:8")
+    ap.add_argument("--configs", default="8:1:1:1,8:1:1:0,12:1:1:1,8:0:1:1,8:1:2:1,4:1:1:1")
     args = ap.parse_args()
     import numpy as np
     import tcp_amd
@@ -61,10 +63,11 @@ def main():
     lens = np.full(1024, 1500, np.uint32)
     configs = [tuple(int(x) for x in c.split(":")) for c in args.configs.split(",")]
     for rnd in range(args.rounds):
-        for th, nt, wb in configs:
+        for th, nt, wb, dma in configs:
             os.environ["TCPCSUM_HOST_THREADS"] = str(th)
             os.environ["TCPCSUM_HOST_NT"] = str(nt)
             os.environ["TCPCSUM_HOST_WIRE_BLOCKS"] = str(wb)
+            os.environ["TCPCSUM_HOST_DMA"] = str(dma)
             with tcp_amd.HostContext(0) as ctx:
                 got = ctx.batch_uniform(big, L, L, n, ss)
                 if want is None:
@@ -73,7 +76,7 @@ def main():
                 s0 = ctx.stats()
                 tmin, tmed = timed(lambda: ctx.batch_uniform(big, L, L, n, ss), 5)
                 s1 = ctx.stats()
-                cfg = {"threads": th, "nt": nt, "wire_blocks": wb, "round": rnd}
+                cfg = {"threads": th, "nt": nt, "wire_blocks": wb, "dma": dma, "round": rnd}
                 print(json.dumps({**cfg, "measure": "uniform_host_1Mx1500_pageable",
                                   "GiB/s_median": round(n * L / tmed / 2**30, 2),
                                   "GiB/s_best": round(n * L / tmin / 2**30, 2),
@@ -83,12 +86,13 @@ def main():
                                  ("ipv4_ptrs_host_loop_fill", lambda: ctx.ipv4_batch_ptrs(ptrs, lens, 0))):
                     fn()
                     s0 = ctx.stats()
-                    tmin, tmed = timed(fn, 100)
+                    reps = 300
+                    tmin, tmed = timed(fn, reps)
                     s1 = ctx.stats()
                     print(json.dumps({**cfg, "measure": name, "us_median": round(tmed * 1e6, 1),
                                       "us_best": round(tmin * 1e6, 1),
-                                      "copy_us_per_call": round((s1["ns_copy"] - s0["ns_copy"]) / 1e5, 1),
-                                      "wait_us_per_call": round((s1["ns_wait"] - s0["ns_wait"]) / 1e5, 1)}),
+                                      "copy_us_per_call": round((s1["ns_copy"] - s0["ns_copy"]) / reps / 1e3, 1),
+                                      "wait_us_per_call": round((s1["ns_wait"] - s0["ns_wait"]) / reps / 1e3, 1)}),
                           flush=True)
 
 
