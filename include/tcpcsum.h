@@ -366,6 +366,9 @@ int tcpcsum_plan_uniform(uint64_t base, uint64_t stride, uint32_t len, uint64_t 
 #define TCPCSUM_TUNE_WIN16 64    /* wire: 16-B (not 128-B) aligned packet windows */
 #define TCPCSUM_TUNE_TX_NT_STORE 128  /* builder: non-temporal payload stores */
 #define TCPCSUM_TUNE_FILL_DWORD 256   /* wire FILL: store check|urg_ptr as one dword when TCP+16 is 4-B aligned */
+/* wire FILL: always the 2-byte store (default: where the 128-B line holding the check lies
+ * inside the packet, the whole line is written back through, the check patched in) */
+#define TCPCSUM_TUNE_FILL_U16 512
 /* 0 if *tune is a valid tuning (NULL counts as valid), else TCPCSUM_EINVAL. */
 int tcpcsum_tuning_check(const tcpcsum_tuning_t *tune);
 

@@ -929,7 +929,7 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const 
                                               const uint32_t* __restrict__ plen,
                                               uint64_t n, uint32_t cap, uint64_t limit, int mode,
                                               uint16_t* __restrict__ out, uint8_t* __restrict__ status,
-                                              uint16_t* __restrict__ ipout, uint32_t amask, bool dword_store) {
+                                              uint16_t* __restrict__ ipout, uint32_t amask, int store_mode) {
     // amask: window alignment - 1. Lane gl of a group loads window chunks k*G+gl,
     // so with 128-B windows every group load instruction covers whole 128-B
     // lines however the packet is aligned. Header fields lie in window bytes
@@ -1107,19 +1107,64 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const 
         // even relative offset, so its native word contributes exactly check_word.
         if (!verify) S -= check_word;
         d.c = fold_ref(S);
-        d.th = th;
-        d.urg = check_dw & 0xffff0000u;
-        d.fill = !verify;
-        uint32_t st = TCPCSUM_PKT_OK;
-        if (verify && d.c != 0 && check_word == (uint32_t)(uint16_t)~fold_ref(ps)) st |= TCPCSUM_PKT_CSUM_PARTIAL;
+        // IPv4 header checksum = csum_continue(0, ip, ihl*4) with check (IP+10) as
+        // zero — the reference's commented-out context.c:179, over ihl*4 bytes.
+        uint16_t ic_fill = 0;
         if (iphdr) {
-            // IPv4 header checksum = csum_continue(0, ip, ihl*4) with check (IP+10)
-            // as zero — the reference's commented-out context.c:179, over ihl*4 bytes.
             const uint64_t WI = group_sum64<G>((uint64_t)wi);
             const uint64_t OI = odd ? group_sum64<G>((uint64_t)oi) : 0;
             uint64_t IS = combine(0, WI, OI, odd);
             if (!verify) IS -= h8 >> 16;
-            d.ic = fold_ref(IS);
+            ic_fill = fold_ref(IS);
+        }
+        d.th = th;
+        d.urg = check_dw & 0xffff0000u;
+        d.fill = !verify;
+        // FILL, line store (store_mode 2, the default): when the 128-B line holding
+        // the check (and, with IPHDR, the IPv4 header checksum) lies inside this
+        // packet and in the group's first-round registers, the group writes the
+        // whole line back — the bytes it read, the checksums patched in — as
+        // write-through (sc0 sc1) 16-B stores, instead of 2-byte stores that leave
+        // partially dirty lines to be written back later: FILL on 1M x 1500-B
+        // packets in 1536-B slots 0.328 -> 0.289 ms (VERIFY 0.246;
+        // tools/fill_line_ab.py, profiles/r03_fill_line_ab.jsonl).
+        if (store_mode == 2 && !verify && amask == 127u && (m & 1u) == 0) {
+            const uint32_t cpos = m + th + 16u;   // window offset of the check (even)
+            const uint32_t ipos = m + 10u;        // ... of the IPv4 header checksum
+            const uint32_t L = cpos >> 7;
+            if ((L << 7) >= m && (L << 7) + 128u <= m + tot && 8u * L + 8u <= (uint32_t)(G * C) &&
+                (!iphdr || (ipos >> 7) == L)) {
+                auto patch = [](u32x4& x, uint32_t pos, uint32_t v16) {
+                    const uint32_t sh = (pos & 2u) * 8u, j = (pos >> 2) & 3u;
+                    const uint32_t keep = ~(0xffffu << sh), val = v16 << sh;
+                    x.x = j == 0u ? (x.x & keep) | val : x.x;
+                    x.y = j == 1u ? (x.y & keep) | val : x.y;
+                    x.z = j == 2u ? (x.z & keep) | val : x.z;
+                    x.w = j == 3u ? (x.w & keep) | val : x.w;
+                };
+#pragma unroll
+                for (int k = 0; k < C; ++k) {
+                    const uint32_t idx = (uint32_t)(k * G + gl);
+                    if ((idx >> 3) == L) {
+                        u32x4 x = v[u][k];
+                        if (idx == (cpos >> 4)) patch(x, cpos, (uint32_t)d.c);
+                        if (iphdr && idx == (ipos >> 4)) patch(x, ipos, (uint32_t)ic_fill);
+                        uint8_t* dst = ip - m + (uint64_t)idx * 16u;
+                        // the compiler cannot see into the asm, so it does not keep the
+                        // VMEM-store data hazard (a VALU write to the store's data VGPRs
+                        // right after a >64-bit store corrupts the stored dwords): the
+                        // s_nop gives the store its wait states before the VGPRs are reused
+                        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 3" ::"v"(dst), "v"(x)
+                                     : "memory");
+                    }
+                }
+                d.fill = false;   // stored
+            }
+        }
+        uint32_t st = TCPCSUM_PKT_OK;
+        if (verify && d.c != 0 && check_word == (uint32_t)(uint16_t)~fold_ref(ps)) st |= TCPCSUM_PKT_CSUM_PARTIAL;
+        if (iphdr) {
+            d.ic = ic_fill;
             if (verify && d.ic != 0) st |= TCPCSUM_PKT_IPHDR_BAD;
         }
         d.st = (uint8_t)st;
@@ -1129,7 +1174,7 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const 
         if (!d.w || gl != 0) return;
         if (d.fill) {
             uint8_t* cp = d.ip + d.th + 16;
-            if (dword_store && ((uintptr_t)cp & 3u) == 0)   // check and the unchanged urg_ptr in one dword
+            if (store_mode == 1 && ((uintptr_t)cp & 3u) == 0)   // check and the unchanged urg_ptr in one dword
                 stg<uint32_t>(cp, d.urg | d.c);
             else
                 store_u16(cp, d.c);   // native u16 store, as context.c:208
@@ -1967,7 +2012,7 @@ void launch_desc(const uint8_t* base, const tcpcsum_desc_t* d, uint64_t n, uint3
 template <int G, int C, int U>
 static void launch_ipv4_t(uint8_t* pkts, const uint64_t* off, const uint32_t* plen, uint64_t n, uint32_t cap,
                           uint64_t limit, int mode, uint16_t* out, uint8_t* status, uint16_t* ipout, hipStream_t s,
-                          int max_blocks, bool nt, uint32_t amask, bool dw) {
+                          int max_blocks, bool nt, uint32_t amask, int dw) {
     constexpr int SPT = (64 / G) * U;
     const dim3 grid(grid_for((n + SPT - 1) / SPT, max_blocks));
     // per-packet bounds only when given: the extra load and register cost the
@@ -1996,7 +2041,9 @@ void launch_ipv4(uint8_t* pkts, const uint64_t* off, const uint32_t* plen, uint6
     const int unroll = tu.unroll ? tu.unroll : 1;
     const bool nt = (tu.flags & TCPCSUM_TUNE_WIRE_CACHED) == 0;
     const uint32_t amask = (tu.flags & TCPCSUM_TUNE_WIN16) ? 15u : 127u;
-    const bool dw = (tu.flags & TCPCSUM_TUNE_FILL_DWORD) != 0;
+    // FILL store: the whole 128-B line written through where it lies inside the
+    // packet (default), one native u16 (context.c:208), or the check|urg_ptr dword
+    const int dw = (tu.flags & TCPCSUM_TUNE_FILL_DWORD) ? 1 : (tu.flags & TCPCSUM_TUNE_FILL_U16) ? 0 : 2;
     // shape by the cap and by the mean packet footprint (region bytes / n; the
     // summed lengths for scatter-gather batches): packed small packets one
     // chunk per lane, MTU slots one round of 96 chunks per packet

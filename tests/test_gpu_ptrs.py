@@ -17,6 +17,7 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
+from tests.isolated import isolated  # noqa: E402
 from tests.tensors import host, to_dev, u16  # noqa: E402
 
 
@@ -135,6 +136,7 @@ def _loop_pool(rng, n, slot=32768, payload=None):
 
 
 @pytest.mark.parametrize("auto_register", [False, True])
+@isolated(lambda auto_register, **_: auto_register)   # page-locks heap buffers: own process
 def test_ipv4_ptrs_host_loop_layout(dev, auto_register):
     """1024 separate pageable buffers: FILL, then VERIFY, then a shuffled sub-batch with short bounds.
     Default: every packet is copied into the context's pinned staging and its check stored back —
@@ -240,6 +242,7 @@ def test_ipv4_ptrs_host_context_tuning(dev):
 
 
 @pytest.mark.parametrize("register", ["none", "whole", "half", "tail"])
+@isolated(lambda register, **_: register != "none")   # page-locks host memory: own process
 def test_ipv4_region_host_registered_pool(dev, register):
     """The region host path over a pageable pool: its packets staged when the pool is pageable or only
     partly registered (first half / second half), read in place when the whole pool is registered

@@ -16,6 +16,7 @@ import numpy as np
 import pytest
 
 import oracle
+from tests.isolated import isolated
 
 FIXTURE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "plumbing_echoes.npz")
 
@@ -64,6 +65,7 @@ def test_oracle_reproduces_captured_checks():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("path", ["staged", "in_place", "region", "device"])
+@isolated(lambda path, **_: path == "in_place")   # page-locks heap buffers: own process
 def test_plumbing_fill_on_gpu(path):
     """The plumbing config's checksum work on the GPU: the 256 captured echoes, zeroed, each in its
     own pageable 32 KiB buffer (the loop's layout) — FILL|IPHDR through tcpcsum_ipv4_batch_ptrs_host
