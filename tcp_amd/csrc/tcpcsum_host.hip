@@ -337,7 +337,7 @@ struct tcpcsum_ctx {
     std::unique_ptr<tcpcsum::CopyPool> pool;
     bool nt_copy = true;   // streaming stores for the uniform chunks (TCPCSUM_HOST_NT=0: plain memcpy)
     bool uniform_dma = true;   // staged uniform chunks go to HBM by DMA (TCPCSUM_HOST_DMA=0: kernel reads them over PCIe)
-    int wire_blocks = 4;   // wire batches: launches per batch, each after its packets are staged
+    int wire_blocks = 1;   // wire batches: launches per batch, each after its packets are staged (measurement knob)
     tcpcsum_ctx_stats_t stats{};
     std::mutex mu;
 };
@@ -514,7 +514,7 @@ int tcpcsum_ctx_create(int device, size_t scratch_bytes, tcpcsum_ctx_t** out) {
     c->stats.copy_threads = (uint64_t)c->pool->threads();
     c->nt_copy = tcpcsum::env_int("TCPCSUM_HOST_NT", 1) != 0;
     c->uniform_dma = tcpcsum::env_int("TCPCSUM_HOST_DMA", 1) != 0;
-    c->wire_blocks = std::max(1, std::min(64, tcpcsum::env_int("TCPCSUM_HOST_WIRE_BLOCKS", 4)));
+    c->wire_blocks = std::max(1, std::min(64, tcpcsum::env_int("TCPCSUM_HOST_WIRE_BLOCKS", 1)));
     for (int i = 0; i < 2; ++i) {
         e = hipStreamCreateWithFlags(&c->st[i], hipStreamNonBlocking);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->slot_ev[i], hipEventDisableTiming);
