@@ -1,0 +1,424 @@
+#!/bin/bash
+# gpu_runs.sh — the GPU experiments behind DESIGN.md, one function each, run on an MI355X
+# box through gpurun:  /usr/local/graft/bin/gpurun -- bash tools/gpu_runs.sh <name>
+# (`bash tools/gpu_runs.sh` alone lists them). Outputs go under gpurun_out/; the
+# summaries judged are copied into profiles/. Every GPU step has its own time limit.
+
+# round 3: wire FILL line store (default) — every GPU test first, then the A/B timing three
+# times (the two FILL stores must agree byte for byte every time)
+gpu_r3_fill() {
+(
+  timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/gputest_fill_line.log 2>&1
+  rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/gputest_fill_line.log
+  if [ $rc -eq 0 ]; then
+    for i in 1 2 3; do
+      timeout -k 10 200 python tools/fill_line_ab.py --rounds 2 >> gpurun_out/fill_line_ab2.jsonl 2> gpurun_out/fill_line_ab.err || { echo "ab failed"; exit 1; }
+    done
+    echo ab ok
+  fi
+)
+}
+
+# round 3: the wire FILL change under every GPU test and the A/B, then an N=8 rehearsal of
+# bench.py on one GPU (all eight ranks share it; every rank checks its 8Mx1500 shard digest)
+gpu_r3_n8() {
+(
+  gpu_r3_fill || exit 1
+  TCPCSUM_BENCH_SHARE_DEVICE=1 timeout -k 10 300 python3 bench.py --gpus 8 --steps 5 --warmup 2 --no-other-configs > gpurun_out/bench_n8_shared.json 2> gpurun_out/bench_n8_shared.err
+  echo "n8 rc=$?"; cat gpurun_out/bench_n8_shared.json | cut -c1-400
+)
+}
+
+# gpu_round3
+gpu_round3() {
+(
+  timeout -k 10 700 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > gpurun_out/gputest_r3b.log 2>&1; rc=$?
+  echo "pytest rc=$rc"; tail -15 gpurun_out/gputest_r3b.log | grep -E "passed|failed|FAILED|Error" 
+  if [ $rc -eq 0 ] || [ $rc -eq 1 ]; then
+    timeout -k 10 300 python bench.py --steps 50 --warmup 5 --cpu-seconds 6 > gpurun_out/bench_r3b.json 2> gpurun_out/bench_r3b.err; echo "bench rc=$?"
+  fi
+)
+}
+
+# New uniform default (blocks 0) against the previous caps (512 / 4096) at small and MTU sizes.
+grid_check() {
+(
+  set -e
+  O=gpurun_out/grid_check
+  mkdir -p $O
+  for L in 64 100 128 200 256 576 1024 1500; do
+    timeout -k 10 200 python3 tools/sweep.py --len $L --blocks 0,512,4096 --unrolls 0 --rounds 5 --steps 20 > $O/len$L.jsonl 2>>$O/err
+  done
+)
+}
+
+# One-wave-per-segment uniform batches (shape 9): default grid against larger ones.
+grid_long() {
+(
+  set -e
+  O=gpurun_out/grid_long
+  mkdir -p $O
+  for L in 9000 12300 20004 65536; do
+    timeout -k 10 200 python3 tools/sweep.py --len $L --blocks 0,4096,16384,16777216 --unrolls 0 --rounds 5 --steps 10 > $O/len$L.jsonl 2>>$O/err
+  done
+)
+}
+
+# Byte-granular (M1) uniform batches: the 4096-workgroup default against larger grids.
+grid_m1() {
+(
+  set -e
+  O=gpurun_out/grid_m1
+  mkdir -p $O
+  for L in 99 577 1499 3001; do
+    timeout -k 10 200 python3 tools/sweep.py --len $L --blocks 0,16384,65536,16777216 --unrolls 0,2 --rounds 5 --steps 20 > $O/len$L.jsonl 2>>$O/err
+  done
+)
+}
+
+# Default grid vs one tile per wave (max_blocks uncapped) for the uniform kernel
+# across the bench configs and a few mid sizes (tools/sweep.py, interleaved rounds).
+grid_sweep() {
+(
+  set -e
+  O=gpurun_out/grid_sweep
+  mkdir -p $O
+  timeout -k 10 200 python3 tools/sweep.py --config 64 --blocks 0,4096,16384,65536,262144 --unrolls 0 --rounds 5 --steps 30 > $O/c64.jsonl 2>>$O/err
+  timeout -k 10 200 python3 tools/sweep.py --config 64k --blocks 0,1024,4096,65536 --unrolls 0 --rounds 5 --steps 10 > $O/c64k.jsonl 2>>$O/err
+  for L in 256 576 4096 8192; do
+    timeout -k 10 200 python3 tools/sweep.py --len $L --blocks 0,16384,65536,262144 --unrolls 0 --rounds 5 --steps 20 > $O/len$L.jsonl 2>>$O/err
+  done
+  timeout -k 10 200 python3 tools/sweep.py --config 1500 --blocks 0,16384 --unrolls 0 --rounds 7 --steps 30 --probe > $O/c1500.jsonl 2>>$O/err
+)
+}
+
+# 64 KiB config: why bench.py (2.47 ms) and the sweep (2.40 ms) differ — steps, warmup, shape.
+k64_check() {
+(
+  set -e
+  O=gpurun_out/k64
+  mkdir -p $O
+  B="python3 bench.py --config 64k --no-cpu-baseline --no-other-configs"
+  for s in 5 40; do
+    timeout -k 10 120 $B --steps $s --warmup 3 > $O/bench_s$s.json 2>>$O/err
+    timeout -k 10 120 $B --steps $s --warmup 3 --shape 9 > $O/bench_s${s}_shape9.json 2>>$O/err
+  done
+  timeout -k 10 200 python3 tools/sweep.py --config 64k --shapes 9,13 --blocks 0 --unrolls 0 --rounds 2 --steps 40 > $O/sweep_s40.jsonl 2>>$O/err
+)
+}
+
+# Balanced kernels: per-lane sums for tiles of small segments, against the previous build.
+lane_ab() {
+(
+  set -e
+  O=gpurun_out/lane
+  mkdir -p $O
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fuzz.py tests/test_gpu_ptrs.py -x -q --timeout 120 --timeout-method thread > $O/parity.log 2>&1
+  timeout -k 10 300 python3 tools/lb_ab.py tcp_amd/ab/libtcpcsum_prev.so > $O/lb_ab.jsonl 2> $O/lb_ab.err
+)
+}
+
+# lb_sweep
+lb_sweep() {
+(
+  set -e
+  for cfg in "0,0,9,0 0,0,8,0" "1024,0,8,0 1024,0,7,0" "2048,0,8,0 2048,0,7,0" "16384,0,8,0 16384,0,7,0"; do
+    set -- $cfg
+    LB_HEAD_WIRE=$1 LB_HEAD_DESC=$2 timeout -k 10 120 python3 tools/lb_ab.py tcp_amd/ab/libtcpcsum_r02a.so > gpurun_out/lbsweep_$1.jsonl 2>>gpurun_out/lbsweep.err
+  done
+)
+}
+
+# Wire shape 10 (window chunks through LDS) against the lane-group defaults.
+lds_ab() {
+(
+  set -e
+  O=gpurun_out/lds
+  mkdir -p $O
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fuzz.py tests/test_gpu_ptrs.py -x -q --timeout 120 --timeout-method thread -k "ipv4 or fuzz or ptrs" > $O/parity.log 2>&1
+  for S in 1536 1024 2048; do
+    SLOT=$S SHAPES=-1,5,7,10 BLOCKS=0 UNROLLS=1 timeout -k 10 300 python3 tools/wiresweep.py > $O/slot$S.jsonl 2>> $O/err
+  done
+)
+}
+
+# pmc_64
+pmc_64() {
+(
+  set -e
+  cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+  B="python3 bench.py --steps 60 --warmup 5 --no-other-configs --no-cpu-baseline --probe"
+  for cfg in 64 64k; do
+    timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_${cfg}_fetch -o p -- $B --config $cfg > gpurun_out/pmc_${cfg}_fetch.log 2>&1
+    timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_${cfg}_write -o p -- $B --config $cfg > gpurun_out/pmc_${cfg}_write.log 2>&1
+  done
+  timeout -s KILL 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/kt_64 -o p -- $B --config 64 > gpurun_out/kt_64.log 2>&1
+  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD --output-format csv -d gpurun_out/pmc_64_sq -o p -- $B --config 64 > gpurun_out/pmc_64_sq.log 2>&1
+)
+}
+
+# Counters for the balanced wire kernel on packed IMIX only (tools/lb_ab.py workload).
+pmc_imix() {
+(
+  set -e
+  cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+  O=gpurun_out/pmc_imix
+  mkdir -p $O
+  export LB_ONLY=ipv4_lb_1M_imix_packed_verify
+  timeout -s KILL 180 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU --output-format csv -d $O/a -o p -- python3 tools/lb_ab.py > $O/a.log 2>&1
+  timeout -s KILL 180 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_VMEM GRBM_GUI_ACTIVE --output-format csv -d $O/b -o p -- python3 tools/lb_ab.py > $O/b.log 2>&1
+  timeout -s KILL 180 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o k -- python3 tools/lb_ab.py > $O/kt.log 2>&1
+  echo done
+)
+}
+
+# Counters for the balanced wire kernel on packed IMIX (tools/lb_ab.py workloads), one pass each.
+pmc_lb() {
+(
+  set -e
+  cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+  O=gpurun_out/pmc_lb
+  mkdir -p $O
+  timeout -k 10 120 ./tests/c/abi_smoke --gpu > $O/abi_smoke.log 2>&1
+  P="python3 tools/lb_ab.py"
+  timeout -s KILL 180 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES --output-format csv -d $O/a -o p -- $P > $O/a.log 2>&1
+  timeout -s KILL 180 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_ANY SQ_INST_CYCLES_VMEM GRBM_GUI_ACTIVE --output-format csv -d $O/b -o p -- $P > $O/b.log 2>&1
+  timeout -s KILL 180 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o k -- $P > $O/kt.log 2>&1
+  echo done
+)
+}
+
+# Round-3 evidence on one MI355X (through gpurun): rocprofv3 kernel trace of the
+# headline bench (its average must agree with bench.py's HIP events), FETCH_SIZE
+# of the headline kernel, FETCH/WRITE_SIZE of the 64-B multi-batch launch, and
+# WRITE_SIZE / FETCH_SIZE of the wire FILL stores (2-byte vs line vs VERIFY).
+# Every pass is its own run (rocprofv3 does not split counters over passes).
+round3_profile() {
+(
+  O=gpurun_out/r3prof
+  mkdir -p $O
+  cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+  B="python3 bench.py --steps 100 --no-other-configs --no-cpu-baseline --probe"
+  run() { echo "== $1"; shift; "$@" || { echo "failed: $?"; exit 1; }; }
+  run kt timeout -s KILL 180 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o k -- $B > $O/bench_under_rocprof.json 2> $O/kt.err
+  run fetch timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o p -- $B > $O/pmc_fetch.log 2>&1
+  M="python3 tools/multi_sweep.py --ks 16 --unrolls 4 --grids 0 --rounds 1 --steps 10"
+  run mfetch timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_multi_fetch -o p -- $M > $O/pmc_multi_fetch.log 2>&1
+  run mwrite timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_multi_write -o p -- $M > $O/pmc_multi_write.log 2>&1
+  W="python3 tools/wire_fill_pmc.py"
+  run wwrite timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_wire_write -o p -- $W > $O/pmc_wire_write.log 2>&1
+  run wfetch timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_wire_fetch -o p -- $W > $O/pmc_wire_fetch.log 2>&1
+  run wkt timeout -s KILL 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_wire -o k -- $W > $O/kt_wire.log 2>&1
+  echo done
+)
+}
+
+# Round-end evidence (gpurun): GPU tests, smoke, default bench, N=2 rehearsal on one GPU
+# (TCPCSUM_BENCH_SHARE_DEVICE=1: both ranks on cuda:0), rocprofv3 kernel trace of the headline.
+round_final() {
+(
+  set -e
+  O=gpurun_out/final
+  mkdir -p $O
+  timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/gputest.log 2>&1
+  timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+  timeout -k 10 400 python3 bench.py > $O/bench.json 2> $O/bench.err
+  TCPCSUM_BENCH_SHARE_DEVICE=1 timeout -k 10 300 python3 bench.py --gpus 2 --steps 50 > $O/bench_n2_shared.json 2> $O/bench_n2.err
+  cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+  timeout -s KILL 180 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o k -- python3 bench.py --steps 100 --no-other-configs --no-cpu-baseline > $O/bench_under_rocprof.json 2> $O/kt.err
+  echo done
+)
+}
+
+# Round-end evidence on one MI355X (run through gpurun): GPU tests, smoke, the
+# default bench line, and rocprofv3 summaries of the headline kernel — kernel
+# trace (average duration must agree with bench.py's HIP events) and a separate
+# FETCH_SIZE pass (traffic) — plus WRITE_SIZE of the wire FILL. Outputs under
+# gpurun_out/round/; copy what is judged into profiles/.
+round_profile() {
+(
+  set -e
+  R=${1:-r02}
+  O=gpurun_out/round
+  mkdir -p $O
+  timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/gputest.log 2>&1
+  timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+  timeout -k 10 400 python3 bench.py > $O/bench.json 2> $O/bench.err
+  cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+  B="python3 bench.py --steps 100 --no-other-configs --no-cpu-baseline --probe"
+  timeout -s KILL 180 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o k -- $B > $O/bench_under_rocprof.json 2> $O/kt.err
+  timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o p -- $B > $O/pmc_fetch.log 2>&1
+  timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_wire_write -o p -- python3 tools/fillbench.py > $O/pmc_wire_write.log 2>&1
+  echo done
+)
+}
+
+# Split-segment kernel (shape 13: four waves per segment) against the
+# one-wave-per-segment kernel (shape 9) on long uniform segments.
+split_sweep() {
+(
+  set -e
+  O=gpurun_out/split
+  mkdir -p $O
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread \
+    -k "forced_shapes or long_segments or two_fold or all_unrolls" > $O/parity.log 2>&1
+  for L in 12300 20004 32768 65536 131072; do
+    timeout -k 10 200 python3 tools/sweep.py --len $L --shapes 9,13 --blocks 0 --unrolls 0,2,4,8 --rounds 5 --steps 10 > $O/len$L.jsonl 2>>$O/err
+  done
+  timeout -k 10 300 python3 tools/sweep.py --config 64k --shapes 9,13 --blocks 0 --unrolls 0,2,4,8 --rounds 3 --steps 5 > $O/cfg64k.jsonl 2>>$O/err
+)
+}
+
+# Split-segment kernel (shape 13) vs shape 9, second pass: jumbo / byte-granular / aligned mid sizes.
+split_sweep2() {
+(
+  set -e
+  O=gpurun_out/split2
+  mkdir -p $O
+  for L in 9000 8999 12301 16384 24576 49152 65536 65532; do
+    timeout -k 10 200 python3 tools/sweep.py --len $L --shapes 9,13 --blocks 0 --unrolls 0,1,2 --rounds 5 --steps 10 > $O/len$L.jsonl 2>>$O/err
+  done
+  timeout -k 10 300 python3 tools/sweep.py --config 64k --shapes 9,13 --blocks 0,1024,4096 --unrolls 0,2 --rounds 3 --steps 5 > $O/cfg64k.jsonl 2>>$O/err
+)
+}
+
+# Balanced ragged kernel with segments-per-wave sized by max_len: parity, sweep, A/B vs the previous build.
+spw_check() {
+(
+  set -e
+  O=gpurun_out/spw
+  mkdir -p $O
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fuzz.py -x -q --timeout 120 --timeout-method thread -k "desc or balanced or fuzz" > $O/parity.log 2>&1
+  SIZES=1500,4096,9000,32768,65536 SHAPES=-1,4,5,6,8 ROUNDS=3 timeout -k 10 400 python3 tools/desc_sweep.py > $O/desc.jsonl 2> $O/err
+  timeout -k 10 300 python3 tools/lb_ab.py tcp_amd/ab/libtcpcsum_prev.so > $O/lb_ab.jsonl 2>> $O/err
+)
+}
+
+# Segment builder shapes across payload sizes (pure ACK .. jumbo).
+tx_size_sweep() {
+(
+  set -e
+  O=gpurun_out/txs
+  mkdir -p $O
+  for L in 0 40 536 1456 4000 8956; do
+    TX_LEN=$L TX_SHAPES=-1,0,1,2,3,4 TX_BLOCKS=32768 TX_UNROLLS=1 timeout -k 10 300 python3 tools/txbench.py --sweep > $O/len$L.jsonl 2>> $O/err
+  done
+)
+}
+
+# Segment builder: (16,2) vs (32,3) lane groups between 256 B and 1.2 KiB payloads.
+tx_size_sweep2() {
+(
+  set -e
+  O=gpurun_out/txs2
+  mkdir -p $O
+  for L in 256 536 768 1024 1200; do
+    TX_LEN=$L TX_SHAPES=2,1,2,1 TX_BLOCKS=32768 TX_UNROLLS=1 timeout -k 10 300 python3 tools/txbench.py --sweep > $O/len$L.jsonl 2>> $O/err
+  done
+)
+}
+
+# Uniform batches across sizes: the auto plan against every shape that covers the size.
+uniform_size_sweep() {
+(
+  set -e
+  O=gpurun_out/usz
+  mkdir -p $O
+  for L in 40 200 576 1024 2048 3000 4096 6000 8192; do
+    timeout -k 10 200 python3 tools/sweep.py --len $L --shapes=-1,2,3,4,5,6,7,8,9,12,13 --blocks 0 --unrolls 0 --rounds 3 --steps 10 > $O/len$L.jsonl 2>>$O/err
+  done
+)
+}
+
+# Uniform 6-8 KiB segments: shape 8 (64 lanes x 8 chunks) against one wave (9) and four waves (13) per segment.
+uniform_size_sweep2() {
+(
+  set -e
+  O=gpurun_out/usz2
+  mkdir -p $O
+  for L in 6400 7000 7600 8000 8192; do
+    timeout -k 10 200 python3 tools/sweep.py --len $L --shapes=-1,9,13 --blocks 0 --unrolls 0,1 --rounds 5 --steps 10 > $O/len$L.jsonl 2>>$O/err
+  done
+)
+}
+
+# Wire lane-group shapes on packets between the MTU and jumbo sizes (slots 2-9 KiB).
+wire_big_sweep() {
+(
+  set -e
+  O=gpurun_out/wbig
+  mkdir -p $O
+  for S in 2048 3072 4608 9216; do
+    SLOT=$S SHAPES=-1,1,2,4,7 BLOCKS=0 UNROLLS=1,2 timeout -k 10 300 python3 tools/wiresweep.py > $O/slot$S.jsonl 2>> $O/err
+  done
+)
+}
+
+# Wire defaults after the size-class rule: parity, then the default shape per slot size.
+wire_default_check() {
+(
+  set -e
+  O=gpurun_out/wdef
+  mkdir -p $O
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fuzz.py tests/test_gpu_ptrs.py -x -q --timeout 120 --timeout-method thread -k "ipv4 or fuzz or ptrs" > $O/parity.log 2>&1
+  for S in 1536 2048 3072 4608 9216; do
+    SLOT=$S SHAPES=-1,1,7 BLOCKS=0 UNROLLS=1 timeout -k 10 300 python3 tools/wiresweep.py > $O/slot$S.jsonl 2>> $O/err
+  done
+)
+}
+
+# Balanced wire kernel on 64K-128K-packet batches: auto (>= 4096 wave tiles) vs forced 64-packet tiles.
+wire_lb_small() {
+(
+  set -e
+  O=gpurun_out/wlbs
+  mkdir -p $O
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fuzz.py tests/test_gpu_ptrs.py -x -q --timeout 120 --timeout-method thread -k "ipv4 or fuzz or ptrs" > $O/parity.log 2>&1
+  for N in 65536 131072; do
+    N=$N SLOT=84 PAYLOAD=40 SHAPES=-1,8,0 BLOCKS=0 UNROLLS=1 timeout -k 10 200 python3 tools/wiresweep.py > $O/s84_n$N.jsonl 2>> $O/err
+    N=$N SLOT=576 PAYLOAD=496 SHAPES=-1,8,7 BLOCKS=0 UNROLLS=1 timeout -k 10 200 python3 tools/wiresweep.py > $O/s576_n$N.jsonl 2>> $O/err
+  done
+)
+}
+
+# wire_mid_sweep
+wire_mid_sweep() {
+(
+  set -e
+  for sp in "768 688" "896 816"; do
+    set -- $sp
+    SLOT=$1 PAYLOAD=$2 SHAPES=8,7 BLOCKS=0,16384 UNROLLS=1 timeout -k 10 200 python3 tools/wiresweep.py | grep -v round > gpurun_out/wire_mtu_sweep_$1.jsonl
+  done
+)
+}
+
+# Lane-group wire kernel shapes across slot sizes, VERIFY and FILL (tools/wiresweep.py):
+# auto (-1), 5 (8 x 12 chunks), 7 (8 x 4 chunks, more rounds), 8 (balanced).
+wire_mtu_sweep() {
+(
+  set -e
+  for sp in "576 496" "1024 944" "1536 1456"; do
+    set -- $sp
+    SLOT=$1 PAYLOAD=$2 SHAPES=${SHAPES:--1,5,7,8} BLOCKS=${BLOCKS:-0,16384} UNROLLS=1 timeout -k 10 200 \
+      python3 tools/wiresweep.py | grep -v round > gpurun_out/wire_mtu_sweep_$1.jsonl
+  done
+)
+}
+
+# Wire shapes on small device-resident batches of MTU packets (1536-B slots).
+wire_small_sweep() {
+(
+  set -e
+  O=gpurun_out/wsm
+  mkdir -p $O
+  for N in 1024 8192 32768; do
+    N=$N SHAPES=-1,1,3,5,7 BLOCKS=0 UNROLLS=1 timeout -k 10 200 python3 tools/wiresweep.py > $O/n$N.jsonl 2>> $O/err
+  done
+)
+}
+
+if [ $# -eq 0 ]; then
+  echo "experiments: gpu_r3_fill gpu_r3_n8 gpu_round3 grid_check grid_long grid_m1 grid_sweep k64_check lane_ab lb_sweep lds_ab pmc_64 pmc_imix pmc_lb round3_profile round_final round_profile split_sweep split_sweep2 spw_check tx_size_sweep tx_size_sweep2 uniform_size_sweep uniform_size_sweep2 wire_big_sweep wire_default_check wire_lb_small wire_mid_sweep wire_mtu_sweep wire_small_sweep"
+  exit 0
+fi
+"$@"
