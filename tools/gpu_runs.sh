@@ -417,8 +417,24 @@ wire_small_sweep() {
 )
 }
 
+# Round 3 rehearsal of the driver's round-end steps at HEAD: every GPU test, smoke(), the
+# default bench line (the driver's command), then the host-path end-to-end rates.
+round3_final() {
+(
+  O=gpurun_out/final3
+  mkdir -p $O
+  timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > $O/gputest.log 2>&1 || { tail -5 $O/gputest.log; exit 1; }
+  tail -1 $O/gputest.log
+  timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { cat $O/smoke.log; exit 1; }
+  tail -1 $O/smoke.log
+  timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { tail $O/bench.err; exit 1; }
+  timeout -k 10 300 python3 tools/e2e.py > $O/e2e.jsonl 2> $O/e2e.err || { tail $O/e2e.err; exit 1; }
+  echo final ok
+)
+}
+
 if [ $# -eq 0 ]; then
-  echo "experiments: gpu_r3_fill gpu_r3_n8 gpu_round3 grid_check grid_long grid_m1 grid_sweep k64_check lane_ab lb_sweep lds_ab pmc_64 pmc_imix pmc_lb round3_profile round_final round_profile split_sweep split_sweep2 spw_check tx_size_sweep tx_size_sweep2 uniform_size_sweep uniform_size_sweep2 wire_big_sweep wire_default_check wire_lb_small wire_mid_sweep wire_mtu_sweep wire_small_sweep"
+  echo "experiments: round3_final gpu_r3_fill gpu_r3_n8 gpu_round3 grid_check grid_long grid_m1 grid_sweep k64_check lane_ab lb_sweep lds_ab pmc_64 pmc_imix pmc_lb round3_profile round_final round_profile split_sweep split_sweep2 spw_check tx_size_sweep tx_size_sweep2 uniform_size_sweep uniform_size_sweep2 wire_big_sweep wire_default_check wire_lb_small wire_mid_sweep wire_mtu_sweep wire_small_sweep"
   exit 0
 fi
 "$@"
