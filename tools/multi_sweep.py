@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--ks", default="1,4,8,16")
     ap.add_argument("--unrolls", default="4,8")
     ap.add_argument("--grids", default="0,8192,32768")
+    ap.add_argument("--shapes", default="-1", help="forced lane-group shapes (-1 = auto)")
     args = ap.parse_args()
     import torch
     import tcp_amd
@@ -44,13 +45,13 @@ def main():
     outs = [torch.empty(n, dtype=torch.int16, device=dev) for _ in range(16)]
     torch.cuda.synchronize()
     st = torch.cuda.current_stream()
-    points = [(k, u, g) for k in map(int, args.ks.split(",")) for u in map(int, args.unrolls.split(","))
-              for g in map(int, args.grids.split(","))]
+    points = [(k, u, g, sh) for k in map(int, args.ks.split(",")) for u in map(int, args.unrolls.split(","))
+              for g in map(int, args.grids.split(",")) for sh in map(int, args.shapes.split(","))]
     for rnd in range(args.rounds):
-        for K, unroll, grid in points:
+        for K, unroll, grid, shape in points:
             groups = [tcp_amd.ubatches([(bufs[(g * K + j) % R], L, L, n, sss[(g * K + j) % R], outs[j])
                                         for j in range(K)]) for g in range(R // K)]
-            tune = tcp_amd.make_tuning(grid, unroll, -1, 0)
+            tune = tcp_amd.make_tuning(grid, unroll, shape, 0)
             for i in range(3):
                 tcp_amd.batch_uniform_multi(groups[i % len(groups)], tune=tune)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -62,7 +63,7 @@ def main():
             ms = e0.elapsed_time(e1) / args.steps
             per = ms / K
             gbs = n * L / (per * 1e-3) / 1e9
-            print(json.dumps({"round": rnd, "len": L, "n": n, "K": K, "unroll": unroll, "max_blocks": grid,
+            print(json.dumps({"round": rnd, "len": L, "n": n, "K": K, "unroll": unroll, "max_blocks": grid, "shape": shape,
                               "ms_per_launch": round(ms, 5), "ms_per_batch": round(per, 5),
                               "GB/s": round(gbs, 1), "frac": round(gbs / 8000.0, 4)}), flush=True)
 
