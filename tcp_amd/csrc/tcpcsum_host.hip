@@ -337,7 +337,6 @@ struct tcpcsum_ctx {
     std::unique_ptr<tcpcsum::CopyPool> pool;
     bool nt_copy = true;   // streaming stores for the uniform chunks (TCPCSUM_HOST_NT=0: plain memcpy)
     bool uniform_dma = true;   // staged uniform chunks go to HBM by DMA (TCPCSUM_HOST_DMA=0: kernel reads them over PCIe)
-    int wire_blocks = 1;   // wire batches: launches per batch, each after its packets are staged (measurement knob)
     tcpcsum_ctx_stats_t stats{};
     std::mutex mu;
 };
@@ -413,69 +412,6 @@ int ensure_pkt_arrays(tcpcsum_ctx* c, uint64_t n) {
     return TCPCSUM_OK;
 }
 
-// Make room for `total` bytes of staged packets and point every listed
-// packet's kernel address into it (the copies themselves: copy_staged).
-int stage_packets(tcpcsum_ctx* c, uint64_t* k_off, size_t total) {
-    const size_t m = c->g_idx.size();
-    if (!m) return TCPCSUM_OK;
-    hipError_t e = c->gath.ensure(total ? total : 16);
-    if (e != hipSuccess) {
-        tcpcsum::note_hip_error((int)e);
-        return TCPCSUM_ENOMEM;
-    }
-    for (size_t k = 0; k < m; ++k) k_off[c->g_idx[k]] = (uint64_t)(uintptr_t)(c->gath.d + c->g_off[k]);
-    c->stats.pkts_staged += m;
-    c->stats.bytes_staged += total;
-    return TCPCSUM_OK;
-}
-
-// Copy staged packets [g0, g1) of the list into c->gath (16 packets a piece).
-void copy_staged(tcpcsum_ctx* c, size_t g0, size_t g1) {
-    if (g1 <= g0) return;
-    const uint64_t t0 = tcpcsum::now_ns();
-    uint8_t* gh = c->gath.h;
-    c->pool->run(g1 - g0, 16, [&](size_t lo, size_t hi) {
-        for (size_t k = g0 + lo; k < g0 + hi; ++k) memcpy(gh + c->g_off[k], c->g_src[k], c->g_len[k]);
-    });
-    c->stats.ns_copy += tcpcsum::now_ns() - t0;
-}
-
-// The scatter-gather wire kernel over packets [0, n) whose addresses / bounds
-// are in c->p_off / c->p_len, in up to c->wire_blocks launches on st: the CPU
-// copies block j+1's staged packets while the kernel runs on block j.
-int launch_wire_blocks(tcpcsum_ctx* c, uint64_t n, uint32_t cap, uint64_t foot, int mode, uint16_t* kout,
-                       uint8_t* kst, hipStream_t st, const tcpcsum::Tuning& tu) {
-    const uint64_t blocks = c->g_idx.empty() || n < 256u ? 1u : (uint64_t)std::max(1, c->wire_blocks);
-    const uint64_t per = (n + blocks - 1) / blocks;
-    size_t g = 0;
-    for (uint64_t i0 = 0; i0 < n; i0 += per) {
-        const uint64_t cnt = std::min<uint64_t>(per, n - i0);
-        size_t g1 = g;
-        while (g1 < c->g_idx.size() && c->g_idx[g1] < i0 + cnt) ++g1;
-        copy_staged(c, g, g1);
-        g = g1;
-        tcpcsum::launch_ipv4(nullptr, (const uint64_t*)c->p_off.d + i0, (const uint32_t*)c->p_len.d + i0, cnt, cap,
-                             ~0ull, foot / n * cnt, mode, kout + i0, kst + i0, nullptr, st, tu);
-        const int rc = check_launch();
-        if (rc) return rc;
-    }
-    return TCPCSUM_OK;
-}
-
-// FILL on staged packets: the kernel stored each check in the staging copy;
-// put it (and the IPv4 header checksum, with IPHDR) into the caller's packet.
-void write_back_checks(tcpcsum_ctx* c, const uint8_t* status, bool iphdr) {
-    const size_t m = c->g_idx.size();
-    for (size_t k = 0; k < m; ++k) {
-        if (status[c->g_idx[k]] != TCPCSUM_PKT_OK) continue;
-        const uint8_t* sp = c->gath.h + c->g_off[k];
-        uint8_t* dp = c->g_src[k];
-        const unsigned tcp = (sp[0] & 15u) * 4u;
-        memcpy(dp + tcp + 16, sp + tcp + 16, 2);   // context.c:208: native u16 at TCP+16
-        if (iphdr) memcpy(dp + 10, sp + 10, 2);
-    }
-}
-
 // Bytes of a wire packet worth copying: its tot_len (at least the 20-byte IP
 // header), never more than `bound` readable bytes. A packet whose tot_len
 // exceeds the bound keeps tot_len > copied bytes and is SKIPPED by the
@@ -484,6 +420,66 @@ inline uint32_t copy_len(const uint8_t* ip, uint64_t bound) {
     const uint32_t tot = ((uint32_t)ip[2] << 8) | ip[3];
     const uint64_t want = tot < 20u ? 20u : tot;
     return (uint32_t)std::min<uint64_t>(want, bound);
+}
+
+// Stage the packets listed in g_* (g_len holds each one's readable bound)
+// into c->gath, all on the copy threads: (1) each packet's byte count — its
+// tot_len, within its bound (copy_len) — read from its header; (2) offsets in
+// the staging, 16-B aligned; (3) the copies. The calling thread never walks
+// the packets itself. Sets k_off / k_len of every staged packet.
+int stage_packets(tcpcsum_ctx* c, uint64_t* k_off, uint32_t* k_len, size_t* staged_bytes) {
+    const size_t m = c->g_idx.size();
+    *staged_bytes = 0;
+    if (!m) return TCPCSUM_OK;
+    const uint64_t t0 = tcpcsum::now_ns();
+    c->pool->run(m, 64, [&](size_t lo, size_t hi) {
+        for (size_t k = lo; k < hi; ++k) {
+            c->g_len[k] = copy_len(c->g_src[k], c->g_len[k]);
+            k_len[c->g_idx[k]] = c->g_len[k];
+        }
+    });
+    size_t total = 0;
+    for (size_t k = 0; k < m; ++k) {
+        c->g_off[k] = total;
+        total += ((size_t)c->g_len[k] + 15u) & ~(size_t)15u;
+    }
+    hipError_t e = c->gath.ensure(total ? total : 16);
+    if (e != hipSuccess) {
+        tcpcsum::note_hip_error((int)e);
+        return TCPCSUM_ENOMEM;
+    }
+    uint8_t* gh = c->gath.h;
+    uint8_t* gd = c->gath.d;
+    c->pool->run(m, 16, [&](size_t lo, size_t hi) {
+        for (size_t k = lo; k < hi; ++k) {
+            memcpy(gh + c->g_off[k], c->g_src[k], c->g_len[k]);
+            k_off[c->g_idx[k]] = (uint64_t)(uintptr_t)(gd + c->g_off[k]);
+        }
+    });
+    c->stats.ns_copy += tcpcsum::now_ns() - t0;
+    c->stats.pkts_staged += m;
+    c->stats.bytes_staged += total;
+    *staged_bytes = total;
+    return TCPCSUM_OK;
+}
+
+// FILL on staged packets: the kernel stored each check in the staging copy;
+// put it (and the IPv4 header checksum, with IPHDR) into the caller's packet,
+// on the copy threads.
+void write_back_checks(tcpcsum_ctx* c, const uint8_t* status, bool iphdr) {
+    const size_t m = c->g_idx.size();
+    const uint64_t t0 = tcpcsum::now_ns();
+    c->pool->run(m, 64, [&](size_t lo, size_t hi) {
+        for (size_t k = lo; k < hi; ++k) {
+            if (status[c->g_idx[k]] != TCPCSUM_PKT_OK) continue;
+            const uint8_t* sp = c->gath.h + c->g_off[k];
+            uint8_t* dp = c->g_src[k];
+            const unsigned tcp = (sp[0] & 15u) * 4u;
+            memcpy(dp + tcp + 16, sp + tcp + 16, 2);   // context.c:208: native u16 at TCP+16
+            if (iphdr) memcpy(dp + 10, sp + 10, 2);
+        }
+    });
+    c->stats.ns_copy += tcpcsum::now_ns() - t0;
 }
 
 }  // namespace
@@ -514,7 +510,6 @@ int tcpcsum_ctx_create(int device, size_t scratch_bytes, tcpcsum_ctx_t** out) {
     c->stats.copy_threads = (uint64_t)c->pool->threads();
     c->nt_copy = tcpcsum::env_int("TCPCSUM_HOST_NT", 1) != 0;
     c->uniform_dma = tcpcsum::env_int("TCPCSUM_HOST_DMA", 1) != 0;
-    c->wire_blocks = std::max(1, std::min(64, tcpcsum::env_int("TCPCSUM_HOST_WIRE_BLOCKS", 1)));
     for (int i = 0; i < 2; ++i) {
         e = hipStreamCreateWithFlags(&c->st[i], hipStreamNonBlocking);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->slot_ev[i], hipEventDisableTiming);
@@ -740,27 +735,22 @@ int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t* c, void* h_pkts, size_t region_bytes,
         uint64_t* k_off = (uint64_t*)c->p_off.h;
         uint32_t* k_len = (uint32_t*)c->p_len.h;
         uint8_t* base = (uint8_t*)h_pkts;
-        size_t total = 0;
-        uint32_t maxl = 20;
         c->g_off.resize(n);
         c->g_src.resize(n);
         c->g_len.resize(n);
         c->g_idx.resize(n);
-        for (uint64_t i = 0; i < n; ++i) {
-            uint8_t* ip = base + h_pkt_off[i];
-            const uint32_t cl = copy_len(ip, std::min<uint64_t>(cap, region_bytes - h_pkt_off[i]));
+        for (uint64_t i = 0; i < n; ++i) {   // bounds only: the copy threads read the headers
             c->g_idx[i] = i;
-            c->g_src[i] = ip;
-            c->g_len[i] = cl;
-            c->g_off[i] = total;
-            total += ((size_t)cl + 15u) & ~(size_t)15u;
-            k_len[i] = cl;
-            maxl = std::max(maxl, cl);
+            c->g_src[i] = base + h_pkt_off[i];
+            c->g_len[i] = (uint32_t)std::min<uint64_t>(cap, region_bytes - h_pkt_off[i]);
         }
-        rc = stage_packets(c, k_off, total);
+        size_t total = 0;
+        rc = stage_packets(c, k_off, k_len, &total);
         if (rc) return rc;
-        rc = launch_wire_blocks(c, n, maxl, total, mode, kout, kst, st, tu);
-        if (rc) return rc;
+        uint32_t maxl = 20;
+        for (uint64_t i = 0; i < n; ++i) maxl = std::max(maxl, c->g_len[i]);
+        tcpcsum::launch_ipv4(nullptr, (const uint64_t*)c->p_off.d, (const uint32_t*)c->p_len.d, n, maxl, ~0ull, total,
+                             mode, kout, kst, nullptr, st, tu);
     }
     rc = check_launch();
     if (rc) return rc;
@@ -800,7 +790,6 @@ int tcpcsum_ipv4_batch_ptrs_host(tcpcsum_ctx_t* c, void* const* h_pkts, const ui
     c->g_src.clear();
     c->g_len.clear();
     uint64_t foot = 0;
-    size_t total = 0;
     uint32_t cap = 20;
     uint64_t in_place = 0;
     for (uint64_t i = 0; i < n; ++i) {
@@ -814,31 +803,33 @@ int tcpcsum_ipv4_batch_ptrs_host(tcpcsum_ctx_t* c, void* const* h_pkts, const ui
         uintptr_t dev = 0;
         if (c->reg.resolve((uintptr_t)p, len, may_lock, kAutoRegisterBudget, &dev) == 0) {
             k_off[i] = dev;
+            k_len[i] = len;
+            foot += len;
+            cap = len > cap ? len : cap;
             ++in_place;
-        } else {
-            len = copy_len(p, len);
+        } else {   // staged: its bound now; its header, size and copy on the copy threads
             c->g_idx.push_back(i);
             c->g_src.push_back(p);
             c->g_len.push_back(len);
-            c->g_off.push_back(total);
-            total += ((size_t)len + 15u) & ~(size_t)15u;
+            c->g_off.push_back(0);
         }
-        k_len[i] = len;
-        foot += len;
-        cap = len > cap ? len : cap;
     }
     if (c->reg.last_lock_error()) tcpcsum::note_hip_error(c->reg.last_lock_error());
     c->stats.pkts_in_place += in_place;
-    rc = stage_packets(c, k_off, total);
+    size_t staged = 0;
+    rc = stage_packets(c, k_off, k_len, &staged);
     if (rc) return rc;
+    foot += staged;
+    for (size_t k = 0; k < c->g_idx.size(); ++k) cap = std::max(cap, c->g_len[k]);
     uint16_t* zout = h_out ? (uint16_t*)pinned_dev_ptr(h_out, n * sizeof(uint16_t)) : nullptr;
     uint8_t* zst = h_status ? (uint8_t*)pinned_dev_ptr(h_status, n) : nullptr;
     // zero-copy over PCIe: the 16-lane group shape for latency-bound batches
     // (as tcpcsum_ipv4_batch_host on a pinned pool)
     tcpcsum::Tuning tu = c->tune;
     if (tu.shape < 0 && n < 65536u) tu.shape = 3;
-    rc = launch_wire_blocks(c, n, cap, foot, mode, zout ? zout : (uint16_t*)c->p_out.d, zst ? zst : c->p_stat.d, st,
-                            tu);
+    tcpcsum::launch_ipv4(nullptr, (const uint64_t*)c->p_off.d, (const uint32_t*)c->p_len.d, n, cap, ~0ull, foot, mode,
+                         zout ? zout : (uint16_t*)c->p_out.d, zst ? zst : c->p_stat.d, nullptr, st, tu);
+    rc = check_launch();
     if (rc) return rc;
     hipError_t e = wait_stream(c, st);
     if (e != hipSuccess) return hip_fail(e);
