@@ -11,6 +11,8 @@
 //   s128_sc01 the whole 128-B line, sc0 sc1
 //   s64_sc01  the 64-B half line holding the check, sc0 sc1
 //   s32_sc01  the 32-B sector holding the check, sc0 sc1
+//   s128      the whole 128-B line, default policy (write-back in L2)
+//   s128_nt   the whole 128-B line, nt (streaming)
 //   dense     the 2 bytes to a dense per-packet array instead (VERIFY's d_out)
 // Vector stores only. Prints one JSON line per variant: median / min ms of
 // 7 x 20 launches, after 3 warm-up launches.
@@ -38,7 +40,8 @@ using gptr = __attribute__((address_space(1))) T*;
 
 __device__ __forceinline__ uint32_t sad16(uint32_t d, uint32_t acc) { return __builtin_amdgcn_sad_u16(d, 0u, acc); }
 
-// V: 0 none, 1 s2, 2 s2 sc1, 3 s2 sc0 sc1, 4 s2 nt, 5 s128 sc0 sc1, 6 dense, 7 s64 sc0 sc1, 8 s32 sc0 sc1
+// V: 0 none, 1 s2, 2 s2 sc1, 3 s2 sc0 sc1, 4 s2 nt, 5 s128 sc0 sc1, 6 dense, 7 s64 sc0 sc1, 8 s32 sc0 sc1,
+//    9 s128 default, 10 s128 nt
 template <int V>
 __global__ __launch_bounds__(256) void k_fill(uint8_t* __restrict__ reg, uint64_t nchunks, uint32_t slot_chunks,
                                               uint16_t* dense, uint64_t* out) {
@@ -73,6 +76,10 @@ __global__ __launch_bounds__(256) void k_fill(uint8_t* __restrict__ reg, uint64_
                 constexpr uint32_t lo = V == 5 ? 0u : V == 7 ? 0u : 2u, hi = V == 5 ? 8u : V == 7 ? 4u : 4u;
                 if (j >= lo && j < hi)
                     asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 3" ::"v"(p), "v"(v[k]) : "memory");
+            } else if constexpr (V == 9) {
+                if (j < 8u) asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 3" ::"v"(p), "v"(v[k]) : "memory");
+            } else if constexpr (V == 10) {
+                if (j < 8u) asm volatile("global_store_dwordx4 %0, %1, off nt\n\ts_nop 3" ::"v"(p), "v"(v[k]) : "memory");
             } else if constexpr (V == 6) {
                 if (j == 2) dense[c / slot_chunks] = (uint16_t)word;
             }
@@ -139,6 +146,8 @@ int main() {
         rc |= run<6>("dense", reg, nchunks, sc, dense, out, 4096);
         rc |= run<7>("s64_sc01", reg, nchunks, sc, dense, out, 4096);
         rc |= run<8>("s32_sc01", reg, nchunks, sc, dense, out, 4096);
+        rc |= run<9>("s128", reg, nchunks, sc, dense, out, 4096);
+        rc |= run<10>("s128_nt", reg, nchunks, sc, dense, out, 4096);
         if (rc) return 1;
     }
     std::vector<uint8_t> back(bytes);
