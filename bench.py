@@ -281,6 +281,10 @@ def run_config(config: str, steps: int, warmup: int, rank: int, world: int, dist
     def rec(evs):
         for e, st in zip(evs, sts):
             e.record(st)
+    # torch creates a HIP event on its first record: do that here, not inside the timed region
+    rec(ev0)
+    rec(ev1)
+    torch.cuda.synchronize()
     wall = timed_region(step, steps, warmup, dist, torch.cuda.synchronize,
                         on_start=lambda: rec(ev0), on_end=lambda: rec(ev1))
     kernel_ms = max(ev0[0].elapsed_time(e) for e in ev1) / steps
