@@ -113,7 +113,7 @@ def main():
             b[:p.size] = p
         bufs.append(b)
     outb = bufs[1::2]
-    ptrs = [b.ctypes.data for b in outb]
+    ptrs = np.array([b.ctypes.data for b in outb], np.uint64)   # an array: no per-call list conversion
     lens = np.full(1024, 1500, np.uint32)
     ctx.close()
     for mode in ("staged", "auto_register"):
