@@ -112,7 +112,7 @@ inline uint64_t now_ns() {
 // done and go back to sleep (nobody waits for a sleeper to wake).
 class CopyPool {
 public:
-    explicit CopyPool(int workers) : nw_(workers < 0 ? 0 : workers) {}
+    CopyPool(int workers, uint64_t spin_ns) : nw_(workers < 0 ? 0 : workers), spin_ns_(spin_ns) {}
     CopyPool(const CopyPool&) = delete;
     CopyPool& operator=(const CopyPool&) = delete;
     ~CopyPool() {
@@ -171,15 +171,16 @@ private:
         } catch (...) {   // fewer threads than asked: the caller still does all the work it must
         }
     }
-    // A worker spins briefly after each job before it sleeps: a wire batch
-    // hands the pool one job per launch block, microseconds apart, and a
-    // condition-variable wake-up costs about as long as a block's copy.
+    // A worker spins briefly after each job before it sleeps: a staged wire
+    // batch hands the pool three jobs (header reads, copies; after the kernel,
+    // the FILL write-back), microseconds apart, and a condition-variable
+    // wake-up costs about as long as one of them.
     void loop() {
         uint64_t seen = 0;
         for (;;) {
             const uint64_t t0 = now_ns();
             while (gen_.load(std::memory_order_acquire) == seen && !quit_.load(std::memory_order_relaxed) &&
-                   now_ns() - t0 < kSpinNs)
+                   now_ns() - t0 < spin_ns_)
                 _mm_pause();
             std::shared_ptr<Job> job;
             {
@@ -192,8 +193,8 @@ private:
             if (job) job->drain();
         }
     }
-    static constexpr uint64_t kSpinNs = 50000;
     int nw_;
+    uint64_t spin_ns_;
     bool started_ = false;
     std::vector<std::thread> th_;
     std::mutex m_;
@@ -336,6 +337,7 @@ struct tcpcsum_ctx {
     tcpcsum::HostRegistry<tcpcsum::HipHostBackend> reg{backend};
     std::unique_ptr<tcpcsum::CopyPool> pool;
     bool nt_copy = true;   // streaming stores for the uniform chunks (TCPCSUM_HOST_NT=0: plain memcpy)
+    bool stage_one_pass = true;   // wire staging laid out by bounds, one pass (TCPCSUM_HOST_STAGE_PASSES=2: by lengths)
     bool uniform_dma = true;   // staged uniform chunks go to HBM by DMA (TCPCSUM_HOST_DMA=0: kernel reads them over PCIe)
     tcpcsum_ctx_stats_t stats{};
     std::mutex mu;
@@ -423,44 +425,79 @@ inline uint32_t copy_len(const uint8_t* ip, uint64_t bound) {
 }
 
 // Stage the packets listed in g_* (g_len holds each one's readable bound)
-// into c->gath, all on the copy threads: (1) each packet's byte count — its
-// tot_len, within its bound (copy_len) — read from its header; (2) offsets in
-// the staging, 16-B aligned; (3) the copies. The calling thread never walks
-// the packets itself. Sets k_off / k_len of every staged packet.
+// into c->gath, all on the copy threads; the calling thread never reads a
+// packet. Each copy thread reads a packet's tot_len (copy_len: the bytes worth
+// copying, within its bound) and copies it. Where the bounds add up to at most
+// kStageByBound, a packet's place in the staging is laid out by its bound and
+// that is one pass; past it (huge bounds: 64 KiB caps over big batches) the
+// lengths are read first and the copies packed by them, two passes. Sets
+// k_off / k_len of every staged packet.
+constexpr size_t kStageByBound = 64u << 20;
 int stage_packets(tcpcsum_ctx* c, uint64_t* k_off, uint32_t* k_len, size_t* staged_bytes) {
     const size_t m = c->g_idx.size();
     *staged_bytes = 0;
     if (!m) return TCPCSUM_OK;
     const uint64_t t0 = tcpcsum::now_ns();
-    c->pool->run(m, 64, [&](size_t lo, size_t hi) {
-        for (size_t k = lo; k < hi; ++k) {
-            c->g_len[k] = copy_len(c->g_src[k], c->g_len[k]);
-            k_len[c->g_idx[k]] = c->g_len[k];
-        }
-    });
-    size_t total = 0;
+    size_t span = 0;
     for (size_t k = 0; k < m; ++k) {
-        c->g_off[k] = total;
-        total += ((size_t)c->g_len[k] + 15u) & ~(size_t)15u;
+        c->g_off[k] = span;
+        span += ((size_t)c->g_len[k] + 15u) & ~(size_t)15u;
     }
-    hipError_t e = c->gath.ensure(total ? total : 16);
+    const bool by_bound = span <= kStageByBound && c->stage_one_pass;
+    if (!by_bound) {
+        c->pool->run(m, 64, [&](size_t lo, size_t hi) {
+            for (size_t k = lo; k < hi; ++k) c->g_len[k] = copy_len(c->g_src[k], c->g_len[k]);
+        });
+        span = 0;
+        for (size_t k = 0; k < m; ++k) {
+            c->g_off[k] = span;
+            span += ((size_t)c->g_len[k] + 15u) & ~(size_t)15u;
+        }
+    }
+    hipError_t e = c->gath.ensure(span ? span : 16);
     if (e != hipSuccess) {
         tcpcsum::note_hip_error((int)e);
         return TCPCSUM_ENOMEM;
     }
     uint8_t* gh = c->gath.h;
     uint8_t* gd = c->gath.d;
+    std::atomic<size_t> copied{0};
     c->pool->run(m, 16, [&](size_t lo, size_t hi) {
+        size_t b = 0;
         for (size_t k = lo; k < hi; ++k) {
+            if (by_bound) c->g_len[k] = copy_len(c->g_src[k], c->g_len[k]);
             memcpy(gh + c->g_off[k], c->g_src[k], c->g_len[k]);
             k_off[c->g_idx[k]] = (uint64_t)(uintptr_t)(gd + c->g_off[k]);
+            k_len[c->g_idx[k]] = c->g_len[k];
+            b += c->g_len[k];
         }
+        copied.fetch_add(b, std::memory_order_relaxed);
     });
     c->stats.ns_copy += tcpcsum::now_ns() - t0;
     c->stats.pkts_staged += m;
-    c->stats.bytes_staged += total;
-    *staged_bytes = total;
+    c->stats.bytes_staged += copied.load();
+    *staged_bytes = copied.load();
     return TCPCSUM_OK;
+}
+
+// Stage the packets in g_* and launch the wire kernel over all n packets on
+// st (k_off / k_len of the packets read in place already set; in_cap /
+// in_foot their largest length and sum). One launch after the copies: queueing
+// the kernel first, in blocks each released by a pinned flag the copy threads
+// set (hipStreamWaitValue64), was measured and lost — 1 / 2 / 4 / 8 blocks
+// against copy-then-launch on 1024 x 1500-B batches: no gain / no gain /
+// +15-30 us / +60-90 us, the host cost of each queued launch landing before
+// the copies (profiles/r03_hostpath_sweep_wire_split.jsonl).
+int stage_and_launch(tcpcsum_ctx* c, uint64_t n, uint32_t in_cap, uint64_t in_foot, int mode, uint16_t* kout,
+                     uint8_t* kst, hipStream_t st, const tcpcsum::Tuning& tu) {
+    size_t staged = 0;
+    int rc = stage_packets(c, (uint64_t*)c->p_off.h, (uint32_t*)c->p_len.h, &staged);
+    if (rc) return rc;
+    uint32_t cap = in_cap;
+    for (size_t k = 0; k < c->g_idx.size(); ++k) cap = std::max(cap, c->g_len[k]);
+    tcpcsum::launch_ipv4(nullptr, (const uint64_t*)c->p_off.d, (const uint32_t*)c->p_len.d, n, cap, ~0ull,
+                         in_foot + staged, mode, kout, kst, nullptr, st, tu);
+    return check_launch();
 }
 
 // FILL on staged packets: the kernel stored each check in the staging copy;
@@ -502,13 +539,16 @@ int tcpcsum_ctx_create(int device, size_t scratch_bytes, tcpcsum_ctx_t** out) {
     if (!c) return TCPCSUM_ENOMEM;
     c->device = device;
     c->chunk = scratch_bytes ? scratch_bytes : kDefaultChunk;
-    c->pool.reset(new (std::nothrow) tcpcsum::CopyPool(tcpcsum::default_copy_threads() - 1));
+    // copy threads spin TCPCSUM_HOST_SPIN_US (default 50) after a job before they sleep
+    const uint64_t spin_ns = (uint64_t)std::max(0, tcpcsum::env_int("TCPCSUM_HOST_SPIN_US", 50)) * 1000u;
+    c->pool.reset(new (std::nothrow) tcpcsum::CopyPool(tcpcsum::default_copy_threads() - 1, spin_ns));
     if (!c->pool) {
         delete c;
         return TCPCSUM_ENOMEM;
     }
     c->stats.copy_threads = (uint64_t)c->pool->threads();
     c->nt_copy = tcpcsum::env_int("TCPCSUM_HOST_NT", 1) != 0;
+    c->stage_one_pass = tcpcsum::env_int("TCPCSUM_HOST_STAGE_PASSES", 1) == 1;
     c->uniform_dma = tcpcsum::env_int("TCPCSUM_HOST_DMA", 1) != 0;
     for (int i = 0; i < 2; ++i) {
         e = hipStreamCreateWithFlags(&c->st[i], hipStreamNonBlocking);
@@ -732,8 +772,6 @@ int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t* c, void* h_pkts, size_t region_bytes,
     } else {
         // the region's packets, copied into staging and addressed one by one
         // (the scatter-gather kernel, bounded per packet by the bytes copied)
-        uint64_t* k_off = (uint64_t*)c->p_off.h;
-        uint32_t* k_len = (uint32_t*)c->p_len.h;
         uint8_t* base = (uint8_t*)h_pkts;
         c->g_off.resize(n);
         c->g_src.resize(n);
@@ -744,13 +782,8 @@ int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t* c, void* h_pkts, size_t region_bytes,
             c->g_src[i] = base + h_pkt_off[i];
             c->g_len[i] = (uint32_t)std::min<uint64_t>(cap, region_bytes - h_pkt_off[i]);
         }
-        size_t total = 0;
-        rc = stage_packets(c, k_off, k_len, &total);
+        rc = stage_and_launch(c, n, 20u, 0u, mode, kout, kst, st, tu);
         if (rc) return rc;
-        uint32_t maxl = 20;
-        for (uint64_t i = 0; i < n; ++i) maxl = std::max(maxl, c->g_len[i]);
-        tcpcsum::launch_ipv4(nullptr, (const uint64_t*)c->p_off.d, (const uint32_t*)c->p_len.d, n, maxl, ~0ull, total,
-                             mode, kout, kst, nullptr, st, tu);
     }
     rc = check_launch();
     if (rc) return rc;
@@ -816,20 +849,13 @@ int tcpcsum_ipv4_batch_ptrs_host(tcpcsum_ctx_t* c, void* const* h_pkts, const ui
     }
     if (c->reg.last_lock_error()) tcpcsum::note_hip_error(c->reg.last_lock_error());
     c->stats.pkts_in_place += in_place;
-    size_t staged = 0;
-    rc = stage_packets(c, k_off, k_len, &staged);
-    if (rc) return rc;
-    foot += staged;
-    for (size_t k = 0; k < c->g_idx.size(); ++k) cap = std::max(cap, c->g_len[k]);
     uint16_t* zout = h_out ? (uint16_t*)pinned_dev_ptr(h_out, n * sizeof(uint16_t)) : nullptr;
     uint8_t* zst = h_status ? (uint8_t*)pinned_dev_ptr(h_status, n) : nullptr;
     // zero-copy over PCIe: the 16-lane group shape for latency-bound batches
     // (as tcpcsum_ipv4_batch_host on a pinned pool)
     tcpcsum::Tuning tu = c->tune;
     if (tu.shape < 0 && n < 65536u) tu.shape = 3;
-    tcpcsum::launch_ipv4(nullptr, (const uint64_t*)c->p_off.d, (const uint32_t*)c->p_len.d, n, cap, ~0ull, foot, mode,
-                         zout ? zout : (uint16_t*)c->p_out.d, zst ? zst : c->p_stat.d, nullptr, st, tu);
-    rc = check_launch();
+    rc = stage_and_launch(c, n, cap, foot, mode, zout ? zout : (uint16_t*)c->p_out.d, zst ? zst : c->p_stat.d, st, tu);
     if (rc) return rc;
     hipError_t e = wait_stream(c, st);
     if (e != hipSuccess) return hip_fail(e);

@@ -4,7 +4,9 @@ context's copy knobs, read at tcpcsum_ctx_create:
   TCPCSUM_HOST_THREADS       copy threads (incl. the caller's)
   TCPCSUM_HOST_NT            streaming stores for the uniform chunks
   TCPCSUM_HOST_DMA           uniform chunks: DMA to HBM then the kernel (0: kernel reads staging over PCIe)
---configs: threads:nt:dma,...
+  TCPCSUM_HOST_SPIN_US       how long an idle copy thread spins before it sleeps
+  TCPCSUM_HOST_STAGE_PASSES  wire staging: 1 = laid out by bounds, one pass; 2 = lengths first, packed
+--configs: threads:nt:dma[:spin_us[:passes]],...
 Wire packets are staged on the copy threads (header reads, copies and the FILL
 write-back) and checksummed by one launch.
 Measures tcpcsum_batch_uniform_host over 1M x 1500 B pageable, and one
@@ -38,7 +40,7 @@ def timed(fn, reps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=2)
-    ap.add_argument("--configs", default="8:1:1,8:1:0,12:1:1,8:0:1,4:1:1,2:1:1")
+    ap.add_argument("--configs", default="8:1:1:50:1,8:1:1:50:2,4:1:1:50:1,2:1:1:50:1,1:1:1:50:1")
     args = ap.parse_args()
     import numpy as np
     import tcp_amd
@@ -62,12 +64,30 @@ def main():
         bufs.append(b)
     ptrs = np.array([b.ctypes.data for b in bufs[1::2]], np.uint64)   # arrays, not lists: no per-call conversion
     lens = np.full(1024, 1500, np.uint32)
-    configs = [tuple(int(x) for x in c.split(":")) for c in args.configs.split(",")]
+    defaults = [8, 1, 1, 50, 1]
+    configs = []
+    for c in args.configs.split(","):
+        v = [int(x) for x in c.split(":")]
+        configs.append(tuple(v + defaults[len(v):]))
+    # one core's memcpy of the batch's 1.5 MB into pageable vs page-locked memory (is the
+    # staging itself slow to write?)
+    import ctypes
+    src = np.frombuffer(rng.bytes(1536000), np.uint8).copy()
+    dst_pg = np.empty(1536000, np.uint8)
+    dst_pin = tcp_amd.pinned_empty(1536000)
+    for name, dst in (("pageable", dst_pg), ("pinned", dst_pin)):
+        dst[:] = 0
+        tmin, tmed = timed(lambda: ctypes.memmove(dst.ctypes.data, src.ctypes.data, src.size), 200)
+        print(json.dumps({"measure": "memcpy_1p5MB_one_core", "dst": name, "us_median": round(tmed * 1e6, 1),
+                          "us_best": round(tmin * 1e6, 1), "GB/s_median": round(src.size / tmed / 1e9, 2)}),
+              flush=True)
     for rnd in range(args.rounds):
-        for th, nt, dma in configs:
+        for th, nt, dma, spin, passes in configs:
             os.environ["TCPCSUM_HOST_THREADS"] = str(th)
             os.environ["TCPCSUM_HOST_NT"] = str(nt)
             os.environ["TCPCSUM_HOST_DMA"] = str(dma)
+            os.environ["TCPCSUM_HOST_SPIN_US"] = str(spin)
+            os.environ["TCPCSUM_HOST_STAGE_PASSES"] = str(passes)
             with tcp_amd.HostContext(0) as ctx:
                 got = ctx.batch_uniform(big, L, L, n, ss)
                 if want is None:
@@ -76,7 +96,7 @@ def main():
                 s0 = ctx.stats()
                 tmin, tmed = timed(lambda: ctx.batch_uniform(big, L, L, n, ss), 5)
                 s1 = ctx.stats()
-                cfg = {"threads": th, "nt": nt, "dma": dma, "round": rnd}
+                cfg = {"threads": th, "nt": nt, "dma": dma, "spin_us": spin, "passes": passes, "round": rnd}
                 print(json.dumps({**cfg, "measure": "uniform_host_1Mx1500_pageable",
                                   "GiB/s_median": round(n * L / tmed / 2**30, 2),
                                   "GiB/s_best": round(n * L / tmin / 2**30, 2),
