@@ -17,7 +17,7 @@ CFLAGS_LIB ?= -O2 -fPIC -Wall -Wextra
 
 LIB := tcp_amd/libtcpcsum.so
 HIP_SRCS := tcp_amd/csrc/tcpcsum_kernels.hip tcp_amd/csrc/tcpcsum_api.hip tcp_amd/csrc/tcpcsum_host.hip
-HDRS := include/tcpcsum.h tcp_amd/csrc/tcpcsum_internal.h tcp_amd/csrc/host_registry.h
+HDRS := include/tcpcsum.h tcp_amd/csrc/tcpcsum_internal.h tcp_amd/csrc/host_registry.h tcp_amd/csrc/copy_pool.h
 OBJDIR := build/obj
 
 PRELOAD := tcp_amd/libtcpcsum_preload.so

@@ -54,6 +54,7 @@
 #include <thread>
 #include <vector>
 
+#include "copy_pool.h"
 #include "host_registry.h"
 #include "tcpcsum.h"
 #include "tcpcsum_internal.h"
@@ -99,159 +100,6 @@ struct HipHostBackend {
         return true;
     }
 };
-
-inline uint64_t now_ns() {
-    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
-               std::chrono::steady_clock::now().time_since_epoch()).count();
-}
-
-// A few host threads for the copies into pinned staging: one core's memcpy
-// (≈10-20 GB/s) is below the PCIe rate the kernel reads staging at
-// (≈50 GiB/s), and the copy of chunk k+1 must keep pace with the kernel on
-// chunk k. The calling thread works too; workers that wake late find the job
-// done and go back to sleep (nobody waits for a sleeper to wake).
-class CopyPool {
-public:
-    CopyPool(int workers, uint64_t spin_ns) : nw_(workers < 0 ? 0 : workers), spin_ns_(spin_ns) {}
-    CopyPool(const CopyPool&) = delete;
-    CopyPool& operator=(const CopyPool&) = delete;
-    ~CopyPool() {
-        {
-            std::lock_guard<std::mutex> lk(m_);
-            quit_ = true;
-        }
-        cv_.notify_all();
-        for (auto& t : th_) t.join();
-    }
-    int threads() const { return nw_ + 1; }
-
-    // body(lo, hi) over [0, n) in pieces of `grain`; returns when every piece is done.
-    void run(size_t n, size_t grain, const std::function<void(size_t, size_t)>& body) {
-        if (n == 0) return;
-        if (grain == 0) grain = 1;
-        if (nw_ == 0 || n <= grain) {
-            body(0, n);
-            return;
-        }
-        start();
-        auto job = std::make_shared<Job>(&body, n, grain);
-        {
-            std::lock_guard<std::mutex> lk(m_);
-            cur_ = job;
-            ++gen_;
-        }
-        cv_.notify_all();
-        job->drain();
-        while (job->done.load(std::memory_order_acquire) < n) std::this_thread::yield();
-        std::lock_guard<std::mutex> lk(m_);
-        if (cur_ == job) cur_.reset();
-    }
-
-private:
-    struct Job {
-        Job(const std::function<void(size_t, size_t)>* b, size_t n_, size_t g) : body(b), n(n_), grain(g) {}
-        const std::function<void(size_t, size_t)>* body;   // valid while done < n
-        size_t n, grain;
-        std::atomic<size_t> next{0}, done{0};
-        void drain() {
-            for (;;) {
-                const size_t i = next.fetch_add(grain, std::memory_order_relaxed);
-                if (i >= n) return;
-                const size_t e = std::min(n, i + grain);
-                (*body)(i, e);
-                done.fetch_add(e - i, std::memory_order_release);
-            }
-        }
-    };
-    void start() {
-        if (started_) return;
-        started_ = true;
-        try {
-            for (int i = 0; i < nw_; ++i) th_.emplace_back([this] { loop(); });
-        } catch (...) {   // fewer threads than asked: the caller still does all the work it must
-        }
-    }
-    // A worker spins briefly after each job before it sleeps: a staged wire
-    // batch hands the pool three jobs (header reads, copies; after the kernel,
-    // the FILL write-back), microseconds apart, and a condition-variable
-    // wake-up costs about as long as one of them.
-    void loop() {
-        uint64_t seen = 0;
-        for (;;) {
-            const uint64_t t0 = now_ns();
-            while (gen_.load(std::memory_order_acquire) == seen && !quit_.load(std::memory_order_relaxed) &&
-                   now_ns() - t0 < spin_ns_)
-                _mm_pause();
-            std::shared_ptr<Job> job;
-            {
-                std::unique_lock<std::mutex> lk(m_);
-                cv_.wait(lk, [&] { return quit_.load() || gen_.load() != seen; });
-                if (quit_) return;
-                seen = gen_.load();
-                job = cur_;
-            }
-            if (job) job->drain();
-        }
-    }
-    int nw_;
-    uint64_t spin_ns_;
-    bool started_ = false;
-    std::vector<std::thread> th_;
-    std::mutex m_;
-    std::condition_variable cv_;
-    std::shared_ptr<Job> cur_;
-    std::atomic<uint64_t> gen_{0};
-    std::atomic<bool> quit_{false};
-};
-
-// Host threads for staging copies: TCPCSUM_HOST_THREADS, else half the CPUs
-// this process may use (the affinity mask, capped by a cgroup CPU quota), 1..8.
-int default_copy_threads() {
-    if (const char* e = getenv("TCPCSUM_HOST_THREADS")) {
-        const int v = atoi(e);
-        if (v >= 1) return std::min(v, 64);
-    }
-    int cpus = 1;
-    cpu_set_t set;
-    if (sched_getaffinity(0, sizeof set, &set) == 0) cpus = std::max(1, CPU_COUNT(&set));
-    if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
-        char q[32] = {0};
-        long long per = 0;
-        if (fscanf(f, "%31s %lld", q, &per) == 2 && strcmp(q, "max") != 0 && per > 0) {
-            const long long quota = atoll(q);
-            if (quota > 0) cpus = std::min<long long>(cpus, std::max<long long>(1, (quota + per - 1) / per));
-        }
-        fclose(f);
-    }
-    return std::max(1, std::min(8, cpus / 2));
-}
-
-// memcpy into staging with non-temporal (streaming) stores: the kernel reads
-// the staging over PCIe, not the CPU, so the copy should not first read the
-// destination lines into the cache (read-for-ownership) nor evict the source
-// stream's own working set. Ends with sfence: streaming stores are weakly
-// ordered, and the piece must be globally visible before the launch.
-inline void copy_nt(uint8_t* d, const uint8_t* s, size_t n) {
-    size_t h = (16u - ((uintptr_t)d & 15u)) & 15u;
-    if (h > n) h = n;
-    memcpy(d, s, h);
-    d += h;
-    s += h;
-    n -= h;
-    const size_t k = n & ~(size_t)63;
-    for (size_t i = 0; i < k; i += 64) {
-        const __m128i a = _mm_loadu_si128((const __m128i*)(s + i));
-        const __m128i b = _mm_loadu_si128((const __m128i*)(s + i + 16));
-        const __m128i c = _mm_loadu_si128((const __m128i*)(s + i + 32));
-        const __m128i e = _mm_loadu_si128((const __m128i*)(s + i + 48));
-        _mm_stream_si128((__m128i*)(d + i), a);
-        _mm_stream_si128((__m128i*)(d + i + 16), b);
-        _mm_stream_si128((__m128i*)(d + i + 32), c);
-        _mm_stream_si128((__m128i*)(d + i + 48), e);
-    }
-    memcpy(d + k, s + k, n - k);
-    _mm_sfence();
-}
 
 inline int env_int(const char* name, int dflt) {
     const char* e = getenv(name);

@@ -52,3 +52,20 @@ def test_host_registry_under_asan_ubsan(tmp_path):
     r = subprocess.run([str(exe), "11"], capture_output=True, text=True, env=env, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.strip().endswith("OK")
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="g++ not available")
+def test_copy_pool_under_tsan(tmp_path):
+    """The host copy threads every staged host batch runs on (tcp_amd/csrc/copy_pool.h) under
+    ThreadSanitizer: each piece of each job exactly once, run() returning only after all of them,
+    sleeping and woken workers, the streaming-store copy at every alignment, teardown."""
+    exe = tmp_path / "copy_pool_test"
+    cmd = ["g++", "-std=c++17", "-O1", "-g", "-fsanitize=thread", "-Wall", "-Wextra",
+           os.path.join(REPO, "tests", "c", "copy_pool_test.cpp"), "-o", str(exe), "-lpthread"]
+    b = subprocess.run(cmd, capture_output=True, text=True)
+    assert b.returncode == 0, b.stderr
+    env = dict(os.environ)
+    env["TSAN_OPTIONS"] = "halt_on_error=1:exitcode=66"
+    r = subprocess.run([str(exe)], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0 and "ThreadSanitizer" not in r.stderr, r.stdout + r.stderr
+    assert "copy_pool_test: OK" in r.stdout
