@@ -256,7 +256,13 @@ int recvmmsg(int fd, struct mmsghdr *vec, unsigned int vlen, int flags, struct t
         unsigned int done = 0, kept = 0;
         while (done < (unsigned int) r) {
             unsigned int cnt = (unsigned int) r - done < 1024 ? (unsigned int) r - done : 1024;
-            for (unsigned int i = 0; i < cnt; ++i) lens[i] = vec[done + i].msg_len;
+            /* the bytes received, never past the buffer: with MSG_TRUNC in flags a
+             * raw or UDP socket reports the datagram's real length in msg_len */
+            for (unsigned int i = 0; i < cnt; ++i) {
+                const struct msghdr *h = &vec[done + i].msg_hdr;
+                const unsigned int cap = h->msg_iovlen == 1 ? (unsigned int) h->msg_iov[0].iov_len : 0;
+                lens[i] = vec[done + i].msg_len < cap ? vec[done + i].msg_len : cap;
+            }
             if (gpu_batch(vec + done, cnt, lens, 0, 0, keep)) return -1;
             if (g_rx == MODE_DROP) {
                 /* stable partition by swaps: passing messages move to the front in
