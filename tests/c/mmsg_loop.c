@@ -3,7 +3,7 @@
  * does (loop.c:27-94 releaseSend, loop.c:22-25 fetchPackageBatch), over UDP
  * loopback so no root is needed. Run under LD_PRELOAD=libtcpcsum_preload.so.
  *
- *   mmsg_loop <npkts> <out-file> [cpu-checks | corrupt]
+ *   mmsg_loop <npkts> <out-file> [cpu-checks | corrupt | trunc]
  *
  * Builds npkts IPv4/TCP packets in separate 32 KiB malloc'd buffers (as
  * loop.c:180-183 allocates them) with the reference's framing
@@ -12,7 +12,9 @@
  * context.c:208). "corrupt": CPU checks, then one TCP header byte (the
  * window's low byte) of every 7th packet flipped after the check was taken,
  * so those no longer verify; the receiver then expects only the others (the
- * interposer's TCPCSUM_PRELOAD_RX=drop). Sends them with sendmmsg in batches
+ * interposer's TCPCSUM_PRELOAD_RX=drop). "trunc": CPU checks, and every
+ * packet received into a 600-byte buffer with MSG_TRUNC, so a longer datagram
+ * is cut short while msg_len reports its full length. Sends them with sendmmsg in batches
  * of <= 1024 and receives them with recvmmsg. Writes to <out-file>: for every
  * packet u32 length + the bytes as built, then u32 length + the bytes as
  * received (length 0: never received). Exit 0 on success; 3 if sendmmsg
@@ -69,7 +71,9 @@ int main(int argc, char **argv) {
     if (argc < 3) { fprintf(stderr, "usage: %s npkts out [cpu-checks]\n", argv[0]); return 2; }
     int n = atoi(argv[1]);
     int corrupt = argc > 3 && !strcmp(argv[3], "corrupt");
-    int cpu_checks = corrupt || (argc > 3 && !strcmp(argv[3], "cpu-checks"));
+    int trunc = argc > 3 && !strcmp(argv[3], "trunc");
+    int cpu_checks = corrupt || trunc || (argc > 3 && !strcmp(argv[3], "cpu-checks"));
+    const size_t rx_cap = trunc ? 600 : 32768;
     FILE *f = fopen(argv[2], "wb");
     if (!f || n <= 0) return 2;
     int rx = socket(AF_INET, SOCK_DGRAM, 0), tx = socket(AF_INET, SOCK_DGRAM, 0);
@@ -113,20 +117,21 @@ int main(int argc, char **argv) {
         while (got < want) {
             memset(mv, 0, sizeof mv);
             for (int k = 0; k < cnt - got; ++k) {
-                iv[k].iov_base = scratch[k]; iv[k].iov_len = 32768;
+                iv[k].iov_base = scratch[k]; iv[k].iov_len = rx_cap;
                 mv[k].msg_hdr.msg_iov = &iv[k]; mv[k].msg_hdr.msg_iovlen = 1;
             }
             struct timespec to = {5, 0};
-            int r = recvmmsg(rx, mv, (unsigned) (cnt - got), MSG_WAITFORONE, &to);
+            int r = recvmmsg(rx, mv, (unsigned) (cnt - got), MSG_WAITFORONE | (trunc ? MSG_TRUNC : 0), &to);
             if (r < 0) { fprintf(stderr, "recvmmsg: %s\n", strerror(errno)); return 4; }
             if (r == 0 && !corrupt) return 5;
             for (int k = 0; k < r; ++k) {
                 /* which packet: daddr = 10.x.y.z carries its index */
                 const uint8_t *b = (const uint8_t *) mv[k].msg_hdr.msg_iov[0].iov_base;
-                const int idx = mv[k].msg_len >= 20 ? (b[17] << 16) | (b[18] << 8) | b[19] : -1;
+                const size_t held = mv[k].msg_len < rx_cap ? mv[k].msg_len : rx_cap;
+                const int idx = held >= 20 ? (b[17] << 16) | (b[18] << 8) | b[19] : -1;
                 if (idx < s0 || idx >= s0 + cnt || ilen[idx]) { fprintf(stderr, "unexpected message\n"); return 5; }
-                memcpy(in[idx], b, mv[k].msg_len);
-                ilen[idx] = mv[k].msg_len;
+                memcpy(in[idx], b, held);
+                ilen[idx] = held;
             }
             got += r;
             if (r == 0) {   /* every message of this receive was dropped: wait for the rest */

@@ -27,13 +27,14 @@ def _ensure_built():
         subprocess.run(["make", "-C", REPO, "tests/c/mmsg_loop", "tcp_amd/libtcpcsum_preload.so"], check=True)
 
 
-def run_loop(tmp_path, n, env_extra, cpu_checks=False, corrupt=False):
+def run_loop(tmp_path, n, env_extra, cpu_checks=False, corrupt=False, trunc=False):
     _ensure_built()
     out = tmp_path / "mm.bin"
     env = {k: v for k, v in os.environ.items() if not k.startswith("TCPCSUM_PRELOAD")}
     env.update({"LD_PRELOAD": PRELOAD, "TCPCSUM_PRELOAD_ANY_SOCKET": "1", "TCPCSUM_PRELOAD_STATS": "1"})
     env.update(env_extra)
-    args = [EXE, str(n), str(out)] + (["corrupt"] if corrupt else ["cpu-checks"] if cpu_checks else [])
+    args = [EXE, str(n), str(out)] + (["trunc"] if trunc else ["corrupt"] if corrupt else
+                                      ["cpu-checks"] if cpu_checks else [])
     r = subprocess.run(args, env=env, capture_output=True, text=True, timeout=120)
     pkts = []
     if r.returncode == 0:
@@ -139,6 +140,25 @@ def test_rx_drop_on_gpu(tmp_path, inplace):
             assert got == b""                        # never delivered
     assert bad == n // 7
     assert stats["rx_verified"] == n and stats["rx_verify_failed"] == bad and stats["rx_dropped"] == bad
+
+
+@pytest.mark.gpu
+def test_rx_truncated_messages_bounded_by_buffer(tmp_path):
+    """recvmmsg with MSG_TRUNC into 600-byte buffers: msg_len reports each datagram's full length,
+    but only the 600 bytes the buffer holds are the segment's. Longer segments are truncated and
+    SKIPPED (tot_len exceeds the bytes received) — never verified from bytes past the buffer —
+    and the ones that fit verify (CPU checks, context.c:208)."""
+    n = 1200
+    r, pkts, stats = run_loop(tmp_path, n, {"TCPCSUM_PRELOAD_TX": "off", "TCPCSUM_PRELOAD_RX": "verify"},
+                              trunc=True)
+    assert r.returncode == 0, r.stderr
+    assert len(pkts) == n
+    fit = sum(len(built) <= 600 for built, _ in pkts)
+    for built, got in pkts:
+        assert got == built[:600]
+    assert 0 < fit < n
+    assert stats["rx_packets"] == n and stats["rx_skipped"] == n - fit
+    assert stats["rx_verified"] == fit and stats["rx_verify_failed"] == 0
 
 
 # ----------------------------------------------------------------- raw sockets
