@@ -278,3 +278,31 @@ def test_ipv4_region_host_registered_pool(dev, register):
             assert np.all(out2[st2 == tcp_amd.PKT_OK] == 0)
         finally:
             ctx.unregister_host()
+
+
+@pytest.mark.parametrize("passes", ["1", "2"])
+def test_ipv4_region_host_staging_large_bounds(dev, passes, monkeypatch):
+    """A pageable region whose packets' readable bounds add up past the one-pass staging limit
+    (64 MiB: 1400 packets in 32 KiB slots with cap 65535, so each bound is up to 64 KiB): the copy
+    threads read every packet's tot_len first and pack the copies by it (two passes). With
+    TCPCSUM_HOST_STAGE_PASSES=2 (read once, at context creation) a small batch takes the same
+    two-pass route. Results, statuses and the caller's bytes match the oracle either way."""
+    import tcp_amd
+    from tests.packets import build_batch
+    monkeypatch.setenv("TCPCSUM_HOST_STAGE_PASSES", passes)
+    rng = np.random.default_rng(31)
+    n = 1400 if passes == "1" else 300
+    region, off, _ = build_batch(rng, n, slot=32768, malformed=True)
+    ref = region.copy()
+    for mode in (tcp_amd.IPV4_FILL | tcp_amd.IPV4_IPHDR, tcp_amd.IPV4_VERIFY | tcp_amd.IPV4_IPHDR):
+        want_out, want_st = oracle.ipv4_batch(ref, off, 65535, mode)
+        with tcp_amd.HostContext(0) as ctx:
+            out, st = ctx.ipv4_batch(region, off, 65535, mode)
+            stats = ctx.stats()
+        assert np.array_equal(st, want_st) and np.array_equal(out, want_out)
+        assert np.array_equal(region, ref)
+        assert stats["pkts_staged"] == n and stats["pkts_in_place"] == 0
+        # only the packets' bytes were copied, not their 64 KiB bounds
+        assert stats["bytes_staged"] <= n * 1600
+    ok = want_st == tcp_amd.PKT_OK
+    assert ok.sum() > n // 2 and np.all(want_out[ok] == 0)
