@@ -171,13 +171,11 @@ struct tcpcsum_ctx {
     uint8_t* d_slot[2] = {nullptr, nullptr};   // ... and its device copy (uniform_dma)
     size_t d_slot_bytes = 0;
     tcpcsum::Pinned gath;      // wire batches: packets copied out of pageable memory
-    uint8_t* d_gath = nullptr;   // ... and their copy in HBM (wire_dma)
-    size_t d_gath_bytes = 0;
     tcpcsum::Pinned ss, res;   // per-segment start values / results, when the caller's are pageable
     // per-packet arrays the wire kernels read (addresses, bounds) and write
     // (results, status), kept in pinned memory so a pageable caller array costs
     // a CPU memcpy rather than a HIP copy
-    tcpcsum::Pinned p_off, p_len, p_out, p_stat, p_ip;
+    tcpcsum::Pinned p_off, p_len, p_out, p_stat;
     // gathered packets of the current batch: index, source, staging offset, bytes
     std::vector<uint64_t> g_idx, g_off;
     std::vector<uint8_t*> g_src;
@@ -189,12 +187,6 @@ struct tcpcsum_ctx {
     bool nt_copy = true;   // streaming stores for the uniform chunks (TCPCSUM_HOST_NT=0: plain memcpy)
     bool stage_one_pass = true;   // wire staging laid out by bounds, one pass (TCPCSUM_HOST_STAGE_PASSES=2: by lengths)
     bool uniform_dma = true;   // staged uniform chunks go to HBM by DMA (TCPCSUM_HOST_DMA=0: kernel reads them over PCIe)
-    // staged wire packets go to HBM by DMA in wire_blocks pieces, each queued as
-    // soon as its packets are copied, and the kernel reads HBM
-    // (TCPCSUM_HOST_WIRE_DMA=0: the kernel reads the pinned staging over PCIe)
-    bool wire_dma = true;
-    int wire_blocks = 2;         // TCPCSUM_HOST_WIRE_BLOCKS
-    bool staged_in_hbm = false;  // the current batch's staged packets were DMA'd (FILL write-back from `out`)
     tcpcsum_ctx_stats_t stats{};
     std::mutex mu;
 };
@@ -263,7 +255,6 @@ int ensure_pkt_arrays(tcpcsum_ctx* c, uint64_t n) {
     if (e == hipSuccess) e = c->p_len.ensure(n * sizeof(uint32_t));
     if (e == hipSuccess) e = c->p_out.ensure(n * sizeof(uint16_t));
     if (e == hipSuccess) e = c->p_stat.ensure(n);
-    if (e == hipSuccess) e = c->p_ip.ensure(n * sizeof(uint16_t));
     if (e != hipSuccess) {
         tcpcsum::note_hip_error((int)e);
         return TCPCSUM_ENOMEM;
@@ -289,15 +280,10 @@ inline uint32_t copy_len(const uint8_t* ip, uint64_t bound) {
 // that is one pass; past it (huge bounds: 64 KiB caps over big batches) the
 // lengths are read first and the copies packed by them, two passes. Sets
 // k_off / k_len of every staged packet.
-//
-// With wire_dma the staging is always packed by length (the DMA moves the
-// packets, not their bounds) and goes to HBM in wire_blocks pieces: the copy
-// threads fill piece b + 1 while the DMA engine moves piece b.
 constexpr size_t kStageByBound = 64u << 20;
-int stage_packets(tcpcsum_ctx* c, uint64_t* k_off, uint32_t* k_len, size_t* staged_bytes, hipStream_t st) {
+int stage_packets(tcpcsum_ctx* c, uint64_t* k_off, uint32_t* k_len, size_t* staged_bytes) {
     const size_t m = c->g_idx.size();
     *staged_bytes = 0;
-    c->staged_in_hbm = false;
     if (!m) return TCPCSUM_OK;
     const uint64_t t0 = tcpcsum::now_ns();
     size_t span = 0;
@@ -305,8 +291,7 @@ int stage_packets(tcpcsum_ctx* c, uint64_t* k_off, uint32_t* k_len, size_t* stag
         c->g_off[k] = span;
         span += ((size_t)c->g_len[k] + 15u) & ~(size_t)15u;
     }
-    const bool dma = c->wire_dma;
-    const bool by_bound = span <= kStageByBound && c->stage_one_pass && !dma;
+    const bool by_bound = span <= kStageByBound && c->stage_one_pass;
     if (!by_bound) {
         c->pool->run(m, 64, [&](size_t lo, size_t hi) {
             for (size_t k = lo; k < hi; ++k) c->g_len[k] = copy_len(c->g_src[k], c->g_len[k]);
@@ -322,54 +307,20 @@ int stage_packets(tcpcsum_ctx* c, uint64_t* k_off, uint32_t* k_len, size_t* stag
         tcpcsum::note_hip_error((int)e);
         return TCPCSUM_ENOMEM;
     }
-    if (dma && span > c->d_gath_bytes) {   // no kernel of this context is running (each call waits)
-        if (c->d_gath) (void)hipFree(c->d_gath);
-        c->d_gath = nullptr;
-        c->d_gath_bytes = 0;
-        size_t nb = 1u << 20;
-        while (nb < span) nb *= 2;
-        e = hipMalloc(&c->d_gath, nb);
-        if (e != hipSuccess) {
-            (void)hipGetLastError();
-            tcpcsum::note_hip_error((int)e);
-            return TCPCSUM_ENOMEM;
-        }
-        c->d_gath_bytes = nb;
-    }
     uint8_t* gh = c->gath.h;
-    uint8_t* gd = dma ? c->d_gath : c->gath.d;
+    uint8_t* gd = c->gath.d;
     std::atomic<size_t> copied{0};
-    auto copy_range = [&](size_t k0, size_t k1) {
-        c->pool->run(k1 - k0, 16, [&](size_t lo, size_t hi) {
-            size_t b = 0;
-            for (size_t k = k0 + lo; k < k0 + hi; ++k) {
-                if (by_bound) c->g_len[k] = copy_len(c->g_src[k], c->g_len[k]);
-                memcpy(gh + c->g_off[k], c->g_src[k], c->g_len[k]);
-                k_off[c->g_idx[k]] = (uint64_t)(uintptr_t)(gd + c->g_off[k]);
-                k_len[c->g_idx[k]] = c->g_len[k];
-                b += c->g_len[k];
-            }
-            copied.fetch_add(b, std::memory_order_relaxed);
-        });
-    };
-    if (!dma) {
-        copy_range(0, m);
-    } else {
-        const size_t nb = (size_t)std::max(1, std::min<int>(c->wire_blocks, 16));
-        for (size_t b = 0; b < nb; ++b) {
-            const size_t k0 = m * b / nb, k1 = m * (b + 1) / nb;
-            if (k0 == k1) continue;
-            copy_range(k0, k1);
-            const size_t lo = c->g_off[k0], hi = k1 < m ? c->g_off[k1] : span;
-            e = hipMemcpyAsync(c->d_gath + lo, gh + lo, hi - lo, hipMemcpyHostToDevice, st);
-            if (e != hipSuccess) {   // pieces already queued must land before the staging is reused
-                (void)hipStreamSynchronize(st);
-                c->stats.ns_copy += tcpcsum::now_ns() - t0;
-                return hip_fail(e);
-            }
+    c->pool->run(m, 16, [&](size_t lo, size_t hi) {
+        size_t b = 0;
+        for (size_t k = lo; k < hi; ++k) {
+            if (by_bound) c->g_len[k] = copy_len(c->g_src[k], c->g_len[k]);
+            memcpy(gh + c->g_off[k], c->g_src[k], c->g_len[k]);
+            k_off[c->g_idx[k]] = (uint64_t)(uintptr_t)(gd + c->g_off[k]);
+            k_len[c->g_idx[k]] = c->g_len[k];
+            b += c->g_len[k];
         }
-        c->staged_in_hbm = true;
-    }
+        copied.fetch_add(b, std::memory_order_relaxed);
+    });
     c->stats.ns_copy += tcpcsum::now_ns() - t0;
     c->stats.pkts_staged += m;
     c->stats.bytes_staged += copied.load();
@@ -385,53 +336,32 @@ int stage_packets(tcpcsum_ctx* c, uint64_t* k_off, uint32_t* k_len, size_t* stag
 // against copy-then-launch on 1024 x 1500-B batches: no gain / no gain /
 // +15-30 us / +60-90 us, the host cost of each queued launch landing before
 // the copies (profiles/r03_hostpath_sweep_wire_split.jsonl).
-//
-// Launch shape: a batch whose packets are all read from HBM takes the
-// built-in shapes; one that reads host memory over PCIe (packets in place, or
-// staged without DMA) takes the 16-lane groups when it is a small batch
-// (512 B per round: more waves with PCIe reads in flight — 1024 x 1500-B FILL
-// batch 49 vs 59 us on MI355X, tools/e2e.py --sweep).
-int stage_and_launch(tcpcsum_ctx* c, uint64_t n, uint32_t in_cap, uint64_t in_foot, uint64_t in_place, int mode,
-                     uint16_t* kout, uint8_t* kst, hipStream_t st, tcpcsum::Tuning tu) {
+int stage_and_launch(tcpcsum_ctx* c, uint64_t n, uint32_t in_cap, uint64_t in_foot, int mode, uint16_t* kout,
+                     uint8_t* kst, hipStream_t st, const tcpcsum::Tuning& tu) {
     size_t staged = 0;
-    int rc = stage_packets(c, (uint64_t*)c->p_off.h, (uint32_t*)c->p_len.h, &staged, st);
+    int rc = stage_packets(c, (uint64_t*)c->p_off.h, (uint32_t*)c->p_len.h, &staged);
     if (rc) return rc;
     uint32_t cap = in_cap;
     for (size_t k = 0; k < c->g_idx.size(); ++k) cap = std::max(cap, c->g_len[k]);
-    const bool pcie = in_place > 0 || (!c->staged_in_hbm && !c->g_idx.empty());
-    if (tu.shape < 0 && n < 65536u && pcie) tu.shape = 3;
-    // FILL from HBM copies: the IPv4 header checksums come back through p_ip
-    uint16_t* kip = c->staged_in_hbm && (mode & TCPCSUM_IPV4_IPHDR) ? (uint16_t*)c->p_ip.d : nullptr;
     tcpcsum::launch_ipv4(nullptr, (const uint64_t*)c->p_off.d, (const uint32_t*)c->p_len.d, n, cap, ~0ull,
-                         in_foot + staged, mode, kout, kst, kip, st, tu);
+                         in_foot + staged, mode, kout, kst, nullptr, st, tu);
     return check_launch();
 }
 
-// FILL on staged packets: put each check (and the IPv4 header checksum, with
-// IPHDR) into the caller's packet, on the copy threads. The kernel stored them
-// in the staged copy — in pinned staging, or in HBM (staged_in_hbm), where
-// they are taken from the results instead: `out` (the check, as stored) and
-// p_ip (the header checksum).
-void write_back_checks(tcpcsum_ctx* c, const uint8_t* status, const uint16_t* out, bool iphdr) {
+// FILL on staged packets: the kernel stored each check in the staging copy;
+// put it (and the IPv4 header checksum, with IPHDR) into the caller's packet,
+// on the copy threads.
+void write_back_checks(tcpcsum_ctx* c, const uint8_t* status, bool iphdr) {
     const size_t m = c->g_idx.size();
     const uint64_t t0 = tcpcsum::now_ns();
-    const bool hbm = c->staged_in_hbm;
-    const uint16_t* ip = (const uint16_t*)c->p_ip.h;
     c->pool->run(m, 64, [&](size_t lo, size_t hi) {
         for (size_t k = lo; k < hi; ++k) {
-            const uint64_t i = c->g_idx[k];
-            if (status[i] != TCPCSUM_PKT_OK) continue;
+            if (status[c->g_idx[k]] != TCPCSUM_PKT_OK) continue;
+            const uint8_t* sp = c->gath.h + c->g_off[k];
             uint8_t* dp = c->g_src[k];
-            if (hbm) {
-                const unsigned tcp = (dp[0] & 15u) * 4u;
-                memcpy(dp + tcp + 16, &out[i], 2);   // context.c:208: native u16 at TCP+16
-                if (iphdr) memcpy(dp + 10, &ip[i], 2);
-            } else {
-                const uint8_t* sp = c->gath.h + c->g_off[k];
-                const unsigned tcp = (sp[0] & 15u) * 4u;
-                memcpy(dp + tcp + 16, sp + tcp + 16, 2);
-                if (iphdr) memcpy(dp + 10, sp + 10, 2);
-            }
+            const unsigned tcp = (sp[0] & 15u) * 4u;
+            memcpy(dp + tcp + 16, sp + tcp + 16, 2);   // context.c:208: native u16 at TCP+16
+            if (iphdr) memcpy(dp + 10, sp + 10, 2);
         }
     });
     c->stats.ns_copy += tcpcsum::now_ns() - t0;
@@ -468,8 +398,6 @@ int tcpcsum_ctx_create(int device, size_t scratch_bytes, tcpcsum_ctx_t** out) {
     c->nt_copy = tcpcsum::env_int("TCPCSUM_HOST_NT", 1) != 0;
     c->stage_one_pass = tcpcsum::env_int("TCPCSUM_HOST_STAGE_PASSES", 1) == 1;
     c->uniform_dma = tcpcsum::env_int("TCPCSUM_HOST_DMA", 1) != 0;
-    c->wire_dma = tcpcsum::env_int("TCPCSUM_HOST_WIRE_DMA", 1) != 0;
-    c->wire_blocks = std::max(1, std::min(16, tcpcsum::env_int("TCPCSUM_HOST_WIRE_BLOCKS", 2)));
     for (int i = 0; i < 2; ++i) {
         e = hipStreamCreateWithFlags(&c->st[i], hipStreamNonBlocking);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->slot_ev[i], hipEventDisableTiming);
@@ -490,7 +418,6 @@ void tcpcsum_ctx_destroy(tcpcsum_ctx_t* c) {
     c->reg.release(0, 0);
     for (int i = 0; i < 2; ++i) {
         if (c->d_slot[i]) hipFree(c->d_slot[i]);
-        if (i == 0 && c->d_gath) hipFree(c->d_gath);
         if (c->slot_ev[i]) hipEventDestroy(c->slot_ev[i]);
         if (c->st[i]) hipStreamDestroy(c->st[i]);
     }
@@ -673,14 +600,15 @@ int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t* c, void* h_pkts, size_t region_bytes,
     uint16_t* kout = zout ? zout : (uint16_t*)c->p_out.d;
     uint8_t* kst = zst ? zst : c->p_stat.d;
     const bool fill = (mode & TCPCSUM_IPV4_VERIFY) == 0;
+    // zero-copy over PCIe: 16-lane groups, 512 B per round (more waves with
+    // reads in flight) beat the HBM-tuned MTU shape — 1024 x 1500-B FILL
+    // batch 49 vs 59 us on MI355X (tools/e2e.py --sweep)
     tcpcsum::Tuning tu = c->tune;
+    if (tu.shape < 0 && n < 65536u) tu.shape = 3;
     hipError_t e;
     uint8_t* zp = (uint8_t*)pinned_dev_ptr(h_pkts, region_bytes);
     c->g_idx.clear();
-    c->staged_in_hbm = false;
     if (zp) {
-        // zero-copy over PCIe: the small-batch shape of stage_and_launch
-        if (tu.shape < 0 && n < 65536u) tu.shape = 3;
         const uint64_t* koff = (const uint64_t*)pinned_dev_ptr(h_pkt_off, n * sizeof(uint64_t));
         if (!koff) {
             memcpy(c->p_off.h, h_pkt_off, n * sizeof(uint64_t));
@@ -702,7 +630,7 @@ int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t* c, void* h_pkts, size_t region_bytes,
             c->g_src[i] = base + h_pkt_off[i];
             c->g_len[i] = (uint32_t)std::min<uint64_t>(cap, region_bytes - h_pkt_off[i]);
         }
-        rc = stage_and_launch(c, n, 20u, 0u, 0u, mode, kout, kst, st, tu);
+        rc = stage_and_launch(c, n, 20u, 0u, mode, kout, kst, st, tu);
         if (rc) return rc;
     }
     rc = check_launch();
@@ -710,8 +638,7 @@ int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t* c, void* h_pkts, size_t region_bytes,
     e = wait_stream(c, st);
     if (e != hipSuccess) return hip_fail(e);
     if (fill && !c->g_idx.empty())
-        write_back_checks(c, zst ? h_status : c->p_stat.h, zout ? h_out : (const uint16_t*)c->p_out.h,
-                          (mode & TCPCSUM_IPV4_IPHDR) != 0);
+        write_back_checks(c, zst ? h_status : c->p_stat.h, (mode & TCPCSUM_IPV4_IPHDR) != 0);
     if (h_out && !zout) memcpy(h_out, c->p_out.h, n * sizeof(uint16_t));
     if (h_status && !zst) memcpy(h_status, c->p_stat.h, n);
     return TCPCSUM_OK;
@@ -772,14 +699,16 @@ int tcpcsum_ipv4_batch_ptrs_host(tcpcsum_ctx_t* c, void* const* h_pkts, const ui
     c->stats.pkts_in_place += in_place;
     uint16_t* zout = h_out ? (uint16_t*)pinned_dev_ptr(h_out, n * sizeof(uint16_t)) : nullptr;
     uint8_t* zst = h_status ? (uint8_t*)pinned_dev_ptr(h_status, n) : nullptr;
-    rc = stage_and_launch(c, n, cap, foot, in_place, mode, zout ? zout : (uint16_t*)c->p_out.d,
-                          zst ? zst : c->p_stat.d, st, c->tune);
+    // zero-copy over PCIe: the 16-lane group shape for latency-bound batches
+    // (as tcpcsum_ipv4_batch_host on a pinned pool)
+    tcpcsum::Tuning tu = c->tune;
+    if (tu.shape < 0 && n < 65536u) tu.shape = 3;
+    rc = stage_and_launch(c, n, cap, foot, mode, zout ? zout : (uint16_t*)c->p_out.d, zst ? zst : c->p_stat.d, st, tu);
     if (rc) return rc;
     hipError_t e = wait_stream(c, st);
     if (e != hipSuccess) return hip_fail(e);
     if ((mode & TCPCSUM_IPV4_VERIFY) == 0 && !c->g_idx.empty())
-        write_back_checks(c, zst ? h_status : c->p_stat.h, zout ? h_out : (const uint16_t*)c->p_out.h,
-                          (mode & TCPCSUM_IPV4_IPHDR) != 0);
+        write_back_checks(c, zst ? h_status : c->p_stat.h, (mode & TCPCSUM_IPV4_IPHDR) != 0);
     if (h_out && !zout) memcpy(h_out, c->p_out.h, n * sizeof(uint16_t));
     if (h_status && !zst) memcpy(h_status, c->p_stat.h, n);
     return TCPCSUM_OK;

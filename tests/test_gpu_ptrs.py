@@ -188,14 +188,11 @@ def test_ipv4_ptrs_host_loop_layout(dev, auto_register):
         assert ctx.registered() == (0, 0)
 
 
-@pytest.mark.parametrize("wire_dma", ["0", "1"])
-def test_ipv4_ptrs_host_pinned_and_mixed(dev, wire_dma, monkeypatch):
+def test_ipv4_ptrs_host_pinned_and_mixed(dev):
     """Packets in page-locked memory (tcpcsum_host_alloc) are used through their existing mapping
-    (no registration, no copy); pageable buffers in the same batch are staged — their copies read
-    over PCIe, or moved to HBM first (TCPCSUM_HOST_WIRE_DMA) — in one launch; NULL and short
+    (no registration, no copy); pageable buffers in the same batch are staged; NULL and short
     messages are SKIPPED."""
     import tcp_amd
-    monkeypatch.setenv("TCPCSUM_HOST_WIRE_DMA", wire_dma)
     rng = np.random.default_rng(12)
     pinned = tcp_amd.pinned_empty(64 * 2048)
     pinned[:] = 0
@@ -283,20 +280,16 @@ def test_ipv4_region_host_registered_pool(dev, register):
             ctx.unregister_host()
 
 
-@pytest.mark.parametrize("passes,wire_dma,blocks", [("1", "0", "1"), ("2", "0", "1"), ("1", "1", "1"),
-                                                    ("1", "1", "3"), ("2", "1", "16")])
-def test_ipv4_region_host_staging_large_bounds(dev, passes, wire_dma, blocks, monkeypatch):
+@pytest.mark.parametrize("passes", ["1", "2"])
+def test_ipv4_region_host_staging_large_bounds(dev, passes, monkeypatch):
     """A pageable region whose packets' readable bounds add up past the one-pass staging limit
     (64 MiB: 1400 packets in 32 KiB slots with cap 65535, so each bound is up to 64 KiB): the copy
     threads read every packet's tot_len first and pack the copies by it (two passes). With
     TCPCSUM_HOST_STAGE_PASSES=2 (read once, at context creation) a small batch takes the same
-    two-pass route, as does every batch moved to HBM by DMA (TCPCSUM_HOST_WIRE_DMA, in 1-16 pieces).
-    Results, statuses and the caller's bytes match the oracle either way."""
+    two-pass route. Results, statuses and the caller's bytes match the oracle either way."""
     import tcp_amd
     from tests.packets import build_batch
     monkeypatch.setenv("TCPCSUM_HOST_STAGE_PASSES", passes)
-    monkeypatch.setenv("TCPCSUM_HOST_WIRE_DMA", wire_dma)
-    monkeypatch.setenv("TCPCSUM_HOST_WIRE_BLOCKS", blocks)
     rng = np.random.default_rng(31)
     n = 1400 if passes == "1" else 300
     region, off, _ = build_batch(rng, n, slot=32768, malformed=True)

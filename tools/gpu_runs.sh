@@ -447,22 +447,8 @@ round3_final() {
 )
 }
 
-# Staged wire batches moved to HBM by DMA (TCPCSUM_HOST_WIRE_DMA, in pieces) against the
-# kernel reading the pinned staging over PCIe: host-path tests, the wire-only sweep, e2e.
-wire_dma_check() {
-(
-  O=gpurun_out/wdma
-  mkdir -p $O
-  timeout -k 10 300 python -u -m pytest tests/test_gpu_ptrs.py tests/test_plumbing.py tests/test_seam.py tests/test_gpu_hostpath.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/t.log 2>&1 || { tail -15 $O/t.log; exit 1; }
-  tail -1 $O/t.log
-  timeout -k 10 300 python3 tools/hostpath_sweep.py --wire-only --rounds 3 --configs 8:1:1:50:1:0:1,8:1:1:50:2:0:1,8:1:1:50:1:1:1,8:1:1:50:1:1:2,8:1:1:50:1:1:4,8:1:1:50:1:1:8 > $O/sweep.jsonl 2> $O/sweep.err || { tail $O/sweep.err; exit 1; }
-  timeout -k 10 200 python3 tools/e2e.py > $O/e2e.jsonl 2> $O/e2e.err || { tail $O/e2e.err; exit 1; }
-  echo wdma ok
-)
-}
-
 if [ $# -eq 0 ]; then
-  echo "experiments: round3_final wire_dma_check hostpath_check gpu_r3_fill gpu_r3_n8 gpu_round3 grid_check grid_long grid_m1 grid_sweep k64_check lane_ab lb_sweep lds_ab pmc_64 pmc_imix pmc_lb round3_profile round_final round_profile split_sweep split_sweep2 spw_check tx_size_sweep tx_size_sweep2 uniform_size_sweep uniform_size_sweep2 wire_big_sweep wire_default_check wire_lb_small wire_mid_sweep wire_mtu_sweep wire_small_sweep"
+  echo "experiments: round3_final hostpath_check gpu_r3_fill gpu_r3_n8 gpu_round3 grid_check grid_long grid_m1 grid_sweep k64_check lane_ab lb_sweep lds_ab pmc_64 pmc_imix pmc_lb round3_profile round_final round_profile split_sweep split_sweep2 spw_check tx_size_sweep tx_size_sweep2 uniform_size_sweep uniform_size_sweep2 wire_big_sweep wire_default_check wire_lb_small wire_mid_sweep wire_mtu_sweep wire_small_sweep"
   exit 0
 fi
 "$@"

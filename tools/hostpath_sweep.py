@@ -6,10 +6,7 @@ context's copy knobs, read at tcpcsum_ctx_create:
   TCPCSUM_HOST_DMA           uniform chunks: DMA to HBM then the kernel (0: kernel reads staging over PCIe)
   TCPCSUM_HOST_SPIN_US       how long an idle copy thread spins before it sleeps
   TCPCSUM_HOST_STAGE_PASSES  wire staging: 1 = laid out by bounds, one pass; 2 = lengths first, packed
-  TCPCSUM_HOST_WIRE_DMA      wire staging goes to HBM by DMA (0: the kernel reads it over PCIe)
-  TCPCSUM_HOST_WIRE_BLOCKS   ... in this many pieces, each queued once its packets are copied
---configs: threads:nt:dma[:spin_us[:passes[:wire_dma[:wire_blocks]]]],...
---wire-only: skip the uniform measure
+--configs: threads:nt:dma[:spin_us[:passes]],...
 Wire packets are staged on the copy threads (header reads, copies and the FILL
 write-back) and checksummed by one launch.
 Measures tcpcsum_batch_uniform_host over 1M x 1500 B pageable, and one
@@ -43,8 +40,7 @@ def timed(fn, reps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=2)
-    ap.add_argument("--configs", default="8:1:1:50:1:0:1,8:1:1:50:1:1:1,8:1:1:50:1:1:2,8:1:1:50:1:1:4")
-    ap.add_argument("--wire-only", action="store_true")
+    ap.add_argument("--configs", default="8:1:1:50:1,8:1:1:50:2,4:1:1:50:1,2:1:1:50:1,1:1:1:50:1")
     args = ap.parse_args()
     import numpy as np
     import tcp_amd
@@ -68,7 +64,7 @@ def main():
         bufs.append(b)
     ptrs = np.array([b.ctypes.data for b in bufs[1::2]], np.uint64)   # arrays, not lists: no per-call conversion
     lens = np.full(1024, 1500, np.uint32)
-    defaults = [8, 1, 1, 50, 1, 1, 2]
+    defaults = [8, 1, 1, 50, 1]
     configs = []
     for c in args.configs.split(","):
         v = [int(x) for x in c.split(":")]
@@ -86,33 +82,26 @@ def main():
                           "us_best": round(tmin * 1e6, 1), "GB/s_median": round(src.size / tmed / 1e9, 2)}),
               flush=True)
     for rnd in range(args.rounds):
-        for th, nt, dma, spin, passes, wdma, wblocks in configs:
+        for th, nt, dma, spin, passes in configs:
             os.environ["TCPCSUM_HOST_THREADS"] = str(th)
             os.environ["TCPCSUM_HOST_NT"] = str(nt)
             os.environ["TCPCSUM_HOST_DMA"] = str(dma)
             os.environ["TCPCSUM_HOST_SPIN_US"] = str(spin)
             os.environ["TCPCSUM_HOST_STAGE_PASSES"] = str(passes)
-            os.environ["TCPCSUM_HOST_WIRE_DMA"] = str(wdma)
-            os.environ["TCPCSUM_HOST_WIRE_BLOCKS"] = str(wblocks)
             with tcp_amd.HostContext(0) as ctx:
-                cfg = {"threads": th, "nt": nt, "dma": dma, "spin_us": spin, "passes": passes, "wire_dma": wdma,
-                       "wire_blocks": wblocks, "round": rnd}
-                if args.wire_only:
-                    pass
-                else:
-                    got = ctx.batch_uniform(big, L, L, n, ss)
-                    if want is None:
-                        want = got
-                    assert np.array_equal(got, want)
-                    s0 = ctx.stats()
-                    tmin, tmed = timed(lambda: ctx.batch_uniform(big, L, L, n, ss), 5)
-                    s1 = ctx.stats()
-                    print(json.dumps({**cfg, "measure": "uniform_host_1Mx1500_pageable",
-                                      "GiB/s_median": round(n * L / tmed / 2**30, 2),
-                                      "GiB/s_best": round(n * L / tmin / 2**30, 2),
-                                      "copy_ms_per_call": round((s1["ns_copy"] - s0["ns_copy"]) / 5e6, 3),
-                                      "wait_ms_per_call": round((s1["ns_wait"] - s0["ns_wait"]) / 5e6, 3)}),
-                          flush=True)
+                got = ctx.batch_uniform(big, L, L, n, ss)
+                if want is None:
+                    want = got
+                assert np.array_equal(got, want)
+                s0 = ctx.stats()
+                tmin, tmed = timed(lambda: ctx.batch_uniform(big, L, L, n, ss), 5)
+                s1 = ctx.stats()
+                cfg = {"threads": th, "nt": nt, "dma": dma, "spin_us": spin, "passes": passes, "round": rnd}
+                print(json.dumps({**cfg, "measure": "uniform_host_1Mx1500_pageable",
+                                  "GiB/s_median": round(n * L / tmed / 2**30, 2),
+                                  "GiB/s_best": round(n * L / tmin / 2**30, 2),
+                                  "copy_ms_per_call": round((s1["ns_copy"] - s0["ns_copy"]) / 5e6, 3),
+                                  "wait_ms_per_call": round((s1["ns_wait"] - s0["ns_wait"]) / 5e6, 3)}), flush=True)
                 for name, fn in (("ipv4_host_pool32k_fill", lambda: ctx.ipv4_batch(pool, offs, 32768, 0)),
                                  ("ipv4_ptrs_host_loop_fill", lambda: ctx.ipv4_batch_ptrs(ptrs, lens, 0))):
                     fn()
