@@ -447,8 +447,21 @@ round3_final() {
 )
 }
 
+# The segment builder against the chip's read+write ceiling: tools/copy_probe (plain 16-B
+# copies of the builder's 1.53 GB of payload, store policies, 44-B destination shift) and
+# tools/txbench.py (k_tx_build, and torch copy_ as before) in the same box.
+copy_ceiling() {
+(
+  O=gpurun_out/copy
+  mkdir -p $O
+  timeout -k 10 200 ./tools/copy_probe > $O/copy_probe.jsonl 2> $O/copy_probe.err || { tail $O/copy_probe.err; exit 1; }
+  timeout -k 10 200 python3 tools/txbench.py > $O/txbench.jsonl 2> $O/txbench.err || { tail $O/txbench.err; exit 1; }
+  echo copy ok
+)
+}
+
 if [ $# -eq 0 ]; then
-  echo "experiments: round3_final hostpath_check gpu_r3_fill gpu_r3_n8 gpu_round3 grid_check grid_long grid_m1 grid_sweep k64_check lane_ab lb_sweep lds_ab pmc_64 pmc_imix pmc_lb round3_profile round_final round_profile split_sweep split_sweep2 spw_check tx_size_sweep tx_size_sweep2 uniform_size_sweep uniform_size_sweep2 wire_big_sweep wire_default_check wire_lb_small wire_mid_sweep wire_mtu_sweep wire_small_sweep"
+  echo "experiments: copy_ceiling round3_final hostpath_check gpu_r3_fill gpu_r3_n8 gpu_round3 grid_check grid_long grid_m1 grid_sweep k64_check lane_ab lb_sweep lds_ab pmc_64 pmc_imix pmc_lb round3_profile round_final round_profile split_sweep split_sweep2 spw_check tx_size_sweep tx_size_sweep2 uniform_size_sweep uniform_size_sweep2 wire_big_sweep wire_default_check wire_lb_small wire_mid_sweep wire_mtu_sweep wire_small_sweep"
   exit 0
 fi
 "$@"
