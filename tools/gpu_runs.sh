@@ -460,8 +460,18 @@ copy_ceiling() {
 )
 }
 
+# Segment builder launch shapes up to one tile per wave (1M x 1456-B payloads)
+tx_grid_sweep() {
+(
+  O=gpurun_out/txgrid
+  mkdir -p $O
+  TX_SHAPES=2,3,4 TX_BLOCKS=16384,32768,65536,131072,262144 TX_UNROLLS=1,2 timeout -k 10 300 python3 tools/txbench.py --sweep > $O/sweep.jsonl 2> $O/sweep.err || { tail $O/sweep.err; exit 1; }
+  echo txgrid ok
+)
+}
+
 if [ $# -eq 0 ]; then
-  echo "experiments: copy_ceiling round3_final hostpath_check gpu_r3_fill gpu_r3_n8 gpu_round3 grid_check grid_long grid_m1 grid_sweep k64_check lane_ab lb_sweep lds_ab pmc_64 pmc_imix pmc_lb round3_profile round_final round_profile split_sweep split_sweep2 spw_check tx_size_sweep tx_size_sweep2 uniform_size_sweep uniform_size_sweep2 wire_big_sweep wire_default_check wire_lb_small wire_mid_sweep wire_mtu_sweep wire_small_sweep"
+  echo "experiments: tx_grid_sweep copy_ceiling round3_final hostpath_check gpu_r3_fill gpu_r3_n8 gpu_round3 grid_check grid_long grid_m1 grid_sweep k64_check lane_ab lb_sweep lds_ab pmc_64 pmc_imix pmc_lb round3_profile round_final round_profile split_sweep split_sweep2 spw_check tx_size_sweep tx_size_sweep2 uniform_size_sweep uniform_size_sweep2 wire_big_sweep wire_default_check wire_lb_small wire_mid_sweep wire_mtu_sweep wire_small_sweep"
   exit 0
 fi
 "$@"
