@@ -37,6 +37,13 @@
 #ifndef TCPCSUM_TUNING_VARIANTS
 #define TCPCSUM_TUNING_VARIANTS 0
 #endif
+// Measurement builds only (tools/tx_ab.py): parts of the segment builder
+// switched off to see what its time is made of — the output is then WRONG.
+// 1: ragged-end stores, 2: header stores, 4: second source loads (B = A),
+// 8: full-chunk stores. 0 in every product build.
+#ifndef TCPCSUM_TX_KNOCKOUT
+#define TCPCSUM_TX_KNOCKOUT 0
+#endif
 
 namespace tcpcsum {
 
@@ -1411,8 +1418,12 @@ __device__ __forceinline__ void tx_full_chunk(const TxPkt& p, uint32_t idx, cons
                                               uint32_t& wsum, uint32_t& osum) {
     const u32x4 v = funnel16(A, B, (int)(p.sh >> 2), p.sh & 3u);
     u32x4* d = reinterpret_cast<u32x4*>(p.dbase + (uint64_t)idx * 16u);
-    if constexpr (NTS) __builtin_nontemporal_store(v, d);
-    else *d = v;
+    if constexpr ((TCPCSUM_TX_KNOCKOUT & 8) != 0) {
+    } else if constexpr (NTS) {
+        __builtin_nontemporal_store(v, d);
+    } else {
+        *d = v;
+    }
     wsum = sad16(v.x, wsum); wsum = sad16(v.y, wsum);
     wsum = sad16(v.z, wsum); wsum = sad16(v.w, wsum);
     if (p.odd) {
@@ -1428,7 +1439,7 @@ __device__ __forceinline__ void tx_edge_chunk_store(const TxPkt& p, int e, const
     const int64_t rel = (int64_t)e * 16 - (int64_t)p.dm;   // dest chunk start - first payload byte
     uint8_t* dc = p.dbase + (uint64_t)e * 16u;
 #pragma unroll
-    for (int b2 = 0; b2 < 16; ++b2) {
+    for (int b2 = 0; b2 < 16 && !(TCPCSUM_TX_KNOCKOUT & 1); ++b2) {
         const uint32_t word = b2 < 4 ? v.x : b2 < 8 ? v.y : b2 < 12 ? v.z : v.w;
         const int64_t pos = rel + b2;
         if (pos >= 0 && pos < (int64_t)p.len) dc[b2] = (uint8_t)(word >> (8 * (b2 & 3)));
@@ -1471,7 +1482,7 @@ __device__ __forceinline__ void tx_header(const TxPkt& p, uint64_t Spay, int mod
         for (int k = 0; k < 5; ++k) is += sum_halves(hd[k]);
         hd[2] |= (uint32_t)fold_ref(is) << 16;
     }
-    for (int j = gl; j < 11; j += G) {   // lane j stores header dword j
+    for (int j = gl; j < 11 && !(TCPCSUM_TX_KNOCKOUT & 2); j += G) {   // lane j stores header dword j
         uint32_t v = hd[0];
 #pragma unroll
         for (int k = 1; k < 11; ++k) v = j == k ? hd[k] : v;
@@ -1520,7 +1531,8 @@ __global__ __launch_bounds__(256) void k_tx_build(const uint8_t* __restrict__ pa
                 const uint32_t idx = p[u].f0 + (uint32_t)(k * G + gl);
                 const uint8_t* a = p[u].sbase + (uint64_t)idx * 16u;
                 A[u][k] = ld16(zsel(idx < p[u].f1, a));
-                B[u][k] = ld16(zsel(idx < p[u].f1 && p[u].sh, a + 16));
+                if constexpr ((TCPCSUM_TX_KNOCKOUT & 4) != 0) B[u][k] = A[u][k];
+                else B[u][k] = ld16(zsel(idx < p[u].f1 && p[u].sh, a + 16));
             }
             e[u] = tx_edge_chunk(p[u], gl);
             tx_edge_load(p[u], e[u], EA[u], EB[u]);

@@ -470,8 +470,18 @@ tx_grid_sweep() {
 )
 }
 
+# Segment builder A/B against the builds in tcp_amd/ab/ (tools/tx_ab.py --build, on the CPU first)
+tx_ab() {
+(
+  O=gpurun_out/txab
+  mkdir -p $O
+  timeout -k 10 300 python3 tools/tx_ab.py > $O/ab.jsonl 2> $O/ab.err || { tail $O/ab.err; exit 1; }
+  cat $O/ab.jsonl
+)
+}
+
 if [ $# -eq 0 ]; then
-  echo "experiments: tx_grid_sweep copy_ceiling round3_final hostpath_check gpu_r3_fill gpu_r3_n8 gpu_round3 grid_check grid_long grid_m1 grid_sweep k64_check lane_ab lb_sweep lds_ab pmc_64 pmc_imix pmc_lb round3_profile round_final round_profile split_sweep split_sweep2 spw_check tx_size_sweep tx_size_sweep2 uniform_size_sweep uniform_size_sweep2 wire_big_sweep wire_default_check wire_lb_small wire_mid_sweep wire_mtu_sweep wire_small_sweep"
+  echo "experiments: tx_ab tx_grid_sweep copy_ceiling round3_final hostpath_check gpu_r3_fill gpu_r3_n8 gpu_round3 grid_check grid_long grid_m1 grid_sweep k64_check lane_ab lb_sweep lds_ab pmc_64 pmc_imix pmc_lb round3_profile round_final round_profile split_sweep split_sweep2 spw_check tx_size_sweep tx_size_sweep2 uniform_size_sweep uniform_size_sweep2 wire_big_sweep wire_default_check wire_lb_small wire_mid_sweep wire_mtu_sweep wire_small_sweep"
   exit 0
 fi
 "$@"
