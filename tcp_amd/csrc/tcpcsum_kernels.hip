@@ -1412,6 +1412,25 @@ __device__ __forceinline__ void tx_edge_load(const TxPkt& p, int e, u32x4& A, u3
     if (p.sh != 0 && (uintptr_t)a + 16 < hi && (uintptr_t)a + 32 > lo) B = ld16(a + 16);   // rare: ragged ends only
 }
 
+// Source chunk idx + 1 for lane gl's load k of a round (lane gl loads chunk
+// base + k*G + gl): lane gl + 1's chunk of the same load, or for the group's
+// last lane lane 0's chunk of load k + 1 — lane 0 offers that one instead of
+// its own, which no lane of its group reads — or, after the round's last load,
+// the chunk the last lane read itself (bl). Every lane runs the bpermutes (no
+// divergence around them); unused when the packet needs no shift.
+template <int G, int C>
+__device__ __forceinline__ u32x4 tx_next_chunk(const u32x4 (&a)[C], int k, const u32x4 bl, int lane, int gl) {
+    if constexpr ((TCPCSUM_TX_KNOCKOUT & 4) != 0) return a[k];
+    const u32x4 x = (gl == 0 && k + 1 < C) ? a[k + 1 < C ? k + 1 : k] : a[k];
+    const uint32_t src = (uint32_t)(gl < G - 1 ? lane + 1 : lane - (G - 1));
+    u32x4 b;
+    b.x = bperm(x.x, src);
+    b.y = bperm(x.y, src);
+    b.z = bperm(x.z, src);
+    b.w = bperm(x.w, src);
+    return (gl == G - 1 && k == C - 1) ? bl : b;
+}
+
 // Phase 1 for a full chunk already loaded: shift into place, store, sum.
 template <bool NTS>
 __device__ __forceinline__ void tx_full_chunk(const TxPkt& p, uint32_t idx, const u32x4 A, const u32x4 B,
@@ -1432,18 +1451,32 @@ __device__ __forceinline__ void tx_full_chunk(const TxPkt& p, uint32_t idx, cons
     }
 }
 
-// Ragged end: byte-masked store and sum of chunk e.
+// Bytes [b0, b1) of the 16-byte chunk v to the 16-B aligned dc, in naturally
+// aligned power-of-two pieces: rising from b0 (1, 2, 4, 8 bytes while the
+// offset has that bit set), then falling (8, 4, 2, 1 while they fit) — at
+// most eight store instructions for any range, instead of one per byte.
+__device__ __forceinline__ void store_range16(uint8_t* dc, const u32x4 v, uint32_t b0, uint32_t b1) {
+    auto dw = [&](uint32_t i) { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; };
+    auto at = [&](uint32_t o) { return dw(o >> 2) >> (8u * (o & 3u)); };   // bytes from offset o (within its dword)
+    uint32_t x = b0;
+    if ((x & 1u) && x + 1u <= b1) { stg<uint8_t>(dc + x, (uint8_t)at(x)); x += 1u; }
+    if ((x & 2u) && x + 2u <= b1) { stg<uint16_t>(dc + x, (uint16_t)at(x)); x += 2u; }
+    if ((x & 4u) && x + 4u <= b1) { stg<uint32_t>(dc + x, dw(x >> 2)); x += 4u; }
+    if ((x & 8u) && x + 8u <= b1) { stg<uint64_t>(dc + x, (uint64_t)v.z | ((uint64_t)v.w << 32)); x += 8u; }
+    if (x + 8u <= b1) { stg<uint64_t>(dc + x, (uint64_t)v.x | ((uint64_t)v.y << 32)); x += 8u; }   // x == 0
+    if (x + 4u <= b1) { stg<uint32_t>(dc + x, dw(x >> 2)); x += 4u; }
+    if (x + 2u <= b1) { stg<uint16_t>(dc + x, (uint16_t)at(x)); x += 2u; }
+    if (x + 1u <= b1) stg<uint8_t>(dc + x, (uint8_t)at(x));
+}
+
+// Ragged end: the payload bytes of chunk e stored, and summed.
 __device__ __forceinline__ void tx_edge_chunk_store(const TxPkt& p, int e, const u32x4 A, const u32x4 B,
                                                     uint32_t& wsum, uint32_t& osum) {
     const u32x4 v = funnel16(A, B, (int)(p.sh >> 2), p.sh & 3u);
     const int64_t rel = (int64_t)e * 16 - (int64_t)p.dm;   // dest chunk start - first payload byte
     uint8_t* dc = p.dbase + (uint64_t)e * 16u;
-#pragma unroll
-    for (int b2 = 0; b2 < 16 && !(TCPCSUM_TX_KNOCKOUT & 1); ++b2) {
-        const uint32_t word = b2 < 4 ? v.x : b2 < 8 ? v.y : b2 < 12 ? v.z : v.w;
-        const int64_t pos = rel + b2;
-        if (pos >= 0 && pos < (int64_t)p.len) dc[b2] = (uint8_t)(word >> (8 * (b2 & 3)));
-    }
+    const int64_t lo = rel < 0 ? -rel : 0, hi = (int64_t)p.len - rel < 16 ? (int64_t)p.len - rel : 16;
+    if (!(TCPCSUM_TX_KNOCKOUT & 1) && lo < hi) store_range16(dc, v, (uint32_t)lo, (uint32_t)hi);
     chunk_wo_bytes(v, rel, (int64_t)p.len, p.odd, wsum, osum);
 }
 
@@ -1522,18 +1555,23 @@ __global__ __launch_bounds__(256) void k_tx_build(const uint8_t* __restrict__ pa
             const uint64_t i = t * SPT + (uint64_t)(u * GPW + q0);
             tx_decode(p[u], rn[u], i < n, payload, outp);
         }
-        u32x4 A[U][C], B[U][C], EA[U], EB[U];
+        // Source chunk idx + 1 (the upper half of a shifted destination chunk) is
+        // the next lane's chunk idx' = idx + 1 of the same load: it comes over
+        // from that lane (ds_bpermute), not from a second load of the same bytes —
+        // the group's last lane takes lane 0's chunk of the next load, and only at
+        // the round's last load does it read one chunk itself (Bl).
+        u32x4 A[U][C], Bl[U], EA[U], EB[U];
         int e[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
 #pragma unroll
-            for (int k = 0; k < C; ++k) {   // every source byte under a full chunk is payload
+            for (int k = 0; k < C; ++k) {   // full chunks, and chunk f1 when the last one needs it
                 const uint32_t idx = p[u].f0 + (uint32_t)(k * G + gl);
-                const uint8_t* a = p[u].sbase + (uint64_t)idx * 16u;
-                A[u][k] = ld16(zsel(idx < p[u].f1, a));
-                if constexpr ((TCPCSUM_TX_KNOCKOUT & 4) != 0) B[u][k] = A[u][k];
-                else B[u][k] = ld16(zsel(idx < p[u].f1 && p[u].sh, a + 16));
+                const bool need = idx < p[u].f1 || (idx == p[u].f1 && p[u].sh && p[u].f1 > p[u].f0);
+                A[u][k] = ld16(zsel(need, p[u].sbase + (uint64_t)idx * 16u));
             }
+            const uint32_t il = p[u].f0 + (uint32_t)((C - 1) * G + gl);
+            Bl[u] = ld16(zsel(gl == G - 1 && il < p[u].f1 && p[u].sh, p[u].sbase + (uint64_t)il * 16u + 16u));
             e[u] = tx_edge_chunk(p[u], gl);
             tx_edge_load(p[u], e[u], EA[u], EB[u]);
         }
@@ -1546,24 +1584,27 @@ __global__ __launch_bounds__(256) void k_tx_build(const uint8_t* __restrict__ pa
 #pragma unroll
             for (int k = 0; k < C; ++k) {
                 const uint32_t idx = p[u].f0 + (uint32_t)(k * G + gl);
-                if (idx < p[u].f1) tx_full_chunk<NTS>(p[u], idx, A[u][k], B[u][k], wsum, osum);
+                const u32x4 B = tx_next_chunk<G, C>(A[u], k, Bl[u], lane, gl);
+                if (idx < p[u].f1) tx_full_chunk<NTS>(p[u], idx, A[u][k], B, wsum, osum);
             }
             uint64_t W = wsum, O = osum;
             // long payloads: further rounds of G*C full chunks
             for (uint32_t rr = p[u].f0 + (uint32_t)(G * C); rr < p[u].f1; rr += (uint32_t)(G * C)) {
-                u32x4 a2[C], b2[C];
+                u32x4 a2[C];
 #pragma unroll
                 for (int k = 0; k < C; ++k) {
                     const uint32_t idx = rr + (uint32_t)(k * G + gl);
-                    const uint8_t* a = p[u].sbase + (uint64_t)idx * 16u;
-                    a2[k] = idx < p[u].f1 ? ld16(a) : u32x4{0u, 0u, 0u, 0u};
-                    b2[k] = (idx < p[u].f1 && p[u].sh) ? ld16(a + 16) : u32x4{0u, 0u, 0u, 0u};
+                    const bool need = idx < p[u].f1 || (idx == p[u].f1 && p[u].sh);
+                    a2[k] = ld16(zsel(need, p[u].sbase + (uint64_t)idx * 16u));
                 }
+                const uint32_t il = rr + (uint32_t)((C - 1) * G + gl);
+                const u32x4 bl = ld16(zsel(gl == G - 1 && il < p[u].f1 && p[u].sh, p[u].sbase + (uint64_t)il * 16u + 16u));
                 uint32_t ws = 0, os = 0;
 #pragma unroll
                 for (int k = 0; k < C; ++k) {
                     const uint32_t idx = rr + (uint32_t)(k * G + gl);
-                    if (idx < p[u].f1) tx_full_chunk<NTS>(p[u], idx, a2[k], b2[k], ws, os);
+                    const u32x4 B = tx_next_chunk<G, C>(a2, k, bl, lane, gl);
+                    if (idx < p[u].f1) tx_full_chunk<NTS>(p[u], idx, a2[k], B, ws, os);
                 }
                 W += ws;
                 O += os;

@@ -475,6 +475,8 @@ tx_ab() {
 (
   O=gpurun_out/txab
   mkdir -p $O
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "tx_build" --timeout 120 --timeout-method thread > $O/t.log 2>&1 || { tail -15 $O/t.log; exit 1; }
+  tail -1 $O/t.log
   timeout -k 10 300 python3 tools/tx_ab.py > $O/ab.jsonl 2> $O/ab.err || { tail $O/ab.err; exit 1; }
   cat $O/ab.jsonl
 )
