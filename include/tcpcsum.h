@@ -369,6 +369,7 @@ int tcpcsum_plan_uniform(uint64_t base, uint64_t stride, uint32_t len, uint64_t 
 /* wire FILL: always the 2-byte store (default: where the 128-B line holding the check lies
  * inside the packet, the whole line is written back through, the check patched in) */
 #define TCPCSUM_TUNE_FILL_U16 512
+#define TCPCSUM_TUNE_TX_WT_STORE 1024  /* builder: payload stores written through (sc0 sc1) */
 /* 0 if *tune is a valid tuning (NULL counts as valid), else TCPCSUM_EINVAL. */
 int tcpcsum_tuning_check(const tcpcsum_tuning_t *tune);
 

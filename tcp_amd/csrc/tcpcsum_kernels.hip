@@ -1432,14 +1432,19 @@ __device__ __forceinline__ u32x4 tx_next_chunk(const u32x4 (&a)[C], int k, const
 }
 
 // Phase 1 for a full chunk already loaded: shift into place, store, sum.
-template <bool NTS>
+// SP: store policy — 0 default (write-back in L2), 1 non-temporal, 2 written
+// through (sc0 sc1; inline asm, so the s_nop gives the store its data wait
+// states before the compiler reuses the VGPRs — see k_ipv4's line store).
+template <int SP>
 __device__ __forceinline__ void tx_full_chunk(const TxPkt& p, uint32_t idx, const u32x4 A, const u32x4 B,
                                               uint32_t& wsum, uint32_t& osum) {
     const u32x4 v = funnel16(A, B, (int)(p.sh >> 2), p.sh & 3u);
     u32x4* d = reinterpret_cast<u32x4*>(p.dbase + (uint64_t)idx * 16u);
     if constexpr ((TCPCSUM_TX_KNOCKOUT & 8) != 0) {
-    } else if constexpr (NTS) {
+    } else if constexpr (SP == 1) {
         __builtin_nontemporal_store(v, d);
+    } else if constexpr (SP == 2) {
+        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 3" ::"v"(d), "v"(v) : "memory");
     } else {
         *d = v;
     }
@@ -1533,7 +1538,7 @@ __device__ __forceinline__ void tx_header(const TxPkt& p, uint64_t Spay, int mod
 // descriptor loads, then all payload loads (bulk chunks and both ragged ends)
 // of the tile are issued before any is consumed. Payloads with more full
 // chunks than G*C take extra (un-overlapped) rounds.
-template <int G, int C, int U, bool NTS>
+template <int G, int C, int U, int SP>
 __global__ __launch_bounds__(256) void k_tx_build(const uint8_t* __restrict__ payload,
                                                   const tcpcsum_txseg_t* __restrict__ segs, uint64_t n,
                                                   uint8_t* __restrict__ outp, int mode,
@@ -1585,7 +1590,7 @@ __global__ __launch_bounds__(256) void k_tx_build(const uint8_t* __restrict__ pa
             for (int k = 0; k < C; ++k) {
                 const uint32_t idx = p[u].f0 + (uint32_t)(k * G + gl);
                 const u32x4 B = tx_next_chunk<G, C>(A[u], k, Bl[u], lane, gl);
-                if (idx < p[u].f1) tx_full_chunk<NTS>(p[u], idx, A[u][k], B, wsum, osum);
+                if (idx < p[u].f1) tx_full_chunk<SP>(p[u], idx, A[u][k], B, wsum, osum);
             }
             uint64_t W = wsum, O = osum;
             // long payloads: further rounds of G*C full chunks
@@ -1604,7 +1609,7 @@ __global__ __launch_bounds__(256) void k_tx_build(const uint8_t* __restrict__ pa
                 for (int k = 0; k < C; ++k) {
                     const uint32_t idx = rr + (uint32_t)(k * G + gl);
                     const u32x4 B = tx_next_chunk<G, C>(a2, k, bl, lane, gl);
-                    if (idx < p[u].f1) tx_full_chunk<NTS>(p[u], idx, a2[k], B, ws, os);
+                    if (idx < p[u].f1) tx_full_chunk<SP>(p[u], idx, a2[k], B, ws, os);
                 }
                 W += ws;
                 O += os;
@@ -2206,13 +2211,15 @@ void launch_ipv4(uint8_t* pkts, const uint64_t* off, const uint32_t* plen, uint6
 
 template <int G, int C, int U>
 static void launch_tx_t(const uint8_t* payload, const tcpcsum_txseg_t* segs, uint64_t n, uint8_t* outp, int mode,
-                        uint16_t* checks, hipStream_t s, int max_blocks, bool nts) {
+                        uint16_t* checks, hipStream_t s, int max_blocks, int sp) {
     constexpr int SPT = (64 / G) * U;
     const dim3 grid(grid_for((n + SPT - 1) / SPT, max_blocks));
-    if (nts)
-        hipLaunchKernelGGL((k_tx_build<G, C, U, true>), grid, dim3(256), 0, s, payload, segs, n, outp, mode, checks);
+    if (sp == 1)
+        hipLaunchKernelGGL((k_tx_build<G, C, U, 1>), grid, dim3(256), 0, s, payload, segs, n, outp, mode, checks);
+    else if (sp == 2)
+        hipLaunchKernelGGL((k_tx_build<G, C, U, 2>), grid, dim3(256), 0, s, payload, segs, n, outp, mode, checks);
     else
-        hipLaunchKernelGGL((k_tx_build<G, C, U, false>), grid, dim3(256), 0, s, payload, segs, n, outp, mode, checks);
+        hipLaunchKernelGGL((k_tx_build<G, C, U, 0>), grid, dim3(256), 0, s, payload, segs, n, outp, mode, checks);
 }
 
 void launch_tx_build(const uint8_t* payload, const tcpcsum_txseg_t* segs, uint64_t n, uint32_t max_len,
@@ -2221,12 +2228,12 @@ void launch_tx_build(const uint8_t* payload, const tcpcsum_txseg_t* segs, uint64
     const int max_blocks = tu.max_blocks > 0 ? tu.max_blocks : 32768;
     const int unroll = tu.unroll ? tu.unroll : 1;
     const uint64_t nfull = ((uint64_t)max_len + 15u) >> 4;   // full chunks a payload can have
-    const bool nts = (tu.flags & TCPCSUM_TUNE_TX_NT_STORE) != 0;
+    const int sp = (tu.flags & TCPCSUM_TUNE_TX_WT_STORE) ? 2 : (tu.flags & TCPCSUM_TUNE_TX_NT_STORE) ? 1 : 0;
 #define TX_U(G, C)                                                                         \
     do {                                                                                   \
-        if (unroll <= 1) launch_tx_t<G, C, 1>(payload, segs, n, outp, mode, checks, s, max_blocks, nts); \
-        else if (unroll == 2) launch_tx_t<G, C, 2>(payload, segs, n, outp, mode, checks, s, max_blocks, nts); \
-        else launch_tx_t<G, C, 4>(payload, segs, n, outp, mode, checks, s, max_blocks, nts);    \
+        if (unroll <= 1) launch_tx_t<G, C, 1>(payload, segs, n, outp, mode, checks, s, max_blocks, sp); \
+        else if (unroll == 2) launch_tx_t<G, C, 2>(payload, segs, n, outp, mode, checks, s, max_blocks, sp); \
+        else launch_tx_t<G, C, 4>(payload, segs, n, outp, mode, checks, s, max_blocks, sp);    \
     } while (0)
     // payloads of 129 B .. 1.25 KiB: 16-lane groups, two chunks per lane per round
     // (256 B 1.76 -> 1.05 ms, 536 B 1.40 -> 1.07, 1024 B 0.92 -> 0.82, 1200 B -1 %;

@@ -431,8 +431,9 @@ def test_tx_build_vs_oracle(dev, layout):
     dpay, dseg = to_dev(payload, dev), to_dev(segs.view(np.uint8), dev)
     try:
         for shape, unroll, hint, fl in ((-1, 0, 16, 0), (0, 2, max_len, 0), (1, 4, max_len, 0), (3, 1, max_len, 0),
-                                        (4, 2, 64, 0), (-1, 0, max_len, 128), (2, 2, max_len, 128)):
-            tcp_amd.set_tuning(0, unroll, shape, fl)   # 128: non-temporal payload stores
+                                        (4, 2, 64, 0), (-1, 0, max_len, 128), (2, 2, max_len, 128), (-1, 0, max_len, 1024),
+                                        (1, 2, max_len, 1024)):
+            tcp_amd.set_tuning(0, unroll, shape, fl)   # 128 / 1024: non-temporal / written-through stores
             dout = to_dev(garbage, dev)
             tcp_amd.tx_build(dpay, dseg, n, hint, dout, 0, None)
             assert np.array_equal(host(dout), want), (shape, unroll, hint, fl)

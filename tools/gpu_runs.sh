@@ -482,8 +482,22 @@ tx_ab() {
 )
 }
 
+# Segment builder after a kernel change: its parity tests, txbench (store policies), and a
+# launch-shape sweep of the default shape
+tx_check() {
+(
+  O=gpurun_out/txcheck
+  mkdir -p $O
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "tx_build" --timeout 120 --timeout-method thread > $O/t.log 2>&1 || { tail -15 $O/t.log; exit 1; }
+  tail -1 $O/t.log
+  timeout -k 10 200 python3 tools/txbench.py > $O/txbench.jsonl 2> $O/txbench.err || { tail $O/txbench.err; exit 1; }
+  TX_SHAPES=2 TX_BLOCKS=16384,32768,65536,131072 TX_UNROLLS=1,2 timeout -k 10 300 python3 tools/txbench.py --sweep > $O/sweep.jsonl 2> $O/sweep.err || { tail $O/sweep.err; exit 1; }
+  grep -v sweep $O/txbench.jsonl
+)
+}
+
 if [ $# -eq 0 ]; then
-  echo "experiments: tx_ab tx_grid_sweep copy_ceiling round3_final hostpath_check gpu_r3_fill gpu_r3_n8 gpu_round3 grid_check grid_long grid_m1 grid_sweep k64_check lane_ab lb_sweep lds_ab pmc_64 pmc_imix pmc_lb round3_profile round_final round_profile split_sweep split_sweep2 spw_check tx_size_sweep tx_size_sweep2 uniform_size_sweep uniform_size_sweep2 wire_big_sweep wire_default_check wire_lb_small wire_mid_sweep wire_mtu_sweep wire_small_sweep"
+  echo "experiments: tx_check tx_ab tx_grid_sweep copy_ceiling round3_final hostpath_check gpu_r3_fill gpu_r3_n8 gpu_round3 grid_check grid_long grid_m1 grid_sweep k64_check lane_ab lb_sweep lds_ab pmc_64 pmc_imix pmc_lb round3_profile round_final round_profile split_sweep split_sweep2 spw_check tx_size_sweep tx_size_sweep2 uniform_size_sweep uniform_size_sweep2 wire_big_sweep wire_default_check wire_lb_small wire_mid_sweep wire_mtu_sweep wire_small_sweep"
   exit 0
 fi
 "$@"

@@ -69,7 +69,7 @@ def main():
         tcp_amd.set_tuning(0, 0, -1, 0)
     # store policy: default vs non-temporal payload stores, interleaved rounds
     moved = n * L + n * (L + 44) + n * 48
-    pol = {0: [], 128: []}
+    pol = {0: [], 128: [], 1024: []}
     for _ in range(5):
         for fl in pol:
             tcp_amd.set_tuning(0, 0, -1, fl)
@@ -77,7 +77,7 @@ def main():
     tcp_amd.set_tuning(0, 0, -1, 0)
     for fl, ts in pol.items():
         ts.sort()
-        print(json.dumps({"measure": "tx_build_store_policy", "flags": fl, "nt_stores": fl == 128,
+        print(json.dumps({"measure": "tx_build_store_policy", "flags": fl, "stores": {0: "default", 128: "nt", 1024: "write-through"}[fl],
                           "ms_median": round(ts[2] * 1e3, 4), "ms_min": round(ts[0] * 1e3, 4),
                           "GB/s_read+write": round(moved / ts[2] / 1e9, 1)}), flush=True)
     t = timeit(lambda: tcp_amd.tx_build(payload, dsegs, n, L, out, 0, chk))
