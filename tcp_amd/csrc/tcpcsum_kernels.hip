@@ -2240,12 +2240,14 @@ void launch_tx_build(const uint8_t* payload, const tcpcsum_txseg_t* segs, uint64
     // 1456 B keeps (32,3): 0.778 vs 0.839; tools/tx_size_sweep*.sh,
     // profiles/r02_tx_size_sweep.jsonl)
     int shape = nfull <= 8 ? 0 : nfull <= 80 ? 1 : nfull <= 96 ? 2 : 4;
-    if (tu.shape >= 0 && tu.shape <= 4) shape = tu.shape;   // any shape is correct (extra rounds)
+    if (tu.shape >= 0 && tu.shape <= 6) shape = tu.shape;   // any shape is correct (extra rounds)
     switch (shape) {
         case 0: TX_U(8, 1); break;
         case 1: TX_U(16, 2); break;
         case 2: TX_U(32, 3); break;
         case 3: TX_U(64, 2); break;
+        case 5: TX_U(16, 6); break;
+        case 6: TX_U(8, 12); break;
         default: TX_U(64, 4);
     }
 #undef TX_U

@@ -432,7 +432,7 @@ def test_tx_build_vs_oracle(dev, layout):
     try:
         for shape, unroll, hint, fl in ((-1, 0, 16, 0), (0, 2, max_len, 0), (1, 4, max_len, 0), (3, 1, max_len, 0),
                                         (4, 2, 64, 0), (-1, 0, max_len, 128), (2, 2, max_len, 128), (-1, 0, max_len, 1024),
-                                        (1, 2, max_len, 1024)):
+                                        (1, 2, max_len, 1024), (5, 1, max_len, 0), (6, 1, max_len, 0), (6, 2, 64, 0)):
             tcp_amd.set_tuning(0, unroll, shape, fl)   # 128 / 1024: non-temporal / written-through stores
             dout = to_dev(garbage, dev)
             tcp_amd.tx_build(dpay, dseg, n, hint, dout, 0, None)

@@ -491,7 +491,7 @@ tx_check() {
   timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "tx_build" --timeout 120 --timeout-method thread > $O/t.log 2>&1 || { tail -15 $O/t.log; exit 1; }
   tail -1 $O/t.log
   timeout -k 10 200 python3 tools/txbench.py > $O/txbench.jsonl 2> $O/txbench.err || { tail $O/txbench.err; exit 1; }
-  TX_SHAPES=2 TX_BLOCKS=16384,32768,65536,131072 TX_UNROLLS=1,2 timeout -k 10 300 python3 tools/txbench.py --sweep > $O/sweep.jsonl 2> $O/sweep.err || { tail $O/sweep.err; exit 1; }
+  TX_SHAPES=${TX_SHAPES:-2} TX_BLOCKS=${TX_BLOCKS:-16384,32768,65536,131072} TX_UNROLLS=${TX_UNROLLS:-1,2} timeout -k 10 300 python3 tools/txbench.py --sweep > $O/sweep.jsonl 2> $O/sweep.err || { tail $O/sweep.err; exit 1; }
   grep -v sweep $O/txbench.jsonl
 )
 }
