@@ -2235,11 +2235,13 @@ void launch_tx_build(const uint8_t* payload, const tcpcsum_txseg_t* segs, uint64
         else if (unroll == 2) launch_tx_t<G, C, 2>(payload, segs, n, outp, mode, checks, s, max_blocks, sp); \
         else launch_tx_t<G, C, 4>(payload, segs, n, outp, mode, checks, s, max_blocks, sp);    \
     } while (0)
-    // payloads of 129 B .. 1.25 KiB: 16-lane groups, two chunks per lane per round
-    // (256 B 1.76 -> 1.05 ms, 536 B 1.40 -> 1.07, 1024 B 0.92 -> 0.82, 1200 B -1 %;
-    // 1456 B keeps (32,3): 0.778 vs 0.839; tools/tx_size_sweep*.sh,
-    // profiles/r02_tx_size_sweep.jsonl)
-    int shape = nfull <= 8 ? 0 : nfull <= 80 ? 1 : nfull <= 96 ? 2 : 4;
+    // payloads of 129 B .. 768 B: 16-lane groups, two chunks per lane per round
+    // (round 2: 256 B 1.76 -> 1.05 ms, 536 B 1.40 -> 1.07; profiles/r02_tx_size_sweep.jsonl);
+    // 769 B .. 1.5 KiB: 16-lane groups, six chunks per lane, one round (round 3, after
+    // the lane-exchange change, 1.5 GB of payload per launch: 896 B 0.734 -> 0.698 ms,
+    // 1024 B 0.719 -> 0.638, 1200 B 0.795 -> 0.644, 1456 B 0.624 -> 0.611 against the
+    // previous (16,2) / (32,3); profiles/r03_tx_size_ab.jsonl); longer: (64,4)
+    int shape = nfull <= 8 ? 0 : nfull <= 48 ? 1 : nfull <= 96 ? 5 : 4;
     if (tu.shape >= 0 && tu.shape <= 6) shape = tu.shape;   // any shape is correct (extra rounds)
     switch (shape) {
         case 0: TX_U(8, 1); break;

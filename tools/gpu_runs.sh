@@ -496,8 +496,20 @@ tx_check() {
 )
 }
 
+# Builder shapes by payload size, interleaved (tools/txbench.py --sweep per TX_LEN)
+tx_size_ab() {
+(
+  O=gpurun_out/txsize
+  mkdir -p $O
+  for L in ${TX_LENS:-256 536 1024 1200 1456 4000 9000}; do
+    TX_LEN=$L TX_SHAPES=${TX_SHAPES:-1,2,4,5,1,2,4,5} TX_BLOCKS=32768 TX_UNROLLS=1 timeout -k 10 200 python3 tools/txbench.py --sweep > $O/len$L.jsonl 2> $O/err || { tail $O/err; exit 1; }
+  done
+  echo txsize ok
+)
+}
+
 if [ $# -eq 0 ]; then
-  echo "experiments: tx_check tx_ab tx_grid_sweep copy_ceiling round3_final hostpath_check gpu_r3_fill gpu_r3_n8 gpu_round3 grid_check grid_long grid_m1 grid_sweep k64_check lane_ab lb_sweep lds_ab pmc_64 pmc_imix pmc_lb round3_profile round_final round_profile split_sweep split_sweep2 spw_check tx_size_sweep tx_size_sweep2 uniform_size_sweep uniform_size_sweep2 wire_big_sweep wire_default_check wire_lb_small wire_mid_sweep wire_mtu_sweep wire_small_sweep"
+  echo "experiments: tx_size_ab tx_check tx_ab tx_grid_sweep copy_ceiling round3_final hostpath_check gpu_r3_fill gpu_r3_n8 gpu_round3 grid_check grid_long grid_m1 grid_sweep k64_check lane_ab lb_sweep lds_ab pmc_64 pmc_imix pmc_lb round3_profile round_final round_profile split_sweep split_sweep2 spw_check tx_size_sweep tx_size_sweep2 uniform_size_sweep uniform_size_sweep2 wire_big_sweep wire_default_check wire_lb_small wire_mid_sweep wire_mtu_sweep wire_small_sweep"
   exit 0
 fi
 "$@"
