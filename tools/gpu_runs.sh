@@ -508,8 +508,20 @@ tx_size_ab() {
 )
 }
 
+# Wire kernel A/B against tcp_amd/ab/libtcpcsum_wire*.so, after its GPU tests
+wire_ab() {
+(
+  O=gpurun_out/wireab
+  mkdir -p $O
+  timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fuzz.py tests/test_plumbing.py tests/test_gpu_ptrs.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/t.log 2>&1 || { tail -15 $O/t.log; exit 1; }
+  tail -1 $O/t.log
+  timeout -k 10 400 python3 tools/wire_lib_ab.py > $O/ab.jsonl 2> $O/ab.err || { tail $O/ab.err; exit 1; }
+  cat $O/ab.jsonl
+)
+}
+
 if [ $# -eq 0 ]; then
-  echo "experiments: tx_size_ab tx_check tx_ab tx_grid_sweep copy_ceiling round3_final hostpath_check gpu_r3_fill gpu_r3_n8 gpu_round3 grid_check grid_long grid_m1 grid_sweep k64_check lane_ab lb_sweep lds_ab pmc_64 pmc_imix pmc_lb round3_profile round_final round_profile split_sweep split_sweep2 spw_check tx_size_sweep tx_size_sweep2 uniform_size_sweep uniform_size_sweep2 wire_big_sweep wire_default_check wire_lb_small wire_mid_sweep wire_mtu_sweep wire_small_sweep"
+  echo "experiments: wire_ab tx_size_ab tx_check tx_ab tx_grid_sweep copy_ceiling round3_final hostpath_check gpu_r3_fill gpu_r3_n8 gpu_round3 grid_check grid_long grid_m1 grid_sweep k64_check lane_ab lb_sweep lds_ab pmc_64 pmc_imix pmc_lb round3_profile round_final round_profile split_sweep split_sweep2 spw_check tx_size_sweep tx_size_sweep2 uniform_size_sweep uniform_size_sweep2 wire_big_sweep wire_default_check wire_lb_small wire_mid_sweep wire_mtu_sweep wire_small_sweep"
   exit 0
 fi
 "$@"
