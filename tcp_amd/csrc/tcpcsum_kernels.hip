@@ -44,6 +44,11 @@
 #ifndef TCPCSUM_TX_KNOCKOUT
 #define TCPCSUM_TX_KNOCKOUT 0
 #endif
+// Measurement builds only: minimum waves per SIMD asked of the lane-group wire
+// kernel (its register budget); 1 = the compiler's choice, as in every product build.
+#ifndef TCPCSUM_WIRE_WAVES
+#define TCPCSUM_WIRE_WAVES 1
+#endif
 
 namespace tcpcsum {
 
@@ -946,7 +951,7 @@ struct IpDone {
 // off[i] = the packet's address, limit = ~0). A packet never reads past
 // min(limit - off[i], plen[i]).
 template <int G, int C, int U, bool NT, bool PL>
-__global__ __launch_bounds__(256) void k_ipv4(uint8_t* __restrict__ pkts, const uint64_t* __restrict__ off,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TCPCSUM_WIRE_WAVES, 8))) void k_ipv4(uint8_t* __restrict__ pkts, const uint64_t* __restrict__ off,
                                               const uint32_t* __restrict__ plen,
                                               uint64_t n, uint32_t cap, uint64_t limit, int mode,
                                               uint16_t* __restrict__ out, uint8_t* __restrict__ status,
