@@ -49,6 +49,9 @@
 #ifndef TCPCSUM_WIRE_WAVES
 #define TCPCSUM_WIRE_WAVES 1
 #endif
+#ifndef TCPCSUM_TX_WAVES   // the same for the segment builder
+#define TCPCSUM_TX_WAVES 1
+#endif
 
 namespace tcpcsum {
 
@@ -1544,7 +1547,7 @@ __device__ __forceinline__ void tx_header(const TxPkt& p, uint64_t Spay, int mod
 // of the tile are issued before any is consumed. Payloads with more full
 // chunks than G*C take extra (un-overlapped) rounds.
 template <int G, int C, int U, int SP>
-__global__ __launch_bounds__(256) void k_tx_build(const uint8_t* __restrict__ payload,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TCPCSUM_TX_WAVES, 8))) void k_tx_build(const uint8_t* __restrict__ payload,
                                                   const tcpcsum_txseg_t* __restrict__ segs, uint64_t n,
                                                   uint8_t* __restrict__ outp, int mode,
                                                   uint16_t* __restrict__ checks) {

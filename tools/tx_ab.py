@@ -57,7 +57,8 @@ def main():
         lib.tcpcsum_tx_build_dev.argtypes = [vp, vp, u64, u32, vp, ctypes.c_int, vp, vp, vp]
         lib.tcpcsum_tx_build_dev.restype = ctypes.c_int
         libs[os.path.basename(p).replace("libtcpcsum_", "").replace(".so", "")] = lib
-    L, n = 1456, 1 << 20
+    L = int(os.environ.get("TX_LEN", "1456"))
+    n = 1 << 20 if L == 1456 else max(1 << 16, min(1 << 22, (3 << 29) // max(L + 44, 1)))
     dev = torch.device("cuda:0")
     payload = torch.empty(n * L, dtype=torch.uint8, device=dev)
     tcp_amd.synth_fill(payload, 0, n * L)
