@@ -4,7 +4,7 @@
 // time memcpy of a 1.5 MB pageable source (first touched on that CPU) into (a) pinned
 // memory from hipHostMalloc and (b) pageable memory first touched on that CPU. Also prints
 // the GPU's NUMA node (sysfs, by PCI bus id). JSON lines.
-//   hipcc -O2 -o tools/numa_copy_probe tools/numa_copy_probe.cpp
+//   hipcc -O2 --offload-arch=gfx950 -o tools/numa_copy_probe tools/numa_copy_probe.cpp
 #include <hip/hip_runtime.h>
 #include <sched.h>
 
@@ -87,7 +87,7 @@ int main() {
         std::printf("{\"node\": %d, \"cpu\": %d, \"us_best_into_pinned\": %.1f, \"us_best_into_pageable\": %.1f}\n",
                     node, cpu, t_pin, t_pg);
         std::fflush(stdout);
-        hipHostFree(pin);
+        (void)hipHostFree(pin);
     }
     return 0;
 }
