@@ -389,7 +389,16 @@ int tcpcsum_ctx_create(int device, size_t scratch_bytes, tcpcsum_ctx_t** out) {
     c->chunk = scratch_bytes ? scratch_bytes : kDefaultChunk;
     // copy threads spin TCPCSUM_HOST_SPIN_US (default 50) after a job before they sleep
     const uint64_t spin_ns = (uint64_t)std::max(0, tcpcsum::env_int("TCPCSUM_HOST_SPIN_US", 50)) * 1000u;
-    c->pool.reset(new (std::nothrow) tcpcsum::CopyPool(tcpcsum::default_copy_threads() - 1, spin_ns));
+    // copy threads on the GPU's NUMA node, where hipHostMalloc put the staging
+    // (TCPCSUM_HOST_NUMA=0: wherever the scheduler puts them)
+    cpu_set_t node_cpus;
+    char bus[64] = {0};
+    const bool numa = tcpcsum::env_int("TCPCSUM_HOST_NUMA", 1) != 0 &&
+                      hipDeviceGetPCIBusId(bus, sizeof bus, device) == hipSuccess &&
+                      tcpcsum::numa_node_cpus(bus, &node_cpus);
+    (void)hipGetLastError();
+    c->pool.reset(new (std::nothrow)
+                      tcpcsum::CopyPool(tcpcsum::default_copy_threads() - 1, spin_ns, numa ? &node_cpus : nullptr));
     if (!c->pool) {
         delete c;
         return TCPCSUM_ENOMEM;

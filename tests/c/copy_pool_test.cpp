@@ -67,6 +67,14 @@ int main() {
         tcpcsum::CopyPool serial(0, 0);   // caller only
         exactly_once(serial, 1000, 7);
     }
+    {   // workers pinned to a CPU set (the GPU's NUMA node on the box): the allowed set here
+        cpu_set_t cpus;
+        EXPECT(sched_getaffinity(0, sizeof cpus, &cpus) == 0);
+        tcpcsum::CopyPool pinned(3, 1000, &cpus);
+        for (int rep = 0; rep < 10; ++rep) exactly_once(pinned, 10000, 16);
+        cpu_set_t none;
+        EXPECT(!tcpcsum::numa_node_cpus("no-such-bus", &none));   // no device: no pinning
+    }
     std::printf(fails ? "copy_pool_test: %d failures\n" : "copy_pool_test: OK\n", fails);
     return fails ? 1 : 0;
 }

@@ -520,8 +520,22 @@ wire_ab() {
 )
 }
 
+# Copy threads on the GPU's NUMA node or anywhere: host-path tests, sweep (numa 0/1), e2e
+numa_check() {
+(
+  O=gpurun_out/numa
+  mkdir -p $O
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_ptrs.py tests/test_plumbing.py tests/test_seam.py tests/test_gpu_hostpath.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/t.log 2>&1 || { tail -15 $O/t.log; exit 1; }
+  tail -1 $O/t.log
+  timeout -k 10 400 python3 tools/hostpath_sweep.py --rounds 3 > $O/sweep.jsonl 2> $O/sweep.err || { tail $O/sweep.err; exit 1; }
+  TCPCSUM_HOST_NUMA=0 timeout -k 10 200 python3 tools/e2e.py > $O/e2e_numa0.jsonl 2> $O/e2e0.err || { tail $O/e2e0.err; exit 1; }
+  timeout -k 10 200 python3 tools/e2e.py > $O/e2e_numa1.jsonl 2> $O/e2e1.err || { tail $O/e2e1.err; exit 1; }
+  echo numa ok
+)
+}
+
 if [ $# -eq 0 ]; then
-  echo "experiments: wire_ab tx_size_ab tx_check tx_ab tx_grid_sweep copy_ceiling round3_final hostpath_check gpu_r3_fill gpu_r3_n8 gpu_round3 grid_check grid_long grid_m1 grid_sweep k64_check lane_ab lb_sweep lds_ab pmc_64 pmc_imix pmc_lb round3_profile round_final round_profile split_sweep split_sweep2 spw_check tx_size_sweep tx_size_sweep2 uniform_size_sweep uniform_size_sweep2 wire_big_sweep wire_default_check wire_lb_small wire_mid_sweep wire_mtu_sweep wire_small_sweep"
+  echo "experiments: numa_check wire_ab tx_size_ab tx_check tx_ab tx_grid_sweep copy_ceiling round3_final hostpath_check gpu_r3_fill gpu_r3_n8 gpu_round3 grid_check grid_long grid_m1 grid_sweep k64_check lane_ab lb_sweep lds_ab pmc_64 pmc_imix pmc_lb round3_profile round_final round_profile split_sweep split_sweep2 spw_check tx_size_sweep tx_size_sweep2 uniform_size_sweep uniform_size_sweep2 wire_big_sweep wire_default_check wire_lb_small wire_mid_sweep wire_mtu_sweep wire_small_sweep"
   exit 0
 fi
 "$@"

@@ -6,7 +6,8 @@ context's copy knobs, read at tcpcsum_ctx_create:
   TCPCSUM_HOST_DMA           uniform chunks: DMA to HBM then the kernel (0: kernel reads staging over PCIe)
   TCPCSUM_HOST_SPIN_US       how long an idle copy thread spins before it sleeps
   TCPCSUM_HOST_STAGE_PASSES  wire staging: 1 = laid out by bounds, one pass; 2 = lengths first, packed
---configs: threads:nt:dma[:spin_us[:passes]],...
+  TCPCSUM_HOST_NUMA          copy threads on the GPU's NUMA node (0: anywhere)
+--configs: threads:nt:dma[:spin_us[:passes[:numa]]],...
 Wire packets are staged on the copy threads (header reads, copies and the FILL
 write-back) and checksummed by one launch.
 Measures tcpcsum_batch_uniform_host over 1M x 1500 B pageable, and one
@@ -40,7 +41,8 @@ def timed(fn, reps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=2)
-    ap.add_argument("--configs", default="8:1:1:50:1,8:1:1:50:2,4:1:1:50:1,2:1:1:50:1,1:1:1:50:1")
+    ap.add_argument("--configs", default="8:1:1:50:1:0,8:1:1:50:1:1,4:1:1:50:1:0,4:1:1:50:1:1")
+    ap.add_argument("--wire-only", action="store_true")
     args = ap.parse_args()
     import numpy as np
     import tcp_amd
@@ -64,7 +66,7 @@ def main():
         bufs.append(b)
     ptrs = np.array([b.ctypes.data for b in bufs[1::2]], np.uint64)   # arrays, not lists: no per-call conversion
     lens = np.full(1024, 1500, np.uint32)
-    defaults = [8, 1, 1, 50, 1]
+    defaults = [8, 1, 1, 50, 1, 1]
     configs = []
     for c in args.configs.split(","):
         v = [int(x) for x in c.split(":")]
@@ -82,26 +84,32 @@ def main():
                           "us_best": round(tmin * 1e6, 1), "GB/s_median": round(src.size / tmed / 1e9, 2)}),
               flush=True)
     for rnd in range(args.rounds):
-        for th, nt, dma, spin, passes in configs:
+        for th, nt, dma, spin, passes, numa in configs:
             os.environ["TCPCSUM_HOST_THREADS"] = str(th)
             os.environ["TCPCSUM_HOST_NT"] = str(nt)
             os.environ["TCPCSUM_HOST_DMA"] = str(dma)
             os.environ["TCPCSUM_HOST_SPIN_US"] = str(spin)
             os.environ["TCPCSUM_HOST_STAGE_PASSES"] = str(passes)
+            os.environ["TCPCSUM_HOST_NUMA"] = str(numa)
             with tcp_amd.HostContext(0) as ctx:
-                got = ctx.batch_uniform(big, L, L, n, ss)
-                if want is None:
-                    want = got
-                assert np.array_equal(got, want)
-                s0 = ctx.stats()
-                tmin, tmed = timed(lambda: ctx.batch_uniform(big, L, L, n, ss), 5)
-                s1 = ctx.stats()
-                cfg = {"threads": th, "nt": nt, "dma": dma, "spin_us": spin, "passes": passes, "round": rnd}
-                print(json.dumps({**cfg, "measure": "uniform_host_1Mx1500_pageable",
-                                  "GiB/s_median": round(n * L / tmed / 2**30, 2),
-                                  "GiB/s_best": round(n * L / tmin / 2**30, 2),
-                                  "copy_ms_per_call": round((s1["ns_copy"] - s0["ns_copy"]) / 5e6, 3),
-                                  "wait_ms_per_call": round((s1["ns_wait"] - s0["ns_wait"]) / 5e6, 3)}), flush=True)
+                cfg = {"threads": th, "nt": nt, "dma": dma, "spin_us": spin, "passes": passes, "numa": numa,
+                       "round": rnd}
+                if args.wire_only:
+                    pass
+                else:
+                    got = ctx.batch_uniform(big, L, L, n, ss)
+                    if want is None:
+                        want = got
+                    assert np.array_equal(got, want)
+                    s0 = ctx.stats()
+                    tmin, tmed = timed(lambda: ctx.batch_uniform(big, L, L, n, ss), 5)
+                    s1 = ctx.stats()
+                    print(json.dumps({**cfg, "measure": "uniform_host_1Mx1500_pageable",
+                                      "GiB/s_median": round(n * L / tmed / 2**30, 2),
+                                      "GiB/s_best": round(n * L / tmin / 2**30, 2),
+                                      "copy_ms_per_call": round((s1["ns_copy"] - s0["ns_copy"]) / 5e6, 3),
+                                      "wait_ms_per_call": round((s1["ns_wait"] - s0["ns_wait"]) / 5e6, 3)}),
+                          flush=True)
                 for name, fn in (("ipv4_host_pool32k_fill", lambda: ctx.ipv4_batch(pool, offs, 32768, 0)),
                                  ("ipv4_ptrs_host_loop_fill", lambda: ctx.ipv4_batch_ptrs(ptrs, lens, 0))):
                     fn()
