@@ -14,6 +14,9 @@
 //   s128      the whole 128-B line, default policy (write-back in L2)
 //   s128_nt   the whole 128-B line, nt (streaming)
 //   dense     the 2 bytes to a dense per-packet array instead (VERIFY's d_out)
+//   dense_scatter      dense, then a second kernel storing each 2-byte word into its
+//                      packet (one thread per packet, default policy): FILL in two launches
+//   dense_scatter_sc01 ... the second kernel's stores sc0 sc1
 // Vector stores only. Prints one JSON line per variant: median / min ms of
 // 7 x 20 launches, after 3 warm-up launches.
 //   hipcc -O3 --offload-arch=gfx950 -o tools/fill_store_probe tools/fill_store_probe.hip
@@ -89,20 +92,42 @@ __global__ __launch_bounds__(256) void k_fill(uint8_t* __restrict__ reg, uint64_
     if ((threadIdx.x & 63) == 0 && acc == 0x12345678u) out[0] = acc;   // keep the sums live
 }
 
+// Second pass of the two-launch FILL: packet i's word from the dense array to slot i + 36.
+template <int P>
+__global__ __launch_bounds__(256) void k_scatter(uint8_t* __restrict__ reg, const uint16_t* __restrict__ dense,
+                                                 uint32_t npk, uint32_t slot) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= npk) return;
+    uint8_t* p = reg + (uint64_t)i * slot + 36u;
+    const uint32_t w = dense[i];
+    if constexpr (P == 0) *(gptr<uint16_t>)p = (uint16_t)w;
+    else asm volatile("global_store_short %0, %1, off sc0 sc1" ::"v"(p), "v"(w) : "memory");
+}
+
+template <int V>
+static void launch(uint8_t* reg, uint64_t nchunks, uint32_t slot_chunks, uint16_t* dense, uint64_t* out, int blocks) {
+    if constexpr (V == 11 || V == 12) {
+        hipLaunchKernelGGL((k_fill<6>), dim3(blocks), dim3(256), 0, 0, reg, nchunks, slot_chunks, dense, out);
+        const uint32_t npk = (uint32_t)(nchunks / slot_chunks);
+        hipLaunchKernelGGL((k_scatter<V - 11>), dim3((npk + 255) / 256), dim3(256), 0, 0, reg, dense, npk,
+                           slot_chunks * 16u);
+    } else {
+        hipLaunchKernelGGL((k_fill<V>), dim3(blocks), dim3(256), 0, 0, reg, nchunks, slot_chunks, dense, out);
+    }
+}
+
 template <int V>
 static int run(const char* name, uint8_t* reg, uint64_t nchunks, uint32_t slot_chunks, uint16_t* dense,
                uint64_t* out, int blocks) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    for (int w = 0; w < 3; ++w)
-        hipLaunchKernelGGL((k_fill<V>), dim3(blocks), dim3(256), 0, 0, reg, nchunks, slot_chunks, dense, out);
+    for (int w = 0; w < 3; ++w) launch<V>(reg, nchunks, slot_chunks, dense, out, blocks);
     CK(hipDeviceSynchronize());
     std::vector<float> ms;
     for (int r = 0; r < 7; ++r) {
         CK(hipEventRecord(e0, 0));
-        for (int k = 0; k < 20; ++k)
-            hipLaunchKernelGGL((k_fill<V>), dim3(blocks), dim3(256), 0, 0, reg, nchunks, slot_chunks, dense, out);
+        for (int k = 0; k < 20; ++k) launch<V>(reg, nchunks, slot_chunks, dense, out, blocks);
         CK(hipEventRecord(e1, 0));
         CK(hipEventSynchronize(e1));
         float t;
@@ -148,6 +173,8 @@ int main() {
         rc |= run<8>("s32_sc01", reg, nchunks, sc, dense, out, 4096);
         rc |= run<9>("s128", reg, nchunks, sc, dense, out, 4096);
         rc |= run<10>("s128_nt", reg, nchunks, sc, dense, out, 4096);
+        rc |= run<11>("dense_scatter", reg, nchunks, sc, dense, out, 4096);
+        rc |= run<12>("dense_scatter_sc01", reg, nchunks, sc, dense, out, 4096);
         if (rc) return 1;
     }
     std::vector<uint8_t> back(bytes);
