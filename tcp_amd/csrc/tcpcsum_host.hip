@@ -397,8 +397,11 @@ int tcpcsum_ctx_create(int device, size_t scratch_bytes, tcpcsum_ctx_t** out) {
                       hipDeviceGetPCIBusId(bus, sizeof bus, device) == hipSuccess &&
                       tcpcsum::numa_node_cpus(bus, &node_cpus);
     (void)hipGetLastError();
-    c->pool.reset(new (std::nothrow)
-                      tcpcsum::CopyPool(tcpcsum::default_copy_threads() - 1, spin_ns, numa ? &node_cpus : nullptr));
+    // never more workers than the node has CPUs this process may use (the caller is one of
+    // the copiers too, wherever it runs)
+    int copiers = tcpcsum::default_copy_threads();
+    if (numa) copiers = std::min(copiers, CPU_COUNT(&node_cpus) + 1);
+    c->pool.reset(new (std::nothrow) tcpcsum::CopyPool(copiers - 1, spin_ns, numa ? &node_cpus : nullptr));
     if (!c->pool) {
         delete c;
         return TCPCSUM_ENOMEM;

@@ -953,8 +953,20 @@ struct IpDone {
 // plen (nullable): per-packet readable bytes (scatter-gather batches: pkts = 0,
 // off[i] = the packet's address, limit = ~0). A packet never reads past
 // min(limit - off[i], plen[i]).
-template <int G, int C, int U, bool NT, bool PL>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TCPCSUM_WIRE_WAVES, 8))) void k_ipv4(uint8_t* __restrict__ pkts, const uint64_t* __restrict__ off,
+// VER: VERIFY (the launch's mode has TCPCSUM_IPV4_VERIFY) as a compile-time
+// constant — the FILL stores and their live registers compiled out of the
+// VERIFY kernel (k_ipv4<8,4,1>: 122 -> 94 VGPRs, 4 -> 5 waves per SIMD).
+// FILL with (8,4) lane groups — the MTU shape — asks the compiler for 5 waves per SIMD:
+// it needs 102 VGPRs (4 waves) and fits in 96 without spilling; 1M x 1500-B packets
+// packed 0.343 -> 0.330 ms, 1024-B slots 0.212 -> 0.206, 1536-B slots 0.297 -> 0.293
+// (tools/wire_lib_ab.py, profiles/r03_wire_verify_template_ab.jsonl). Elsewhere the
+// compiler's choice (TCPCSUM_WIRE_WAVES, a measurement knob, default 1).
+constexpr int wire_waves(int G, int C, bool VER) {
+    return (!VER && G == 8 && C == 4 && TCPCSUM_WIRE_WAVES < 5) ? 5 : TCPCSUM_WIRE_WAVES;
+}
+
+template <int G, int C, int U, bool NT, bool PL, bool VER>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(wire_waves(G, C, VER), 8))) void k_ipv4(uint8_t* __restrict__ pkts, const uint64_t* __restrict__ off,
                                               const uint32_t* __restrict__ plen,
                                               uint64_t n, uint32_t cap, uint64_t limit, int mode,
                                               uint16_t* __restrict__ out, uint8_t* __restrict__ status,
@@ -972,7 +984,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TCPCSUM_WIR
     const int gbase = lane - gl;
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
     const uint64_t ntiles = (n + SPT - 1) / SPT;
-    const bool verify = (mode & TCPCSUM_IPV4_VERIFY) != 0;
+    constexpr bool verify = VER;
     const bool iphdr = (mode & TCPCSUM_IPV4_IPHDR) != 0;
     uint64_t t = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
     // offsets of packet i and of packet i + 1 (0 past the end: no bound)
@@ -1161,7 +1173,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TCPCSUM_WIR
             const uint32_t cpos = m + th + 16u;   // window offset of the check (even)
             const uint32_t ipos = m + 10u;        // ... of the IPv4 header checksum
             const uint32_t L = cpos >> 7;
-            if ((L << 7) >= m && (L << 7) + 128u <= m + tot && 8u * L + 8u <= (uint32_t)(G * C) &&
+            // Only the group's first round of registers stays live to the store (FILL
+            // k_ipv4<8,4,1>: 122 VGPRs with all four rounds kept, 102 with one): lines 0
+            // and 1 for G >= 16 (L <= 1 always: m < 128, ihl*4 <= 60), line 0 — packets
+            // starting on a 128-B boundary — for G = 8; the rest take the 2-byte store
+            constexpr int KL = 1;
+            if (L <= 1u && (L << 7) >= m && (L << 7) + 128u <= m + tot && 8u * L + 8u <= (uint32_t)(G * KL) &&
                 (!iphdr || (ipos >> 7) == L)) {
                 auto patch = [](u32x4& x, uint32_t pos, uint32_t v16) {
                     const uint32_t sh = (pos & 2u) * 8u, j = (pos >> 2) & 3u;
@@ -1172,7 +1189,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TCPCSUM_WIR
                     x.w = j == 3u ? (x.w & keep) | val : x.w;
                 };
 #pragma unroll
-                for (int k = 0; k < C; ++k) {
+                for (int k = 0; k < KL; ++k) {
                     const uint32_t idx = (uint32_t)(k * G + gl);
                     if ((idx >> 3) == L) {
                         u32x4 x = v[u][k];
@@ -2094,26 +2111,36 @@ void launch_desc(const uint8_t* base, const tcpcsum_desc_t* d, uint64_t n, uint3
 #undef DS_U
 }
 
+template <int G, int C, int U, bool VER>
+static void launch_ipv4_m(uint8_t* pkts, const uint64_t* off, const uint32_t* plen, uint64_t n, uint32_t cap,
+                          uint64_t limit, int mode, uint16_t* out, uint8_t* status, uint16_t* ipout, hipStream_t s,
+                          const dim3 grid, bool nt, uint32_t amask, int dw) {
+    // per-packet bounds only when given: the extra load and register cost the
+    // region-bounded MTU batches 4-8 % (tools/wire_ab.py)
+    if (plen && nt)
+        hipLaunchKernelGGL((k_ipv4<G, C, U, true, true, VER>), grid, dim3(256), 0, s, pkts, off, plen, n, cap, limit,
+                           mode, out, status, ipout, amask, dw);
+    else if (plen)
+        hipLaunchKernelGGL((k_ipv4<G, C, U, false, true, VER>), grid, dim3(256), 0, s, pkts, off, plen, n, cap, limit,
+                           mode, out, status, ipout, amask, dw);
+    else if (nt)
+        hipLaunchKernelGGL((k_ipv4<G, C, U, true, false, VER>), grid, dim3(256), 0, s, pkts, off, plen, n, cap, limit,
+                           mode, out, status, ipout, amask, dw);
+    else
+        hipLaunchKernelGGL((k_ipv4<G, C, U, false, false, VER>), grid, dim3(256), 0, s, pkts, off, plen, n, cap, limit,
+                           mode, out, status, ipout, amask, dw);
+}
+
 template <int G, int C, int U>
 static void launch_ipv4_t(uint8_t* pkts, const uint64_t* off, const uint32_t* plen, uint64_t n, uint32_t cap,
                           uint64_t limit, int mode, uint16_t* out, uint8_t* status, uint16_t* ipout, hipStream_t s,
                           int max_blocks, bool nt, uint32_t amask, int dw) {
     constexpr int SPT = (64 / G) * U;
     const dim3 grid(grid_for((n + SPT - 1) / SPT, max_blocks));
-    // per-packet bounds only when given: the extra load and register cost the
-    // region-bounded MTU batches 4-8 % (tools/wire_ab.py)
-    if (plen && nt)
-        hipLaunchKernelGGL((k_ipv4<G, C, U, true, true>), grid, dim3(256), 0, s, pkts, off, plen, n, cap, limit, mode,
-                           out, status, ipout, amask, dw);
-    else if (plen)
-        hipLaunchKernelGGL((k_ipv4<G, C, U, false, true>), grid, dim3(256), 0, s, pkts, off, plen, n, cap, limit, mode,
-                           out, status, ipout, amask, dw);
-    else if (nt)
-        hipLaunchKernelGGL((k_ipv4<G, C, U, true, false>), grid, dim3(256), 0, s, pkts, off, plen, n, cap, limit, mode,
-                           out, status, ipout, amask, dw);
+    if (mode & TCPCSUM_IPV4_VERIFY)
+        launch_ipv4_m<G, C, U, true>(pkts, off, plen, n, cap, limit, mode, out, status, ipout, s, grid, nt, amask, dw);
     else
-        hipLaunchKernelGGL((k_ipv4<G, C, U, false, false>), grid, dim3(256), 0, s, pkts, off, plen, n, cap, limit,
-                           mode, out, status, ipout, amask, dw);
+        launch_ipv4_m<G, C, U, false>(pkts, off, plen, n, cap, limit, mode, out, status, ipout, s, grid, nt, amask, dw);
 }
 
 void launch_ipv4(uint8_t* pkts, const uint64_t* off, const uint32_t* plen, uint64_t n, uint32_t cap, uint64_t limit,
