@@ -955,18 +955,20 @@ struct IpDone {
 // min(limit - off[i], plen[i]).
 // VER: VERIFY (the launch's mode has TCPCSUM_IPV4_VERIFY) as a compile-time
 // constant — the FILL stores and their live registers compiled out of the
-// VERIFY kernel (k_ipv4<8,4,1>: 122 -> 94 VGPRs, 4 -> 5 waves per SIMD).
-// FILL with (8,4) lane groups — the MTU shape — asks the compiler for 5 waves per SIMD:
-// it needs 102 VGPRs (4 waves) and fits in 96 without spilling; 1M x 1500-B packets
+// VERIFY kernel (k_ipv4<8,4,1>: 120 -> 88 VGPRs, 4 -> 5 waves per SIMD).
+// FILL with (8,4) lane groups, one packet per group — the default MTU shape — asks the
+// compiler for 5 waves per SIMD: it needs 102 VGPRs (4 waves) and fits in 96 with two
+// spilled to scratch (12 bytes per lane, off the summation loop); 1M x 1500-B packets
 // packed 0.343 -> 0.330 ms, 1024-B slots 0.212 -> 0.206, 1536-B slots 0.297 -> 0.293
 // (tools/wire_lib_ab.py, profiles/r03_wire_verify_template_ab.jsonl). Elsewhere the
-// compiler's choice (TCPCSUM_WIRE_WAVES, a measurement knob, default 1).
-constexpr int wire_waves(int G, int C, bool VER) {
-    return (!VER && G == 8 && C == 4 && TCPCSUM_WIRE_WAVES < 5) ? 5 : TCPCSUM_WIRE_WAVES;
+// compiler's choice (TCPCSUM_WIRE_WAVES, a measurement knob, default 1) — forced
+// unrolls would spill dozens of registers at 5 waves.
+constexpr int wire_waves(int G, int C, int U, bool VER) {
+    return (!VER && G == 8 && C == 4 && U == 1 && TCPCSUM_WIRE_WAVES < 5) ? 5 : TCPCSUM_WIRE_WAVES;
 }
 
 template <int G, int C, int U, bool NT, bool PL, bool VER>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(wire_waves(G, C, VER), 8))) void k_ipv4(uint8_t* __restrict__ pkts, const uint64_t* __restrict__ off,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(wire_waves(G, C, U, VER), 8))) void k_ipv4(uint8_t* __restrict__ pkts, const uint64_t* __restrict__ off,
                                               const uint32_t* __restrict__ plen,
                                               uint64_t n, uint32_t cap, uint64_t limit, int mode,
                                               uint16_t* __restrict__ out, uint8_t* __restrict__ status,
@@ -1174,7 +1176,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(wire_waves(
             const uint32_t ipos = m + 10u;        // ... of the IPv4 header checksum
             const uint32_t L = cpos >> 7;
             // Only the group's first round of registers stays live to the store (FILL
-            // k_ipv4<8,4,1>: 122 VGPRs with all four rounds kept, 102 with one): lines 0
+            // k_ipv4<8,4,1>: 108 VGPRs with two rounds kept, 102 with one): lines 0
             // and 1 for G >= 16 (L <= 1 always: m < 128, ihl*4 <= 60), line 0 — packets
             // starting on a 128-B boundary — for G = 8; the rest take the 2-byte store
             constexpr int KL = 1;
