@@ -18,11 +18,13 @@
  *                                       (the reference verifies nothing,
  *                                       loop.c:314-399); failures are counted
  *             TCPCSUM_PRELOAD_RX=drop   verify, and return only the segments
- *                                       that pass: the vector is reordered (a
- *                                       permutation of the caller's entries, so
- *                                       every buffer stays referenced) with the
- *                                       passing segments first, and the count
- *                                       returned is theirs
+ *                                       that pass: the received messages are
+ *                                       reordered (the caller's iovecs swap
+ *                                       contents, so every buffer stays
+ *                                       referenced and loop.c:97's by-index
+ *                                       reads see them) with the passing
+ *                                       segments first, and the count returned
+ *                                       is theirs
  *             TCPCSUM_PRELOAD_RX=off    (default)
  *   TCPCSUM_PRELOAD_IPHDR=1      also fill / verify the IPv4 header checksum
  *   TCPCSUM_PRELOAD_ANY_SOCKET=1 act on every socket, not only SOCK_RAW ones
@@ -247,6 +249,44 @@ int sendmmsg(int fd, struct mmsghdr *vec, unsigned int vlen, int flags) {
     return real_sendmmsg(fd, vec, vlen, flags);
 }
 
+/* Exchange two received messages for rx drop. The reference reads packet i of a
+ * receive through its own iovec array, by index (getIpPacket, loop.c:96-100:
+ * loop->iovecs[index].iov_base), not through the mmsghdr vector, so the data
+ * must move with the iovec CONTENTS (buffer and length) — the vector's msg_iov
+ * pointers stay where the caller put them. Length, flags, and the name and
+ * control buffers (by pointer) travel with the data. A message with several
+ * iovecs (SKIPPED, always kept) moves as a whole vector entry instead. */
+static void swap_msgs(struct mmsghdr *a, struct mmsghdr *b) {
+    struct msghdr *x = &a->msg_hdr, *y = &b->msg_hdr;
+    if (x->msg_iovlen != 1 || y->msg_iovlen != 1 || x->msg_iov == y->msg_iov) {
+        struct mmsghdr t = *a;
+        *a = *b;
+        *b = t;
+        return;
+    }
+    struct iovec tv = x->msg_iov[0];
+    x->msg_iov[0] = y->msg_iov[0];
+    y->msg_iov[0] = tv;
+    unsigned int tl = a->msg_len;
+    a->msg_len = b->msg_len;
+    b->msg_len = tl;
+    int tf = x->msg_flags;
+    x->msg_flags = y->msg_flags;
+    y->msg_flags = tf;
+    void *tn = x->msg_name;
+    socklen_t tnl = x->msg_namelen;
+    x->msg_name = y->msg_name;
+    x->msg_namelen = y->msg_namelen;
+    y->msg_name = tn;
+    y->msg_namelen = tnl;
+    void *tc = x->msg_control;
+    size_t tcl = x->msg_controllen;
+    x->msg_control = y->msg_control;
+    x->msg_controllen = y->msg_controllen;
+    y->msg_control = tc;
+    y->msg_controllen = tcl;
+}
+
 int recvmmsg(int fd, struct mmsghdr *vec, unsigned int vlen, int flags, struct timespec *timeout) {
     pthread_once(&g_once, init_once);
     int r = real_recvmmsg(fd, vec, vlen, flags, timeout);
@@ -270,11 +310,7 @@ int recvmmsg(int fd, struct mmsghdr *vec, unsigned int vlen, int flags, struct t
                  * vector (the caller's buffers all stay referenced) */
                 for (unsigned int i = 0; i < cnt; ++i) {
                     if (!keep[i]) continue;
-                    if (kept != done + i) {
-                        struct mmsghdr t = vec[kept];
-                        vec[kept] = vec[done + i];
-                        vec[done + i] = t;
-                    }
+                    if (kept != done + i) swap_msgs(&vec[kept], &vec[done + i]);
                     ++kept;
                 }
             } else {

@@ -125,8 +125,10 @@ int main(int argc, char **argv) {
             if (r < 0) { fprintf(stderr, "recvmmsg: %s\n", strerror(errno)); return 4; }
             if (r == 0 && !corrupt) return 5;
             for (int k = 0; k < r; ++k) {
-                /* which packet: daddr = 10.x.y.z carries its index */
-                const uint8_t *b = (const uint8_t *) mv[k].msg_hdr.msg_iov[0].iov_base;
+                /* which packet: daddr = 10.x.y.z carries its index. Read through the
+                 * iovec array by position, as the reference does (getIpPacket,
+                 * loop.c:96-100: loop->iovecs[index]), not through mv[k].msg_iov */
+                const uint8_t *b = (const uint8_t *) iv[k].iov_base;
                 const size_t held = mv[k].msg_len < rx_cap ? mv[k].msg_len : rx_cap;
                 const int idx = held >= 20 ? (b[17] << 16) | (b[18] << 8) | b[19] : -1;
                 if (idx < s0 || idx >= s0 + cnt || ilen[idx]) { fprintf(stderr, "unexpected message\n"); return 5; }
