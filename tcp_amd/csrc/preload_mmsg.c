@@ -66,6 +66,7 @@
 #include <sys/socket.h>
 #include <sys/types.h>
 
+#include "rx_compact.h"
 #include "tcpcsum.h"
 
 typedef int (*sendmmsg_fn)(int, struct mmsghdr *, unsigned int, int);
@@ -249,44 +250,6 @@ int sendmmsg(int fd, struct mmsghdr *vec, unsigned int vlen, int flags) {
     return real_sendmmsg(fd, vec, vlen, flags);
 }
 
-/* Exchange two received messages for rx drop. The reference reads packet i of a
- * receive through its own iovec array, by index (getIpPacket, loop.c:96-100:
- * loop->iovecs[index].iov_base), not through the mmsghdr vector, so the data
- * must move with the iovec CONTENTS (buffer and length) — the vector's msg_iov
- * pointers stay where the caller put them. Length, flags, and the name and
- * control buffers (by pointer) travel with the data. A message with several
- * iovecs (SKIPPED, always kept) moves as a whole vector entry instead. */
-static void swap_msgs(struct mmsghdr *a, struct mmsghdr *b) {
-    struct msghdr *x = &a->msg_hdr, *y = &b->msg_hdr;
-    if (x->msg_iovlen != 1 || y->msg_iovlen != 1 || x->msg_iov == y->msg_iov) {
-        struct mmsghdr t = *a;
-        *a = *b;
-        *b = t;
-        return;
-    }
-    struct iovec tv = x->msg_iov[0];
-    x->msg_iov[0] = y->msg_iov[0];
-    y->msg_iov[0] = tv;
-    unsigned int tl = a->msg_len;
-    a->msg_len = b->msg_len;
-    b->msg_len = tl;
-    int tf = x->msg_flags;
-    x->msg_flags = y->msg_flags;
-    y->msg_flags = tf;
-    void *tn = x->msg_name;
-    socklen_t tnl = x->msg_namelen;
-    x->msg_name = y->msg_name;
-    x->msg_namelen = y->msg_namelen;
-    y->msg_name = tn;
-    y->msg_namelen = tnl;
-    void *tc = x->msg_control;
-    size_t tcl = x->msg_controllen;
-    x->msg_control = y->msg_control;
-    x->msg_controllen = y->msg_controllen;
-    y->msg_control = tc;
-    y->msg_controllen = tcl;
-}
-
 int recvmmsg(int fd, struct mmsghdr *vec, unsigned int vlen, int flags, struct timespec *timeout) {
     pthread_once(&g_once, init_once);
     int r = real_recvmmsg(fd, vec, vlen, flags, timeout);
@@ -294,6 +257,7 @@ int recvmmsg(int fd, struct mmsghdr *vec, unsigned int vlen, int flags, struct t
         unsigned int lens[1024];
         unsigned char keep[1024];
         unsigned int done = 0, kept = 0;
+        const int by_entry = g_rx == MODE_DROP && rx_by_entry(vec, (unsigned int) r);
         while (done < (unsigned int) r) {
             unsigned int cnt = (unsigned int) r - done < 1024 ? (unsigned int) r - done : 1024;
             /* the bytes received, never past the buffer: with MSG_TRUNC in flags a
@@ -308,11 +272,7 @@ int recvmmsg(int fd, struct mmsghdr *vec, unsigned int vlen, int flags, struct t
                 /* stable partition by swaps: passing messages move to the front in
                  * arrival order; failing ones end up behind them, still in the
                  * vector (the caller's buffers all stay referenced) */
-                for (unsigned int i = 0; i < cnt; ++i) {
-                    if (!keep[i]) continue;
-                    if (kept != done + i) swap_msgs(&vec[kept], &vec[done + i]);
-                    ++kept;
-                }
+                kept = rx_keep_passing(vec, kept, done, cnt, keep, by_entry);
             } else {
                 kept += cnt;
             }

@@ -69,3 +69,22 @@ def test_copy_pool_under_tsan(tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True, env=env, timeout=300)
     assert r.returncode == 0 and "ThreadSanitizer" not in r.stderr, r.stdout + r.stderr
     assert "copy_pool_test: OK" in r.stdout
+
+
+@pytest.mark.skipif(shutil.which("gcc") is None, reason="gcc not available")
+def test_rx_drop_compaction_under_asan_ubsan(tmp_path):
+    """The interposer's rx drop (tcp_amd/csrc/rx_compact.h): after the drop, the caller's own
+    iovec array read by index — the reference's getIpPacket, loop.c:96-100 — holds exactly the
+    passing messages in arrival order, with their lengths, flags and senders; no buffer is lost or
+    doubled; a receive with a scatter-gather message is reordered by vector entries instead."""
+    exe = tmp_path / "rx_compact_test"
+    cmd = ["gcc", "-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
+           "-fno-sanitize-recover=all", "-Wall", "-Wextra",
+           os.path.join(REPO, "tests", "c", "rx_compact_test.c"), "-o", str(exe)]
+    b = subprocess.run(cmd, capture_output=True, text=True)
+    assert b.returncode == 0, b.stderr
+    env = dict(os.environ)
+    env["ASAN_OPTIONS"] = "detect_leaks=1:abort_on_error=0:verify_asan_link_order=0"
+    r = subprocess.run([str(exe)], capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "rx_compact_test: OK" in r.stdout
