@@ -37,13 +37,15 @@ def main():
     shapes = [int(x) for x in os.environ.get("SHAPES", "-1,1,3,4,5,7").split(",")]
     blocks = [int(x) for x in os.environ.get("BLOCKS", "0,512,1024,2048,4096").split(",")]
     unrolls = [int(x) for x in os.environ.get("UNROLLS", "1,2").split(",")]
-    cfgs = [(m, sh, mb, un) for m in ("VERIFY", "FILL") for sh in shapes for mb in blocks for un in unrolls]
+    flags = [int(x) for x in os.environ.get("FLAGS", "0").split(",")]   # TCPCSUM_TUNE_* bits
+    cfgs = [(m, sh, mb, un, fl) for m in ("VERIFY", "FILL") for sh in shapes for mb in blocks for un in unrolls
+            for fl in flags]
     res = {c: [] for c in cfgs}
     checked = {}
     for rnd in range(5):
         for c in cfgs:
-            m, sh, mb, un = c
-            tcp_amd.set_tuning(mb, un, sh, 0)
+            m, sh, mb, un, fl = c
+            tcp_amd.set_tuning(mb, un, sh, fl)
             mode = tcp_amd.IPV4_VERIFY if m == "VERIFY" else tcp_amd.IPV4_FILL
             fn = lambda: tcp_amd.ipv4_batch(data, offs, n, slot, mode, out, stat)
             fn()
@@ -53,7 +55,7 @@ def main():
                 if m == "FILL":
                     tcp_amd.set_tuning(0, 0, -1, 0)
                     tcp_amd.ipv4_batch(data, offs, n, slot, tcp_amd.IPV4_VERIFY, out, stat)
-                    tcp_amd.set_tuning(mb, un, sh, 0)
+                    tcp_amd.set_tuning(mb, un, sh, fl)
                 checked[c] = bool((out == 0).all().item()) and bool((stat == 0).all().item())
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(st)
@@ -65,10 +67,10 @@ def main():
         tcp_amd.set_tuning(0, 0, -1, 0)
         print(json.dumps({"round": rnd}), flush=True)
     for c, ts in sorted(res.items(), key=lambda kv: (kv[0][0], sorted(kv[1])[2])):
-        m, sh, mb, un = c
+        m, sh, mb, un, fl = c
         ms = sorted(ts)[len(ts) // 2]
         print(json.dumps({"measure": f"ipv4_shape_sweep_1Mx{pay + 44}_slots{slot}", "mode": m, "shape": sh,
-                          "max_blocks": mb, "unroll": un, "ms": round(ms, 4),
+                          "max_blocks": mb, "unroll": un, "flags": fl, "ms": round(ms, 4),
                           "GB/s_tcp_bytes": round(n * (pay + 24) / (ms * 1e-3) / 1e9, 1),
                           "verify_ok": checked[c]}), flush=True)
 
