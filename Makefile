@@ -8,25 +8,34 @@ ROCM ?= /opt/rocm
 HIPCC ?= $(ROCM)/bin/hipcc
 CC ?= gcc
 ARCH ?= gfx950
-# TUNING_VARIANTS=1 also compiles the pipelined / default-load kernel variants the
-# TCPCSUM_TUNE_PIPE_* / NT_* flags select (tuning experiments only)
-TUNING_VARIANTS ?= 0
-HIPFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Wno-unused-parameter -Wno-unused-value -Wno-unused-result \
-	-DTCPCSUM_TUNING_VARIANTS=$(TUNING_VARIANTS)
+# Product build only: the tuning / knock-out knobs of tcp_amd/csrc/tcpcsum_internal.h
+# are refused here (#error); measurement builds compile their own objects (tools/*_ab.py).
+HIPFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Wno-unused-parameter -Wno-unused-value -Wno-unused-result
 CFLAGS_LIB ?= -O2 -fPIC -Wall -Wextra
 
 LIB := tcp_amd/libtcpcsum.so
 HIP_SRCS := tcp_amd/csrc/tcpcsum_kernels.hip tcp_amd/csrc/tcpcsum_api.hip tcp_amd/csrc/tcpcsum_host.hip
 HDRS := include/tcpcsum.h tcp_amd/csrc/tcpcsum_internal.h tcp_amd/csrc/host_registry.h tcp_amd/csrc/copy_pool.h
 OBJDIR := build/obj
+# Build provenance (tcpcsum_build_info): sha256 over these files, in this order —
+# tcp_amd/provenance.py computes the same over the tree it runs in.
+HASH_SRCS := include/tcpcsum.h tcp_amd/csrc/tcpcsum_internal.h tcp_amd/csrc/host_registry.h tcp_amd/csrc/copy_pool.h \
+	tcp_amd/csrc/tcpcsum_kernels.hip tcp_amd/csrc/tcpcsum_api.hip tcp_amd/csrc/tcpcsum_host.hip \
+	tcp_amd/csrc/scalar_dropin.c Makefile
+SRC_HASH := $(shell cat $(HASH_SRCS) | sha256sum | cut -c1-64)
 
 PRELOAD := tcp_amd/libtcpcsum_preload.so
 
 all: $(LIB) $(PRELOAD) oracle tests/c/abi_smoke tests/c/mmsg_loop tests/c/raw_echo tools/mmsg_bench
 
-$(OBJDIR)/%.o: tcp_amd/csrc/%.hip $(HDRS)
+$(OBJDIR)/%.o: tcp_amd/csrc/%.hip $(HDRS) Makefile
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -Iinclude -c $< -o $@
+
+# the one object that carries the source hash: rebuilt whenever any hashed file changes
+$(OBJDIR)/tcpcsum_api.o: tcp_amd/csrc/tcpcsum_api.hip $(HASH_SRCS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -Iinclude '-DTCPCSUM_SRC_HASH="$(SRC_HASH)"' -c $< -o $@
 
 $(OBJDIR)/scalar_dropin.o: tcp_amd/csrc/scalar_dropin.c include/tcpcsum.h
 	@mkdir -p $(OBJDIR)

@@ -24,13 +24,11 @@
  *     state: launch shapes come from an explicit per-call tcpcsum_tuning_t
  *     (NULL = built-in defaults) or from the tcpcsum_ctx_t they run in; no
  *     call keeps a pointer after it returns (async calls: until the stream
- *     reaches that point), except the host-buffer registrations a context
- *     holds when asked to (tcpcsum_ctx_register_host, or
- *     TCPCSUM_CTX_AUTO_REGISTER).
- *   - The library never page-locks (hipHostRegister) memory on its own: only
- *     ranges its caller hands to tcpcsum_ctx_register_host, or packet buffers
- *     under the opt-in TCPCSUM_CTX_AUTO_REGISTER. Pageable host memory is
- *     copied by CPU threads into the context's pinned staging instead.
+ *     reaches that point).
+ *   - The library page-locks only memory it allocates itself (pinned staging,
+ *     tcpcsum_host_alloc); it never registers, locks or unlocks memory it was
+ *     handed (ABI v4; DESIGN.md §7 says why). Pageable host memory is copied
+ *     by CPU threads into the context's pinned staging instead.
  *   - The caller owns every buffer.
  *   - The batch API covers sum_start < 2^32 (getPseudoHeaderSum returns at
  *     most 6 * 0xFFFF) and segment lengths <= INT32_MAX (csum_continue's
@@ -52,7 +50,7 @@ extern "C" {
 #define TCPCSUM_EHIP (-3)     /* a HIP call failed (tcpcsum_last_hip_error) */
 #define TCPCSUM_ENOMEM (-4)   /* allocation failed */
 
-#define TCPCSUM_ABI_VERSION 3
+#define TCPCSUM_ABI_VERSION 4
 
 /* Launch-shape override, passed per call (NULL = the built-in shapes measured
  * on MI355X). Fields: max_blocks (0 = per-shape default, else
@@ -98,6 +96,12 @@ int tcpcsum_last_hip_error(void);      /* hipError_t of the last failing HIP cal
 /* 0 if a gfx950 device is usable; TCPCSUM_ENODEV otherwise. Fills the name
  * of the current device's gfx arch into arch (may be NULL). */
 int tcpcsum_device_check(char *arch, size_t arch_len);
+/* Build provenance: a NUL-terminated one-line JSON object naming the source
+ * hash the library was compiled from (sha256 over the product sources and the
+ * Makefile, computed by the Makefile), the compile-time knobs, the offload arch
+ * and whether it is a product build ("product": true) or a measurement build
+ * (knock-outs / register-budget knobs set; never shipped). Static storage. */
+const char *tcpcsum_build_info(void);
 
 /* ------------------------------------------------------ scalar drop-ins
  * Synchronous, reference-identical per-segment helpers for code that needs a
@@ -224,15 +228,17 @@ int tcpcsum_tx_build_dev(const void *d_payload, const tcpcsum_txseg_t *d_segs, u
  * The path as the reference sees it: segments start and end in host memory
  * (raw-socket buffers). A context owns one device, two streams, pinned
  * staging and a few host copy threads (TCPCSUM_HOST_THREADS, default half the
- * CPUs the process may use, at most 8). Host memory is used one of two ways:
- *   - page-locked memory (tcpcsum_host_alloc / hipHostMalloc, a caller's own
- *     hipHostRegister, tcpcsum_ctx_register_host) is read — FILL: written —
- *     in place by the kernel over PCIe;
+ * CPUs the process may use, at most 8; a staged wire batch of up to 8 MiB
+ * copies on TCPCSUM_HOST_WIRE_THREADS of them, default 1 = the calling thread).
+ * Host memory is used one of two ways:
+ *   - memory its owner page-locked (tcpcsum_host_alloc / hipHostMalloc, or the
+ *     application's own hipHostRegister) is read — FILL: written — in place by
+ *     the kernel over PCIe;
  *   - pageable memory is copied by the CPU threads into the context's pinned
  *     staging (uniform batches chunk by chunk, overlapped with the kernel on
  *     the previous chunk; wire batches only the packets' bytes), the kernel
  *     reads the staging, and FILL's checks are stored back into the caller's
- *     packets by the CPU. Nothing is page-locked behind the caller's back.
+ *     packets by the CPU. It is never page-locked.
  * All host calls are synchronous: they return when every result is in place. */
 typedef struct tcpcsum_ctx tcpcsum_ctx_t;
 
@@ -245,16 +251,12 @@ void tcpcsum_ctx_destroy(tcpcsum_ctx_t *ctx);
  * this context is affected; other contexts and the device calls are not. */
 int tcpcsum_ctx_set_tuning(tcpcsum_ctx_t *ctx, const tcpcsum_tuning_t *tune);
 
-/* Context flags (0 = default). */
-/* tcpcsum_ipv4_batch_ptrs_host: page-lock each pageable packet buffer on first
- * use (whole pages, hipHostRegister) and keep it registered — later batches
- * over the same buffers read and write them in place with no copy — up to
- * 256 MiB of registrations, past which new buffers are copied. Opt-in: the
- * caller promises that the pages under those buffers are neither freed nor
- * page-locked / unlocked by anyone else (including HIP copies of other data
- * sharing those pages) until tcpcsum_ctx_unregister_host / _destroy. The
- * reference's buffers qualify (allocated once, never freed, loop.c:180-183). */
-#define TCPCSUM_CTX_AUTO_REGISTER 1u
+/* Context flags (0 = default). (ABI v3's TCPCSUM_CTX_AUTO_REGISTER = 1 is gone
+ * with the registration calls: the value is refused.) */
+/* Wait for the device by sleeping until it signals (a hipEventBlockingSync
+ * event) instead of HIP's spin in hipStreamSynchronize: the calling thread
+ * uses no CPU while the kernel runs, for a few microseconds more latency. */
+#define TCPCSUM_CTX_BLOCKING_WAIT 2u
 int tcpcsum_ctx_set_flags(tcpcsum_ctx_t *ctx, uint32_t flags);
 
 /* Counters of what the context did (cumulative since creation). */
@@ -263,17 +265,18 @@ typedef struct tcpcsum_ctx_stats {
     uint64_t pkts_in_place;      /* wire packets read / written in page-locked memory */
     uint64_t pkts_staged;        /* wire packets copied through pinned staging */
     uint64_t bytes_staged;       /* bytes copied into pinned staging (all host paths) */
-    uint64_t registered_ranges;  /* current registrations of this context */
-    uint64_t registered_bytes;
-    uint64_t copy_threads;       /* host threads used for staging copies (incl. the caller's) */
+    uint64_t copy_threads;       /* threads a staged wire batch (<= 8 MiB) copies on, caller included */
+    uint64_t bulk_threads;       /* threads a staged uniform or large wire batch copies on */
     uint64_t ns_copy;            /* wall time spent copying into / out of staging (CPU) */
     uint64_t ns_wait;            /* wall time spent waiting for the device after the last launch */
-    uint64_t reserved;
+    uint64_t ns_cpu_caller;      /* CPU time of the calling threads inside this context's host calls */
+    uint64_t ns_cpu_workers;     /* CPU time of its copy threads since creation (copies, spin, wake-ups) */
 } tcpcsum_ctx_stats_t;
 int tcpcsum_ctx_get_stats(tcpcsum_ctx_t *ctx, tcpcsum_ctx_stats_t *out);
 
-/* Page-locked host memory for packet pools: the host calls read it in place
- * over PCIe. NULL on failure. */
+/* Page-locked host memory for packet pools — e.g. the loop's 1024 out-buffers
+ * (loop.c:180-183) carved from one allocation: the host calls read and FILL it
+ * in place over PCIe, with no copy. NULL on failure. */
 void *tcpcsum_host_alloc(size_t bytes);
 void tcpcsum_host_free(void *p);
 
@@ -287,9 +290,9 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t *ctx, const void *h_base, uint64_t 
 /* Wire layout in host memory: n packets at h_pkts + h_pkt_off[i] (offsets
  * within one host region of region_bytes; each header must lie inside it).
  * FILL patches check in place in host memory. A region that one page-locked
- * allocation covers (tcpcsum_host_alloc, or a pool registered once with
- * tcpcsum_ctx_register_host) is read in place; otherwise only the packets are
- * copied into staging. Results exactly as tcpcsum_ipv4_batch_dev. */
+ * allocation covers (tcpcsum_host_alloc, or the application's own
+ * hipHostRegister) is read in place; otherwise only the packets are copied
+ * into staging. Results exactly as tcpcsum_ipv4_batch_dev. */
 int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t *ctx, void *h_pkts, size_t region_bytes,
                             const uint64_t *h_pkt_off, uint64_t n, uint32_t cap, int mode,
                             uint16_t *h_out, uint8_t *h_status);
@@ -298,23 +301,11 @@ int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t *ctx, void *h_pkts, size_t region_byte
  * layout: 1024 separately malloc'd 32 KiB out-buffers, loop.c:180-183, one
  * iov_base per message, loop.c:53-54): packet i at h_pkts[i] with h_lens[i]
  * readable bytes (results and status as tcpcsum_ipv4_batch_ptrs_dev). A
- * packet inside one page-locked mapping (this context's registrations, or
- * memory someone else page-locked) is read and FILLed in place; any other is
- * copied into staging and its check stored back — unless the context has
- * TCPCSUM_CTX_AUTO_REGISTER, which page-locks its buffer now and keeps it. */
+ * packet inside one page-locked allocation (tcpcsum_host_alloc, the
+ * application's own hipHostRegister) is read and FILLed in place; any other is
+ * copied into staging and its check stored back. */
 int tcpcsum_ipv4_batch_ptrs_host(tcpcsum_ctx_t *ctx, void *const *h_pkts, const uint32_t *h_lens, uint64_t n,
                                  int mode, uint16_t *h_out, uint8_t *h_status);
-
-/* Page-lock [p, p+bytes) (whole pages) for this context, e.g. once per pool
- * at loop.c:180-183; later host batches over it run in place. The contract
- * is hipHostRegister's: the caller keeps those pages mapped, and does not
- * page-lock or unlock them elsewhere, until it unregisters them. */
-int tcpcsum_ctx_register_host(tcpcsum_ctx_t *ctx, void *p, size_t bytes);
-/* Drop every registration of this context that overlaps [p, p+bytes)
- * (p = NULL: all of them). Call before freeing registered buffers. */
-int tcpcsum_ctx_unregister_host(tcpcsum_ctx_t *ctx, void *p, size_t bytes);
-/* Host memory this context has page-locked: ranges and bytes (either may be NULL). */
-int tcpcsum_ctx_registered(tcpcsum_ctx_t *ctx, uint64_t *ranges, uint64_t *bytes);
 
 /* ------------------------------------------------------ synthetic workload
  * Device-side generation of the SURVEY.md Appendix B batches, so benchmarks
@@ -369,7 +360,7 @@ int tcpcsum_plan_uniform(uint64_t base, uint64_t stride, uint32_t len, uint64_t 
 /* wire FILL: always the 2-byte store (default: where the 128-B line holding the check lies
  * inside the packet, the whole line is written back through, the check patched in) */
 #define TCPCSUM_TUNE_FILL_U16 512
-#define TCPCSUM_TUNE_TX_WT_STORE 1024  /* builder: payload stores written through (sc0 sc1) */
+#define TCPCSUM_TUNE_TX_WT_STORE 1024  /* builder: payload stores written through (sc0 sc1 buffer stores) */
 /* 0 if *tune is a valid tuning (NULL counts as valid), else TCPCSUM_EINVAL. */
 int tcpcsum_tuning_check(const tcpcsum_tuning_t *tune);
 

@@ -22,9 +22,9 @@ except Exception:  # pragma: no cover - torch is always present in this image
 
 __all__ = [
     "DESC_DTYPE", "TXSEG_DTYPE", "IPV4_FILL", "IPV4_VERIFY", "IPV4_IPHDR", "PKT_OK", "PKT_SKIPPED",
-    "PKT_IPHDR_BAD", "PKT_CSUM_PARTIAL", "CTX_AUTO_REGISTER", "TUNE_WIRE_CACHED", "TUNE_WIN16", "TUNE_TX_NT_STORE", "TUNE_FILL_DWORD", "TUNE_FILL_U16",
+    "PKT_IPHDR_BAD", "PKT_CSUM_PARTIAL", "CTX_BLOCKING_WAIT", "TUNE_WIRE_CACHED", "TUNE_WIN16", "TUNE_TX_NT_STORE", "TUNE_FILL_DWORD", "TUNE_FILL_U16",
     "TUNE_TX_WT_STORE",
-    "TcpCsumError", "Tuning", "HostContext", "lib", "lib_path", "device_check", "make_tuning", "set_tuning",
+    "TcpCsumError", "Tuning", "HostContext", "lib", "lib_path", "device_check", "build_info", "make_tuning", "set_tuning",
     "get_tuning", "plan_uniform", "getPseudoHeaderSum", "csum_continue", "batch_uniform", "batch_uniform_multi",
     "ubatches", "batch_desc",
     "ipv4_batch", "ipv4_batch_ptrs", "tx_build", "synth_fill", "synth_pseudo", "stream_probe", "pinned_empty",
@@ -45,7 +45,7 @@ PKT_OK = 0
 PKT_SKIPPED = 1
 PKT_IPHDR_BAD = 2
 PKT_CSUM_PARTIAL = 4
-CTX_AUTO_REGISTER = 1
+CTX_BLOCKING_WAIT = 2
 
 # tcpcsum_desc_t {u64 offset; u32 len; u32 sum_start}
 DESC_DTYPE = np.dtype([("offset", "<u8"), ("len", "<u4"), ("sum_start", "<u4")])
@@ -105,9 +105,9 @@ MULTI_MAX = 16
 class CtxStats(ctypes.Structure):
     """tcpcsum_ctx_stats_t."""
     _fields_ = [("batches", ctypes.c_uint64), ("pkts_in_place", ctypes.c_uint64), ("pkts_staged", ctypes.c_uint64),
-                ("bytes_staged", ctypes.c_uint64), ("registered_ranges", ctypes.c_uint64),
-                ("registered_bytes", ctypes.c_uint64), ("copy_threads", ctypes.c_uint64),
-                ("ns_copy", ctypes.c_uint64), ("ns_wait", ctypes.c_uint64), ("reserved", ctypes.c_uint64)]
+                ("bytes_staged", ctypes.c_uint64), ("copy_threads", ctypes.c_uint64),
+                ("bulk_threads", ctypes.c_uint64), ("ns_copy", ctypes.c_uint64), ("ns_wait", ctypes.c_uint64),
+                ("ns_cpu_caller", ctypes.c_uint64), ("ns_cpu_workers", ctypes.c_uint64)]
 
 # name -> (restype, argtypes); must cover every function in include/tcpcsum.h
 SIGNATURES = {
@@ -115,6 +115,7 @@ SIGNATURES = {
     "tcpcsum_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "tcpcsum_last_hip_error": (ctypes.c_int, []),
     "tcpcsum_device_check": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t]),
+    "tcpcsum_build_info": (ctypes.c_char_p, []),
     "tcpcsum_pseudo": (ctypes.c_ulong, [u32, u32, ctypes.c_uint16]),
     "tcpcsum_continue": (ctypes.c_ushort, [ctypes.c_ulong, ctypes.c_char_p, ctypes.c_int]),
     "tcpcsum_batch_uniform_dev": (ctypes.c_int, [vp, u64, u32, vp, u32, vp, u64, vp, tunep]),
@@ -132,9 +133,6 @@ SIGNATURES = {
     "tcpcsum_batch_uniform_host": (ctypes.c_int, [vp, vp, u64, u32, vp, u32, vp, u64]),
     "tcpcsum_ipv4_batch_host": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp, u64, u32, ctypes.c_int, vp, vp]),
     "tcpcsum_ipv4_batch_ptrs_host": (ctypes.c_int, [vp, vp, vp, u64, ctypes.c_int, vp, vp]),
-    "tcpcsum_ctx_register_host": (ctypes.c_int, [vp, vp, ctypes.c_size_t]),
-    "tcpcsum_ctx_unregister_host": (ctypes.c_int, [vp, vp, ctypes.c_size_t]),
-    "tcpcsum_ctx_registered": (ctypes.c_int, [vp, c_u64p, c_u64p]),
     "tcpcsum_tx_build_dev": (ctypes.c_int, [vp, vp, u64, u32, vp, ctypes.c_int, vp, vp, tunep]),
     "tcpcsum_synth_fill_dev": (ctypes.c_int, [vp, u64, u64, vp]),
     "tcpcsum_synth_pseudo_dev": (ctypes.c_int, [vp, u64, u64, u32, vp]),
@@ -189,6 +187,12 @@ def csum_continue(sumStart: int, p: bytes, nbytes: Optional[int] = None) -> int:
     if nbytes > len(p):
         raise ValueError("nbytes exceeds buffer")
     return int(lib().tcpcsum_continue(sumStart & 0xFFFFFFFFFFFFFFFF, bytes(p), int(nbytes)))
+
+
+def build_info() -> dict:
+    """tcpcsum_build_info(): source hash, compile-time knobs, product or measurement build."""
+    import json
+    return json.loads(lib().tcpcsum_build_info().decode())
 
 
 def device_check() -> tuple[int, str]:
@@ -422,16 +426,17 @@ def pinned_empty(nbytes: int, dtype=np.uint8) -> np.ndarray:
 
 
 class HostContext:
-    """tcpcsum_ctx_t: host-memory batches, synchronous. Page-locked memory is read in place; pageable
-    memory is copied into the context's pinned staging (never page-locked behind the caller's back),
-    unless ``auto_register`` (TCPCSUM_CTX_AUTO_REGISTER) lets ipv4_batch_ptrs lock packet buffers."""
+    """tcpcsum_ctx_t: host-memory batches, synchronous. Memory its owner page-locked (pinned_empty /
+    tcpcsum_host_alloc) is read in place; pageable memory is copied into the context's pinned staging
+    and never page-locked. ``blocking_wait`` (TCPCSUM_CTX_BLOCKING_WAIT): sleep, not spin, while the
+    device works."""
 
-    def __init__(self, device: int = 0, scratch_bytes: int = 0, auto_register: bool = False):
+    def __init__(self, device: int = 0, scratch_bytes: int = 0, blocking_wait: bool = False):
         h = vp()
         _check(lib().tcpcsum_ctx_create(device, scratch_bytes, ctypes.byref(h)), "tcpcsum_ctx_create")
         self._h = h
-        if auto_register:
-            self.set_flags(CTX_AUTO_REGISTER)
+        if blocking_wait:
+            self.set_flags(CTX_BLOCKING_WAIT)
 
     def set_flags(self, flags: int) -> None:
         _check(lib().tcpcsum_ctx_set_flags(self._h, flags), "tcpcsum_ctx_set_flags")
@@ -439,7 +444,7 @@ class HostContext:
     def stats(self) -> dict:
         st = CtxStats()
         _check(lib().tcpcsum_ctx_get_stats(self._h, ctypes.byref(st)), "tcpcsum_ctx_get_stats")
-        return {k: int(getattr(st, k)) for k, _ in CtxStats._fields_ if k != "reserved"}
+        return {k: int(getattr(st, k)) for k, _ in CtxStats._fields_}
 
     def close(self) -> None:
         if self._h:
@@ -493,8 +498,8 @@ class HostContext:
 
     def ipv4_batch_ptrs(self, ptrs, lens, mode: int):
         """Scatter-gather wire batch over host buffers: ``ptrs`` host addresses (ints), ``lens`` readable
-        bytes per packet. Page-locked buffers are used in place; pageable ones are copied into staging
-        (or, with auto_register, page-locked on first use and kept). FILL patches the checks in place."""
+        bytes per packet. Page-locked buffers are used in place; pageable ones are copied into staging.
+        FILL patches the checks in place."""
         p = np.ascontiguousarray(np.asarray(ptrs, dtype=np.uint64))
         ln = np.ascontiguousarray(np.asarray(lens, dtype=np.uint32))
         if p.size != ln.size:
@@ -506,14 +511,3 @@ class HostContext:
                                                 status.ctypes.data)
         _check(rc, "tcpcsum_ipv4_batch_ptrs_host")
         return out, status
-
-    def register_host(self, addr: int, nbytes: int) -> None:
-        _check(lib().tcpcsum_ctx_register_host(self._h, addr, nbytes), "tcpcsum_ctx_register_host")
-
-    def unregister_host(self, addr: int = 0, nbytes: int = 0) -> None:
-        _check(lib().tcpcsum_ctx_unregister_host(self._h, addr or None, nbytes), "tcpcsum_ctx_unregister_host")
-
-    def registered(self) -> tuple[int, int]:
-        r, b = ctypes.c_uint64(), ctypes.c_uint64()
-        _check(lib().tcpcsum_ctx_registered(self._h, ctypes.byref(r), ctypes.byref(b)), "tcpcsum_ctx_registered")
-        return r.value, b.value

@@ -12,6 +12,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include <algorithm>
 #include <atomic>
@@ -62,22 +63,43 @@ public:
     }
     int threads() const { return nw_ + 1; }
 
+    // CPU time the workers have used since they started (copies, the spin after
+    // each job, wake-ups), from their per-thread CPU clocks. Call from the thread
+    // that runs jobs (the workers are started there).
+    uint64_t worker_cpu_ns() const {
+        uint64_t ns = 0;
+        for (const auto& t : th_) {
+            clockid_t cid;
+            timespec ts;
+            if (pthread_getcpuclockid(const_cast<std::thread&>(t).native_handle(), &cid) == 0 &&
+                clock_gettime(cid, &ts) == 0)
+                ns += (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+        }
+        return ns;
+    }
+
     // body(lo, hi) over [0, n) in pieces of `grain`; returns when every piece is done.
-    void run(size_t n, size_t grain, const std::function<void(size_t, size_t)>& body) {
+    // max_threads: at most this many threads work on it, the caller included
+    // (0 = every worker; 1 = the caller alone, no worker is woken).
+    void run(size_t n, size_t grain, const std::function<void(size_t, size_t)>& body, int max_threads = 0) {
         if (n == 0) return;
         if (grain == 0) grain = 1;
-        if (nw_ == 0 || n <= grain) {
+        const int helpers = max_threads <= 0 ? nw_ : std::min(nw_, max_threads - 1);
+        if (helpers <= 0 || n <= grain) {
             body(0, n);
             return;
         }
         start();
-        auto job = std::make_shared<Job>(&body, n, grain);
+        auto job = std::make_shared<Job>(&body, n, grain, helpers);
         {
             std::lock_guard<std::mutex> lk(m_);
             cur_ = job;
             ++gen_;
         }
-        cv_.notify_all();
+        if (helpers >= nw_)
+            cv_.notify_all();
+        else
+            for (int i = 0; i < helpers; ++i) cv_.notify_one();
         job->drain();
         while (job->done.load(std::memory_order_acquire) < n) std::this_thread::yield();
         std::lock_guard<std::mutex> lk(m_);
@@ -86,10 +108,12 @@ public:
 
 private:
     struct Job {
-        Job(const std::function<void(size_t, size_t)>* b, size_t n_, size_t g) : body(b), n(n_), grain(g) {}
+        Job(const std::function<void(size_t, size_t)>* b, size_t n_, size_t g, int helpers)
+            : body(b), n(n_), grain(g), seats(helpers) {}
         const std::function<void(size_t, size_t)>* body;   // valid while done < n
         size_t n, grain;
         std::atomic<size_t> next{0}, done{0};
+        std::atomic<int> seats;   // workers that may still join
         void drain() {
             for (;;) {
                 const size_t i = next.fetch_add(grain, std::memory_order_relaxed);
@@ -130,7 +154,7 @@ private:
                 seen = gen_.load();
                 job = cur_;
             }
-            if (job) job->drain();
+            if (job && job->seats.fetch_sub(1, std::memory_order_relaxed) > 0) job->drain();
         }
     }
     int nw_;

@@ -30,30 +30,34 @@
  *   TCPCSUM_PRELOAD_ANY_SOCKET=1 act on every socket, not only SOCK_RAW ones
  *                                (tests run it over UDP loopback, no root)
  *   TCPCSUM_PRELOAD_STATS=1      print counters to stderr at exit
- *   TCPCSUM_PRELOAD_INPLACE=1    page-lock each packet buffer on first use and
- *                                keep it (TCPCSUM_CTX_AUTO_REGISTER): the
- *                                kernel then reads the caller's buffers in
- *                                place and stores the checks there, with no
- *                                CPU copy. Only for applications that never
- *                                free their packet buffers and do not
- *                                page-lock them themselves — the reference
- *                                qualifies (loop.c:180-183).
+ *   TCPCSUM_PRELOAD_WAIT=spin    wait for the GPU in HIP's spin (default: block,
+ *                                TCPCSUM_CTX_BLOCKING_WAIT — the thread sleeps
+ *                                while the kernel runs)
  *
- * Default: every message's bytes are copied by the library's host threads
- * into pinned staging (tcpcsum_ipv4_batch_ptrs_host), checksummed there, and
- * FILL's 2-byte checks are written back into the caller's buffers. Nothing
- * is page-locked behind the application's back. Buffers the application
- * page-locked itself (hipHostMalloc, hipHostRegister) are read in place.
- * If the GPU path cannot run, the call fails with errno = ENXIO rather than
- * sending (or accepting) packets with unchecked checksums: there is no silent
- * CPU fallback.
+ * Buffers the application page-locked (tcpcsum_host_alloc for its out-buffer
+ * pool, loop.c:180-183 — INTEGRATION.md level 2 — or its own hipHostRegister)
+ * are read and filled in place, with no copy. Any other message's bytes are
+ * copied by the library's host threads into pinned staging
+ * (tcpcsum_ipv4_batch_ptrs_host), checksummed there, and FILL's 2-byte checks
+ * are written back into the caller's buffers. Nothing is ever page-locked
+ * behind the application's back (round 3's TCPCSUM_PRELOAD_INPLACE=1, which
+ * did that, is gone with ABI v4: DESIGN.md §7). If the GPU path cannot run,
+ * the call fails with errno = ENXIO rather than sending (or accepting) packets
+ * with unchecked checksums: there is no silent CPU fallback.
  *
- * A segment passes RX verification when its TCP checksum verifies to 0, or it
- * is CHECKSUM_PARTIAL (checksum left to offload — Linux loopback does this for
- * the kernel's own segments), and (with IPHDR) its IPv4 header
- * checksum verifies. Messages that are not IPv4/TCP, or are truncated, are
- * not TCP segments the library can verify: they are passed through untouched
- * (the reference filters them itself, loop.c:319).
+ * A segment passes RX verification when its TCP checksum verifies to 0 — or it
+ * is CHECKSUM_PARTIAL (its checksum left to offload: Linux loopback does this
+ * for locally generated segments) AND both its addresses are
+ * in 127.0.0.0/8, which Linux accepts on the loopback interface only (a packet
+ * with a 127/8 source arriving on any other interface is a martian and dropped
+ * by the kernel) — and (with IPHDR) its IPv4 header checksum verifies. A
+ * forged or corrupted segment from anywhere else whose check word happens to
+ * equal the un-complemented pseudo-header fold is therefore rejected.
+ * Messages that are not IPv4/TCP are passed through untouched (the reference
+ * filters them itself, loop.c:319). IPv4/TCP messages the library cannot
+ * verify — truncated (tot_len past the bytes received), bad IHL or lengths —
+ * are counted as skipped; in drop mode they are dropped, since they would
+ * reach the application's TCP handler unverified.
  */
 #define _GNU_SOURCE
 #include <dlfcn.h>
@@ -84,7 +88,7 @@ static pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;
 static pthread_once_t g_once = PTHREAD_ONCE_INIT;
 static sendmmsg_fn real_sendmmsg;
 static recvmmsg_fn real_recvmmsg;
-static int g_tx = MODE_FILL, g_rx = MODE_OFF, g_iphdr, g_any, g_stats, g_inplace;
+static int g_tx = MODE_FILL, g_rx = MODE_OFF, g_iphdr, g_any, g_stats;
 static tcpcsum_ctx_t *g_ctx;
 static int g_ctx_failed;
 static uint16_t *g_out;     /* pinned: the kernel writes results straight here */
@@ -108,13 +112,22 @@ static int env_flag(const char *name) {
 
 static void print_stats(void) {
     if (!g_stats) return;
+    tcpcsum_ctx_stats_t cs;
+    memset(&cs, 0, sizeof cs);
+    pthread_mutex_lock(&g_mu);
+    if (g_ctx) tcpcsum_ctx_get_stats(g_ctx, &cs);
+    pthread_mutex_unlock(&g_mu);
     fprintf(stderr,
             "tcpcsum_preload: tx batches=%llu packets=%llu filled=%llu verified=%llu verify_failed=%llu "
             "skipped=%llu | rx batches=%llu packets=%llu verified=%llu verify_failed=%llu skipped=%llu "
-            "partial=%llu dropped=%llu | errors=%llu\n",
+            "partial=%llu dropped=%llu | errors=%llu | ctx in_place=%llu staged=%llu copy_threads=%llu "
+            "cpu_caller_us=%llu cpu_workers_us=%llu\n",
             g_st.tx_batches, g_st.tx_packets, g_st.tx_filled, g_st.tx_verified, g_st.tx_verify_failed,
             g_st.tx_skipped, g_st.rx_batches, g_st.rx_packets, g_st.rx_verified, g_st.rx_verify_failed,
-            g_st.rx_skipped, g_st.rx_partial, g_st.rx_dropped, g_st.errors);
+            g_st.rx_skipped, g_st.rx_partial, g_st.rx_dropped, g_st.errors,
+            (unsigned long long) cs.pkts_in_place, (unsigned long long) cs.pkts_staged,
+            (unsigned long long) cs.copy_threads, (unsigned long long) (cs.ns_cpu_caller / 1000),
+            (unsigned long long) (cs.ns_cpu_workers / 1000));
 }
 
 static void init_once(void) {
@@ -126,8 +139,9 @@ static void init_once(void) {
     g_iphdr = env_flag("TCPCSUM_PRELOAD_IPHDR");
     g_any = env_flag("TCPCSUM_PRELOAD_ANY_SOCKET");
     g_stats = env_flag("TCPCSUM_PRELOAD_STATS");
-    /* TCPCSUM_PRELOAD_COPY=1 (round 2) named what is now the default */
-    g_inplace = env_flag("TCPCSUM_PRELOAD_INPLACE") && !env_flag("TCPCSUM_PRELOAD_COPY");
+    if (env_flag("TCPCSUM_PRELOAD_INPLACE"))
+        fprintf(stderr, "tcpcsum_preload: TCPCSUM_PRELOAD_INPLACE is gone (ABI v4): buffers from "
+                        "tcpcsum_host_alloc are filled in place, all others are copied\n");
     atexit(print_stats);
 }
 
@@ -151,7 +165,8 @@ static int ensure_ctx(void) {
     if (g_ctx_failed) return -1;
     if (!g_ctx) {
         int rc = tcpcsum_ctx_create(0, 0, &g_ctx);
-        if (!rc && g_inplace) rc = tcpcsum_ctx_set_flags(g_ctx, TCPCSUM_CTX_AUTO_REGISTER);
+        const char *w = getenv("TCPCSUM_PRELOAD_WAIT");
+        if (!rc && !(w && !strcmp(w, "spin"))) rc = tcpcsum_ctx_set_flags(g_ctx, TCPCSUM_CTX_BLOCKING_WAIT);
         if (!rc) {
             g_out = (uint16_t *) tcpcsum_host_alloc(1024 * sizeof(uint16_t));
             g_status = (uint8_t *) tcpcsum_host_alloc(1024);
@@ -169,21 +184,35 @@ static int ensure_ctx(void) {
     return 0;
 }
 
+/* Message bytes as received: IPv4 carrying TCP (enough of the header to say so). */
+static int is_ipv4_tcp(const uint8_t *p, uint32_t len) {
+    return p && len >= 10 && (p[0] >> 4) == 4 && p[9] == 6;
+}
+
+/* Both addresses in 127.0.0.0/8: a segment Linux accepted on the loopback
+ * interface only (martian source anywhere else). len >= 20 (verified packets). */
+static int loopback_pair(const uint8_t *p) {
+    return p[12] == 127 && p[16] == 127;
+}
+
 /* g_mu held. Whether message k of a finished batch is kept (rx drop), and its
- * accounting. */
-static int account(int k, int fill, int is_tx) {
+ * accounting. p / len: its bytes as the GPU batch saw them. */
+static int account(int k, int fill, int is_tx, const uint8_t *p, uint32_t len) {
     const int skipped = (g_status[k] & TCPCSUM_PKT_SKIPPED) != 0;
     if (skipped) {
         if (is_tx) g_st.tx_skipped++; else g_st.rx_skipped++;
-        return 1;
+        /* an IPv4/TCP segment that could not be verified (truncated, bad IHL or
+         * lengths) is not passed on unverified in drop mode; anything else is
+         * not TCP and goes through (the reference filters it, loop.c:319) */
+        return !(g_rx == MODE_DROP && !is_tx && is_ipv4_tcp(p, len));
     }
     if (fill) {
         g_st.tx_filled++;
         return 1;
     }
-    /* CHECKSUM_PARTIAL segments (checksum left to offload, e.g. Linux
-     * loopback) are counted apart, not as corrupt */
-    const int partial = (g_status[k] & TCPCSUM_PKT_CSUM_PARTIAL) != 0;
+    /* CHECKSUM_PARTIAL segments (checksum left to offload, Linux loopback;
+     * SURVEY.md §4.5) are counted apart, not as corrupt — on 127/8 only */
+    const int partial = (g_status[k] & TCPCSUM_PKT_CSUM_PARTIAL) != 0 && loopback_pair(p);
     const int bad = (g_out[k] != 0 && !partial) || (g_status[k] & TCPCSUM_PKT_IPHDR_BAD);
     if (is_tx) { g_st.tx_verified++; if (bad) g_st.tx_verify_failed++; }
     else { g_st.rx_verified++; if (bad) g_st.rx_verify_failed++; if (partial) g_st.rx_partial++; }
@@ -199,10 +228,20 @@ static int gpu_batch(struct mmsghdr *vec, unsigned int vlen, const unsigned int 
                      unsigned char *keep) {
     void *ptrs[1024];
     uint32_t plen[1024];
+    const uint8_t *head[1024];   /* the message's first bytes, to tell IPv4/TCP from the rest */
+    uint32_t hlen[1024];
     for (unsigned int i = 0; i < vlen; ++i) {
-        const int one = vec[i].msg_hdr.msg_iovlen == 1;
-        ptrs[i] = one ? vec[i].msg_hdr.msg_iov[0].iov_base : NULL;
+        const struct msghdr *h = &vec[i].msg_hdr;
+        const int one = h->msg_iovlen == 1;
+        ptrs[i] = one ? h->msg_iov[0].iov_base : NULL;
         plen[i] = one ? lens[i] : 0;   /* < 20 bytes: SKIPPED, nothing read */
+        head[i] = h->msg_iovlen >= 1 && h->msg_iov ? (const uint8_t *) h->msg_iov[0].iov_base : NULL;
+        hlen[i] = 0;
+        if (head[i]) {
+            const size_t cap = h->msg_iov[0].iov_len;
+            const unsigned int got = is_tx ? (unsigned int) cap : vec[i].msg_len;
+            hlen[i] = (uint32_t) (got < cap ? got : cap);
+        }
     }
     pthread_mutex_lock(&g_mu);
     if (ensure_ctx()) {
@@ -221,7 +260,7 @@ static int gpu_batch(struct mmsghdr *vec, unsigned int vlen, const unsigned int 
         return -1;
     }
     for (unsigned int i = 0; i < vlen; ++i) {
-        const int ok = account((int) i, fill, is_tx);
+        const int ok = account((int) i, fill, is_tx, head[i], hlen[i]);
         if (keep) keep[i] = (unsigned char) ok;
     }
     pthread_mutex_unlock(&g_mu);

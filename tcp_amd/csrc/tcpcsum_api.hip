@@ -17,6 +17,12 @@
 #include "tcpcsum.h"
 #include "tcpcsum_internal.h"
 
+#if TCPCSUM_MEASUREMENT_BUILD
+#define TCPCSUM_PRODUCT_JSON false
+#else
+#define TCPCSUM_PRODUCT_JSON true
+#endif
+
 static_assert(sizeof(tcpcsum_desc_t) == 16, "descriptor is read as one 16-B load");
 static_assert(sizeof(tcpcsum_txseg_t) == 48, "tx descriptor is read as three 16-B loads");
 static_assert(sizeof(tcpcsum_ubatch_t) == 48 && sizeof(tcpcsum::UniformMultiEntry) == 48, "batch descriptor layout");
@@ -101,6 +107,20 @@ using tcpcsum::require_device;
 extern "C" {
 
 int tcpcsum_abi_version(void) { return TCPCSUM_ABI_VERSION; }
+
+#define TCPCSUM_STR2(x) #x
+#define TCPCSUM_STR(x) TCPCSUM_STR2(x)
+const char* tcpcsum_build_info(void) {
+    static const char info[] =
+        "{\"abi\": " TCPCSUM_STR(TCPCSUM_ABI_VERSION) ", \"src_sha256\": \"" TCPCSUM_SRC_HASH
+        "\", \"arch\": \"gfx950\", \"product\": " TCPCSUM_STR(TCPCSUM_PRODUCT_JSON)
+        ", \"knobs\": {\"TCPCSUM_MEASUREMENT_BUILD\": " TCPCSUM_STR(TCPCSUM_MEASUREMENT_BUILD)
+        ", \"TCPCSUM_TUNING_VARIANTS\": " TCPCSUM_STR(TCPCSUM_TUNING_VARIANTS)
+        ", \"TCPCSUM_TX_KNOCKOUT\": " TCPCSUM_STR(TCPCSUM_TX_KNOCKOUT)
+        ", \"TCPCSUM_WIRE_WAVES\": " TCPCSUM_STR(TCPCSUM_WIRE_WAVES)
+        ", \"TCPCSUM_TX_WAVES\": " TCPCSUM_STR(TCPCSUM_TX_WAVES) "}}";
+    return info;
+}
 
 const char* tcpcsum_strerror(int code) {
     switch (code) {

@@ -6,30 +6,31 @@
 // (loop.c:27-94). A context turns such batches into kernel launches.
 //
 // Which host memory a kernel touches, and how:
-//   * memory the caller page-locked — tcpcsum_host_alloc / hipHostMalloc, a
-//     hipHostRegister of its own, or tcpcsum_ctx_register_host — is read in
-//     place by the kernel over PCIe (zero-copy), and FILL stores the checks
-//     there;
-//   * pageable memory is never page-locked behind the caller's back and never
-//     handed to a HIP copy. CPU threads copy its bytes into the context's own
-//     pinned staging — uniform batches chunk by chunk, wire batches packet by
-//     packet (only the packets, not the slack between them) — which the kernel
-//     reads over PCIe; FILL results go back as 2-byte CPU stores at TCP+16
-//     (and IP+10), exactly where context.c:208 puts them.
-//   * opt-in only (TCPCSUM_CTX_AUTO_REGISTER): tcpcsum_ipv4_batch_ptrs_host
-//     page-locks each pageable packet buffer on first use and keeps it, which
-//     suits the reference's buffers (allocated once, never freed).
+//   * memory its owner page-locked — tcpcsum_host_alloc / hipHostMalloc, or a
+//     hipHostRegister of the application's own — is read in place by the
+//     kernel over PCIe (zero-copy), and FILL stores the checks there;
+//   * pageable memory is never page-locked and never handed to a HIP copy.
+//     CPU threads copy its bytes into the context's own pinned staging —
+//     uniform batches chunk by chunk, wire batches packet by packet (only the
+//     packets, not the slack between them) — which the kernel reads over PCIe;
+//     FILL results go back as 2-byte CPU stores at TCP+16 (and IP+10), exactly
+//     where context.c:208 puts them.
 //
-// Why no per-call page-locking (round 2 did that): a registration is visible
-// to the whole process and HIP keeps page-lock state per page, shared with
-// its own pin-in-place of pageable copy sources, which it caches and which
-// hipPointerGetAttributes does not report (tools/pin_cache_probe.cpp). A
-// hipHostRegister / hipHostUnregister of a pageable range's page hull — pages
-// that can also hold other heap objects — can therefore undo a page lock HIP
-// still counts on; a later pageable hipMemcpy through that cached pin then
-// reads an unmapped page (hipErrorIllegalAddress, seen three times in round 2
-// on exactly such copies after host-path calls). A context now locks only
-// what its caller asked it to, and unlocks only that, on request.
+// The library page-locks only memory it allocates itself (round 4). Rounds 2
+// and 3 page-locked pageable heap memory — per call (round 2), then on request
+// (tcpcsum_ctx_register_host, TCPCSUM_CTX_AUTO_REGISTER, round 3) — and a
+// later pageable HIP copy faulted (hipErrorIllegalAddress) each time, over
+// addresses those registrations had covered. GPU mappings of host memory are
+// per page; HIP pins the pages of pageable copy buffers in place behind the
+// scenes and keeps those pins cached (hipPointerGetAttributes does not show
+// them, and a hipHostRegister over them succeeds: tools/pin_cache_probe.cpp);
+// a malloc'd buffer shares its first and last page with heap neighbours. So a
+// library hipHostRegister / hipHostUnregister of heap pages can change the
+// mapping under a pin HIP still uses, and the other way round — and neither
+// side can see the other. Nothing here changes any foreign page's state
+// (host_registry.h is a lookup only), so it cannot happen through the library;
+// a caller that wants zero copy allocates its packet buffers with
+// tcpcsum_host_alloc (the pool at loop.c:180-183, INTEGRATION.md level 2).
 //
 // All checksum arithmetic runs in the gfx950 kernels of tcpcsum_kernels.hip;
 // this file reads header fields (IHL, tot_len) only to size the copies.
@@ -61,29 +62,10 @@
 
 namespace tcpcsum {
 
-// HostRegistry backend over HIP: hipHostRegister'ed pages are mapped for the
-// device (on MI355X hosts at their host address: tools/hostreg_probe.py).
+// PinnedLookup backend over HIP: where memory its owner page-locked is mapped
+// for the device (on MI355X hosts at its host address: tools/hostreg_probe.py).
+// Queries only — nothing here locks or unlocks a page.
 struct HipHostBackend {
-    int lock(uintptr_t lo, size_t bytes, intptr_t* delta) {
-        hipError_t e = hipHostRegister((void*)lo, bytes, hipHostRegisterMapped);
-        if (e != hipSuccess) {
-            (void)hipGetLastError();
-            return (int)e;
-        }
-        void* d = nullptr;
-        e = hipHostGetDevicePointer(&d, (void*)lo, 0);
-        if (e != hipSuccess || !d) {
-            (void)hipGetLastError();
-            (void)hipHostUnregister((void*)lo);
-            (void)hipGetLastError();
-            return (int)(e != hipSuccess ? e : hipErrorInvalidValue);
-        }
-        *delta = (intptr_t)d - (intptr_t)lo;
-        return 0;
-    }
-    void unlock(uintptr_t lo) {
-        if (hipHostUnregister((void*)lo) != hipSuccess) (void)hipGetLastError();   // nothing to undo
-    }
     bool pinned_extent(uintptr_t p, uintptr_t* lo, uintptr_t* hi, intptr_t* delta) {
         hipPointerAttribute_t a;
         bool ok = hipPointerGetAttributes(&a, (const void*)p) == hipSuccess && a.type == hipMemoryTypeHost &&
@@ -153,10 +135,6 @@ using tcpcsum::get_tuning;
 using tcpcsum::hip_fail;
 using tcpcsum::require_device;
 
-// Auto-registration budget (TCPCSUM_CTX_AUTO_REGISTER): the reference's two
-// pools are 2 x 1024 x 32 KiB = 64 MiB (loop.c:180-183); past this much, new
-// buffers are copied instead of page-locked.
-constexpr uint64_t kAutoRegisterBudget = 256ull << 20;
 // Staging chunk per pipeline slot for pageable uniform batches (0 = default).
 constexpr size_t kDefaultChunk = 16u << 20;
 
@@ -182,8 +160,15 @@ struct tcpcsum_ctx {
     std::vector<uint32_t> g_len;
     tcpcsum::Tuning tune;
     tcpcsum::HipHostBackend backend;
-    tcpcsum::HostRegistry<tcpcsum::HipHostBackend> reg{backend};
+    tcpcsum::PinnedLookup<tcpcsum::HipHostBackend> pinned{backend};
     std::unique_ptr<tcpcsum::CopyPool> pool;
+    // threads a staged wire batch copies on, the caller included (TCPCSUM_HOST_WIRE_THREADS):
+    // a releaseSend batch is ~1.5 MB, where extra threads cost more CPU than they save time
+    int wire_threads = 1;
+    int stage_threads = 1;   // the current staged batch's: wire_threads, or all for a large batch
+    // TCPCSUM_CTX_BLOCKING_WAIT: wait for the device by sleeping on this event
+    // (hipEventBlockingSync) instead of HIP's spin-wait in hipStreamSynchronize
+    hipEvent_t done_ev = nullptr;
     bool nt_copy = true;   // streaming stores for the uniform chunks (TCPCSUM_HOST_NT=0: plain memcpy)
     bool stage_one_pass = true;   // wire staging laid out by bounds, one pass (TCPCSUM_HOST_STAGE_PASSES=2: by lengths)
     bool uniform_dma = true;   // staged uniform chunks go to HBM by DMA (TCPCSUM_HOST_DMA=0: kernel reads them over PCIe)
@@ -242,13 +227,34 @@ void par_copy(tcpcsum_ctx* c, void* dst, const void* src, size_t n, bool nt = fa
     c->stats.ns_copy += tcpcsum::now_ns() - t0;
 }
 
-// hipStreamSynchronize, timed into stats.ns_wait.
+// Wait for everything queued on st, timed into stats.ns_wait: hipStreamSynchronize
+// (HIP spins), or with TCPCSUM_CTX_BLOCKING_WAIT a blocking-sync event (the
+// thread sleeps until the device signals).
 hipError_t wait_stream(tcpcsum_ctx* c, hipStream_t st) {
     const uint64_t t0 = tcpcsum::now_ns();
-    const hipError_t e = hipStreamSynchronize(st);
+    hipError_t e;
+    if (c->flags & TCPCSUM_CTX_BLOCKING_WAIT) {
+        e = hipEventRecord(c->done_ev, st);
+        if (e == hipSuccess) e = hipEventSynchronize(c->done_ev);
+    } else {
+        e = hipStreamSynchronize(st);
+    }
     c->stats.ns_wait += tcpcsum::now_ns() - t0;
     return e;
 }
+
+// CPU time of the calling thread inside one host call, into stats.ns_cpu_caller.
+struct CallerCpu {
+    tcpcsum_ctx* c;
+    uint64_t t0;
+    static uint64_t now() {
+        timespec ts;
+        clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+        return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+    }
+    explicit CallerCpu(tcpcsum_ctx* ctx) : c(ctx), t0(now()) {}
+    ~CallerCpu() { c->stats.ns_cpu_caller += now() - t0; }
+};
 
 int ensure_pkt_arrays(tcpcsum_ctx* c, uint64_t n) {
     hipError_t e = c->p_off.ensure(n * sizeof(uint64_t));
@@ -281,6 +287,7 @@ inline uint32_t copy_len(const uint8_t* ip, uint64_t bound) {
 // lengths are read first and the copies packed by them, two passes. Sets
 // k_off / k_len of every staged packet.
 constexpr size_t kStageByBound = 64u << 20;
+constexpr size_t kSmallStage = 8u << 20;
 int stage_packets(tcpcsum_ctx* c, uint64_t* k_off, uint32_t* k_len, size_t* staged_bytes) {
     const size_t m = c->g_idx.size();
     *staged_bytes = 0;
@@ -292,10 +299,12 @@ int stage_packets(tcpcsum_ctx* c, uint64_t* k_off, uint32_t* k_len, size_t* stag
         span += ((size_t)c->g_len[k] + 15u) & ~(size_t)15u;
     }
     const bool by_bound = span <= kStageByBound && c->stage_one_pass;
+    // small (releaseSend-sized) batches copy on wire_threads; large ones on every copy thread
+    c->stage_threads = span <= kSmallStage ? c->wire_threads : 0;
     if (!by_bound) {
         c->pool->run(m, 64, [&](size_t lo, size_t hi) {
             for (size_t k = lo; k < hi; ++k) c->g_len[k] = copy_len(c->g_src[k], c->g_len[k]);
-        });
+        }, c->stage_threads);
         span = 0;
         for (size_t k = 0; k < m; ++k) {
             c->g_off[k] = span;
@@ -320,7 +329,7 @@ int stage_packets(tcpcsum_ctx* c, uint64_t* k_off, uint32_t* k_len, size_t* stag
             b += c->g_len[k];
         }
         copied.fetch_add(b, std::memory_order_relaxed);
-    });
+    }, c->stage_threads);
     c->stats.ns_copy += tcpcsum::now_ns() - t0;
     c->stats.pkts_staged += m;
     c->stats.bytes_staged += copied.load();
@@ -363,7 +372,7 @@ void write_back_checks(tcpcsum_ctx* c, const uint8_t* status, bool iphdr) {
             memcpy(dp + tcp + 16, sp + tcp + 16, 2);   // context.c:208: native u16 at TCP+16
             if (iphdr) memcpy(dp + 10, sp + 10, 2);
         }
-    });
+    }, c->stage_threads);
     c->stats.ns_copy += tcpcsum::now_ns() - t0;
 }
 
@@ -406,7 +415,9 @@ int tcpcsum_ctx_create(int device, size_t scratch_bytes, tcpcsum_ctx_t** out) {
         delete c;
         return TCPCSUM_ENOMEM;
     }
-    c->stats.copy_threads = (uint64_t)c->pool->threads();
+    c->wire_threads = std::max(1, std::min(c->pool->threads(), tcpcsum::env_int("TCPCSUM_HOST_WIRE_THREADS", 1)));
+    c->stats.copy_threads = (uint64_t)c->wire_threads;
+    c->stats.bulk_threads = (uint64_t)c->pool->threads();
     c->nt_copy = tcpcsum::env_int("TCPCSUM_HOST_NT", 1) != 0;
     c->stage_one_pass = tcpcsum::env_int("TCPCSUM_HOST_STAGE_PASSES", 1) == 1;
     c->uniform_dma = tcpcsum::env_int("TCPCSUM_HOST_DMA", 1) != 0;
@@ -418,6 +429,11 @@ int tcpcsum_ctx_create(int device, size_t scratch_bytes, tcpcsum_ctx_t** out) {
             return hip_fail(e);
         }
     }
+    e = hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming | hipEventBlockingSync);
+    if (e != hipSuccess) {
+        tcpcsum_ctx_destroy(c);
+        return hip_fail(e);
+    }
     *out = c;
     return TCPCSUM_OK;
 }
@@ -427,7 +443,7 @@ void tcpcsum_ctx_destroy(tcpcsum_ctx_t* c) {
     DeviceGuard g(c->device);
     for (int i = 0; i < 2; ++i)
         if (c->st[i]) hipStreamSynchronize(c->st[i]);
-    c->reg.release(0, 0);
+    if (c->done_ev) hipEventDestroy(c->done_ev);
     for (int i = 0; i < 2; ++i) {
         if (c->d_slot[i]) hipFree(c->d_slot[i]);
         if (c->slot_ev[i]) hipEventDestroy(c->slot_ev[i]);
@@ -446,7 +462,7 @@ int tcpcsum_ctx_set_tuning(tcpcsum_ctx_t* c, const tcpcsum_tuning_t* tune) {
 }
 
 int tcpcsum_ctx_set_flags(tcpcsum_ctx_t* c, uint32_t flags) {
-    if (!c || (flags & ~(uint32_t)TCPCSUM_CTX_AUTO_REGISTER)) return TCPCSUM_EINVAL;
+    if (!c || (flags & ~(uint32_t)TCPCSUM_CTX_BLOCKING_WAIT)) return TCPCSUM_EINVAL;
     std::lock_guard<std::mutex> lk(c->mu);
     c->flags = flags;
     return TCPCSUM_OK;
@@ -455,8 +471,7 @@ int tcpcsum_ctx_set_flags(tcpcsum_ctx_t* c, uint32_t flags) {
 int tcpcsum_ctx_get_stats(tcpcsum_ctx_t* c, tcpcsum_ctx_stats_t* out) {
     if (!c || !out) return TCPCSUM_EINVAL;
     std::lock_guard<std::mutex> lk(c->mu);
-    c->stats.registered_ranges = c->reg.owned_ranges();
-    c->stats.registered_bytes = c->reg.owned_bytes();
+    c->stats.ns_cpu_workers = c->pool->worker_cpu_ns();
     *out = c->stats;
     return TCPCSUM_OK;
 }
@@ -487,6 +502,7 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t st
     if (n == 0) return TCPCSUM_OK;
     if (!h_base || !h_out || len > (uint32_t)INT_MAX) return TCPCSUM_EINVAL;
     std::lock_guard<std::mutex> lk(c->mu);
+    CallerCpu cpu(c);
     DeviceGuard g(c->device);
     const tcpcsum::Tuning tu = c->tune;
     c->stats.batches++;
@@ -602,6 +618,7 @@ int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t* c, void* h_pkts, size_t region_bytes,
     for (uint64_t i = 0; i < n; ++i)
         if (h_pkt_off[i] > region_bytes || region_bytes - h_pkt_off[i] < 20u) return TCPCSUM_EINVAL;
     std::lock_guard<std::mutex> lk(c->mu);
+    CallerCpu cpu(c);
     DeviceGuard g(c->device);
     hipStream_t st = c->st[0];
     c->stats.batches++;
@@ -657,25 +674,23 @@ int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t* c, void* h_pkts, size_t region_bytes,
 }
 
 // Wire batch over the caller's own per-packet buffers (the loop's layout).
-// Each packet is read in place when one page-locked mapping covers it (the
-// context's registrations, or memory someone else page-locked), else copied
-// into pinned staging — or, with TCPCSUM_CTX_AUTO_REGISTER, its pages are
-// locked now and kept (within kAutoRegisterBudget).
+// Each packet is read in place when one page-locked allocation covers it
+// (memory its owner page-locked: tcpcsum_host_alloc, hipHostRegister), else
+// copied into pinned staging and its check stored back.
 int tcpcsum_ipv4_batch_ptrs_host(tcpcsum_ctx_t* c, void* const* h_pkts, const uint32_t* h_lens, uint64_t n, int mode,
                                  uint16_t* h_out, uint8_t* h_status) {
     if (!c) return TCPCSUM_EINVAL;
     if (n == 0) return TCPCSUM_OK;
     if (!h_pkts || !h_lens || (mode & ~3)) return TCPCSUM_EINVAL;
     std::lock_guard<std::mutex> lk(c->mu);
+    CallerCpu cpu(c);
     DeviceGuard g(c->device);
     hipStream_t st = c->st[0];
     c->stats.batches++;
     int rc = ensure_pkt_arrays(c, n);
     if (rc) return rc;
-    const bool may_lock = (c->flags & TCPCSUM_CTX_AUTO_REGISTER) != 0;
-    // memory page-locked by someone else is looked up afresh each batch (its
-    // owner may have freed it)
-    c->reg.forget_foreign();
+    // page-locked memory is looked up afresh each batch (its owner may have freed it)
+    c->pinned.begin_batch();
     uint64_t* k_off = (uint64_t*)c->p_off.h;
     uint32_t* k_len = (uint32_t*)c->p_len.h;
     c->g_idx.clear();
@@ -694,7 +709,7 @@ int tcpcsum_ipv4_batch_ptrs_host(tcpcsum_ctx_t* c, void* const* h_pkts, const ui
             continue;
         }
         uintptr_t dev = 0;
-        if (c->reg.resolve((uintptr_t)p, len, may_lock, kAutoRegisterBudget, &dev) == 0) {
+        if (c->pinned.resolve((uintptr_t)p, len, &dev) == 0) {
             k_off[i] = dev;
             k_len[i] = len;
             foot += len;
@@ -707,7 +722,6 @@ int tcpcsum_ipv4_batch_ptrs_host(tcpcsum_ctx_t* c, void* const* h_pkts, const ui
             c->g_off.push_back(0);
         }
     }
-    if (c->reg.last_lock_error()) tcpcsum::note_hip_error(c->reg.last_lock_error());
     c->stats.pkts_in_place += in_place;
     uint16_t* zout = h_out ? (uint16_t*)pinned_dev_ptr(h_out, n * sizeof(uint16_t)) : nullptr;
     uint8_t* zst = h_status ? (uint8_t*)pinned_dev_ptr(h_status, n) : nullptr;
@@ -723,35 +737,6 @@ int tcpcsum_ipv4_batch_ptrs_host(tcpcsum_ctx_t* c, void* const* h_pkts, const ui
         write_back_checks(c, zst ? h_status : c->p_stat.h, (mode & TCPCSUM_IPV4_IPHDR) != 0);
     if (h_out && !zout) memcpy(h_out, c->p_out.h, n * sizeof(uint16_t));
     if (h_status && !zst) memcpy(h_status, c->p_stat.h, n);
-    return TCPCSUM_OK;
-}
-
-int tcpcsum_ctx_register_host(tcpcsum_ctx_t* c, void* p, size_t bytes) {
-    if (!c || !p || !bytes) return TCPCSUM_EINVAL;
-    std::lock_guard<std::mutex> lk(c->mu);
-    DeviceGuard g(c->device);
-    const int rc = c->reg.lock_range((uintptr_t)p, bytes);
-    if (rc) {
-        tcpcsum::note_hip_error(rc);
-        return TCPCSUM_EHIP;
-    }
-    return TCPCSUM_OK;
-}
-
-int tcpcsum_ctx_unregister_host(tcpcsum_ctx_t* c, void* p, size_t bytes) {
-    if (!c) return TCPCSUM_EINVAL;
-    std::lock_guard<std::mutex> lk(c->mu);
-    DeviceGuard g(c->device);
-    for (int i = 0; i < 2; ++i) (void)hipStreamSynchronize(c->st[i]);
-    c->reg.release((uintptr_t)p, bytes);
-    return TCPCSUM_OK;
-}
-
-int tcpcsum_ctx_registered(tcpcsum_ctx_t* c, uint64_t* ranges, uint64_t* bytes) {
-    if (!c) return TCPCSUM_EINVAL;
-    std::lock_guard<std::mutex> lk(c->mu);
-    if (ranges) *ranges = c->reg.owned_ranges();
-    if (bytes) *bytes = c->reg.owned_bytes();
     return TCPCSUM_OK;
 }
 

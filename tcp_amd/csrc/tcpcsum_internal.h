@@ -6,6 +6,42 @@
 
 #include "tcpcsum.h"
 
+// ---------------------------------------------------------------- build knobs
+// Compile-time knobs. A product library leaves every one at its default; only a
+// measurement build (tools/*_ab.py, -DTCPCSUM_MEASUREMENT_BUILD=1) may set them,
+// and tcpcsum_build_info() reports them either way ("product": false there).
+//   TCPCSUM_TUNING_VARIANTS  1: also compile the pipelined / default-load kernel
+//                            variants the TCPCSUM_TUNE_PIPE_* / NT_* flags select
+//   TCPCSUM_TX_KNOCKOUT      parts of the segment builder switched off to see what
+//                            its time is made of — the output is then WRONG. 1:
+//                            ragged-end stores, 2: header stores, 4: second source
+//                            loads, 8: full-chunk stores
+//   TCPCSUM_WIRE_WAVES       minimum waves per SIMD asked of the lane-group wire
+//   TCPCSUM_TX_WAVES         kernel / the segment builder (1 = the compiler's choice)
+#ifndef TCPCSUM_MEASUREMENT_BUILD
+#define TCPCSUM_MEASUREMENT_BUILD 0
+#endif
+#ifndef TCPCSUM_TUNING_VARIANTS
+#define TCPCSUM_TUNING_VARIANTS 0
+#endif
+#ifndef TCPCSUM_TX_KNOCKOUT
+#define TCPCSUM_TX_KNOCKOUT 0
+#endif
+#ifndef TCPCSUM_WIRE_WAVES
+#define TCPCSUM_WIRE_WAVES 1
+#endif
+#ifndef TCPCSUM_TX_WAVES
+#define TCPCSUM_TX_WAVES 1
+#endif
+#if !TCPCSUM_MEASUREMENT_BUILD && \
+    (TCPCSUM_TUNING_VARIANTS != 0 || TCPCSUM_TX_KNOCKOUT != 0 || TCPCSUM_WIRE_WAVES != 1 || TCPCSUM_TX_WAVES != 1)
+#error "tuning / knock-out / waves knobs are for measurement builds only (-DTCPCSUM_MEASUREMENT_BUILD=1), never a product library"
+#endif
+// Hash of the sources the library was compiled from (the Makefile passes it).
+#ifndef TCPCSUM_SRC_HASH
+#define TCPCSUM_SRC_HASH "unknown"
+#endif
+
 namespace tcpcsum {
 
 // 256 CUs x 8 workgroups of 256 threads = 32 waves per CU: the whole grid is

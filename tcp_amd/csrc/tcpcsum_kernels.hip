@@ -34,24 +34,9 @@
 #include "tcpcsum.h"
 #include "tcpcsum_internal.h"
 
-#ifndef TCPCSUM_TUNING_VARIANTS
-#define TCPCSUM_TUNING_VARIANTS 0
-#endif
-// Measurement builds only (tools/tx_ab.py): parts of the segment builder
-// switched off to see what its time is made of — the output is then WRONG.
-// 1: ragged-end stores, 2: header stores, 4: second source loads (B = A),
-// 8: full-chunk stores. 0 in every product build.
-#ifndef TCPCSUM_TX_KNOCKOUT
-#define TCPCSUM_TX_KNOCKOUT 0
-#endif
-// Measurement builds only: minimum waves per SIMD asked of the lane-group wire
-// kernel (its register budget); 1 = the compiler's choice, as in every product build.
-#ifndef TCPCSUM_WIRE_WAVES
-#define TCPCSUM_WIRE_WAVES 1
-#endif
-#ifndef TCPCSUM_TX_WAVES   // the same for the segment builder
-#define TCPCSUM_TX_WAVES 1
-#endif
+// The compile-time knobs (TCPCSUM_TUNING_VARIANTS, TCPCSUM_TX_KNOCKOUT,
+// TCPCSUM_WIRE_WAVES, TCPCSUM_TX_WAVES) live in tcpcsum_internal.h: a product
+// build refuses any of them set, tcpcsum_build_info() reports them.
 
 namespace tcpcsum {
 
@@ -879,6 +864,13 @@ struct IpPkt {
     bool hdr;     // its 20-byte IP header is readable
 };
 
+// x, computed here: an identity DPP move (quad_perm 0,1,2,3) is convergent, so
+// the compiler can neither sink the computation of x past control flow nor
+// rematerialize it from its operands later — it holds one VGPR from here on.
+__device__ __forceinline__ uint32_t pin_vgpr(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xE4, 0xF, 0xF, false);
+}
+
 // A native u16 at p: one 2-byte store when p is even, two byte stores otherwise.
 __device__ __forceinline__ void store_u16(uint8_t* p, uint16_t v) {
     if (((uintptr_t)p & 1u) == 0) {
@@ -889,17 +881,52 @@ __device__ __forceinline__ void store_u16(uint8_t* p, uint16_t v) {
     }
 }
 
-// The same, written through (sc0 sc1) rather than left dirty in L2: a lone
-// 2-byte store per packet in the middle of a read stream costs less that way
-// (tools/fill_store_probe.hip: +62 vs +72 us per 1M stores).
-__device__ __forceinline__ void store_u16_wt(uint8_t* p, uint16_t v) {
-    const uint32_t w = v;
-    if (((uintptr_t)p & 1u) == 0) {
-        asm volatile("global_store_short %0, %1, off sc0 sc1" ::"v"(p), "v"(w) : "memory");
+// Write-through (sc0 sc1) stores, rather than lines left dirty in L2 — all
+// compiler-visible, so the hazard recognizer owns the store-data wait states
+// (round 3's inline-asm stores hid them: the compiler reused a dwordx4 store's
+// data VGPRs one instruction later and 4 of 1M packets were corrupted until a
+// hand-counted s_nop went in). A relaxed atomic store at system scope is
+// exactly global_store_{byte,short} sc0 sc1 on gfx950 (the memory model's
+// system-scope store: no wait, no fence); a 16-byte one is a raw buffer store
+// with cache policy sc0|sc1 (CPol bits 1 | 16).
+constexpr int kCpolSc0Sc1 = 1 | 16;
+
+template <class T>
+__device__ __forceinline__ void stg_wt(uint8_t* p, T v) {
+    __hip_atomic_store((gptr<T>)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// 16 bytes at the 16-B aligned p, written through. A buffer store's base sits in
+// scalar registers, so it is the wave's: its first active lane's address less
+// 2 GiB, and each lane stores at its 32-bit offset from there. A lane whose
+// address lies outside that 4 GiB window (never, for the packets of one wave
+// tile in any batch layout tested; possible only for pointer batches scattered
+// over more than 2 GiB) takes a default-policy store — same bytes, only not
+// written through.
+__device__ __forceinline__ void stg_wt16(uint8_t* p, u32x4 v) {
+    const uint64_t a = (uint64_t)(uintptr_t)p;
+    const uint64_t first = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32) |
+                           (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint64_t base = first > 0x80000000ull ? first - 0x80000000ull : 0ull;
+    const uint64_t rel = a - base;
+    if (a >= base && rel <= 0xFFFFFF00ull) {
+        const __amdgpu_buffer_rsrc_t r =
+            __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>((uintptr_t)base), 0, -1, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)(uint32_t)rel, 0, kCpolSc0Sc1);
     } else {
-        const uint32_t hi = w >> 8;
-        asm volatile("global_store_byte %0, %1, off sc0 sc1" ::"v"(p), "v"(w) : "memory");
-        asm volatile("global_store_byte %0, %1, off sc0 sc1" ::"v"(p + 1), "v"(hi) : "memory");
+        *(gptr<u32x4>)(p) = v;
+    }
+}
+
+// A native u16 at p, written through: a lone 2-byte store per packet in the
+// middle of a read stream costs less that way (tools/fill_store_probe.hip: +62
+// vs +72 us per 1M stores).
+__device__ __forceinline__ void store_u16_wt(uint8_t* p, uint16_t v) {
+    if (((uintptr_t)p & 1u) == 0) {
+        stg_wt<uint16_t>(p, v);
+    } else {
+        stg_wt<uint8_t>(p, (uint8_t)(v & 0xffu));
+        stg_wt<uint8_t>(p + 1, (uint8_t)(v >> 8));
     }
 }
 
@@ -1074,7 +1101,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(wire_waves(
         const uint32_t th = ihl * 4u;   // TCP start, packet-relative (even)
         const bool odd = (m & 1u) != 0;
         const uint32_t sa = grp_bytes4<G, C>(v[u], gbase, m + 12u), da = grp_bytes4<G, C>(v[u], gbase, m + 16u);
-        const uint32_t check_dw = grp_bytes4<G, C>(v[u], gbase, m + th + 16u);   // check | urg_ptr
+        const uint32_t tcp_len = tot - th;
+        const uint32_t len_be = ((tcp_len & 0xffu) << 8) | ((tcp_len >> 8) & 0xffu);   // htons
+        // context.c:104-119 closed form: six native u16 words of the pseudo header.
+        // Pinned here (pin_vgpr): left to itself the compiler computes it — and the
+        // check word — after the long-packet rounds below, keeping the two raw
+        // dwords of each field live across them, which spilled two VGPRs of the
+        // FILL kernel to scratch at its 5 waves per SIMD.
+        const uint32_t ps32 = pin_vgpr((sa & 0xffffu) + (sa >> 16) + (da & 0xffffu) + (da >> 16) + 0x0600u + len_be);
+        const uint32_t check_dw = pin_vgpr(grp_bytes4<G, C>(v[u], gbase, m + th + 16u));   // check | urg_ptr
         const uint32_t check_word = check_dw & 0xffffu;
         const uint32_t nch_tot = (m + tot + 15u) >> 4;
         if (nch_tot > p[u].spec) {   // longer than its span hint (group-uniform, rare)
@@ -1141,10 +1176,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(wire_waves(
         }
         W = group_sum64<G>(W);
         O = odd ? group_sum64<G>(O) : 0;
-        const uint32_t tcp_len = tot - th;
-        const uint32_t len_be = ((tcp_len & 0xffu) << 8) | ((tcp_len >> 8) & 0xffu);   // htons
-        // context.c:104-119 closed form: six native u16 words of the pseudo header.
-        const uint64_t ps = (sa & 0xffffu) + (sa >> 16) + (da & 0xffffu) + (da >> 16) + 0x0600u + len_be;
+        const uint64_t ps = ps32;
         uint64_t S = combine(ps, W, O, odd);
         // FILL: the reference sums with check == 0 (context.c:182); TCP+16 is an
         // even relative offset, so its native word contributes exactly check_word.
@@ -1197,13 +1229,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(wire_waves(
                         u32x4 x = v[u][k];
                         if (idx == (cpos >> 4)) patch(x, cpos, (uint32_t)d.c);
                         if (iphdr && idx == (ipos >> 4)) patch(x, ipos, (uint32_t)ic_fill);
-                        uint8_t* dst = ip - m + (uint64_t)idx * 16u;
-                        // the compiler cannot see into the asm, so it does not keep the
-                        // VMEM-store data hazard (a VALU write to the store's data VGPRs
-                        // right after a >64-bit store corrupts the stored dwords): the
-                        // s_nop gives the store its wait states before the VGPRs are reused
-                        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 3" ::"v"(dst), "v"(x)
-                                     : "memory");
+                        stg_wt16(ip - m + (uint64_t)idx * 16u, x);
                     }
                 }
                 d.fill = false;   // stored
@@ -1460,8 +1486,7 @@ __device__ __forceinline__ u32x4 tx_next_chunk(const u32x4 (&a)[C], int k, const
 
 // Phase 1 for a full chunk already loaded: shift into place, store, sum.
 // SP: store policy — 0 default (write-back in L2), 1 non-temporal, 2 written
-// through (sc0 sc1; inline asm, so the s_nop gives the store its data wait
-// states before the compiler reuses the VGPRs — see k_ipv4's line store).
+// through (sc0 sc1, stg_wt16).
 template <int SP>
 __device__ __forceinline__ void tx_full_chunk(const TxPkt& p, uint32_t idx, const u32x4 A, const u32x4 B,
                                               uint32_t& wsum, uint32_t& osum) {
@@ -1471,7 +1496,7 @@ __device__ __forceinline__ void tx_full_chunk(const TxPkt& p, uint32_t idx, cons
     } else if constexpr (SP == 1) {
         __builtin_nontemporal_store(v, d);
     } else if constexpr (SP == 2) {
-        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 3" ::"v"(d), "v"(v) : "memory");
+        stg_wt16(reinterpret_cast<uint8_t*>(d), v);
     } else {
         *d = v;
     }

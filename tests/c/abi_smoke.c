@@ -26,6 +26,8 @@ static int fails;
 int main(int argc, char **argv) {
     int gpu = argc > 1 && strcmp(argv[1], "--gpu") == 0;
     CHECK(tcpcsum_abi_version() == TCPCSUM_ABI_VERSION);
+    CHECK(strstr(tcpcsum_build_info(), "\"product\": true") != NULL);
+    printf("build: %s\n", tcpcsum_build_info());
     /* SURVEY.md Appendix A KATs (from the reference's own code) */
     CHECK(tcpcsum_continue(0, "\0\0", 2) == 0xffff);
     CHECK(tcpcsum_continue(0, "\0\0\x7f", 3) == 0xff80);
@@ -80,11 +82,24 @@ int main(int argc, char **argv) {
         }
         uint16_t pout[P];
         uint8_t pst[P];
-        /* pass 0: default (packets copied through the context's pinned staging,
-         * nothing page-locked); pass 1: TCPCSUM_CTX_AUTO_REGISTER (each buffer
-         * page-locked on first use and filled in place) */
-        for (int pass = 0; pass < 2; ++pass) {
-            CHECK(tcpcsum_ctx_set_flags(ctx, pass ? TCPCSUM_CTX_AUTO_REGISTER : 0u) == TCPCSUM_OK);
+        /* pass 0: default (the malloc'd packets copied through the context's
+         * pinned staging, nothing page-locked); pass 1: the same packets in an
+         * out-buffer pool from tcpcsum_host_alloc (INTEGRATION.md level 2: the
+         * pool at loop.c:180-183), filled in place, with the blocking wait */
+        uint8_t *pool = (uint8_t *) tcpcsum_host_alloc((size_t) P * 32768);
+        CHECK(pool != NULL);
+        void *mal[P];
+        for (int i = 0; i < P; ++i) mal[i] = pkt[i];
+        for (int pass = 0; pass < 2 && pool; ++pass) {
+            if (pass == 1)
+                for (int i = 0; i < P; ++i) {
+                    memcpy(pool + (size_t) i * 32768, mal[i], 32768);
+                    pkt[i] = pool + (size_t) i * 32768;
+                }
+            CHECK(tcpcsum_ctx_set_flags(ctx, pass ? TCPCSUM_CTX_BLOCKING_WAIT : 0u) == TCPCSUM_OK);
+            CHECK(tcpcsum_ctx_set_flags(ctx, 1u) == TCPCSUM_EINVAL);   /* ABI v3's AUTO_REGISTER: gone */
+            tcpcsum_ctx_stats_t st0;
+            CHECK(tcpcsum_ctx_get_stats(ctx, &st0) == TCPCSUM_OK);
             CHECK(tcpcsum_ipv4_batch_ptrs_host(ctx, pkt, plen, P, TCPCSUM_IPV4_FILL, pout, pst) == TCPCSUM_OK);
             int pbad = 0;
             for (int i = 0; i < P; ++i) {
@@ -98,18 +113,18 @@ int main(int argc, char **argv) {
                                         (const char *) b + 20, (int) plen[i] - 20);
                 pbad += got != want || pout[i] != want || pst[i] != TCPCSUM_PKT_OK;
             }
-            uint64_t nreg = 0, nbytes = 0;
             tcpcsum_ctx_stats_t st;
-            CHECK(tcpcsum_ctx_registered(ctx, &nreg, &nbytes) == TCPCSUM_OK);
             CHECK(tcpcsum_ctx_get_stats(ctx, &st) == TCPCSUM_OK);
-            if (pass == 0) CHECK(nreg == 0 && nbytes == 0 && st.pkts_staged == P && st.pkts_in_place == 0);
-            else CHECK(nreg > 0 && nbytes >= P * 4096u && st.pkts_in_place == P);
+            const uint64_t staged = st.pkts_staged - st0.pkts_staged, inplace = st.pkts_in_place - st0.pkts_in_place;
+            if (pass == 0) CHECK(staged == P && inplace == 0);
+            else CHECK(inplace == P && staged == 0);
+            CHECK(st.ns_cpu_caller > st0.ns_cpu_caller);
             CHECK(pbad == 0);
-            printf("gpu pointer-batch (%s) mismatches: %d / %d (%llu registrations)\n", pass ? "in place" : "staged",
-                   pbad, P, (unsigned long long) nreg);
+            printf("gpu pointer-batch (%s) mismatches: %d / %d (caller cpu %.1f us)\n", pass ? "in place" : "staged",
+                   pbad, P, (st.ns_cpu_caller - st0.ns_cpu_caller) / 1e3);
         }
-        CHECK(tcpcsum_ctx_unregister_host(ctx, NULL, 0) == TCPCSUM_OK);
-        for (int i = 0; i < P; ++i) free(pkt[i]);
+        for (int i = 0; i < P; ++i) free(mal[i]);
+        tcpcsum_host_free(pool);
         tcpcsum_ctx_destroy(ctx);
         free(h); free(ref); free(got); free(ss);
     }

@@ -9,6 +9,7 @@
 #include "../../tcp_amd/csrc/copy_pool.h"
 
 #include <cstdio>
+#include <set>
 #include <vector>
 
 static int fails = 0;
@@ -20,14 +21,20 @@ static int fails = 0;
         }                                                               \
     } while (0)
 
-static void exactly_once(tcpcsum::CopyPool& pool, size_t n, size_t grain) {
+static void exactly_once(tcpcsum::CopyPool& pool, size_t n, size_t grain, int max_threads = 0) {
     std::vector<std::atomic<uint32_t>> hit(n);
     for (auto& h : hit) h.store(0, std::memory_order_relaxed);
+    std::mutex m;
+    std::set<std::thread::id> who;
     pool.run(n, grain, [&](size_t lo, size_t hi) {
         EXPECT(lo < hi && hi <= n);
         for (size_t i = lo; i < hi; ++i) hit[i].fetch_add(1, std::memory_order_relaxed);
-    });
+        std::lock_guard<std::mutex> lk(m);
+        who.insert(std::this_thread::get_id());
+    }, max_threads);
     for (size_t i = 0; i < n; ++i) EXPECT(hit[i].load(std::memory_order_relaxed) == 1u);
+    if (max_threads > 0) EXPECT(who.size() <= (size_t)max_threads);   // never more threads than allowed
+    if (max_threads == 1 && n) EXPECT(who.size() == 1 && *who.begin() == std::this_thread::get_id());
 }
 
 int main() {
@@ -37,6 +44,10 @@ int main() {
         for (int rep = 0; rep < 20; ++rep)
             for (size_t n : sizes)
                 for (size_t g : {(size_t)1, (size_t)16, (size_t)64, (size_t)4096}) exactly_once(pool, n, g);
+        // at most max_threads participants (the caller included); 1 = the caller alone
+        for (int rep = 0; rep < 10; ++rep)
+            for (int mt : {1, 2, 3, 4, 9}) exactly_once(pool, 20000, 16, mt);
+        EXPECT(pool.worker_cpu_ns() > 0);   // the workers ran and their CPU clocks are read
         // idle longer than the spin: the workers sleep on the condition variable and are woken
         for (int rep = 0; rep < 5; ++rep) {
             std::this_thread::sleep_for(std::chrono::milliseconds(2));

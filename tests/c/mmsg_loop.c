@@ -3,7 +3,7 @@
  * does (loop.c:27-94 releaseSend, loop.c:22-25 fetchPackageBatch), over UDP
  * loopback so no root is needed. Run under LD_PRELOAD=libtcpcsum_preload.so.
  *
- *   mmsg_loop <npkts> <out-file> [cpu-checks | corrupt | trunc]
+ *   mmsg_loop <npkts> <out-file> [cpu-checks | corrupt | trunc | forge | plain] [pinned]
  *
  * Builds npkts IPv4/TCP packets in separate 32 KiB malloc'd buffers (as
  * loop.c:180-183 allocates them) with the reference's framing
@@ -14,7 +14,17 @@
  * so those no longer verify; the receiver then expects only the others (the
  * interposer's TCPCSUM_PRELOAD_RX=drop). "trunc": CPU checks, and every
  * packet received into a 600-byte buffer with MSG_TRUNC, so a longer datagram
- * is cut short while msg_len reports its full length. Sends them with sendmmsg in batches
+ * is cut short while msg_len reports its full length. "forge": CPU checks,
+ * except that every 7th packet (i % 7 == 3) carries a forged CHECKSUM_PARTIAL
+ * check word (the un-complemented pseudo-header fold, which is what Linux
+ * loopback leaves for offload) from a non-loopback source, 192.0.2.1, and
+ * every 7th packet at i % 7 == 5 a genuine-looking one with both addresses
+ * in 127/8 (daddr 127.x.y.z). "pinned": the out-buffers are carved from one
+ * tcpcsum_host_alloc pool (INTEGRATION.md level 2: loop.c:180-183 allocating
+ * its pool page-locked), so the interposer fills them in place.
+ * Under TCPCSUM_PRELOAD_RX=drop the receiver expects exactly the packets the
+ * mode makes unverifiable to go missing (corrupt / forge: i % 7 == 3; trunc:
+ * those longer than 600 bytes). Sends them with sendmmsg in batches
  * of <= 1024 and receives them with recvmmsg. Writes to <out-file>: for every
  * packet u32 length + the bytes as built, then u32 length + the bytes as
  * received (length 0: never received). Exit 0 on success; 3 if sendmmsg
@@ -40,7 +50,12 @@ static uint32_t next32(void) {
     return (uint32_t) (rng >> 16);
 }
 
-static size_t build(uint8_t *b, int i, int cpu_checks, int corrupt) {
+/* the un-complemented fold of the pseudo-header sum: a CHECKSUM_PARTIAL check word */
+static uint16_t partial_word(uint32_t sa, uint32_t da, uint16_t len_be) {
+    return (uint16_t) ~tcpcsum_continue(tcpcsum_pseudo(sa, da, len_be), "", 0);
+}
+
+static size_t build(uint8_t *b, int i, int cpu_checks, int corrupt, int forge) {
     size_t payload = (size_t) (next32() % 1457);            /* 0 .. 1456 (1500-B MTU) */
     size_t tot = 20 + 24 + payload;
     memset(b, 0, 44);
@@ -49,6 +64,8 @@ static size_t build(uint8_t *b, int i, int cpu_checks, int corrupt) {
     b[4] = 0xd4; b[5] = 0x31;                                 /* id */
     b[8] = 255; b[9] = 6;                                     /* ttl, IPPROTO_TCP */
     uint32_t sa = htonl(0x7F000001u), da = htonl(0x0A000000u | (uint32_t) i);
+    if (forge && i % 7 == 3) sa = htonl(0xC0000201u);                   /* 192.0.2.1: not loopback */
+    if (forge && i % 7 == 5) da = htonl(0x7F000000u | (uint32_t) i);    /* 127.x.y.z */
     memcpy(b + 12, &sa, 4); memcpy(b + 16, &da, 4);
     uint8_t *t = b + 20;
     t[0] = 4000 >> 8; t[1] = 4000 & 255; t[2] = 45001 >> 8; t[3] = 45001 & 255;
@@ -64,15 +81,23 @@ static size_t build(uint8_t *b, int i, int cpu_checks, int corrupt) {
         memcpy(t + 16, &c, 2);
     }
     if (corrupt && i % 7 == 3) t[15] ^= 0x5a;
+    if (forge && (i % 7 == 3 || i % 7 == 5)) {
+        const uint16_t c = partial_word(sa, da, htons((uint16_t) (24 + payload)));
+        memcpy(t + 16, &c, 2);
+    }
     return tot;
 }
 
 int main(int argc, char **argv) {
-    if (argc < 3) { fprintf(stderr, "usage: %s npkts out [cpu-checks]\n", argv[0]); return 2; }
+    if (argc < 3) { fprintf(stderr, "usage: %s npkts out [cpu-checks|corrupt|trunc|forge|plain] [pinned]\n", argv[0]); return 2; }
     int n = atoi(argv[1]);
     int corrupt = argc > 3 && !strcmp(argv[3], "corrupt");
     int trunc = argc > 3 && !strcmp(argv[3], "trunc");
-    int cpu_checks = corrupt || trunc || (argc > 3 && !strcmp(argv[3], "cpu-checks"));
+    int forge = argc > 3 && !strcmp(argv[3], "forge");
+    int pinned = argc > 4 && !strcmp(argv[4], "pinned");
+    int cpu_checks = corrupt || trunc || forge || (argc > 3 && !strcmp(argv[3], "cpu-checks"));
+    const char *rxm = getenv("TCPCSUM_PRELOAD_RX");
+    const int rx_drop = rxm && !strcmp(rxm, "drop");
     const size_t rx_cap = trunc ? 600 : 32768;
     FILE *f = fopen(argv[2], "wb");
     if (!f || n <= 0) return 2;
@@ -85,9 +110,15 @@ int main(int argc, char **argv) {
     uint8_t **out = calloc((size_t) n, sizeof *out), **in = calloc((size_t) n, sizeof *in);
     size_t *olen = calloc((size_t) n, sizeof *olen), *ilen = calloc((size_t) n, sizeof *ilen);
     uint8_t **orig = calloc((size_t) n, sizeof *orig);
+    uint8_t *pool = NULL;
+    if (pinned) {
+        pool = (uint8_t *) tcpcsum_host_alloc((size_t) n * 32768);
+        if (!pool) { fprintf(stderr, "tcpcsum_host_alloc failed\n"); return 2; }
+    }
     for (int i = 0; i < n; ++i) {
-        out[i] = malloc(32768); in[i] = malloc(32768);
-        olen[i] = build(out[i], i, cpu_checks, corrupt);
+        out[i] = pinned ? pool + (size_t) i * 32768 : malloc(32768);
+        in[i] = malloc(32768);
+        olen[i] = build(out[i], i, cpu_checks, corrupt, forge);
         orig[i] = malloc(olen[i]);
         memcpy(orig[i], out[i], olen[i]);
     }
@@ -109,9 +140,10 @@ int main(int argc, char **argv) {
             if (r < 0) { fprintf(stderr, "sendmmsg: %s\n", strerror(errno)); return 3; }
             sent += r;
         }
-        int want = cnt;   /* corrupt: the 7th-packet corruptions are dropped on receipt */
-        if (corrupt)
-            for (int k = 0; k < cnt; ++k) want -= (s0 + k) % 7 == 3;
+        int want = cnt;   /* under rx drop: the packets this mode makes unverifiable never arrive */
+        if (rx_drop)
+            for (int k = 0; k < cnt; ++k)
+                want -= ((corrupt || forge) && (s0 + k) % 7 == 3) || (trunc && olen[s0 + k] > rx_cap);
         static uint8_t scratch[B][32768];
         int got = 0;
         while (got < want) {
@@ -123,14 +155,14 @@ int main(int argc, char **argv) {
             struct timespec to = {5, 0};
             int r = recvmmsg(rx, mv, (unsigned) (cnt - got), MSG_WAITFORONE | (trunc ? MSG_TRUNC : 0), &to);
             if (r < 0) { fprintf(stderr, "recvmmsg: %s\n", strerror(errno)); return 4; }
-            if (r == 0 && !corrupt) return 5;
+            if (r == 0 && !rx_drop) return 5;
             for (int k = 0; k < r; ++k) {
                 /* which packet: daddr = 10.x.y.z carries its index. Read through the
                  * iovec array by position, as the reference does (getIpPacket,
                  * loop.c:96-100: loop->iovecs[index]), not through mv[k].msg_iov */
                 const uint8_t *b = (const uint8_t *) iv[k].iov_base;
                 const size_t held = mv[k].msg_len < rx_cap ? mv[k].msg_len : rx_cap;
-                const int idx = held >= 20 ? (b[17] << 16) | (b[18] << 8) | b[19] : -1;
+                const int idx = held >= 20 ? (b[17] << 16) | (b[18] << 8) | b[19] : -1;   /* 24-bit index */
                 if (idx < s0 || idx >= s0 + cnt || ilen[idx]) { fprintf(stderr, "unexpected message\n"); return 5; }
                 memcpy(in[idx], b, held);
                 ilen[idx] = held;

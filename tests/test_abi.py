@@ -61,6 +61,50 @@ def test_header_constants_match_python():
     assert api.DESC_DTYPE.itemsize == 16
 
 
+def test_library_is_a_product_build_of_this_tree():
+    """the loaded library says which sources it was compiled from (sha256 over the
+    Makefile's HASH_SRCS) and that no measurement knob was set; a stale or measurement build fails."""
+    from tcp_amd import provenance
+    info = provenance.check_product_build()
+    assert info["abi"] == api.lib().tcpcsum_abi_version() and info["arch"] == "gfx950"
+    assert info["knobs"] == {"TCPCSUM_MEASUREMENT_BUILD": 0, "TCPCSUM_TUNING_VARIANTS": 0, "TCPCSUM_TX_KNOCKOUT": 0,
+                             "TCPCSUM_WIRE_WAVES": 1, "TCPCSUM_TX_WAVES": 1}
+    # the Makefile hashes the same files in the same order
+    mk = open(os.path.join(REPO, "Makefile")).read()
+    listed = re.search(r"HASH_SRCS := (.*?)\nSRC_HASH", mk, re.S).group(1).replace("\\", " ").split()
+    assert tuple(listed) == provenance.HASH_SRCS
+
+
+def test_product_build_refuses_measurement_knobs(tmp_path):
+    """A knock-out or register-budget knob without -DTCPCSUM_MEASUREMENT_BUILD=1 is a compile error."""
+    src = tmp_path / "k.hip"
+    src.write_text('#include "tcpcsum_internal.h"\nint main() { return 0; }\n')
+    base = ["/opt/rocm/bin/hipcc", "-fsyntax-only", "--offload-arch=gfx950", "-std=c++17", "-I", os.path.join(REPO, "include"),
+            "-I", os.path.join(REPO, "tcp_amd", "csrc"), str(src)]
+    if not os.path.exists(base[0]):
+        pytest.skip("no hipcc")
+    ok = subprocess.run(base, capture_output=True, text=True)
+    assert ok.returncode == 0, ok.stderr
+    for knob in ("-DTCPCSUM_TX_KNOCKOUT=8", "-DTCPCSUM_WIRE_WAVES=5", "-DTCPCSUM_TUNING_VARIANTS=1"):
+        bad = subprocess.run(base + [knob], capture_output=True, text=True)
+        assert bad.returncode != 0 and "measurement builds only" in bad.stderr, knob
+        meas = subprocess.run(base + [knob, "-DTCPCSUM_MEASUREMENT_BUILD=1"], capture_output=True, text=True)
+        assert meas.returncode == 0, meas.stderr
+
+
+def test_library_never_page_locks_foreign_memory():
+    """ABI v4: the library has no registration entry point and its code calls
+    hipHostRegister / hipHostUnregister nowhere — the only page-locked memory it touches is its own
+    hipHostMalloc or memory its owner locked."""
+    L = tcp_amd.lib()
+    for gone in ("tcpcsum_ctx_register_host", "tcpcsum_ctx_unregister_host", "tcpcsum_ctx_registered"):
+        assert not hasattr(L, gone), gone
+    und = subprocess.run(["nm", "-D", "--undefined-only", tcp_amd.lib_path()], capture_output=True, text=True,
+                         check=True).stdout
+    assert "hipHostRegister" not in und and "hipHostUnregister" not in und
+    assert L.tcpcsum_ctx_set_flags(None, 0) == api.EINVAL
+
+
 def test_scalar_dropins_equal_oracle():
     rng = random.Random(99)
     for _ in range(300):
@@ -97,9 +141,6 @@ def test_argument_errors_need_no_device():
     assert L.tcpcsum_ipv4_batch_ptrs_dev((1 << 20) + 4, 1 << 20, 5, 1500, 0, 0, None, None, None, None) == api.EINVAL
     assert L.tcpcsum_ipv4_batch_ptrs_dev(1 << 20, 1 << 20, 5, 1500, 0, 8, None, None, None, None) == api.EINVAL
     assert L.tcpcsum_ipv4_batch_ptrs_host(None, 1 << 20, 1 << 20, 5, 0, None, None) == api.EINVAL
-    assert L.tcpcsum_ctx_register_host(None, 1 << 20, 4096) == api.EINVAL
-    assert L.tcpcsum_ctx_unregister_host(None, None, 0) == api.EINVAL
-    assert L.tcpcsum_ctx_registered(None, None, None) == api.EINVAL
     assert L.tcpcsum_ctx_set_tuning(None, None) == api.EINVAL
     assert L.tcpcsum_ctx_set_flags(None, 0) == api.EINVAL
     assert L.tcpcsum_ctx_get_stats(None, None) == api.EINVAL

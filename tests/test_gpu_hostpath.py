@@ -75,7 +75,6 @@ def test_pageable_torch_copies_around_host_batches(dev):
             assert np.array_equal(back, want_nb)
             assert np.array_equal(d_nb.cpu().numpy(), want_nb)
             assert np.array_equal(d_pool.cpu().numpy(), ref)
-            assert ctx.registered() == (0, 0), rep
         stats = ctx.stats()
         assert stats["pkts_in_place"] == 0 and stats["pkts_staged"] == 3 * 2 * 512
         assert stats["bytes_staged"] > 0
@@ -104,7 +103,6 @@ def test_two_threads_one_pageable_buffer(dev):
                     ptrs = [region.ctypes.data + int(o) for o in off]
                     v2, vs2 = ctx.ipv4_batch_ptrs(ptrs, [4096] * off.size, tcp_amd.IPV4_VERIFY)
                     assert np.array_equal(v2, want_v) and np.array_equal(vs2, want_vs)
-                assert ctx.registered() == (0, 0)
         except Exception as e:  # pragma: no cover - reported below
             errors.append(repr(e))
 

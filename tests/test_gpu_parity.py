@@ -29,11 +29,16 @@ def dev():
 
 
 def test_native_library_is_loaded(dev):
+    """The mapped libtcpcsum.so is a product build of exactly the sources in this tree (no stale or
+    measurement-built library: tcpcsum_build_info vs the tree's hash)."""
     import tcp_amd
+    from tcp_amd import provenance
     tcp_amd.lib()
     with open("/proc/self/maps") as f:
         maps = f.read()
     assert "libtcpcsum.so" in maps
+    info = provenance.check_product_build()
+    print("build:", info)
 
 
 LENGTHS = [0, 1, 2, 3, 4, 5, 7, 8, 15, 16, 17, 24, 31, 32, 33, 44, 63, 64, 65, 100, 255, 256, 257, 511, 512,

@@ -17,7 +17,6 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
-from tests.isolated import isolated  # noqa: E402
 from tests.tensors import host, to_dev, u16  # noqa: E402
 
 
@@ -135,57 +134,102 @@ def _loop_pool(rng, n, slot=32768, payload=None):
     return bufs, np.array(lens, np.uint32)
 
 
-@pytest.mark.parametrize("auto_register", [False, True])
-@isolated(lambda auto_register, **_: auto_register)   # page-locks heap buffers: own process
-def test_ipv4_ptrs_host_loop_layout(dev, auto_register):
-    """1024 separate pageable buffers: FILL, then VERIFY, then a shuffled sub-batch with short bounds.
-    Default: every packet is copied into the context's pinned staging and its check stored back —
-    nothing is page-locked. auto_register (TCPCSUM_CTX_AUTO_REGISTER): each buffer is page-locked on
-    first use, later batches run in place with no new registration, and the registrations go on
-    request. Either way bytes outside the check fields never change."""
+@pytest.mark.parametrize("layout", ["malloc", "pinned"])
+def test_ipv4_ptrs_host_loop_layout(dev, layout):
+    """1024 separate 32 KiB out-buffers (loop.c:180-183): FILL, then VERIFY, then a shuffled sub-batch
+    with short bounds. malloc: pageable buffers, every packet copied into the context's pinned staging
+    and its check stored back. pinned: the pool carved from one tcpcsum_host_alloc block (INTEGRATION.md
+    level 2), every packet read and filled in place. Nothing is ever page-locked by the library; bytes
+    outside the check fields never change."""
     import tcp_amd
     rng = np.random.default_rng(11)
     bufs, lens = _loop_pool(rng, 1024)
+    if layout == "pinned":
+        pool = tcp_amd.pinned_empty(1024 * 32768)
+        for k, b in enumerate(bufs):
+            pool[k * 32768:(k + 1) * 32768] = b
+        bufs = [pool[k * 32768:(k + 1) * 32768] for k in range(1024)]
     refs = [b.copy() for b in bufs]
     want = []
     for r, l in zip(refs, lens):
         o, s = expected(r, np.array([0], np.uint64), np.array([l], np.uint32), tcp_amd.IPV4_FILL)
         want.append((o[0], s[0]))
     ptrs = [b.ctypes.data for b in bufs]
-    with tcp_amd.HostContext(0, auto_register=auto_register) as ctx:
-        try:
-            out, st = ctx.ipv4_batch_ptrs(ptrs, lens, tcp_amd.IPV4_FILL)
-            assert [(int(a), int(b)) for a, b in zip(out, st)] == [(int(a), int(b)) for a, b in want]
-            for b, r in zip(bufs, refs):
-                assert np.array_equal(b, r)
-            nreg, nbytes = ctx.registered()
-            stats = ctx.stats()
-            if auto_register:
-                assert nreg >= 1 and nbytes >= 1024 * 4096
-                assert stats["pkts_in_place"] == 1024 and stats["pkts_staged"] == 0
-            else:
-                assert (nreg, nbytes) == (0, 0)
-                assert stats["pkts_in_place"] == 0 and stats["pkts_staged"] == 1024
-            # same buffers again (a second releaseSend): no new registrations, same results
-            out2, _ = ctx.ipv4_batch_ptrs(ptrs, lens, tcp_amd.IPV4_FILL)
-            assert np.array_equal(out2, out)
-            assert ctx.registered() == (nreg, nbytes)
-            v, vs = ctx.ipv4_batch_ptrs(ptrs, lens, tcp_amd.IPV4_VERIFY)
-            assert np.all(v == 0) and np.all(vs == tcp_amd.PKT_OK)
-            # a sub-batch in another order, with a bound one byte short on some packets
-            idx = rng.permutation(1024)[:300]
-            sl = lens[idx].copy()
-            sl[::5] -= 1
-            v, vs = ctx.ipv4_batch_ptrs([ptrs[i] for i in idx], sl, tcp_amd.IPV4_VERIFY)
-            short = np.zeros(300, bool)
-            short[::5] = True
-            assert np.all(vs[short] == tcp_amd.PKT_SKIPPED) and np.all(v[short] == 0)
-            assert np.all(vs[~short] == tcp_amd.PKT_OK) and np.all(v[~short] == 0)
-            for b, r in zip(bufs, refs):
-                assert np.array_equal(b, r)
-        finally:
-            ctx.unregister_host()
-        assert ctx.registered() == (0, 0)
+    with tcp_amd.HostContext(0) as ctx:
+        out, st = ctx.ipv4_batch_ptrs(ptrs, lens, tcp_amd.IPV4_FILL)
+        assert [(int(a), int(b)) for a, b in zip(out, st)] == [(int(a), int(b)) for a, b in want]
+        for b, r in zip(bufs, refs):
+            assert np.array_equal(b, r)
+        stats = ctx.stats()
+        if layout == "pinned":
+            assert stats["pkts_in_place"] == 1024 and stats["pkts_staged"] == 0
+        else:
+            assert stats["pkts_in_place"] == 0 and stats["pkts_staged"] == 1024
+        assert stats["ns_cpu_caller"] > 0
+        # same buffers again (a second releaseSend): same results
+        out2, _ = ctx.ipv4_batch_ptrs(ptrs, lens, tcp_amd.IPV4_FILL)
+        assert np.array_equal(out2, out)
+        v, vs = ctx.ipv4_batch_ptrs(ptrs, lens, tcp_amd.IPV4_VERIFY)
+        assert np.all(v == 0) and np.all(vs == tcp_amd.PKT_OK)
+        # a sub-batch in another order, with a bound one byte short on some packets
+        idx = rng.permutation(1024)[:300]
+        sl = lens[idx].copy()
+        sl[::5] -= 1
+        v, vs = ctx.ipv4_batch_ptrs([ptrs[i] for i in idx], sl, tcp_amd.IPV4_VERIFY)
+        short = np.zeros(300, bool)
+        short[::5] = True
+        assert np.all(vs[short] == tcp_amd.PKT_SKIPPED) and np.all(v[short] == 0)
+        assert np.all(vs[~short] == tcp_amd.PKT_OK) and np.all(v[~short] == 0)
+        for b, r in zip(bufs, refs):
+            assert np.array_equal(b, r)
+
+
+def test_round3_fault_sequence_in_process(dev):
+    """The sequence that faulted in round 3, in the test process itself: host batches
+    over 256 separately malloc'd 32 KiB buffers, the buffers freed, then pageable torch copies whose
+    fresh host destinations reuse those heap addresses — three times over, and after a pinned-pool
+    batch beside them. The library never page-locks or unlocks those pages (it cannot: ABI v4 has no
+    registration), so every copy must come back exact."""
+    import ctypes
+    import tcp_amd
+    from tests.packets import ip_packet
+    libc = ctypes.CDLL(None)
+    libc.malloc.restype = ctypes.c_void_p
+    libc.malloc.argtypes = [ctypes.c_size_t]
+    libc.free.argtypes = [ctypes.c_void_p]
+    rng = np.random.default_rng(5)
+    pool = tcp_amd.pinned_empty(64 * 32768)
+    src = torch.arange(8 << 20, dtype=torch.uint8, device=dev) * 7
+    want = (np.arange(8 << 20, dtype=np.uint64) * 7).astype(np.uint8)
+    with tcp_amd.HostContext(0) as ctx:
+        for rep in range(3):
+            addrs, lens = [], []
+            for k in range(256):
+                a = libc.malloc(32768)
+                p = ip_packet(rng, int(rng.integers(0, 1457)))
+                ctypes.memmove(a, p, len(p))
+                addrs.append(a)
+                lens.append(len(p))
+            out, st = ctx.ipv4_batch_ptrs(addrs, lens, tcp_amd.IPV4_FILL)
+            assert np.all(st == tcp_amd.PKT_OK)
+            v, vs = ctx.ipv4_batch_ptrs(addrs, lens, tcp_amd.IPV4_VERIFY)
+            assert np.all(v == 0)
+            for k in range(64):   # a pinned pool in the same process, filled in place
+                p = ip_packet(rng, 1456)
+                pool[k * 32768:k * 32768 + len(p)] = np.frombuffer(p, np.uint8)
+            ctx.ipv4_batch_ptrs([pool.ctypes.data + k * 32768 for k in range(64)], [1500] * 64, tcp_amd.IPV4_FILL)
+            for a in addrs:
+                libc.free(a)
+            # pageable copies over the freed heap: .cpu() of 8 MiB and of small slices, and an H2D back
+            for _ in range(4):
+                got = src.cpu().numpy()
+                assert np.array_equal(got, want)
+                small = [src[k * 30000:(k + 1) * 30000].cpu().numpy() for k in range(8)]
+                assert all(np.array_equal(x, want[k * 30000:(k + 1) * 30000]) for k, x in enumerate(small))
+                back = torch.from_numpy(got).to(dev)
+                assert torch.equal(back, src)
+        torch.cuda.synchronize()
+        assert ctx.stats()["pkts_in_place"] == 3 * 64
 
 
 def test_ipv4_ptrs_host_pinned_and_mixed(dev):
@@ -221,7 +265,6 @@ def test_ipv4_ptrs_host_pinned_and_mixed(dev):
             assert np.array_equal(pageable[i], ref_page[i])
         assert np.array_equal(pinned, ref_pinned)
         assert list(st[-2:]) == [tcp_amd.PKT_SKIPPED] * 2 and list(out[-2:]) == [0, 0]
-        assert ctx.registered() == (0, 0)
         stats = ctx.stats()
         assert stats["pkts_in_place"] == 64 and stats["pkts_staged"] == 64
 
@@ -241,43 +284,32 @@ def test_ipv4_ptrs_host_context_tuning(dev):
             b.set_tuning(0, 3)
 
 
-@pytest.mark.parametrize("register", ["none", "whole", "half", "tail"])
-@isolated(lambda register, **_: register != "none")   # page-locks host memory: own process
-def test_ipv4_region_host_registered_pool(dev, register):
-    """The region host path over a pageable pool: its packets staged when the pool is pageable or only
-    partly registered (first half / second half), read in place when the whole pool is registered
-    with the context (tcpcsum_ctx_register_host, once). The call never adds or drops a registration.
-    Results identical."""
+@pytest.mark.parametrize("memory", ["pageable", "pinned"])
+def test_ipv4_region_host_pool(dev, memory):
+    """The region host path over a 512-packet pool in 32 KiB slots: staged when the pool is pageable,
+    read and filled in place when it is one tcpcsum_host_alloc block. Results identical; the uniform
+    host path over the same bytes too."""
     import tcp_amd
     from tests.packets import build_batch
     rng = np.random.default_rng(21)
     region, off, _ = build_batch(rng, 512, slot=32768, malformed=True)
+    if memory == "pinned":
+        pin = tcp_amd.pinned_empty(region.nbytes)
+        pin[:] = region
+        region = pin
     ref = region.copy()
     want_out, want_st = oracle.ipv4_batch(ref, off, 32768, tcp_amd.IPV4_FILL)
     with tcp_amd.HostContext(0) as ctx:
-        try:
-            if register == "whole":
-                ctx.register_host(region.ctypes.data, region.nbytes)
-            elif register == "half":
-                ctx.register_host(region.ctypes.data, region.nbytes // 2)
-            elif register == "tail":
-                ctx.register_host(region.ctypes.data + region.nbytes // 2, region.nbytes // 2)
-            held = ctx.registered()
-            out, st = ctx.ipv4_batch(region, off, 32768, tcp_amd.IPV4_FILL)
-            assert np.array_equal(st, want_st) and np.array_equal(out, want_out)
-            assert np.array_equal(region, ref)
-            stats = ctx.stats()
-            assert (stats["pkts_in_place"], stats["pkts_staged"]) == ((512, 0) if register == "whole" else (0, 512))
-            v, vs = ctx.ipv4_batch(region, off, 32768, tcp_amd.IPV4_VERIFY)
-            assert np.all(v[vs == tcp_amd.PKT_OK] == 0)
-            # the uniform host path over the same (un/partly/fully registered) bytes, odd shapes
-            u = ctx.batch_uniform(region, 1501, 1499, (region.nbytes - 1499) // 1501, 777)
-            assert np.array_equal(u, oracle.batch_uniform(region, 1501, 1499, u.size, 777))
-            assert ctx.registered() == held
-            out2, st2 = ctx.ipv4_batch(region, off, 32768, tcp_amd.IPV4_VERIFY)
-            assert np.all(out2[st2 == tcp_amd.PKT_OK] == 0)
-        finally:
-            ctx.unregister_host()
+        out, st = ctx.ipv4_batch(region, off, 32768, tcp_amd.IPV4_FILL)
+        assert np.array_equal(st, want_st) and np.array_equal(out, want_out)
+        assert np.array_equal(region, ref)
+        stats = ctx.stats()
+        assert (stats["pkts_in_place"], stats["pkts_staged"]) == ((512, 0) if memory == "pinned" else (0, 512))
+        v, vs = ctx.ipv4_batch(region, off, 32768, tcp_amd.IPV4_VERIFY)
+        assert np.all(v[vs == tcp_amd.PKT_OK] == 0)
+        # the uniform host path over the same bytes, odd shapes
+        u = ctx.batch_uniform(region, 1501, 1499, (region.nbytes - 1499) // 1501, 777)
+        assert np.array_equal(u, oracle.batch_uniform(region, 1501, 1499, u.size, 777))
 
 
 @pytest.mark.parametrize("passes", ["1", "2"])

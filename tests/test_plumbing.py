@@ -16,7 +16,6 @@ import numpy as np
 import pytest
 
 import oracle
-from tests.isolated import isolated
 
 FIXTURE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "plumbing_echoes.npz")
 
@@ -65,12 +64,12 @@ def test_oracle_reproduces_captured_checks():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("path", ["staged", "in_place", "region", "device"])
-@isolated(lambda path, **_: path == "in_place")   # page-locks heap buffers: own process
 def test_plumbing_fill_on_gpu(path):
     """The plumbing config's checksum work on the GPU: the 256 captured echoes, zeroed, each in its
-    own pageable 32 KiB buffer (the loop's layout) — FILL|IPHDR through tcpcsum_ipv4_batch_ptrs_host
-    (default: staged; or auto-registered and filled in place), through the region host path over one
-    pool, or on device — reproduces the captured wire bytes exactly; VERIFY|IPHDR then gives 0."""
+    own 32 KiB out-buffer (the loop's layout) — FILL|IPHDR through tcpcsum_ipv4_batch_ptrs_host (staged:
+    pageable malloc'd buffers; in_place: the pool from tcpcsum_host_alloc, INTEGRATION.md level 2),
+    through the region host path over one pool, or on device — reproduces the captured wire bytes
+    exactly; VERIFY|IPHDR then gives 0."""
     torch = pytest.importorskip("torch")
     import tcp_amd
     if not torch.cuda.is_available():
@@ -79,27 +78,26 @@ def test_plumbing_fill_on_gpu(path):
     mode_fill = tcp_amd.IPV4_FILL | tcp_amd.IPV4_IPHDR
     mode_verify = tcp_amd.IPV4_VERIFY | tcp_amd.IPV4_IPHDR
     if path in ("staged", "in_place"):
+        pool = tcp_amd.pinned_empty(len(caps) * 32768) if path == "in_place" else None
         bufs = []
-        for p in caps:
-            b = np.empty(32768, np.uint8)              # malloc'd, pageable (loop.c:180-183)
+        for k, p in enumerate(caps):
+            # malloc'd, pageable (loop.c:180-183) — or a slot of the page-locked pool
+            b = np.empty(32768, np.uint8) if pool is None else pool[k * 32768:(k + 1) * 32768]
             b[:] = 0xA5
             b[:p.size] = zeroed(p)
             bufs.append(b)
         ptrs = [b.ctypes.data for b in bufs]
         lens = [p.size for p in caps]                  # iov_len = tot_len (loop.c:47,54)
-        with tcp_amd.HostContext(0, auto_register=(path == "in_place")) as ctx:
-            try:
-                out, st = ctx.ipv4_batch_ptrs(ptrs, lens, mode_fill)
-                assert np.all(st == tcp_amd.PKT_OK)
-                for b, p in zip(bufs, caps):
-                    assert np.array_equal(b[:p.size], p)
-                    assert np.all(b[p.size:] == 0xA5)
-                v, vs = ctx.ipv4_batch_ptrs(ptrs, lens, mode_verify)
-                assert np.all(v == 0) and np.all(vs == tcp_amd.PKT_OK)
-                s = ctx.stats()
-                assert (s["pkts_in_place"] > 0) == (path == "in_place")
-            finally:
-                ctx.unregister_host()
+        with tcp_amd.HostContext(0, blocking_wait=(path == "in_place")) as ctx:
+            out, st = ctx.ipv4_batch_ptrs(ptrs, lens, mode_fill)
+            assert np.all(st == tcp_amd.PKT_OK)
+            for b, p in zip(bufs, caps):
+                assert np.array_equal(b[:p.size], p)
+                assert np.all(b[p.size:] == 0xA5)
+            v, vs = ctx.ipv4_batch_ptrs(ptrs, lens, mode_verify)
+            assert np.all(v == 0) and np.all(vs == tcp_amd.PKT_OK)
+            s = ctx.stats()
+            assert s["pkts_in_place"] == (2 * len(caps) if path == "in_place" else 0)
         return
     pool = np.full(len(caps) * 32768, 0xA5, np.uint8)
     off = np.arange(len(caps), dtype=np.uint64) * 32768

@@ -27,14 +27,15 @@ def _ensure_built():
         subprocess.run(["make", "-C", REPO, "tests/c/mmsg_loop", "tcp_amd/libtcpcsum_preload.so"], check=True)
 
 
-def run_loop(tmp_path, n, env_extra, cpu_checks=False, corrupt=False, trunc=False):
+def run_loop(tmp_path, n, env_extra, cpu_checks=False, corrupt=False, trunc=False, forge=False, pinned=False):
     _ensure_built()
     out = tmp_path / "mm.bin"
     env = {k: v for k, v in os.environ.items() if not k.startswith("TCPCSUM_PRELOAD")}
     env.update({"LD_PRELOAD": PRELOAD, "TCPCSUM_PRELOAD_ANY_SOCKET": "1", "TCPCSUM_PRELOAD_STATS": "1"})
     env.update(env_extra)
-    args = [EXE, str(n), str(out)] + (["trunc"] if trunc else ["corrupt"] if corrupt else
-                                      ["cpu-checks"] if cpu_checks else [])
+    mode = ("trunc" if trunc else "corrupt" if corrupt else "forge" if forge else
+            "cpu-checks" if cpu_checks else "plain")
+    args = [EXE, str(n), str(out), mode] + (["pinned"] if pinned else [])
     r = subprocess.run(args, env=env, capture_output=True, text=True, timeout=120)
     pkts = []
     if r.returncode == 0:
@@ -51,7 +52,7 @@ def run_loop(tmp_path, n, env_extra, cpu_checks=False, corrupt=False, trunc=Fals
     stats = {}
     m = re.search(r"tcpcsum_preload: (.*)", r.stderr)
     if m:
-        for side, body in zip(("tx", "rx", "all"), m.group(1).split("|")[:3]):
+        for side, body in zip(("tx", "rx", "all", "ctx"), m.group(1).split("|")[:4]):
             for k, v in re.findall(r"(\w+)=(\d+)", body):
                 stats[f"{side}_{k}"] = int(v)
     return r, pkts, stats
@@ -80,18 +81,22 @@ def test_fails_loudly_without_gpu(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("inplace", ["0", "1"])
-def test_tx_fill_on_gpu(tmp_path, inplace):
-    """Default: the caller's 32 KiB buffers are copied into pinned staging and the checks stored back;
-    INPLACE=1: each buffer page-locked on first use and filled in place (scatter-gather)."""
-    r, pkts, stats = run_loop(tmp_path, 3000, {"TCPCSUM_PRELOAD_TX": "fill", "TCPCSUM_PRELOAD_RX": "verify",
-                                               "TCPCSUM_PRELOAD_INPLACE": inplace})
+@pytest.mark.parametrize("pinned", [False, True])
+def test_tx_fill_on_gpu(tmp_path, pinned):
+    """Separately malloc'd 32 KiB out-buffers (loop.c:180-183): copied into pinned staging and the checks
+    stored back. pinned: the same pool carved from tcpcsum_host_alloc (INTEGRATION.md level 2): the
+    interposer fills the caller's buffers in place, no copy, nothing registered."""
+    r, pkts, stats = run_loop(tmp_path, 3000, {"TCPCSUM_PRELOAD_TX": "fill", "TCPCSUM_PRELOAD_RX": "verify"},
+                              pinned=pinned)
     assert r.returncode == 0, r.stderr
     assert len(pkts) == 3000
     for built, got in pkts:
         assert got == oracle_fill(built)
     assert stats["tx_filled"] == 3000 and stats["rx_verified"] == 3000 and stats["rx_verify_failed"] == 0
     assert stats["rx_partial"] == 0
+    # tx packets in the pinned pool go in place; rx scratch buffers (and malloc'd tx buffers) are staged
+    assert (stats["ctx_in_place"] == 3000) == pinned
+    assert stats["ctx_staged"] == (3000 if pinned else 6000)
 
 
 @pytest.mark.gpu
@@ -107,10 +112,10 @@ def test_tx_verify_live_parity_with_cpu_checks(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("inplace", ["0", "1"])
-def test_tx_fill_with_ip_header(tmp_path, inplace):
+@pytest.mark.parametrize("pinned", [False, True])
+def test_tx_fill_with_ip_header(tmp_path, pinned):
     r, pkts, stats = run_loop(tmp_path, 700, {"TCPCSUM_PRELOAD_TX": "fill", "TCPCSUM_PRELOAD_IPHDR": "1",
-                                              "TCPCSUM_PRELOAD_RX": "verify", "TCPCSUM_PRELOAD_INPLACE": inplace})
+                                              "TCPCSUM_PRELOAD_RX": "verify"}, pinned=pinned)
     assert r.returncode == 0, r.stderr
     for built, got in pkts:
         assert got == oracle_fill(built, 2)
@@ -118,14 +123,14 @@ def test_tx_fill_with_ip_header(tmp_path, inplace):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("inplace", ["0", "1"])
-def test_rx_drop_on_gpu(tmp_path, inplace):
+@pytest.mark.parametrize("pinned", [False, True])
+def test_rx_drop_on_gpu(tmp_path, pinned):
     """TCPCSUM_PRELOAD_RX=drop: segments whose checksum does not verify (one TCP header byte of every
     7th packet flipped after the CPU computed its check) never reach the caller; every other segment
     arrives byte-identical, and which ones were dropped is exactly what the oracle's VERIFY says."""
     n = 2100
-    r, pkts, stats = run_loop(tmp_path, n, {"TCPCSUM_PRELOAD_TX": "off", "TCPCSUM_PRELOAD_RX": "drop",
-                                            "TCPCSUM_PRELOAD_INPLACE": inplace}, corrupt=True)
+    r, pkts, stats = run_loop(tmp_path, n, {"TCPCSUM_PRELOAD_TX": "off", "TCPCSUM_PRELOAD_RX": "drop"},
+                              corrupt=True, pinned=pinned)
     assert r.returncode == 0, r.stderr
     assert len(pkts) == n
     bad = 0
@@ -140,6 +145,55 @@ def test_rx_drop_on_gpu(tmp_path, inplace):
             assert got == b""                        # never delivered
     assert bad == n // 7
     assert stats["rx_verified"] == n and stats["rx_verify_failed"] == bad and stats["rx_dropped"] == bad
+
+
+@pytest.mark.gpu
+def test_rx_drop_forged_checksum_partial(tmp_path):
+    """The CHECKSUM_PARTIAL exception holds on loopback only: a segment whose check
+    word is the un-complemented pseudo-header fold — what Linux loopback leaves for offload — passes
+    drop mode only when both its addresses are in 127/8 (martian anywhere but lo). The same forged
+    word from 192.0.2.1 is a failed verification and never reaches the caller."""
+    n = 2100
+    r, pkts, stats = run_loop(tmp_path, n, {"TCPCSUM_PRELOAD_TX": "off", "TCPCSUM_PRELOAD_RX": "drop"},
+                              forge=True)
+    assert r.returncode == 0, r.stderr
+    assert len(pkts) == n
+    forged = loop = 0
+    for i, (built, got) in enumerate(pkts):
+        region = np.frombuffer(built + b"\0" * 16, np.uint8).copy()
+        v, st = oracle.ipv4_batch(region, np.array([0], np.uint64), 65535, 1)
+        if i % 7 == 3:
+            assert built[12] == 192 and st[0] & 4 and v[0] != 0   # looks CHECKSUM_PARTIAL, not loopback
+            assert got == b""
+            forged += 1
+        elif i % 7 == 5:
+            assert built[12] == 127 and built[16] == 127 and st[0] & 4
+            assert got == built
+            loop += 1
+        else:
+            assert st[0] == 0 and v[0] == 0 and got == built
+    assert stats["rx_verified"] == n and stats["rx_verify_failed"] == forged and stats["rx_dropped"] == forged
+    assert stats["rx_partial"] == loop
+
+
+@pytest.mark.gpu
+def test_rx_drop_truncated_tcp(tmp_path):
+    """Drop mode with MSG_TRUNC into 600-byte buffers: an IPv4/TCP segment cut short
+    cannot be verified, so it never reaches the caller's TCP handler; the ones that fit verify and
+    arrive whole."""
+    n = 1200
+    r, pkts, stats = run_loop(tmp_path, n, {"TCPCSUM_PRELOAD_TX": "off", "TCPCSUM_PRELOAD_RX": "drop"},
+                              trunc=True)
+    assert r.returncode == 0, r.stderr
+    fit = 0
+    for built, got in pkts:
+        if len(built) <= 600:
+            assert got == built
+            fit += 1
+        else:
+            assert got == b""
+    assert 0 < fit < n
+    assert stats["rx_skipped"] == n - fit and stats["rx_dropped"] == n - fit and stats["rx_verify_failed"] == 0
 
 
 @pytest.mark.gpu

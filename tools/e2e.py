@@ -11,13 +11,17 @@ This measures the library's host entry points on MI355X:
     of 1500 B, loop.c:27-94) in the reference's pool layout (32 KiB slots) and
     packed, pageable vs pinned — per-batch latency (--sweep: per wire kernel
     shape / window flag);
-  * tcpcsum_ipv4_batch_ptrs_host FILL over 1024 separately allocated pageable
-    buffers (the loop's own layout, loop.c:180-183): default (packets copied
-    into pinned staging) and TCPCSUM_CTX_AUTO_REGISTER (buffers page-locked
-    on first use, then read in place): first batch and steady state;
+  * tcpcsum_ipv4_batch_ptrs_host FILL over 1024 separately allocated 32 KiB
+    out-buffers (the loop's own layout, loop.c:180-183): malloc'd (packets
+    copied into pinned staging, checks stored back) and carved from one
+    tcpcsum_host_alloc pool (filled in place), for 1 / 2 / 4 / 8 copy threads
+    (TCPCSUM_HOST_WIRE_THREADS) and spin vs blocking wait — wall time and the
+    CPU time per batch (the calling thread + the copy threads, from the
+    context's counters: "core-us");
   * the sendmmsg seam itself (tools/mmsg_bench under libtcpcsum_preload.so,
-    default = staged, and TCPCSUM_PRELOAD_INPLACE=1) beside the reference's
-    CPU path for the same batch (one csum_continue per packet, -O2, one core).
+    the same variants, CPU time of the whole process per batch) beside the
+    reference's CPU path for the same batch (one csum_continue per packet,
+    -O2, one core).
 
   python tools/e2e.py  -> one JSON line per measurement
 """
@@ -88,9 +92,7 @@ def main():
         pin[:] = reg
         variants = ([(sh, fl) for sh in (-1, 0, 1, 3, 5) for fl in (0, tcp_amd.TUNE_WIN16)]
                     if "--sweep" in sys.argv else [(-1, 0)])
-        for name, r in (("pageable", reg), ("pinned_zero_copy", pin), ("pageable_registered", reg)):
-            if name == "pageable_registered":   # the pool page-locked once (tcpcsum_ctx_register_host)
-                ctx.register_host(reg.ctypes.data, reg.nbytes)
+        for name, r in (("pageable", reg), ("pinned_zero_copy", pin)):
             for sh, fl in variants:
                 ctx.set_tuning(0, 0, sh, fl)
                 ctx.ipv4_batch(r, offs, 32768, tcp_amd.IPV4_FILL)
@@ -102,9 +104,9 @@ def main():
                                   "GiB/s_packet_bytes_median": round(1024 * 1500 / tmed / 2**30, 2)}),
                       flush=True)
             ctx.set_tuning(0, 0, -1, 0)
-        ctx.unregister_host()
 
-    # the loop's own layout: 1024 separate pageable buffers, in and out alternating
+    # the loop's own layout: 1024 separate 32 KiB buffers, in and out alternating (malloc'd), or the
+    # out-buffers carved from one page-locked pool (INTEGRATION.md level 2)
     bufs = []
     for i in range(2048):
         b = np.empty(32768, np.uint8)
@@ -113,49 +115,54 @@ def main():
             b[:p.size] = p
         bufs.append(b)
     outb = bufs[1::2]
-    ptrs = np.array([b.ctypes.data for b in outb], np.uint64)   # an array: no per-call list conversion
+    pool = tcp_amd.pinned_empty(1024 * 32768)
+    for k, b in enumerate(outb):
+        pool[k * 32768:(k + 1) * 32768] = b
     lens = np.full(1024, 1500, np.uint32)
     ctx.close()
-    for mode in ("staged", "auto_register"):
-        ctx = tcp_amd.HostContext(0, auto_register=(mode == "auto_register"))
-        t0 = time.perf_counter()
-        ctx.ipv4_batch_ptrs(ptrs, lens, tcp_amd.IPV4_FILL)
-        first = time.perf_counter() - t0
-        tmin, tmed = best_of(lambda: ctx.ipv4_batch_ptrs(ptrs, lens, tcp_amd.IPV4_FILL), 200)
-        nreg, nbytes = ctx.registered()
-        print(json.dumps({"measure": "ipv4_fill_ptrs_host_1024x1500", "mode": mode,
-                          "layout": "1024 separate 32 KiB buffers (pageable)",
-                          "first_batch_us": round(first * 1e6, 1), "us_best": round(tmin * 1e6, 1),
-                          "us_median": round(tmed * 1e6, 1), "registrations": nreg, "registered_bytes": nbytes,
-                          "GiB/s_packet_bytes_median": round(1024 * 1500 / tmed / 2**30, 2),
-                          "ctx": ctx.stats()}), flush=True)
-        if "--sweep" in sys.argv:
-            for sh in (0, 1, 3, 4, 5, 6, 7, 8):
-                for fl in (0, tcp_amd.TUNE_WIN16, tcp_amd.TUNE_WIRE_CACHED):
-                    ctx.set_tuning(0, 0, sh, fl)
-                    tmin, tmed = best_of(lambda: ctx.ipv4_batch_ptrs(ptrs, lens, tcp_amd.IPV4_FILL), 100)
-                    print(json.dumps({"measure": "ipv4_fill_ptrs_host_1024x1500", "mode": mode, "shape": sh,
-                                      "flags": fl, "us_best": round(tmin * 1e6, 1), "us_median": round(tmed * 1e6, 1)}),
-                          flush=True)
-            ctx.set_tuning(0, 0, -1, 0)
-        ctx.unregister_host()
-    ctx.close()
+    reps = 200
+    for layout, ptrs in (("malloc", np.array([b.ctypes.data for b in outb], np.uint64)),
+                         ("pinned_pool", np.array([pool.ctypes.data + k * 32768 for k in range(1024)], np.uint64))):
+        for threads in ((1, 2, 4, 8) if layout == "malloc" else (1,)):
+            for wait in ("spin", "block"):
+                os.environ["TCPCSUM_HOST_WIRE_THREADS"] = str(threads)
+                ctx = tcp_amd.HostContext(0, blocking_wait=(wait == "block"))
+                t0 = time.perf_counter()
+                ctx.ipv4_batch_ptrs(ptrs, lens, tcp_amd.IPV4_FILL)
+                first = time.perf_counter() - t0
+                s0 = ctx.stats()
+                tmin, tmed = best_of(lambda: ctx.ipv4_batch_ptrs(ptrs, lens, tcp_amd.IPV4_FILL), reps)
+                s1 = ctx.stats()
+                print(json.dumps({"measure": "ipv4_fill_ptrs_host_1024x1500", "layout": layout, "wait": wait,
+                                  "copy_threads": s1["copy_threads"],
+                                  "first_batch_us": round(first * 1e6, 1), "us_best": round(tmin * 1e6, 1),
+                                  "us_median": round(tmed * 1e6, 1),
+                                  "cpu_caller_us_per_batch": round((s1["ns_cpu_caller"] - s0["ns_cpu_caller"]) / reps / 1e3, 1),
+                                  "cpu_workers_us_per_batch": round((s1["ns_cpu_workers"] - s0["ns_cpu_workers"]) / reps / 1e3, 1),
+                                  "in_place": s1["pkts_in_place"] - s0["pkts_in_place"],
+                                  "staged": s1["pkts_staged"] - s0["pkts_staged"]}), flush=True)
+                ctx.close()
+    os.environ.pop("TCPCSUM_HOST_WIRE_THREADS", None)
 
     # the seam itself: the interposer's per-batch latency vs the reference's CPU path
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     exe = os.path.join(repo, "tools", "mmsg_bench")
     pre = os.path.join(repo, "tcp_amd", "libtcpcsum_preload.so")
     import subprocess
-    for label, mode, env_extra in (("cpu_reference_O2", "cpu", {}),
-                                   ("preload_off", "gpu", {"TCPCSUM_PRELOAD_TX": "off"}),
-                                   ("preload_fill_staged", "gpu", {"TCPCSUM_PRELOAD_TX": "fill"}),
-                                   ("preload_fill_inplace", "gpu", {"TCPCSUM_PRELOAD_TX": "fill",
-                                                                    "TCPCSUM_PRELOAD_INPLACE": "1"})):
-        env = {k: v for k, v in os.environ.items() if not k.startswith("TCPCSUM_PRELOAD")}
+    variants = [("cpu_reference_O2", "cpu", {}, []), ("preload_off", "gpu", {"TCPCSUM_PRELOAD_TX": "off"}, [])]
+    for wait in ("block", "spin"):
+        for threads in (1, 2, 4, 8):
+            variants.append((f"preload_fill_staged_t{threads}_{wait}", "gpu",
+                             {"TCPCSUM_PRELOAD_TX": "fill", "TCPCSUM_PRELOAD_WAIT": wait,
+                              "TCPCSUM_HOST_WIRE_THREADS": str(threads)}, []))
+        variants.append((f"preload_fill_pinned_pool_{wait}", "gpu",
+                         {"TCPCSUM_PRELOAD_TX": "fill", "TCPCSUM_PRELOAD_WAIT": wait}, ["pinned"]))
+    for label, mode, env_extra, extra_args in variants:
+        env = {k: v for k, v in os.environ.items() if not k.startswith(("TCPCSUM_PRELOAD", "TCPCSUM_HOST"))}
         if mode == "gpu":
             env.update({"LD_PRELOAD": pre, "TCPCSUM_PRELOAD_ANY_SOCKET": "1"})
         env.update(env_extra)
-        r = subprocess.run([exe, mode, "300"], env=env, capture_output=True, text=True, timeout=300)
+        r = subprocess.run([exe, mode, "300"] + extra_args, env=env, capture_output=True, text=True, timeout=300)
         line = r.stdout.strip().splitlines()[-1] if r.stdout.strip() else "{}"
         d = json.loads(line)
         d.update({"measure": "sendmmsg_seam_1024x1500", "variant": label, "rc": r.returncode})

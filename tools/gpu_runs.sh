@@ -4,6 +4,25 @@
 # (`bash tools/gpu_runs.sh` alone lists them). Outputs go under gpurun_out/; the
 # summaries judged are copied into profiles/. Every GPU step has its own time limit.
 
+# round 4, first pass: every GPU test in one process (no child isolation left), the smoke, the
+# wire A/B against the round-3 build (asm stores + spilled FILL) and the host-path / seam sweeps
+# (wall time and CPU time per batch). Stops at the first GPU step that faults, aborts or times out.
+ok_rc() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
+gpu_r4_first() {
+(
+  timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > gpurun_out/r4_gputest1.log 2>&1; rc=$?
+  echo "pytest rc=$rc"; grep -E "passed|failed" gpurun_out/r4_gputest1.log | tail -2; grep FAILED gpurun_out/r4_gputest1.log | head -20
+  ok_rc $rc || exit $rc
+  timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r4_smoke.log 2>&1; rc=$?
+  echo "smoke rc=$rc"; tail -2 gpurun_out/r4_smoke.log
+  ok_rc $rc || exit $rc
+  timeout -k 10 300 python -u tools/wire_lib_ab.py tcp_amd/ab/libtcpcsum_wire_r3.so > gpurun_out/r4_wire_ab_r3.jsonl 2> gpurun_out/r4_wire_ab_r3.err; rc=$?
+  echo "wire ab rc=$rc"; ok_rc $rc || exit $rc
+  timeout -k 10 500 python -u tools/e2e.py > gpurun_out/r4_e2e.jsonl 2> gpurun_out/r4_e2e.err; rc=$?
+  echo "e2e rc=$rc"
+)
+}
+
 # round 3: wire FILL line store (default) — every GPU test first, then the A/B timing three
 # times (the two FILL stores must agree byte for byte every time)
 gpu_r3_fill() {

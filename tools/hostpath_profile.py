@@ -62,7 +62,6 @@ def main():
             ts.append(time.perf_counter() - t0)
         res[f"ptrs_{k}_packets"] = {"us_median": round(statistics.median(ts) * 1e6, 1),
                                     "us_min": round(min(ts) * 1e6, 1)}
-    ctx.unregister_host()
     ctx.close()
     print(json.dumps({"measure": "host_zero_copy_paths_1024x1500", "iters": iters, **res}))
 

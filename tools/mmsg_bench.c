@@ -13,9 +13,15 @@
  *                            csum_continue(getPseudoHeaderSum(...)) per packet
  *                            (tcpcsum_continue / tcpcsum_pseudo == context.c:104-145,
  *                            gcc -O2), stored at TCP+16 as context.c:208 does
+ *   mmsg_bench gpu <iters> pinned   the out-buffers carved from one tcpcsum_host_alloc
+ *                            pool instead (INTEGRATION.md level 2: loop.c:180-183
+ *                            allocating page-locked memory): filled in place
  *
  * Prints one JSON line: first-call and steady-state (min / median) latency
- * per 1024-packet batch, and whether every check equals the CPU's.
+ * per 1024-packet batch, the CPU time the whole process spent per batch
+ * (CLOCK_PROCESS_CPUTIME_ID: the calling thread, the library's copy threads
+ * and the HIP runtime's own threads — "core-us"), and whether every check
+ * equals the CPU's.
  */
 #define _GNU_SOURCE
 #include <arpa/inet.h>
@@ -71,20 +77,29 @@ static double now_us(void) {
     return ts.tv_sec * 1e6 + ts.tv_nsec * 1e-3;
 }
 
+static double cpu_us(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_PROCESS_CPUTIME_ID, &ts);
+    return ts.tv_sec * 1e6 + ts.tv_nsec * 1e-3;
+}
+
 static int cmp_d(const void *a, const void *b) {
     const double x = *(const double *) a, y = *(const double *) b;
     return x < y ? -1 : x > y;
 }
 
 int main(int argc, char **argv) {
-    if (argc < 3) { fprintf(stderr, "usage: %s gpu|cpu iters\n", argv[0]); return 2; }
+    if (argc < 3) { fprintf(stderr, "usage: %s gpu|cpu iters [pinned]\n", argv[0]); return 2; }
     const int gpu = !strcmp(argv[1], "gpu");
     const int iters = atoi(argv[2]) > 1 ? atoi(argv[2]) : 2;
+    const int pinned = argc > 3 && !strcmp(argv[3], "pinned");
     static uint8_t *inb[NPKT], *outb[NPKT];
+    uint8_t *pool = pinned ? (uint8_t *) tcpcsum_host_alloc((size_t) NPKT * SLOT) : NULL;
+    if (pinned && !pool) { fprintf(stderr, "tcpcsum_host_alloc failed\n"); return 2; }
     for (int i = 0; i < NPKT; ++i) {   /* loop.c:180-183: in and out buffers alternate */
         inb[i] = malloc(SLOT);
         memset(inb[i], 0, SLOT);          /* the rx buffers, touched as recvmmsg would */
-        outb[i] = malloc(SLOT);
+        outb[i] = pinned ? pool + (size_t) i * SLOT : malloc(SLOT);
         build(outb[i], i);
     }
     static struct iovec iov[NPKT];
@@ -97,8 +112,10 @@ int main(int argc, char **argv) {
     }
     const int fd = socket(AF_INET, SOCK_DGRAM, 0);
     double *t = malloc(sizeof(double) * (size_t) iters);
+    double *c = malloc(sizeof(double) * (size_t) iters);
     for (int k = 0; k < iters; ++k) {
         for (int i = 0; i < NPKT; ++i) memset(outb[i] + 36, 0, 2);   /* check = 0 (context.c:182) */
+        const double c0 = cpu_us();
         const double t0 = now_us();
         if (gpu) {
             (void) sendmmsg(fd, vec, NPKT, 0);
@@ -109,6 +126,7 @@ int main(int argc, char **argv) {
             }
         }
         t[k] = now_us() - t0;
+        c[k] = cpu_us() - c0;
     }
     int mismatches = 0;
     for (int i = 0; i < NPKT; ++i) {
@@ -119,11 +137,15 @@ int main(int argc, char **argv) {
     }
     const double first = t[0];
     qsort(t + 1, (size_t) (iters - 1), sizeof(double), cmp_d);
-    printf("{\"path\": \"%s\", \"batch\": \"1024 x 1500-B packets, separate 32 KiB malloc'd buffers (loop.c:180-183)\", "
-           "\"first_us\": %.1f, \"min_us\": %.1f, \"median_us\": %.1f, \"iters\": %d, \"checks_match_cpu\": %s, "
-           "\"mismatches\": %d}\n",
-           gpu ? "sendmmsg under libtcpcsum_preload.so" : "cpu csum_continue per packet (-O2)", first, t[1],
-           t[1 + (iters - 1) / 2], iters, mismatches ? "false" : "true", mismatches);
+    qsort(c + 1, (size_t) (iters - 1), sizeof(double), cmp_d);
+    double csum = 0;
+    for (int k = 1; k < iters; ++k) csum += c[k];
+    printf("{\"path\": \"%s\", \"batch\": \"1024 x 1500-B packets, separate 32 KiB %s buffers (loop.c:180-183)\", "
+           "\"first_us\": %.1f, \"min_us\": %.1f, \"median_us\": %.1f, \"cpu_us_median\": %.1f, "
+           "\"cpu_us_mean\": %.1f, \"iters\": %d, \"checks_match_cpu\": %s, \"mismatches\": %d}\n",
+           gpu ? "sendmmsg under libtcpcsum_preload.so" : "cpu csum_continue per packet (-O2)",
+           pinned ? "tcpcsum_host_alloc'd" : "malloc'd", first, t[1], t[1 + (iters - 1) / 2],
+           c[1 + (iters - 1) / 2], csum / (iters - 1), iters, mismatches ? "false" : "true", mismatches);
     close(fd);
     return 0;
 }

@@ -30,7 +30,7 @@ def build(kos):
     procs = []
     for ko in kos:
         obj = os.path.join(AB, f"kernels_txko{ko}.o")
-        procs.append((ko, obj, subprocess.Popen(["/opt/rocm/bin/hipcc"] + flags + [f"-DTCPCSUM_TX_KNOCKOUT={ko}", "-c",
+        procs.append((ko, obj, subprocess.Popen(["/opt/rocm/bin/hipcc"] + flags + ["-DTCPCSUM_MEASUREMENT_BUILD=1", f"-DTCPCSUM_TX_KNOCKOUT={ko}", "-c",
                       os.path.join(REPO, "tcp_amd", "csrc", "tcpcsum_kernels.hip"), "-o", obj])))
     objs = [os.path.join(REPO, "build", "obj", o) for o in ("tcpcsum_api.o", "tcpcsum_host.o", "scalar_dropin.o")]
     for ko, obj, p in procs:
