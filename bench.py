@@ -388,6 +388,110 @@ def run_wire(steps: int, warmup: int, device) -> dict:
     return res
 
 
+def gpu_numa_cpus(device_index: int):
+    """(NUMA node, CPUs of that node this process may use) of GPU `device_index`, from sysfs via its
+    PCI address; (None, None) when unknown."""
+    import torch
+    try:
+        p = torch.cuda.get_device_properties(device_index)
+        bus = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+        node = int(open(f"/sys/bus/pci/devices/{bus}/numa_node").read())
+        if node < 0:
+            return None, None
+        cpus = set()
+        for part in open(f"/sys/devices/system/node/node{node}/cpulist").read().strip().split(","):
+            a, _, b = part.partition("-")
+            cpus.update(range(int(a), int(b or a) + 1))
+        cpus &= os.sched_getaffinity(0)
+        return node, (cpus or None)
+    except Exception:
+        return None, None
+
+
+def gather_walls(wall: float, dist, world: int) -> list:
+    """Every rank's wall time, on every rank (gloo object gather; [wall] without a group)."""
+    if dist is None:
+        return [wall]
+    walls = [None] * world
+    dist.all_gather_object(walls, wall)
+    return walls
+
+
+def host_path_rate(bytes_per_rank: list, walls: list, steps: int) -> dict:
+    """Whole-job end-to-end rate: every rank's bytes x steps over the slowest rank's wall time."""
+    wmax = max(walls)
+    return {"GiB/s": round(sum(bytes_per_rank) * steps / wmax / (1 << 30), 2),
+            "per_rank_GiB/s": [round(b * steps / w / (1 << 30), 2) for b, w in zip(bytes_per_rank, walls)],
+            "wall_max_s": round(wmax, 6)}
+
+
+def run_host_path(steps: int, warmup: int, rank: int, world: int, local: int, dist, device,
+                  memory: str = "pageable") -> dict:
+    """The path as north_star states it — starting and ending in host memory (raw-socket buffers) —
+    one context per GPU (tcpcsum_ctx_*), every rank at once. Rank r owns its contiguous shard of
+    the global 1500-B config (N=8: BASELINE's 8M x 1500 config, Appendix B shard r), held in host
+    memory first touched from the CPUs of its GPU's NUMA node (the calling thread is moved there;
+    the context pins its copy threads there and its pinned staging comes from hipHostMalloc for
+    the current device). memory="pageable": each step is tcpcsum_batch_uniform_host over the
+    pageable shard (copied by the context's threads into pinned staging chunk by chunk, DMA to
+    HBM, kernel, results back into host memory); "pinned": the shard lives in tcpcsum_host_alloc
+    memory and the kernel reads it over PCIe in place. Inputs and results in host memory: PCIe and
+    host DRAM are the bound, not HBM. Rank 0 returns the whole-job rate, every
+    rank's results checked against its Appendix B digest."""
+    import numpy as np
+    import torch
+    import tcp_amd
+
+    per_gpu, L, _ = CONFIGS["1500"]
+    total = per_gpu * world
+    s0, cnt = shard_range(total, world, rank)
+    nbytes = cnt * L
+    node, cpus = gpu_numa_cpus(local)
+    saved = os.sched_getaffinity(0)
+    if cpus:
+        os.sched_setaffinity(0, cpus)
+    try:
+        # generated in HBM (Appendix B stream), then copied into host memory first touched here
+        d = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        tcp_amd.synth_fill(d, s0 * L, nbytes)
+        dss = torch.empty(cnt, dtype=torch.int32, device=device)
+        tcp_amd.synth_pseudo(dss, s0, cnt, L)
+        host = tcp_amd.pinned_empty(nbytes) if memory == "pinned" else np.empty(nbytes, np.uint8)
+        host[::4096] = 0   # first touch, page by page, from this node
+        torch.from_numpy(host).copy_(d)
+        ss = dss.cpu().numpy().view(np.uint32).copy()
+        del d, dss
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        ctx = tcp_amd.HostContext(local)
+        try:
+            res = ctx.batch_uniform(host, L, L, cnt, ss)
+            try:
+                check = digest_matches(res, "1500", world, rank, per_gpu)
+            except Exception:
+                check = None
+            if dist is not None:
+                flag = 1.0 if check else (0.0 if check is False else -1.0)
+                fl = -max_over_ranks(-flag, dist, device)
+                check = None if fl < 0 else bool(fl == 1.0)
+            s_before = ctx.stats()
+            wall = timed_region(lambda: ctx.batch_uniform(host, L, L, cnt, ss), steps, warmup, dist, lambda: None)
+            s_after = ctx.stats()
+        finally:
+            ctx.close()
+    finally:
+        os.sched_setaffinity(0, saved)
+    walls = gather_walls(wall, dist, world)
+    cpu_ns = (s_after["ns_cpu_caller"] - s_before["ns_cpu_caller"]) + (s_after["ns_cpu_workers"] - s_before["ns_cpu_workers"])
+    r = {"workload": f"{cnt} x {L}-byte segments per GPU in {memory} host memory "
+                     f"({'Appendix B shard ' + str(rank) + ' of ' + str(total) if world > 1 else 'Appendix B 1M x 1500'}), "
+                     "results back in host memory (tcpcsum_batch_uniform_host)",
+         "memory": memory, "steps": steps, **host_path_rate([nbytes] * world, walls, steps),
+         "digest_check": check, "numa_node_rank0": node, "copy_threads": s_after["bulk_threads"],
+         "cpu_core_s_per_step_rank0": round(cpu_ns / max(steps, 1) / 1e9, 4)}
+    return r
+
+
 def spawn_ranks(args, argv, script=None) -> int:
     """`bench.py --gpus N` with no launcher: start ranks 0..N-1 as child processes (this process
     has made no GPU call), rendezvous on 127.0.0.1, relay rank 0's JSON line, return the worst
@@ -477,6 +581,11 @@ def main(argv=None) -> int:
     ap.add_argument("--rotate", type=int, default=0, help="distinct batches to rotate (0 = auto)")
     ap.add_argument("--streams", type=int, default=1, choices=[1, 2],
                     help="2: consecutive launches alternate between two streams (pipelined batches)")
+    ap.add_argument("--no-host-path", action="store_true",
+                    help="skip the end-to-end host-memory leg (pageable and pinned shards, every rank)")
+    ap.add_argument("--host-path-only", action="store_true",
+                    help="only the end-to-end host-memory leg: one JSON line for it (tools/e2e_multi.sh)")
+    ap.add_argument("--host-steps", type=int, default=5)
     args = ap.parse_args(argv)
 
     rank, world, local = dist_env()
@@ -521,6 +630,20 @@ def main(argv=None) -> int:
     if rc != 0:
         raise SystemExit(f"bench.py: no usable gfx950 device ({rc}, '{arch}')")
     tcp_amd.set_tuning(args.max_blocks, args.unroll, args.shape, args.flags)
+
+    if args.host_path_only:
+        legs = {m: run_host_path(args.host_steps, min(args.warmup, 2), rank, world, local, dist, device, m)
+                for m in ("pageable", "pinned")}
+        if rank == 0:
+            print(json.dumps({"metric": "GiB/s checksummed end-to-end (host memory in and out, PCIe-inclusive)",
+                              "value": legs["pageable"]["GiB/s"], "unit": "GiB/s", "n_gpus": world,
+                              "higher_is_better": True, "scaling": "weak", "dtype": "u16",
+                              "data": "synthetic (SURVEY.md Appendix B generator)",
+                              "ranks_share_one_gpu": os.environ.get("TCPCSUM_BENCH_SHARE_DEVICE") == "1",
+                              "host_path": legs, "arch": arch}), flush=True)
+        if dist is not None:
+            dist.destroy_process_group()
+        return 0
 
     r, bufs, rot = run_config(args.config, args.steps, args.warmup, rank, world, dist, device, args.rotate,
                               streams=args.streams)
@@ -599,6 +722,14 @@ def main(argv=None) -> int:
         extra["wire_1500"] = run_wire(max(10, min(args.steps, 100)), min(args.warmup, 5), device)
         torch.cuda.empty_cache()
 
+    # end to end from host memory, every rank at once (PCIe and host DRAM bound; never `value`)
+    host_path = None
+    if not args.no_host_path:
+        del bufs
+        torch.cuda.empty_cache()
+        host_path = {m: run_host_path(args.host_steps, min(args.warmup, 2), rank, world, local, dist, device, m)
+                     for m in ("pageable", "pinned")}
+
     if rank == 0:
         total_bytes = batch_bytes * world * args.steps
         value = total_bytes / wall_max / (1 << 30)
@@ -638,6 +769,8 @@ def main(argv=None) -> int:
             line["stream_probe"] = probe
         if extra:
             line["other_configs"] = extra
+        if host_path:
+            line["host_path"] = host_path
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         print(json.dumps(line), flush=True)

@@ -76,6 +76,71 @@ def test_sharded_equals_unsharded_gloo(world, total):
     assert all(abs(o[4] - max(walls)) < 1e-12 for o in outs)
 
 
+def _host_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    import bench
+    import oracle
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # the host leg's sharding (bench.run_host_path): rank r's shard of world x 4096 segments,
+        # summed here by the oracle in place of the context
+        total = 4096 * world
+        s0, cnt = bench.shard_range(total, world, rank)
+        import time
+        out = {}
+
+        def step():
+            out["r"] = oracle.synth_batch(s0, cnt, 1500, threads=1)
+            time.sleep(0.002)
+
+        wall = bench.timed_region(step, 3, 1, dist, lambda: None)
+        walls = bench.gather_walls(wall, dist, world)
+        rate = bench.host_path_rate([cnt * 1500] * world, walls, 3)
+        objs = [None] * world
+        dist.all_gather_object(objs, (s0, cnt, out["r"].tobytes(), wall, walls, rate))
+        if rank == 0:
+            q.put(objs)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_host_path_sharding_and_aggregation_gloo(world):
+    """bench.run_host_path at N > 1 on CPU ranks: contiguous shards covering the global batch, every
+    rank sees every rank's wall time, and the whole-job rate is all ranks' bytes over the slowest."""
+    import torch.multiprocessing as mp
+
+    import oracle
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_host_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    objs = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    total = 4096 * world
+    gathered = np.concatenate([np.frombuffer(o[2], np.uint16) for o in objs])
+    assert np.array_equal(gathered, oracle.synth_batch(0, total, 1500))
+    walls = [o[3] for o in objs]
+    for o in objs:
+        assert o[4] == walls                                  # the same list on every rank
+        assert o[5]["wall_max_s"] == round(max(walls), 6)
+        assert abs(o[5]["GiB/s"] - total * 1500 * 3 / max(walls) / 2**30) < 0.01
+
+
+def test_host_path_rate_single():
+    import bench
+    r = bench.host_path_rate([1 << 30], [0.5], 2)
+    assert r["GiB/s"] == 4.0 and r["per_rank_GiB/s"] == [4.0]
+
+
 def test_shard_range_matches_appendix_b_shards(golden):
     import bench
     for k in range(8):

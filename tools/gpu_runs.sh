@@ -19,7 +19,11 @@ gpu_r4_first() {
   timeout -k 10 300 python -u tools/wire_lib_ab.py tcp_amd/ab/libtcpcsum_wire_r3.so > gpurun_out/r4_wire_ab_r3.jsonl 2> gpurun_out/r4_wire_ab_r3.err; rc=$?
   echo "wire ab rc=$rc"; ok_rc $rc || exit $rc
   timeout -k 10 500 python -u tools/e2e.py > gpurun_out/r4_e2e.jsonl 2> gpurun_out/r4_e2e.err; rc=$?
-  echo "e2e rc=$rc"
+  echo "e2e rc=$rc"; ok_rc $rc || exit $rc
+  timeout -k 10 300 bash tools/e2e_multi.sh 1 > gpurun_out/r4_e2e_multi_n1.json 2> gpurun_out/r4_e2e_multi_n1.err; rc=$?
+  echo "e2e n1 rc=$rc"; ok_rc $rc || exit $rc
+  TCPCSUM_BENCH_SHARE_DEVICE=1 timeout -k 10 300 bash tools/e2e_multi.sh 2 > gpurun_out/r4_e2e_multi_n2_shared.json 2> gpurun_out/r4_e2e_multi_n2_shared.err; rc=$?
+  echo "e2e n2 shared rc=$rc"
 )
 }
 
