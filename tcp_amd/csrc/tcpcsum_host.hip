@@ -169,7 +169,7 @@ struct tcpcsum_ctx {
     // TCPCSUM_CTX_BLOCKING_WAIT: wait for the device by sleeping on this event
     // (hipEventBlockingSync) instead of HIP's spin-wait in hipStreamSynchronize
     hipEvent_t done_ev = nullptr;
-    bool nt_copy = true;   // streaming stores for the uniform chunks (TCPCSUM_HOST_NT=0: plain memcpy)
+    bool nt_copy = true;   // streaming stores for staging copies, uniform and wire (TCPCSUM_HOST_NT=0: plain memcpy)
     bool stage_one_pass = true;   // wire staging laid out by bounds, one pass (TCPCSUM_HOST_STAGE_PASSES=2: by lengths)
     bool uniform_dma = true;   // staged uniform chunks go to HBM by DMA (TCPCSUM_HOST_DMA=0: kernel reads them over PCIe)
     tcpcsum_ctx_stats_t stats{};
@@ -323,7 +323,12 @@ int stage_packets(tcpcsum_ctx* c, uint64_t* k_off, uint32_t* k_len, size_t* stag
         size_t b = 0;
         for (size_t k = lo; k < hi; ++k) {
             if (by_bound) c->g_len[k] = copy_len(c->g_src[k], c->g_len[k]);
-            memcpy(gh + c->g_off[k], c->g_src[k], c->g_len[k]);
+            // streaming stores (TCPCSUM_HOST_NT, default on): the staging is read by the
+            // kernel over PCIe, never by this CPU — no read-for-ownership of its lines
+            if (c->nt_copy)
+                tcpcsum::copy_nt(gh + c->g_off[k], c->g_src[k], c->g_len[k]);
+            else
+                memcpy(gh + c->g_off[k], c->g_src[k], c->g_len[k]);
             k_off[c->g_idx[k]] = (uint64_t)(uintptr_t)(gd + c->g_off[k]);
             k_len[c->g_idx[k]] = c->g_len[k];
             b += c->g_len[k];
