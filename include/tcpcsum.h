@@ -253,9 +253,9 @@ int tcpcsum_ctx_set_tuning(tcpcsum_ctx_t *ctx, const tcpcsum_tuning_t *tune);
 
 /* Context flags (0 = default). (ABI v3's TCPCSUM_CTX_AUTO_REGISTER = 1 is gone
  * with the registration calls: the value is refused.) */
-/* Wait for the device by sleeping until it signals (a hipEventBlockingSync
- * event) instead of HIP's spin in hipStreamSynchronize: the calling thread
- * uses no CPU while the kernel runs, for a few microseconds more latency. */
+/* Wait for the device by polling its completion between short sleeps instead
+ * of HIP's spin in hipStreamSynchronize: the calling thread leaves its core
+ * while the kernel runs, for a few microseconds more latency. */
 #define TCPCSUM_CTX_BLOCKING_WAIT 2u
 int tcpcsum_ctx_set_flags(tcpcsum_ctx_t *ctx, uint32_t flags);
 

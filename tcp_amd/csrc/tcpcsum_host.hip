@@ -38,6 +38,8 @@
 #include <emmintrin.h>
 #include <hip/hip_runtime.h>
 #include <sched.h>
+#include <sys/prctl.h>
+#include <time.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -166,10 +168,12 @@ struct tcpcsum_ctx {
     // a releaseSend batch is ~1.5 MB, where extra threads cost more CPU than they save time
     int wire_threads = 1;
     int stage_threads = 1;   // the current staged batch's: wire_threads, or all for a large batch
-    // TCPCSUM_CTX_BLOCKING_WAIT: wait for the device by sleeping on this event
-    // (hipEventBlockingSync) instead of HIP's spin-wait in hipStreamSynchronize
+    // TCPCSUM_CTX_BLOCKING_WAIT: wait for the device by polling this event between
+    // short sleeps instead of HIP's spin in hipStreamSynchronize
     hipEvent_t done_ev = nullptr;
-    bool nt_copy = true;   // streaming stores for staging copies, uniform and wire (TCPCSUM_HOST_NT=0: plain memcpy)
+    uint64_t last_wait_ns = 0;   // the previous sleeping wait's length: the first sleep's guide
+    uint64_t poll_ns = 5000;     // sleep between polls (TCPCSUM_HOST_POLL_US, default 5)
+    bool nt_copy = true;   // streaming stores for the uniform chunks (TCPCSUM_HOST_NT=0: plain memcpy)
     bool stage_one_pass = true;   // wire staging laid out by bounds, one pass (TCPCSUM_HOST_STAGE_PASSES=2: by lengths)
     bool uniform_dma = true;   // staged uniform chunks go to HBM by DMA (TCPCSUM_HOST_DMA=0: kernel reads them over PCIe)
     tcpcsum_ctx_stats_t stats{};
@@ -228,14 +232,35 @@ void par_copy(tcpcsum_ctx* c, void* dst, const void* src, size_t n, bool nt = fa
 }
 
 // Wait for everything queued on st, timed into stats.ns_wait: hipStreamSynchronize
-// (HIP spins), or with TCPCSUM_CTX_BLOCKING_WAIT a blocking-sync event (the
-// thread sleeps until the device signals).
+// (HIP spins: the waiting thread burns a core for the kernel's whole length), or
+// with TCPCSUM_CTX_BLOCKING_WAIT a poll of the stream's completion event between
+// short sleeps — first for most of the previous wait's length, then every poll_ns
+// (1 us timer slack on this thread for the wait, restored after). A
+// hipEventBlockingSync event did not help: the runtime waits on its signal
+// actively for about a batch kernel's length, and the thread used as much CPU as
+// with hipStreamSynchronize (48.7 vs 48.5 us per 1024-packet in-place batch,
+// profiles/r04_e2e_first.jsonl).
 hipError_t wait_stream(tcpcsum_ctx* c, hipStream_t st) {
     const uint64_t t0 = tcpcsum::now_ns();
     hipError_t e;
     if (c->flags & TCPCSUM_CTX_BLOCKING_WAIT) {
         e = hipEventRecord(c->done_ev, st);
-        if (e == hipSuccess) e = hipEventSynchronize(c->done_ev);
+        const int slack = prctl(PR_GET_TIMERSLACK, 0, 0, 0, 0);
+        if (slack > 0) prctl(PR_SET_TIMERSLACK, 1000, 0, 0, 0);
+        uint64_t nap = c->last_wait_ns - c->last_wait_ns / 4;   // 3/4 of the last wait
+        if (nap > 2000000u) nap = 2000000u;
+        while (e == hipSuccess) {
+            e = hipEventQuery(c->done_ev);
+            if (e != hipErrorNotReady) break;
+            (void)hipGetLastError();   // not ready is not an error for us
+            e = hipSuccess;
+            const uint64_t ns = nap ? nap : c->poll_ns;
+            nap = 0;
+            timespec ts{(time_t)(ns / 1000000000u), (long)(ns % 1000000000u)};
+            nanosleep(&ts, nullptr);
+        }
+        if (slack > 0) prctl(PR_SET_TIMERSLACK, (unsigned long)slack, 0, 0, 0);
+        c->last_wait_ns = tcpcsum::now_ns() - t0;
     } else {
         e = hipStreamSynchronize(st);
     }
@@ -323,12 +348,11 @@ int stage_packets(tcpcsum_ctx* c, uint64_t* k_off, uint32_t* k_len, size_t* stag
         size_t b = 0;
         for (size_t k = lo; k < hi; ++k) {
             if (by_bound) c->g_len[k] = copy_len(c->g_src[k], c->g_len[k]);
-            // streaming stores (TCPCSUM_HOST_NT, default on): the staging is read by the
-            // kernel over PCIe, never by this CPU — no read-for-ownership of its lines
-            if (c->nt_copy)
-                tcpcsum::copy_nt(gh + c->g_off[k], c->g_src[k], c->g_len[k]);
-            else
-                memcpy(gh + c->g_off[k], c->g_src[k], c->g_len[k]);
+            // plain memcpy: streaming stores (copy_nt, with its sfence per packet) made a
+            // 1024 x 1500-B staged batch 4.6 x slower on one thread (618 vs 135 us,
+            // profiles/r04_e2e_first.jsonl) — they pay off only for the uniform path's
+            // 256 KiB pieces
+            memcpy(gh + c->g_off[k], c->g_src[k], c->g_len[k]);
             k_off[c->g_idx[k]] = (uint64_t)(uintptr_t)(gd + c->g_off[k]);
             k_len[c->g_idx[k]] = c->g_len[k];
             b += c->g_len[k];
@@ -424,6 +448,7 @@ int tcpcsum_ctx_create(int device, size_t scratch_bytes, tcpcsum_ctx_t** out) {
     c->stats.copy_threads = (uint64_t)c->wire_threads;
     c->stats.bulk_threads = (uint64_t)c->pool->threads();
     c->nt_copy = tcpcsum::env_int("TCPCSUM_HOST_NT", 1) != 0;
+    c->poll_ns = (uint64_t)std::max(1, tcpcsum::env_int("TCPCSUM_HOST_POLL_US", 5)) * 1000u;
     c->stage_one_pass = tcpcsum::env_int("TCPCSUM_HOST_STAGE_PASSES", 1) == 1;
     c->uniform_dma = tcpcsum::env_int("TCPCSUM_HOST_DMA", 1) != 0;
     for (int i = 0; i < 2; ++i) {
@@ -434,7 +459,7 @@ int tcpcsum_ctx_create(int device, size_t scratch_bytes, tcpcsum_ctx_t** out) {
             return hip_fail(e);
         }
     }
-    e = hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming | hipEventBlockingSync);
+    e = hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming);
     if (e != hipSuccess) {
         tcpcsum_ctx_destroy(c);
         return hip_fail(e);

@@ -27,6 +27,17 @@ gpu_r4_first() {
 )
 }
 
+# round 4: GPU tests, then the host-path / seam sweep again (wait modes, copy threads)
+gpu_r4_e2e() {
+(
+  timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/r4_gputest2.log 2>&1; rc=$?
+  echo "pytest rc=$rc"; grep -E "passed|failed" gpurun_out/r4_gputest2.log | tail -2; grep FAILED gpurun_out/r4_gputest2.log | head -20
+  ok_rc $rc || exit $rc
+  timeout -k 10 500 python -u tools/e2e.py > gpurun_out/r4_e2e_${TAG:-b}.jsonl 2> gpurun_out/r4_e2e_${TAG:-b}.err; rc=$?
+  echo "e2e rc=$rc"
+)
+}
+
 # round 3: wire FILL line store (default) — every GPU test first, then the A/B timing three
 # times (the two FILL stores must agree byte for byte every time)
 gpu_r3_fill() {
