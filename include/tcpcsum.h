@@ -361,6 +361,8 @@ int tcpcsum_plan_uniform(uint64_t base, uint64_t stride, uint32_t len, uint64_t 
  * inside the packet, the whole line is written back through, the check patched in) */
 #define TCPCSUM_TUNE_FILL_U16 512
 #define TCPCSUM_TUNE_TX_WT_STORE 1024  /* builder: payload stores written through (sc0 sc1 buffer stores) */
+/* wire FILL: the 64-B block holding the checks written through instead of the 128-B line */
+#define TCPCSUM_TUNE_FILL_HALF 2048
 /* 0 if *tune is a valid tuning (NULL counts as valid), else TCPCSUM_EINVAL. */
 int tcpcsum_tuning_check(const tcpcsum_tuning_t *tune);
 

@@ -23,7 +23,7 @@ except Exception:  # pragma: no cover - torch is always present in this image
 __all__ = [
     "DESC_DTYPE", "TXSEG_DTYPE", "IPV4_FILL", "IPV4_VERIFY", "IPV4_IPHDR", "PKT_OK", "PKT_SKIPPED",
     "PKT_IPHDR_BAD", "PKT_CSUM_PARTIAL", "CTX_BLOCKING_WAIT", "TUNE_WIRE_CACHED", "TUNE_WIN16", "TUNE_TX_NT_STORE", "TUNE_FILL_DWORD", "TUNE_FILL_U16",
-    "TUNE_TX_WT_STORE",
+    "TUNE_TX_WT_STORE", "TUNE_FILL_HALF",
     "TcpCsumError", "Tuning", "HostContext", "lib", "lib_path", "device_check", "build_info", "make_tuning", "set_tuning",
     "get_tuning", "plan_uniform", "getPseudoHeaderSum", "csum_continue", "batch_uniform", "batch_uniform_multi",
     "ubatches", "batch_desc",
@@ -204,7 +204,7 @@ def device_check() -> tuple[int, str]:
 PROBE_SLOTS = 8192
 TUNE_PIPE_ON, TUNE_PIPE_OFF, TUNE_NT_ON, TUNE_NT_OFF = 1, 2, 4, 8
 TUNE_WIRE_CACHED, TUNE_WIN16 = 32, 64   # wire kernel variants (tcpcsum.h)
-TUNE_TX_NT_STORE, TUNE_FILL_DWORD, TUNE_FILL_U16, TUNE_TX_WT_STORE = 128, 256, 512, 1024
+TUNE_TX_NT_STORE, TUNE_FILL_DWORD, TUNE_FILL_U16, TUNE_TX_WT_STORE, TUNE_FILL_HALF = 128, 256, 512, 1024, 2048
 
 
 # The C library holds no tuning state: every device call takes an explicit

@@ -1203,17 +1203,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(wire_waves(
         // partially dirty lines to be written back later: FILL on 1M x 1500-B
         // packets in 1536-B slots 0.328 -> 0.289 ms (VERIFY 0.246;
         // tools/fill_line_ab.py, profiles/r03_fill_line_ab.jsonl).
-        if (store_mode == 2 && !verify && amask == 127u && (m & 1u) == 0) {
+        // store_mode 3: the same with the 64-B block holding the checks (half the
+        // bytes written; of packed packets more qualify, since a 64-B block inside
+        // the packet is found for any start up to 64 B into a 128-B line).
+        if ((store_mode == 2 || store_mode == 3) && !verify && amask == 127u && (m & 1u) == 0) {
             const uint32_t cpos = m + th + 16u;   // window offset of the check (even)
             const uint32_t ipos = m + 10u;        // ... of the IPv4 header checksum
-            const uint32_t L = cpos >> 7;
+            const uint32_t bsz = store_mode == 3 ? 64u : 128u;   // the block written (wave-uniform)
+            const uint32_t b0 = cpos & ~(bsz - 1u);               // its window offset
             // Only the group's first round of registers stays live to the store (FILL
-            // k_ipv4<8,4,1>: 108 VGPRs with two rounds kept, 102 with one): lines 0
-            // and 1 for G >= 16 (L <= 1 always: m < 128, ihl*4 <= 60), line 0 — packets
-            // starting on a 128-B boundary — for G = 8; the rest take the 2-byte store
-            constexpr int KL = 1;
-            if (L <= 1u && (L << 7) >= m && (L << 7) + 128u <= m + tot && 8u * L + 8u <= (uint32_t)(G * KL) &&
-                (!iphdr || (ipos >> 7) == L)) {
+            // k_ipv4<8,4,1>: 108 VGPRs with two rounds kept, 102 with one): the block
+            // must lie in the group's first G chunks (128 B for G = 8) — for 128-B
+            // lines, packets starting on a 128-B boundary — the rest take the 2-byte store
+            constexpr uint32_t KB = 16u * (uint32_t)G;
+            if (b0 >= m && b0 + bsz <= m + tot && b0 + bsz <= KB && (!iphdr || (ipos & ~(bsz - 1u)) == b0)) {
                 auto patch = [](u32x4& x, uint32_t pos, uint32_t v16) {
                     const uint32_t sh = (pos & 2u) * 8u, j = (pos >> 2) & 3u;
                     const uint32_t keep = ~(0xffffu << sh), val = v16 << sh;
@@ -1222,15 +1225,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(wire_waves(
                     x.z = j == 2u ? (x.z & keep) | val : x.z;
                     x.w = j == 3u ? (x.w & keep) | val : x.w;
                 };
-#pragma unroll
-                for (int k = 0; k < KL; ++k) {
-                    const uint32_t idx = (uint32_t)(k * G + gl);
-                    if ((idx >> 3) == L) {
-                        u32x4 x = v[u][k];
-                        if (idx == (cpos >> 4)) patch(x, cpos, (uint32_t)d.c);
-                        if (iphdr && idx == (ipos >> 4)) patch(x, ipos, (uint32_t)ic_fill);
-                        stg_wt16(ip - m + (uint64_t)idx * 16u, x);
-                    }
+                const uint32_t idx = (uint32_t)gl;   // this lane's first-round chunk
+                if (idx * 16u - b0 < bsz) {
+                    u32x4 x = v[u][0];
+                    if (idx == (cpos >> 4)) patch(x, cpos, (uint32_t)d.c);
+                    if (iphdr && idx == (ipos >> 4)) patch(x, ipos, (uint32_t)ic_fill);
+                    stg_wt16(ip - m + (uint64_t)idx * 16u, x);
                 }
                 d.fill = false;   // stored
             }
@@ -1250,12 +1250,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(wire_waves(
             uint8_t* cp = d.ip + d.th + 16;
             if (store_mode == 1 && ((uintptr_t)cp & 3u) == 0)   // check and the unchanged urg_ptr in one dword
                 stg<uint32_t>(cp, d.urg | d.c);
-            else if (store_mode == 2)
+            else if (store_mode >= 2)
                 store_u16_wt(cp, d.c);   // native u16 store, as context.c:208, written through
             else
                 store_u16(cp, d.c);
             if (iphdr) {
-                if (store_mode == 2) store_u16_wt(d.ip + 10, d.ic);
+                if (store_mode >= 2) store_u16_wt(d.ip + 10, d.ic);
                 else store_u16(d.ip + 10, d.ic);
             }
         }
@@ -2182,7 +2182,8 @@ void launch_ipv4(uint8_t* pkts, const uint64_t* off, const uint32_t* plen, uint6
     const uint32_t amask = (tu.flags & TCPCSUM_TUNE_WIN16) ? 15u : 127u;
     // FILL store: the whole 128-B line written through where it lies inside the
     // packet (default), one native u16 (context.c:208), or the check|urg_ptr dword
-    const int dw = (tu.flags & TCPCSUM_TUNE_FILL_DWORD) ? 1 : (tu.flags & TCPCSUM_TUNE_FILL_U16) ? 0 : 2;
+    const int dw = (tu.flags & TCPCSUM_TUNE_FILL_DWORD) ? 1 : (tu.flags & TCPCSUM_TUNE_FILL_U16) ? 0
+                 : (tu.flags & TCPCSUM_TUNE_FILL_HALF) ? 3 : 2;
     // shape by the cap and by the mean packet footprint (region bytes / n; the
     // summed lengths for scatter-gather batches): packed small packets one
     // chunk per lane, MTU slots one round of 96 chunks per packet

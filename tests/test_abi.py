@@ -150,7 +150,7 @@ def test_argument_errors_need_no_device():
     for bad in (T(-1, 0, -1, 0), T(0, 3, -1, 0), T(0, 0, 14, 0), T(0, 0, -2, 0),
                 T(0, 0, -1, 3),      # PIPE_ON | PIPE_OFF
                 T(0, 0, -1, 12),     # NT_ON | NT_OFF
-                T(0, 0, -1, 2048)):
+                T(0, 0, -1, 4096)):
         assert L.tcpcsum_tuning_check(ctypes.byref(bad)) == api.EINVAL
         # every entry point rejects it before touching anything else (n == 0 included)
         assert L.tcpcsum_batch_uniform_dev(None, 0, 0, None, 0, None, 0, None, ctypes.byref(bad)) == api.EINVAL

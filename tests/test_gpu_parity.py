@@ -696,12 +696,12 @@ def test_ipv4_span_hint_mispredicted(dev, shape):
 @pytest.mark.parametrize("shape,flags", [(-1, 0), (-1, 32), (-1, 64), (-1, 96), (8, 0), (9, 0),
                                          (-1, 256), (-1, 320), (0, 256), (1, 256),
                                          (-1, 512), (-1, 576), (5, 512), (1, 0), (2, 0), (4, 0), (5, 0), (7, 0),
-                                         (-1, 544)])
+                                         (-1, 544), (-1, 2048), (1, 2048), (5, 2048), (7, 2048)])
 @pytest.mark.parametrize("layout", ["odd", "slot64", "slot16", "packed", "jumbo"])
 def test_ipv4_window_and_store_variants(dev, shape, flags, layout):
     """Wire kernel variants (128-B or 16-B packet windows; non-temporal or default-policy loads;
-    check|urg_ptr dword stores; the default whole-line write-through stores or forced 2-byte
-    stores) are exact and FILL rewrites nothing but the checks, in every
+    check|urg_ptr dword stores; the default whole-line write-through stores, 64-B block stores
+    (TUNE_FILL_HALF) or forced 2-byte stores) are exact and FILL rewrites nothing but the checks, in every
     layout: odd packed offsets, 64-B aligned slots, 16-B (not 64-B) aligned slots, packed tiny
     packets, 9000-B jumbo frames at odd offsets (the multi-round path)."""
     import tcp_amd

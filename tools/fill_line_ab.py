@@ -57,13 +57,17 @@ def main():
         out = torch.empty(m, dtype=torch.int16, device=dev)
         sta = torch.empty(m, dtype=torch.uint8, device=dev)
         u16 = tcp_amd.make_tuning(0, 0, -1, tcp_amd.TUNE_FILL_U16)
+        half = tcp_amd.make_tuning(0, 0, -1, tcp_amd.TUNE_FILL_HALF)
         paths = {"fill_u16": lambda: tcp_amd.ipv4_batch(reg, doff, m, cap, 0, out, sta, tune=u16),
                  "fill_line": lambda: tcp_amd.ipv4_batch(reg, doff, m, cap, 0, out, sta),
+                 "fill_half": lambda: tcp_amd.ipv4_batch(reg, doff, m, cap, 0, out, sta, tune=half),
                  "verify": lambda: tcp_amd.ipv4_batch(reg, doff, m, cap, 1, out, sta)}
         paths["fill_u16"]()
         a = (out.clone(), reg.clone())
         paths["fill_line"]()
         equal = bool(torch.equal(a[0], out) and torch.equal(a[1], reg))
+        paths["fill_half"]()
+        equal = equal and bool(torch.equal(a[0], out) and torch.equal(a[1], reg))
         if not equal:   # where the variants differ (bytes of the region, and results)
             d = (a[1] != reg).nonzero().flatten()
             dd = d.cpu().numpy()[:20]

@@ -38,6 +38,20 @@ gpu_r4_e2e() {
 )
 }
 
+# round 4: the wire FILL block-store variants (128-B line vs 64-B block vs 2-byte) — parity of the
+# store variants first, then the interleaved A/B, then the e2e sweep
+gpu_r4_fillhalf() {
+(
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -q --timeout 120 --timeout-method thread -k "window_and_store or ipv4" > gpurun_out/r4_fillhalf_parity.log 2>&1; rc=$?
+  echo "parity rc=$rc"; grep -E "passed|failed" gpurun_out/r4_fillhalf_parity.log | tail -1
+  ok_rc $rc || exit $rc
+  timeout -k 10 300 python -u tools/fill_line_ab.py --rounds 5 > gpurun_out/r4_fill_half_ab.jsonl 2> gpurun_out/r4_fill_half_ab.err; rc=$?
+  echo "ab rc=$rc"; ok_rc $rc || exit $rc
+  timeout -k 10 500 python -u tools/e2e.py > gpurun_out/r4_e2e_b.jsonl 2> gpurun_out/r4_e2e_b.err; rc=$?
+  echo "e2e rc=$rc"
+)
+}
+
 # round 3: wire FILL line store (default) — every GPU test first, then the A/B timing three
 # times (the two FILL stores must agree byte for byte every time)
 gpu_r3_fill() {
@@ -239,6 +253,26 @@ round3_profile() {
   M="python3 tools/multi_sweep.py --ks 16 --unrolls 4 --grids 0 --rounds 1 --steps 10"
   run mfetch timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_multi_fetch -o p -- $M > $O/pmc_multi_fetch.log 2>&1
   run mwrite timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_multi_write -o p -- $M > $O/pmc_multi_write.log 2>&1
+  W="python3 tools/wire_fill_pmc.py"
+  run wwrite timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_wire_write -o p -- $W > $O/pmc_wire_write.log 2>&1
+  run wfetch timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_wire_fetch -o p -- $W > $O/pmc_wire_fetch.log 2>&1
+  run wkt timeout -s KILL 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_wire -o k -- $W > $O/kt_wire.log 2>&1
+  echo done
+)
+}
+
+# Round-4 evidence: rocprofv3 kernel trace of the headline bench, FETCH_SIZE of the headline
+# kernel (traffic.json "1500"), WRITE_SIZE / FETCH_SIZE / kernel trace of the wire FILL stores
+# (the FILL instantiation no longer spills: its scratch write-back should be gone).
+round4_profile() {
+(
+  O=gpurun_out/r4prof
+  mkdir -p $O
+  cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+  B="python3 bench.py --steps 100 --no-other-configs --no-cpu-baseline --no-host-path"
+  run() { echo "== $1"; shift; "$@" || { echo "failed: $?"; exit 1; }; }
+  run kt timeout -s KILL 180 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o k -- $B > $O/bench_under_rocprof.json 2> $O/kt.err
+  run fetch timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o p -- $B > $O/pmc_fetch.log 2>&1
   W="python3 tools/wire_fill_pmc.py"
   run wwrite timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_wire_write -o p -- $W > $O/pmc_wire_write.log 2>&1
   run wfetch timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_wire_fetch -o p -- $W > $O/pmc_wire_fetch.log 2>&1
