@@ -52,6 +52,16 @@ gpu_r4_fillhalf() {
 )
 }
 
+# round 4: the default bench line once (new host_path leg at N=1) and N=2 with both ranks on one GPU
+gpu_r4_bench() {
+(
+  timeout -k 10 500 python3 bench.py > gpurun_out/r4_bench_${TAG:-a}.json 2> gpurun_out/r4_bench_${TAG:-a}.err; rc=$?
+  echo "bench rc=$rc"; ok_rc $rc || exit $rc
+  TCPCSUM_BENCH_SHARE_DEVICE=1 timeout -k 10 400 python3 bench.py --gpus 2 --steps 50 > gpurun_out/r4_bench_n2_shared_${TAG:-a}.json 2> gpurun_out/r4_bench_n2_shared_${TAG:-a}.err; rc=$?
+  echo "bench n2 rc=$rc"
+)
+}
+
 # round 3: wire FILL line store (default) — every GPU test first, then the A/B timing three
 # times (the two FILL stores must agree byte for byte every time)
 gpu_r3_fill() {
