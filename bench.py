@@ -448,7 +448,7 @@ def run_host_path(steps: int, warmup: int, rank: int, world: int, local: int, di
     nbytes = cnt * L
     node, cpus = gpu_numa_cpus(local)
     saved = os.sched_getaffinity(0)
-    if cpus:
+    if cpus and os.environ.get("TCPCSUM_BENCH_HOST_NUMA", "1") != "0":
         os.sched_setaffinity(0, cpus)
     try:
         # generated in HBM (Appendix B stream), then copied into host memory first touched here

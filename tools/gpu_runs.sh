@@ -62,6 +62,23 @@ gpu_r4_bench() {
 )
 }
 
+# round 4: NUMA placement of the host-path leg — the bench's thread affinity (first touch) and
+# the context's copy-thread pinning on / off, interleaved twice, N=1
+gpu_r4_numa() {
+(
+  for rep in 1 2; do
+    for a in 1 0; do
+      for n in 1 0; do
+        TCPCSUM_BENCH_HOST_NUMA=$a TCPCSUM_HOST_NUMA=$n timeout -k 10 200 python3 bench.py --host-path-only --host-steps 10 > gpurun_out/r4_numa_a${a}_n${n}_rep$rep.json 2>> gpurun_out/r4_numa.err; rc=$?
+        echo "a=$a n=$n rc=$rc $(python3 -c "import json,sys; d=json.load(open('gpurun_out/r4_numa_a${a}_n${n}_rep$rep.json'))['host_path']; print(d['pageable']['GiB/s'], d['pinned']['GiB/s'], d['pageable']['numa_node_rank0'], d['pageable']['cpu_core_s_per_step_rank0'])")"
+        ok_rc $rc || exit $rc
+      done
+    done
+  done
+  lscpu | grep -i numa >> gpurun_out/r4_numa_topology.txt; cat /sys/fs/cgroup/cpu.max >> gpurun_out/r4_numa_topology.txt 2>/dev/null; true
+)
+}
+
 # round 3: wire FILL line store (default) — every GPU test first, then the A/B timing three
 # times (the two FILL stores must agree byte for byte every time)
 gpu_r3_fill() {
