@@ -417,6 +417,21 @@ def gather_walls(wall: float, dist, world: int) -> list:
     return walls
 
 
+def page_node_of(arr) -> int | None:
+    """NUMA node of the first page of a numpy array (get_mempolicy MPOL_F_NODE|MPOL_F_ADDR), or None."""
+    import ctypes
+    try:
+        libc = ctypes.CDLL(None, use_errno=True)
+        node = ctypes.c_int(-1)
+        # SYS_get_mempolicy = 239 on x86-64; flags MPOL_F_NODE | MPOL_F_ADDR = 3
+        if libc.syscall(239, ctypes.byref(node), None, ctypes.c_ulong(0), ctypes.c_void_p(arr.ctypes.data),
+                        ctypes.c_ulong(3)) != 0:
+            return None
+        return node.value
+    except Exception:
+        return None
+
+
 def host_path_rate(bytes_per_rank: list, walls: list, steps: int) -> dict:
     """Whole-job end-to-end rate: every rank's bytes x steps over the slowest rank's wall time."""
     wmax = max(walls)
@@ -477,6 +492,7 @@ def run_host_path(steps: int, warmup: int, rank: int, world: int, local: int, di
             s_before = ctx.stats()
             wall = timed_region(lambda: ctx.batch_uniform(host, L, L, cnt, ss), steps, warmup, dist, lambda: None)
             s_after = ctx.stats()
+            data_node = page_node_of(host)
         finally:
             ctx.close()
     finally:
@@ -488,6 +504,7 @@ def run_host_path(steps: int, warmup: int, rank: int, world: int, local: int, di
                      "results back in host memory (tcpcsum_batch_uniform_host)",
          "memory": memory, "steps": steps, **host_path_rate([nbytes] * world, walls, steps),
          "digest_check": check, "numa_node_rank0": node, "copy_threads": s_after["bulk_threads"],
+         "staging_numa_node_rank0": s_after["staging_numa_node"], "data_numa_node_rank0": data_node,
          "cpu_core_s_per_step_rank0": round(cpu_ns / max(steps, 1) / 1e9, 4)}
     return r
 

@@ -271,6 +271,8 @@ typedef struct tcpcsum_ctx_stats {
     uint64_t ns_wait;            /* wall time spent waiting for the device after the last launch */
     uint64_t ns_cpu_caller;      /* CPU time of the calling threads inside this context's host calls */
     uint64_t ns_cpu_workers;     /* CPU time of its copy threads since creation (copies, spin, wake-ups) */
+    uint64_t gpu_numa_node;      /* the device's NUMA node (UINT64_MAX: unknown); staging and copy threads go there */
+    uint64_t staging_numa_node;  /* where the pinned staging's first page lives (UINT64_MAX: none yet / unknown) */
 } tcpcsum_ctx_stats_t;
 int tcpcsum_ctx_get_stats(tcpcsum_ctx_t *ctx, tcpcsum_ctx_stats_t *out);
 

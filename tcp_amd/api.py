@@ -107,7 +107,8 @@ class CtxStats(ctypes.Structure):
     _fields_ = [("batches", ctypes.c_uint64), ("pkts_in_place", ctypes.c_uint64), ("pkts_staged", ctypes.c_uint64),
                 ("bytes_staged", ctypes.c_uint64), ("copy_threads", ctypes.c_uint64),
                 ("bulk_threads", ctypes.c_uint64), ("ns_copy", ctypes.c_uint64), ("ns_wait", ctypes.c_uint64),
-                ("ns_cpu_caller", ctypes.c_uint64), ("ns_cpu_workers", ctypes.c_uint64)]
+                ("ns_cpu_caller", ctypes.c_uint64), ("ns_cpu_workers", ctypes.c_uint64),
+                ("gpu_numa_node", ctypes.c_uint64), ("staging_numa_node", ctypes.c_uint64)]
 
 # name -> (restype, argtypes); must cover every function in include/tcpcsum.h
 SIGNATURES = {
@@ -444,7 +445,11 @@ class HostContext:
     def stats(self) -> dict:
         st = CtxStats()
         _check(lib().tcpcsum_ctx_get_stats(self._h, ctypes.byref(st)), "tcpcsum_ctx_get_stats")
-        return {k: int(getattr(st, k)) for k, _ in CtxStats._fields_}
+        d = {k: int(getattr(st, k)) for k, _ in CtxStats._fields_}
+        for k in ("gpu_numa_node", "staging_numa_node"):   # UINT64_MAX: unknown
+            if d[k] == 2**64 - 1:
+                d[k] = None
+        return d
 
     def close(self) -> None:
         if self._h:

@@ -193,8 +193,8 @@ int default_copy_threads() {
 }
 
 // The CPUs of `device_pci_bus`'s NUMA node (sysfs, "0000:8e:00.0" style) that
-// this process may run on; false when unknown or none.
-inline bool numa_node_cpus(const char* device_pci_bus, cpu_set_t* out) {
+// this process may run on, and the node (nullable); false when unknown or none.
+inline bool numa_node_cpus(const char* device_pci_bus, cpu_set_t* out, int* node_out = nullptr) {
     char path[256], buf[4096];
     std::string bus(device_pci_bus);
     for (auto& ch : bus) ch = (char)tolower((unsigned char)ch);
@@ -205,6 +205,7 @@ inline bool numa_node_cpus(const char* device_pci_bus, cpu_set_t* out) {
         fclose(f);
     }
     if (node < 0) return false;
+    if (node_out) *node_out = node;
     snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
     FILE* f = fopen(path, "r");
     if (!f) return false;

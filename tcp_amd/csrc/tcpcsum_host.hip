@@ -38,7 +38,10 @@
 #include <emmintrin.h>
 #include <hip/hip_runtime.h>
 #include <sched.h>
+#include <linux/mempolicy.h>
 #include <sys/prctl.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 #include <time.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -90,11 +93,37 @@ inline int env_int(const char* name, int dflt) {
     return e && *e ? atoi(e) : dflt;
 }
 
+// NUMA node of the (touched) host page at p, or -1.
+inline int page_node(const void* p) {
+    int node = -1;
+    if (!p || syscall(SYS_get_mempolicy, &node, nullptr, 0, p, MPOL_F_NODE | MPOL_F_ADDR) != 0) return -1;
+    return node;
+}
+
+// hipHostMalloc on NUMA node `node` (-1: HIP's choice): the calling thread's memory
+// policy is set to prefer that node for the allocation (hipHostMallocNumaUser: the
+// pages follow the thread's policy) and restored after. On a box whose GPU sits on
+// node 1, the default placement put the staging elsewhere: the pageable end-to-end
+// path ran at 32 GiB/s there against 50 on node-0 boxes (profiles/r04_bench_first.json).
+inline hipError_t host_malloc_on(void** p, size_t bytes, int node) {
+    if (node < 0 || node >= 1024) return hipHostMalloc(p, bytes, hipHostMallocDefault);
+    int mode = 0;
+    unsigned long old_mask[16] = {0};
+    const bool saved = syscall(SYS_get_mempolicy, &mode, old_mask, 1024ul, nullptr, 0ul) == 0;
+    unsigned long mask[16] = {0};
+    mask[node / 64] = 1ul << (node % 64);
+    const bool set = saved && syscall(SYS_set_mempolicy, MPOL_PREFERRED, mask, 1024ul) == 0;
+    hipError_t e = hipHostMalloc(p, bytes, set ? hipHostMallocNumaUser : hipHostMallocDefault);
+    if (set) syscall(SYS_set_mempolicy, mode, (mode == MPOL_DEFAULT) ? nullptr : old_mask, 1024ul);
+    return e;
+}
+
 // Page-locked host memory owned by a context, with its device view.
 struct Pinned {
     uint8_t* h = nullptr;
     uint8_t* d = nullptr;
     size_t bytes = 0;
+    int node = -1;   // NUMA node to allocate on (the GPU's), -1: HIP's choice
     Pinned() = default;
     Pinned(const Pinned&) = delete;
     Pinned& operator=(const Pinned&) = delete;
@@ -106,7 +135,7 @@ struct Pinned {
         while (nb < need) nb *= 2;
         release();
         void* p = nullptr;
-        hipError_t e = hipHostMalloc(&p, nb, hipHostMallocDefault);
+        hipError_t e = host_malloc_on(&p, nb, node);
         if (e != hipSuccess) {
             (void)hipGetLastError();
             return e;
@@ -166,6 +195,7 @@ struct tcpcsum_ctx {
     std::unique_ptr<tcpcsum::CopyPool> pool;
     // threads a staged wire batch copies on, the caller included (TCPCSUM_HOST_WIRE_THREADS):
     // a releaseSend batch is ~1.5 MB, where extra threads cost more CPU than they save time
+    int gpu_node = -1;   // the GPU's NUMA node, where the staging is allocated (-1: unknown / off)
     int wire_threads = 1;
     int stage_threads = 1;   // the current staged batch's: wire_threads, or all for a large batch
     // TCPCSUM_CTX_BLOCKING_WAIT: wait for the device by polling this event between
@@ -431,10 +461,16 @@ int tcpcsum_ctx_create(int device, size_t scratch_bytes, tcpcsum_ctx_t** out) {
     // (TCPCSUM_HOST_NUMA=0: wherever the scheduler puts them)
     cpu_set_t node_cpus;
     char bus[64] = {0};
+    int gpu_node = -1;
     const bool numa = tcpcsum::env_int("TCPCSUM_HOST_NUMA", 1) != 0 &&
                       hipDeviceGetPCIBusId(bus, sizeof bus, device) == hipSuccess &&
-                      tcpcsum::numa_node_cpus(bus, &node_cpus);
+                      tcpcsum::numa_node_cpus(bus, &node_cpus, &gpu_node);
     (void)hipGetLastError();
+    // pinned staging on the GPU's node too (the copy threads write it, the DMA reads it)
+    c->gpu_node = numa ? gpu_node : -1;
+    for (tcpcsum::Pinned* pp : {&c->slot[0], &c->slot[1], &c->gath, &c->ss, &c->res, &c->p_off, &c->p_len, &c->p_out,
+                                &c->p_stat})
+        pp->node = c->gpu_node;
     // never more workers than the node has CPUs this process may use (the caller is one of
     // the copiers too, wherever it runs)
     int copiers = tcpcsum::default_copy_threads();
@@ -502,6 +538,10 @@ int tcpcsum_ctx_get_stats(tcpcsum_ctx_t* c, tcpcsum_ctx_stats_t* out) {
     if (!c || !out) return TCPCSUM_EINVAL;
     std::lock_guard<std::mutex> lk(c->mu);
     c->stats.ns_cpu_workers = c->pool->worker_cpu_ns();
+    c->stats.gpu_numa_node = c->gpu_node < 0 ? UINT64_MAX : (uint64_t)c->gpu_node;
+    const void* st = c->slot[0].h ? (const void*)c->slot[0].h : c->gath.h ? (const void*)c->gath.h : (const void*)c->p_off.h;
+    const int sn = tcpcsum::page_node(st);
+    c->stats.staging_numa_node = sn < 0 ? UINT64_MAX : (uint64_t)sn;
     *out = c->stats;
     return TCPCSUM_OK;
 }

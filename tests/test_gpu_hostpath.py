@@ -116,3 +116,28 @@ def test_two_threads_one_pageable_buffer(dev):
         t.join()
     torch.cuda.synchronize()
     assert not errors, errors
+
+
+def test_staging_on_the_gpus_numa_node(dev):
+    """The context's pinned staging is allocated on its GPU's NUMA node (hipHostMallocNumaUser under a
+    preferred-node policy that is restored afterwards), where its copy threads run."""
+    import ctypes
+    import tcp_amd
+    libc = ctypes.CDLL(None, use_errno=True)
+
+    def policy():
+        mode = ctypes.c_int(-1)
+        mask = (ctypes.c_ulong * 16)()
+        assert libc.syscall(239, ctypes.byref(mode), mask, ctypes.c_ulong(1024), None, ctypes.c_ulong(0)) == 0
+        return mode.value, list(mask)
+
+    before = policy()
+    rng = np.random.default_rng(3)
+    region = rng.integers(0, 256, 1 << 22, dtype=np.uint8)
+    with tcp_amd.HostContext(0) as ctx:
+        u = ctx.batch_uniform(region, 1500, 1500, (region.size - 1500) // 1500, 7)
+        assert np.array_equal(u, oracle.batch_uniform(region, 1500, 1500, u.size, 7))
+        s = ctx.stats()
+    assert policy() == before                      # the calling thread's memory policy is untouched
+    if s["gpu_numa_node"] is not None and s["staging_numa_node"] is not None:
+        assert s["staging_numa_node"] == s["gpu_numa_node"], s

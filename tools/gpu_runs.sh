@@ -79,6 +79,20 @@ gpu_r4_numa() {
 )
 }
 
+# round 4: GPU tests after the NUMA staging change, then the host-path leg twice (NUMA nodes reported)
+gpu_r4_numa2() {
+(
+  timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/r4_gputest3.log 2>&1; rc=$?
+  echo "pytest rc=$rc"; grep -E "passed|failed" gpurun_out/r4_gputest3.log | tail -2; grep FAILED gpurun_out/r4_gputest3.log | head -20
+  ok_rc $rc || exit $rc
+  for rep in 1 2; do
+    timeout -k 10 200 python3 bench.py --host-path-only --host-steps 10 > gpurun_out/r4_numa2_rep$rep.json 2>> gpurun_out/r4_numa2.err; rc=$?
+    echo "rep $rep rc=$rc $(python3 -c "import json; d=json.load(open('gpurun_out/r4_numa2_rep$rep.json'))['host_path']; print({m: (d[m]['GiB/s'], d[m]['numa_node_rank0'], d[m]['staging_numa_node_rank0'], d[m]['data_numa_node_rank0']) for m in d})")"
+    ok_rc $rc || exit $rc
+  done
+)
+}
+
 # round 3: wire FILL line store (default) — every GPU test first, then the A/B timing three
 # times (the two FILL stores must agree byte for byte every time)
 gpu_r3_fill() {
