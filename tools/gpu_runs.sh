@@ -93,6 +93,15 @@ gpu_r4_numa2() {
 )
 }
 
+# round 4: N=8 rehearsal of the whole bench (device headline + the host-memory leg on every rank)
+# with all eight ranks on the one GPU of this box
+gpu_r4_n8() {
+(
+  TCPCSUM_BENCH_SHARE_DEVICE=1 timeout -k 10 600 python3 bench.py --gpus 8 --steps 5 --warmup 2 > gpurun_out/r4_bench_n8_shared.json 2> gpurun_out/r4_bench_n8_shared.err; rc=$?
+  echo "n8 rc=$rc"; cut -c1-300 gpurun_out/r4_bench_n8_shared.json
+)
+}
+
 # round 3: wire FILL line store (default) — every GPU test first, then the A/B timing three
 # times (the two FILL stores must agree byte for byte every time)
 gpu_r3_fill() {
