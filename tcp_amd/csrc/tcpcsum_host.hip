@@ -206,6 +206,7 @@ struct tcpcsum_ctx {
     bool nt_copy = true;   // streaming stores for the uniform chunks (TCPCSUM_HOST_NT=0: plain memcpy)
     bool stage_one_pass = true;   // wire staging laid out by bounds, one pass (TCPCSUM_HOST_STAGE_PASSES=2: by lengths)
     bool uniform_dma = true;   // staged uniform chunks go to HBM by DMA (TCPCSUM_HOST_DMA=0: kernel reads them over PCIe)
+    bool pinned_dma = true;    // large page-locked uniform batches go to HBM by DMA (TCPCSUM_HOST_PINNED_DMA=0: in place)
     tcpcsum_ctx_stats_t stats{};
     std::mutex mu;
 };
@@ -487,6 +488,7 @@ int tcpcsum_ctx_create(int device, size_t scratch_bytes, tcpcsum_ctx_t** out) {
     c->poll_ns = (uint64_t)std::max(1, tcpcsum::env_int("TCPCSUM_HOST_POLL_US", 5)) * 1000u;
     c->stage_one_pass = tcpcsum::env_int("TCPCSUM_HOST_STAGE_PASSES", 1) == 1;
     c->uniform_dma = tcpcsum::env_int("TCPCSUM_HOST_DMA", 1) != 0;
+    c->pinned_dma = tcpcsum::env_int("TCPCSUM_HOST_PINNED_DMA", 1) != 0;
     for (int i = 0; i < 2; ++i) {
         e = hipStreamCreateWithFlags(&c->st[i], hipStreamNonBlocking);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->slot_ev[i], hipEventDisableTiming);
@@ -561,7 +563,11 @@ void tcpcsum_host_free(void* p) {
     if (p) hipHostFree(p);
 }
 
-// Page-locked input: one launch reads the segments in place. Pageable input:
+// Page-locked input: small batches (< 2 chunks) are read in place by one launch
+// over PCIe; larger ones go to HBM by DMA straight from the caller's pages,
+// chunk by chunk, alternating between two streams and two HBM slots — every
+// copy and kernel queued at once, stream order keeping a slot's next copy behind
+// its last kernel (TCPCSUM_HOST_PINNED_DMA=0: always in place). Pageable input:
 // chunks alternate between two streams and two pinned staging slots; the copy
 // threads fill slot k&1 with chunk k while the kernel reads chunk k-1 from the
 // other slot. Start values and results use the caller's arrays when those are
@@ -596,34 +602,62 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t st
         kout = (uint16_t*)c->res.d;
     }
     const size_t span = (size_t)((n - 1) * stride + len);
-    if (const uint8_t* zb = (const uint8_t*)pinned_dev_ptr(h_base, span)) {
+    // segments per chunk: (cnt-1)*stride + len <= chunk (at least one segment)
+    uint64_t per = 1;
+    if (stride == 0) per = n;
+    else if (c->chunk > len) per = (c->chunk - len) / stride + 1;
+    if (per > n) per = n;
+    const size_t slot_bytes = (size_t)((per - 1) * stride + len) + 16;
+    auto ensure_hbm_slots = [&]() -> hipError_t {
+        if (slot_bytes <= c->d_slot_bytes) return hipSuccess;
+        for (int i = 0; i < 2; ++i) {
+            if (c->d_slot[i]) (void)hipFree(c->d_slot[i]);
+            c->d_slot[i] = nullptr;
+        }
+        c->d_slot_bytes = 0;
+        for (int i = 0; i < 2; ++i) {
+            const hipError_t he = hipMalloc(&c->d_slot[i], slot_bytes);
+            if (he != hipSuccess) return he;
+        }
+        c->d_slot_bytes = slot_bytes;
+        return hipSuccess;
+    };
+    const uint8_t* zb = (const uint8_t*)pinned_dev_ptr(h_base, span);
+    if (zb && (!c->pinned_dma || per * 2 > n)) {
         tcpcsum::launch_uniform(zb, stride, len, kss, sum_start, kout, n, c->st[0], tu);
         rc = check_launch();
         if (rc) return rc;
         e = wait_stream(c, c->st[0]);
         if (e != hipSuccess) return hip_fail(e);
+    } else if (zb) {   // page-locked, large: DMA from the caller's pages, every chunk queued up front
+        e = ensure_hbm_slots();
+        if (e != hipSuccess) return hip_fail(e);
+        uint64_t k = 0;
+        for (uint64_t s0 = 0; s0 < n; s0 += per, ++k) {
+            const int s = (int)(k & 1);
+            const uint64_t cnt = (n - s0) < per ? (n - s0) : per;
+            const size_t bytes = (size_t)((cnt - 1) * stride + len);
+            const uint8_t* src = (const uint8_t*)h_base + s0 * stride;
+            const size_t mis = (uintptr_t)src & 15u;   // the in-place shape's alignment
+            e = hipMemcpyAsync(c->d_slot[s] + mis, src, bytes, hipMemcpyHostToDevice, c->st[s]);
+            if (e != hipSuccess) return hip_fail(e);
+            tcpcsum::launch_uniform(c->d_slot[s] + mis, stride, len, kss ? kss + s0 : nullptr, sum_start, kout + s0,
+                                    cnt, c->st[s], tu);
+            rc = check_launch();
+            if (rc) return rc;
+        }
+        for (int i = 0; i < 2; ++i) {
+            e = wait_stream(c, c->st[i]);
+            if (e != hipSuccess) return hip_fail(e);
+        }
     } else {
-        // segments per chunk: (cnt-1)*stride + len <= chunk (at least one segment)
-        uint64_t per = 1;
-        if (stride == 0) per = n;
-        else if (c->chunk > len) per = (c->chunk - len) / stride + 1;
-        if (per > n) per = n;
-        const size_t slot_bytes = (size_t)((per - 1) * stride + len) + 16;
         for (int i = 0; i < 2; ++i) {
             e = c->slot[i].ensure(slot_bytes);
             if (e != hipSuccess) return hip_fail(e);
         }
-        if (c->uniform_dma && slot_bytes > c->d_slot_bytes) {
-            for (int i = 0; i < 2; ++i) {
-                if (c->d_slot[i]) (void)hipFree(c->d_slot[i]);
-                c->d_slot[i] = nullptr;
-            }
-            c->d_slot_bytes = 0;
-            for (int i = 0; i < 2; ++i) {
-                e = hipMalloc(&c->d_slot[i], slot_bytes);
-                if (e != hipSuccess) return hip_fail(e);
-            }
-            c->d_slot_bytes = slot_bytes;
+        if (c->uniform_dma) {
+            e = ensure_hbm_slots();
+            if (e != hipSuccess) return hip_fail(e);
         }
         uint64_t k = 0;
         for (uint64_t s0 = 0; s0 < n; s0 += per, ++k) {

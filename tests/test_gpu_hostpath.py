@@ -141,3 +141,29 @@ def test_staging_on_the_gpus_numa_node(dev):
     assert policy() == before                      # the calling thread's memory policy is untouched
     if s["gpu_numa_node"] is not None and s["staging_numa_node"] is not None:
         assert s["staging_numa_node"] == s["gpu_numa_node"], s
+
+
+@pytest.mark.parametrize("offset,stride,length", [(0, 1500, 1500), (3, 1501, 1499), (16, 4096, 4000), (1, 64, 64)])
+def test_uniform_host_pinned_dma_chunks(dev, offset, stride, length):
+    """Page-locked input of two chunks or more goes to HBM by DMA straight from the caller's pages,
+    chunk by chunk on two streams (1 MiB chunks here, so a 6 MiB batch takes six); every segment
+    matches the oracle, and so does the in-place path the same batch takes with
+    TCPCSUM_HOST_PINNED_DMA=0 (read at context creation)."""
+    import os
+    import tcp_amd
+    rng = np.random.default_rng(offset * 7 + length)
+    buf = tcp_amd.pinned_empty(6 << 20)
+    buf[:] = rng.integers(0, 256, buf.size, dtype=np.uint8)
+    n = (buf.size - offset - length) // stride + 1
+    ss = rng.integers(0, 393211, n, dtype=np.uint32)
+    want = oracle.batch_uniform(buf, stride, length, n, ss, offset=offset)
+    with tcp_amd.HostContext(0, scratch_bytes=1 << 20) as ctx:
+        got = ctx.batch_uniform(buf, stride, length, n, ss, offset=offset)
+        assert ctx.stats()["bytes_staged"] == 0      # no CPU copy: DMA from the caller's pages
+    assert np.array_equal(got, want)
+    os.environ["TCPCSUM_HOST_PINNED_DMA"] = "0"
+    try:
+        with tcp_amd.HostContext(0, scratch_bytes=1 << 20) as ctx:
+            assert np.array_equal(ctx.batch_uniform(buf, stride, length, n, ss, offset=offset), want)
+    finally:
+        os.environ.pop("TCPCSUM_HOST_PINNED_DMA", None)
