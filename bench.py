@@ -450,7 +450,9 @@ def run_host_path(steps: int, warmup: int, rank: int, world: int, local: int, di
     the current device). memory="pageable": each step is tcpcsum_batch_uniform_host over the
     pageable shard (copied by the context's threads into pinned staging chunk by chunk, DMA to
     HBM, kernel, results back into host memory); "pinned": the shard lives in tcpcsum_host_alloc
-    memory and the kernel reads it over PCIe in place. Inputs and results in host memory: PCIe and
+    memory and goes to HBM by DMA straight from those pages. The context sleeps while the GPU works
+    (TCPCSUM_CTX_BLOCKING_WAIT), so cpu_core_s_per_step is the copying and launching only.
+    Inputs and results in host memory: PCIe and
     host DRAM are the bound, not HBM. Rank 0 returns the whole-job rate, every
     rank's results checked against its Appendix B digest."""
     import numpy as np
@@ -478,7 +480,7 @@ def run_host_path(steps: int, warmup: int, rank: int, world: int, local: int, di
         del d, dss
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
-        ctx = tcp_amd.HostContext(local)
+        ctx = tcp_amd.HostContext(local, blocking_wait=True)   # sleep, not spin, while the GPU works
         try:
             res = ctx.batch_uniform(host, L, L, cnt, ss)
             try:
