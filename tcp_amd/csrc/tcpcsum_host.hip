@@ -198,6 +198,7 @@ struct tcpcsum_ctx {
     int gpu_node = -1;   // the GPU's NUMA node, where the staging is allocated (-1: unknown / off)
     int wire_threads = 1;
     int stage_threads = 1;   // the current staged batch's: wire_threads, or all for a large batch
+    int stage_blocks = 1;    // a small single-threaded staged batch copied and launched in this many blocks
     // TCPCSUM_CTX_BLOCKING_WAIT: wait for the device by polling this event between
     // short sleeps instead of HIP's spin in hipStreamSynchronize
     hipEvent_t done_ev = nullptr;
@@ -405,8 +406,60 @@ int stage_packets(tcpcsum_ctx* c, uint64_t* k_off, uint32_t* k_len, size_t* stag
 // against copy-then-launch on 1024 x 1500-B batches: no gain / no gain /
 // +15-30 us / +60-90 us, the host cost of each queued launch landing before
 // the copies (profiles/r03_hostpath_sweep_wire_split.jsonl).
+// Single-threaded staging of a small batch in B blocks (TCPCSUM_HOST_STAGE_BLOCKS): the
+// packets of block b are copied, then the kernel over packet indices [n*b/B, n*(b+1)/B)
+// is queued, so block b's kernel runs over PCIe while block b+1 is copied. Returns
+// -1 when the batch does not qualify (the caller stages it in one piece).
+int stage_and_launch_blocks(tcpcsum_ctx* c, uint64_t n, uint32_t in_cap, uint64_t in_foot, int mode,
+                            uint16_t* kout, uint8_t* kst, hipStream_t st, const tcpcsum::Tuning& tu) {
+    const size_t m = c->g_idx.size();
+    const int B = c->stage_blocks;
+    if (B <= 1 || m == 0 || n < (uint64_t)B * 16u || !c->stage_one_pass) return -1;
+    size_t span = 0;
+    uint32_t cap = in_cap;
+    for (size_t k = 0; k < m; ++k) {
+        c->g_off[k] = span;
+        span += ((size_t)c->g_len[k] + 15u) & ~(size_t)15u;
+        cap = std::max(cap, c->g_len[k]);
+    }
+    if (span > kSmallStage || c->wire_threads != 1) return -1;
+    const uint64_t t0 = tcpcsum::now_ns();
+    hipError_t e = c->gath.ensure(span ? span : 16);
+    if (e != hipSuccess) {
+        tcpcsum::note_hip_error((int)e);
+        return TCPCSUM_ENOMEM;
+    }
+    uint64_t* k_off = (uint64_t*)c->p_off.h;
+    uint32_t* k_len = (uint32_t*)c->p_len.h;
+    size_t k = 0, copied = 0;
+    uint64_t ns_launch = 0;
+    for (int b = 0; b < B; ++b) {
+        const uint64_t i0 = n * (uint64_t)b / (uint64_t)B, i1 = n * (uint64_t)(b + 1) / (uint64_t)B;
+        for (; k < m && c->g_idx[k] < i1; ++k) {
+            c->g_len[k] = copy_len(c->g_src[k], c->g_len[k]);
+            memcpy(c->gath.h + c->g_off[k], c->g_src[k], c->g_len[k]);
+            k_off[c->g_idx[k]] = (uint64_t)(uintptr_t)(c->gath.d + c->g_off[k]);
+            k_len[c->g_idx[k]] = c->g_len[k];
+            copied += c->g_len[k];
+        }
+        const uint64_t l0 = tcpcsum::now_ns();
+        tcpcsum::launch_ipv4(nullptr, (const uint64_t*)c->p_off.d + i0, (const uint32_t*)c->p_len.d + i0, i1 - i0,
+                             cap, ~0ull, (in_foot + span) * (i1 - i0) / n, mode, kout + i0, kst + i0, nullptr, st, tu);
+        const int rc = check_launch();
+        if (rc) return rc;
+        ns_launch += tcpcsum::now_ns() - l0;
+    }
+    c->stats.ns_copy += tcpcsum::now_ns() - t0 - ns_launch;
+    c->stats.pkts_staged += m;
+    c->stats.bytes_staged += copied;
+    c->stage_threads = 1;
+    return TCPCSUM_OK;
+}
+
 int stage_and_launch(tcpcsum_ctx* c, uint64_t n, uint32_t in_cap, uint64_t in_foot, int mode, uint16_t* kout,
                      uint8_t* kst, hipStream_t st, const tcpcsum::Tuning& tu) {
+    const int rb = stage_and_launch_blocks(c, n, in_cap, in_foot, mode, kout, kst, st, tu);
+    if (rb != -1) return rb;
     size_t staged = 0;
     int rc = stage_packets(c, (uint64_t*)c->p_off.h, (uint32_t*)c->p_len.h, &staged);
     if (rc) return rc;
@@ -489,6 +542,7 @@ int tcpcsum_ctx_create(int device, size_t scratch_bytes, tcpcsum_ctx_t** out) {
     c->stage_one_pass = tcpcsum::env_int("TCPCSUM_HOST_STAGE_PASSES", 1) == 1;
     c->uniform_dma = tcpcsum::env_int("TCPCSUM_HOST_DMA", 1) != 0;
     c->pinned_dma = tcpcsum::env_int("TCPCSUM_HOST_PINNED_DMA", 1) != 0;
+    c->stage_blocks = std::max(1, std::min(16, tcpcsum::env_int("TCPCSUM_HOST_STAGE_BLOCKS", 1)));
     for (int i = 0; i < 2; ++i) {
         e = hipStreamCreateWithFlags(&c->st[i], hipStreamNonBlocking);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->slot_ev[i], hipEventDisableTiming);

@@ -232,11 +232,14 @@ def test_round3_fault_sequence_in_process(dev):
         assert ctx.stats()["pkts_in_place"] == 3 * 64
 
 
-def test_ipv4_ptrs_host_pinned_and_mixed(dev):
+@pytest.mark.parametrize("blocks", ["1", "3"])
+def test_ipv4_ptrs_host_pinned_and_mixed(dev, blocks, monkeypatch):
     """Packets in page-locked memory (tcpcsum_host_alloc) are used through their existing mapping
     (no registration, no copy); pageable buffers in the same batch are staged; NULL and short
-    messages are SKIPPED."""
+    messages are SKIPPED. blocks=3 (TCPCSUM_HOST_STAGE_BLOCKS): the staged packets copied and
+    launched in three blocks of packet indices, each block's kernel queued before the next is copied."""
     import tcp_amd
+    monkeypatch.setenv("TCPCSUM_HOST_STAGE_BLOCKS", blocks)
     rng = np.random.default_rng(12)
     pinned = tcp_amd.pinned_empty(64 * 2048)
     pinned[:] = 0

@@ -133,9 +133,10 @@ def main():
     reps = 200
     for layout, ptrs in (("malloc", np.array([b.ctypes.data for b in outb], np.uint64)),
                          ("pinned_pool", np.array([pool.ctypes.data + k * 32768 for k in range(1024)], np.uint64))):
-        for threads in ((1, 2, 4, 8) if layout == "malloc" else (1,)):
+        for threads, blocks in (((1, 1), (1, 2), (1, 4), (2, 1), (4, 1), (8, 1)) if layout == "malloc" else ((1, 1),)):
             for wait in ("spin", "block"):
                 os.environ["TCPCSUM_HOST_WIRE_THREADS"] = str(threads)
+                os.environ["TCPCSUM_HOST_STAGE_BLOCKS"] = str(blocks)
                 ctx = tcp_amd.HostContext(0, blocking_wait=(wait == "block"))
                 t0 = time.perf_counter()
                 ctx.ipv4_batch_ptrs(ptrs, lens, tcp_amd.IPV4_FILL)
@@ -144,7 +145,7 @@ def main():
                 tmin, tmed = best_of(lambda: ctx.ipv4_batch_ptrs(ptrs, lens, tcp_amd.IPV4_FILL), reps)
                 s1 = ctx.stats()
                 print(json.dumps({"measure": "ipv4_fill_ptrs_host_1024x1500", "layout": layout, "wait": wait,
-                                  "copy_threads": s1["copy_threads"],
+                                  "copy_threads": s1["copy_threads"], "stage_blocks": blocks,
                                   "first_batch_us": round(first * 1e6, 1), "us_best": round(tmin * 1e6, 1),
                                   "us_median": round(tmed * 1e6, 1),
                                   "cpu_caller_us_per_batch": round((s1["ns_cpu_caller"] - s0["ns_cpu_caller"]) / reps / 1e3, 1),
@@ -153,6 +154,7 @@ def main():
                                   "staged": s1["pkts_staged"] - s0["pkts_staged"]}), flush=True)
                 ctx.close()
     os.environ.pop("TCPCSUM_HOST_WIRE_THREADS", None)
+    os.environ.pop("TCPCSUM_HOST_STAGE_BLOCKS", None)
 
     # the seam itself: the interposer's per-batch latency vs the reference's CPU path
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -161,10 +163,10 @@ def main():
     import subprocess
     variants = [("cpu_reference_O2", "cpu", {}, []), ("preload_off", "gpu", {"TCPCSUM_PRELOAD_TX": "off"}, [])]
     for wait in ("block", "spin"):
-        for threads in (1, 2, 4, 8):
-            variants.append((f"preload_fill_staged_t{threads}_{wait}", "gpu",
+        for threads, blocks in ((1, 1), (1, 2), (1, 4), (2, 1), (4, 1), (8, 1)):
+            variants.append((f"preload_fill_staged_t{threads}_b{blocks}_{wait}", "gpu",
                              {"TCPCSUM_PRELOAD_TX": "fill", "TCPCSUM_PRELOAD_WAIT": wait,
-                              "TCPCSUM_HOST_WIRE_THREADS": str(threads)}, []))
+                              "TCPCSUM_HOST_WIRE_THREADS": str(threads), "TCPCSUM_HOST_STAGE_BLOCKS": str(blocks)}, []))
         variants.append((f"preload_fill_pinned_pool_{wait}", "gpu",
                          {"TCPCSUM_PRELOAD_TX": "fill", "TCPCSUM_PRELOAD_WAIT": wait}, ["pinned"]))
     for label, mode, env_extra, extra_args in variants:
