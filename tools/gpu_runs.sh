@@ -102,6 +102,25 @@ gpu_r4_n8() {
 )
 }
 
+# round 4, final rehearsal at HEAD: every GPU test, the smoke, the default bench line, and a
+# rocprofv3 kernel trace of the headline (its average must agree with the line's HIP events)
+gpu_r4_final() {
+(
+  O=gpurun_out/r4final
+  mkdir -p $O
+  timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > $O/gputest.log 2>&1; rc=$?
+  echo "pytest rc=$rc"; grep -E "passed|failed" $O/gputest.log | tail -1; grep FAILED $O/gputest.log | head
+  ok_rc $rc || exit $rc
+  timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1; rc=$?
+  echo "smoke rc=$rc"; tail -1 $O/smoke.log; ok_rc $rc || exit $rc
+  timeout -k 10 500 python3 bench.py > $O/bench.json 2> $O/bench.err; rc=$?
+  echo "bench rc=$rc"; ok_rc $rc || exit $rc
+  cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+  timeout -s KILL 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o k -- python3 bench.py --steps 100 --no-other-configs --no-cpu-baseline --no-host-path > $O/bench_under_rocprof.json 2> $O/kt.err; rc=$?
+  echo "kt rc=$rc"
+)
+}
+
 # round 3: wire FILL line store (default) — every GPU test first, then the A/B timing three
 # times (the two FILL stores must agree byte for byte every time)
 gpu_r3_fill() {
