@@ -497,6 +497,18 @@ def run_host_path(steps: int, warmup: int, rank: int, world: int, local: int, di
             data_node = page_node_of(host)
         finally:
             ctx.close()
+        # the link's own rate, same rank, same moment: a raw DMA of the pinned shard to HBM
+        # (every rank at once, between barriers), the ceiling both legs are held against
+        raw = None
+        if memory == "pinned":
+            dst = torch.empty(nbytes, dtype=torch.uint8, device=device)
+            src = torch.from_numpy(host)
+            dst.copy_(src, non_blocking=True)
+            torch.cuda.synchronize()
+            rwall = timed_region(lambda: dst.copy_(src, non_blocking=True), 3, 1, dist, torch.cuda.synchronize)
+            raw = host_path_rate([nbytes] * world, gather_walls(rwall, dist, world), 3)["GiB/s"]
+            del dst
+            torch.cuda.empty_cache()
     finally:
         os.sched_setaffinity(0, saved)
     walls = gather_walls(wall, dist, world)
@@ -507,7 +519,10 @@ def run_host_path(steps: int, warmup: int, rank: int, world: int, local: int, di
          "memory": memory, "steps": steps, **host_path_rate([nbytes] * world, walls, steps),
          "digest_check": check, "numa_node_rank0": node, "copy_threads": s_after["bulk_threads"],
          "staging_numa_node_rank0": s_after["staging_numa_node"], "data_numa_node_rank0": data_node,
+         "raw_pinned_h2d_GiB/s": raw,
          "cpu_core_s_per_step_rank0": round(cpu_ns / max(steps, 1) / 1e9, 4)}
+    if raw:
+        r["frac_of_raw_pinned_h2d"] = round(r["GiB/s"] / raw, 3)
     return r
 
 
