@@ -202,8 +202,7 @@ struct tcpcsum_ctx {
     // TCPCSUM_CTX_BLOCKING_WAIT: wait for the device by polling this event between
     // short sleeps instead of HIP's spin in hipStreamSynchronize
     hipEvent_t done_ev = nullptr;
-    uint64_t last_wait_ns = 0;   // the previous sleeping wait's length: the first sleep's guide
-    uint64_t poll_ns = 5000;     // sleep between polls (TCPCSUM_HOST_POLL_US, default 5)
+    uint64_t poll_ns = 5000;     // first sleep between polls after the expected time (TCPCSUM_HOST_POLL_US, default 5)
     bool nt_copy = true;   // streaming stores for the uniform chunks (TCPCSUM_HOST_NT=0: plain memcpy)
     bool stage_one_pass = true;   // wire staging laid out by bounds, one pass (TCPCSUM_HOST_STAGE_PASSES=2: by lengths)
     bool uniform_dma = true;   // staged uniform chunks go to HBM by DMA (TCPCSUM_HOST_DMA=0: kernel reads them over PCIe)
@@ -266,37 +265,59 @@ void par_copy(tcpcsum_ctx* c, void* dst, const void* src, size_t n, bool nt = fa
 // Wait for everything queued on st, timed into stats.ns_wait: hipStreamSynchronize
 // (HIP spins: the waiting thread burns a core for the kernel's whole length), or
 // with TCPCSUM_CTX_BLOCKING_WAIT a poll of the stream's completion event between
-// short sleeps — first for most of the previous wait's length, then every poll_ns
+// sleeps — first for 3/4 of expect_ns (what the queued work should take: the
+// caller's estimate from its bytes), then every poll_ns, doubling up to 100 us
 // (1 us timer slack on this thread for the wait, restored after). A
 // hipEventBlockingSync event did not help: the runtime waits on its signal
 // actively for about a batch kernel's length, and the thread used as much CPU as
 // with hipStreamSynchronize (48.7 vs 48.5 us per 1024-packet in-place batch,
 // profiles/r04_e2e_first.jsonl).
-hipError_t wait_stream(tcpcsum_ctx* c, hipStream_t st) {
+hipError_t wait_stream(tcpcsum_ctx* c, hipStream_t st, uint64_t expect_ns) {
     const uint64_t t0 = tcpcsum::now_ns();
     hipError_t e;
     if (c->flags & TCPCSUM_CTX_BLOCKING_WAIT) {
         e = hipEventRecord(c->done_ev, st);
         const int slack = prctl(PR_GET_TIMERSLACK, 0, 0, 0, 0);
-        if (slack > 0) prctl(PR_SET_TIMERSLACK, 1000, 0, 0, 0);
-        uint64_t nap = c->last_wait_ns - c->last_wait_ns / 4;   // 3/4 of the last wait
-        if (nap > 2000000u) nap = 2000000u;
+        bool slack_set = false;
+        uint64_t nap = expect_ns - expect_ns / 4;
+        if (nap > 50000000u) nap = 50000000u;
+        uint64_t step = c->poll_ns;
         while (e == hipSuccess) {
             e = hipEventQuery(c->done_ev);
             if (e != hipErrorNotReady) break;
             (void)hipGetLastError();   // not ready is not an error for us
             e = hipSuccess;
-            const uint64_t ns = nap ? nap : c->poll_ns;
+            if (!slack_set && slack > 0) {
+                prctl(PR_SET_TIMERSLACK, 1000, 0, 0, 0);
+                slack_set = true;
+            }
+            uint64_t ns = nap;
+            if (!ns) {
+                ns = step;
+                step = std::min<uint64_t>(step * 2, 100000u);
+            }
             nap = 0;
             timespec ts{(time_t)(ns / 1000000000u), (long)(ns % 1000000000u)};
             nanosleep(&ts, nullptr);
         }
-        if (slack > 0) prctl(PR_SET_TIMERSLACK, (unsigned long)slack, 0, 0, 0);
-        c->last_wait_ns = tcpcsum::now_ns() - t0;
+        if (slack_set) prctl(PR_SET_TIMERSLACK, (unsigned long)slack, 0, 0, 0);
     } else {
         e = hipStreamSynchronize(st);
     }
     c->stats.ns_wait += tcpcsum::now_ns() - t0;
+    return e;
+}
+
+// What a host batch's device work should take: its bytes over PCIe (~50 GB/s,
+// 50 bytes per ns) plus a launch's latency — the sleeping wait's first nap.
+inline uint64_t expect_ns(uint64_t bytes) { return bytes / 50u + 8000u; }
+
+// Both streams drained, waited for once: st[1] waits on st[0]'s last work, and
+// the caller sleeps on st[1] only (the pipelined paths queue on both).
+hipError_t wait_both(tcpcsum_ctx* c, uint64_t expect) {
+    hipError_t e = hipEventRecord(c->slot_ev[0], c->st[0]);
+    if (e == hipSuccess) e = hipStreamWaitEvent(c->st[1], c->slot_ev[0], 0);
+    if (e == hipSuccess) e = wait_stream(c, c->st[1], expect);
     return e;
 }
 
@@ -681,7 +702,7 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t st
         tcpcsum::launch_uniform(zb, stride, len, kss, sum_start, kout, n, c->st[0], tu);
         rc = check_launch();
         if (rc) return rc;
-        e = wait_stream(c, c->st[0]);
+        e = wait_stream(c, c->st[0], expect_ns(span));
         if (e != hipSuccess) return hip_fail(e);
     } else if (zb) {   // page-locked, large: DMA from the caller's pages, every chunk queued up front
         e = ensure_hbm_slots();
@@ -700,10 +721,8 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t st
             rc = check_launch();
             if (rc) return rc;
         }
-        for (int i = 0; i < 2; ++i) {
-            e = wait_stream(c, c->st[i]);
-            if (e != hipSuccess) return hip_fail(e);
-        }
+        e = wait_both(c, expect_ns(span));
+        if (e != hipSuccess) return hip_fail(e);
     } else {
         for (int i = 0; i < 2; ++i) {
             e = c->slot[i].ensure(slot_bytes);
@@ -749,11 +768,11 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t st
             }
             c->slot_busy[s] = true;
         }
-        for (int i = 0; i < 2; ++i) {
-            c->slot_busy[i] = false;
-            e = wait_stream(c, c->st[i]);
-            if (e != hipSuccess) return hip_fail(e);
-        }
+        // the last chunk's DMA and kernel: all earlier chunks have been waited for
+        // slot by slot, so what is left is about one chunk's work
+        c->slot_busy[0] = c->slot_busy[1] = false;
+        e = wait_both(c, expect_ns(std::min<uint64_t>(span, slot_bytes)));
+        if (e != hipSuccess) return hip_fail(e);
     }
     if (out_staged) par_copy(c, h_out, c->res.h, n * sizeof(uint16_t));
     return TCPCSUM_OK;
@@ -822,7 +841,7 @@ int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t* c, void* h_pkts, size_t region_bytes,
     }
     rc = check_launch();
     if (rc) return rc;
-    e = wait_stream(c, st);
+    e = wait_stream(c, st, expect_ns(std::min<uint64_t>((uint64_t)n * std::min<uint64_t>(cap, 1500u), region_bytes)));
     if (e != hipSuccess) return hip_fail(e);
     if (fill && !c->g_idx.empty())
         write_back_checks(c, zst ? h_status : c->p_stat.h, (mode & TCPCSUM_IPV4_IPHDR) != 0);
@@ -856,6 +875,7 @@ int tcpcsum_ipv4_batch_ptrs_host(tcpcsum_ctx_t* c, void* const* h_pkts, const ui
     c->g_src.clear();
     c->g_len.clear();
     uint64_t foot = 0;
+    const uint64_t staged_before = c->stats.bytes_staged;
     uint32_t cap = 20;
     uint64_t in_place = 0;
     for (uint64_t i = 0; i < n; ++i) {
@@ -889,7 +909,7 @@ int tcpcsum_ipv4_batch_ptrs_host(tcpcsum_ctx_t* c, void* const* h_pkts, const ui
     if (tu.shape < 0 && n < 65536u) tu.shape = 3;
     rc = stage_and_launch(c, n, cap, foot, mode, zout ? zout : (uint16_t*)c->p_out.d, zst ? zst : c->p_stat.d, st, tu);
     if (rc) return rc;
-    hipError_t e = wait_stream(c, st);
+    hipError_t e = wait_stream(c, st, expect_ns(foot + c->stats.bytes_staged - staged_before));
     if (e != hipSuccess) return hip_fail(e);
     if ((mode & TCPCSUM_IPV4_VERIFY) == 0 && !c->g_idx.empty())
         write_back_checks(c, zst ? h_status : c->p_stat.h, (mode & TCPCSUM_IPV4_IPHDR) != 0);
