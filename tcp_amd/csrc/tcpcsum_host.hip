@@ -193,9 +193,9 @@ struct tcpcsum_ctx {
     tcpcsum::HipHostBackend backend;
     tcpcsum::PinnedLookup<tcpcsum::HipHostBackend> pinned{backend};
     std::unique_ptr<tcpcsum::CopyPool> pool;
+    int gpu_node = -1;   // the GPU's NUMA node, where the staging is allocated (-1: unknown / off)
     // threads a staged wire batch copies on, the caller included (TCPCSUM_HOST_WIRE_THREADS):
     // a releaseSend batch is ~1.5 MB, where extra threads cost more CPU than they save time
-    int gpu_node = -1;   // the GPU's NUMA node, where the staging is allocated (-1: unknown / off)
     int wire_threads = 1;
     int stage_threads = 1;   // the current staged batch's: wire_threads, or all for a large batch
     int stage_blocks = 1;    // a small single-threaded staged batch copied and launched in this many blocks
@@ -419,14 +419,6 @@ int stage_packets(tcpcsum_ctx* c, uint64_t* k_off, uint32_t* k_len, size_t* stag
     return TCPCSUM_OK;
 }
 
-// Stage the packets in g_* and launch the wire kernel over all n packets on
-// st (k_off / k_len of the packets read in place already set; in_cap /
-// in_foot their largest length and sum). One launch after the copies: queueing
-// the kernel first, in blocks each released by a pinned flag the copy threads
-// set (hipStreamWaitValue64), was measured and lost — 1 / 2 / 4 / 8 blocks
-// against copy-then-launch on 1024 x 1500-B batches: no gain / no gain /
-// +15-30 us / +60-90 us, the host cost of each queued launch landing before
-// the copies (profiles/r03_hostpath_sweep_wire_split.jsonl).
 // Single-threaded staging of a small batch in B blocks (TCPCSUM_HOST_STAGE_BLOCKS): the
 // packets of block b are copied, then the kernel over packet indices [n*b/B, n*(b+1)/B)
 // is queued, so block b's kernel runs over PCIe while block b+1 is copied. Returns
@@ -477,6 +469,14 @@ int stage_and_launch_blocks(tcpcsum_ctx* c, uint64_t n, uint32_t in_cap, uint64_
     return TCPCSUM_OK;
 }
 
+// Stage the packets in g_* and launch the wire kernel over all n packets on
+// st (k_off / k_len of the packets read in place already set; in_cap /
+// in_foot their largest length and sum). One launch after the copies: queueing
+// the kernel first, in blocks each released by a pinned flag the copy threads
+// set (hipStreamWaitValue64), was measured and lost — 1 / 2 / 4 / 8 blocks
+// against copy-then-launch on 1024 x 1500-B batches: no gain / no gain /
+// +15-30 us / +60-90 us, the host cost of each queued launch landing before
+// the copies (profiles/r03_hostpath_sweep_wire_split.jsonl).
 int stage_and_launch(tcpcsum_ctx* c, uint64_t n, uint32_t in_cap, uint64_t in_foot, int mode, uint16_t* kout,
                      uint8_t* kst, hipStream_t st, const tcpcsum::Tuning& tu) {
     const int rb = stage_and_launch_blocks(c, n, in_cap, in_foot, mode, kout, kst, st, tu);
