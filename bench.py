@@ -432,6 +432,27 @@ def page_node_of(arr) -> int | None:
         return None
 
 
+def thp_share(arr) -> float | None:
+    """Share of the array's mapping backed by transparent huge pages (/proc/self/smaps AnonHugePages
+    over Rss of the VMA holding its first byte), or None."""
+    a = arr.ctypes.data
+    try:
+        cur = None
+        with open("/proc/self/smaps") as f:
+            for line in f:
+                head = line.split()
+                if "-" in head[0] and len(head) >= 5 and all(c in "0123456789abcdef-" for c in head[0]):
+                    lo, hi = (int(x, 16) for x in head[0].split("-"))
+                    cur = {} if lo <= a < hi else None
+                elif cur is not None and head[0] in ("Rss:", "AnonHugePages:"):
+                    cur[head[0]] = int(head[1])
+                    if len(cur) == 2:
+                        return round(cur["AnonHugePages:"] / max(cur["Rss:"], 1), 3)
+    except Exception:
+        pass
+    return None
+
+
 def host_path_rate(bytes_per_rank: list, walls: list, steps: int) -> dict:
     """Whole-job end-to-end rate: every rank's bytes x steps over the slowest rank's wall time."""
     wmax = max(walls)
@@ -495,6 +516,7 @@ def run_host_path(steps: int, warmup: int, rank: int, world: int, local: int, di
             wall = timed_region(lambda: ctx.batch_uniform(host, L, L, cnt, ss), steps, warmup, dist, lambda: None)
             s_after = ctx.stats()
             data_node = page_node_of(host)
+            thp = thp_share(host) if memory == "pageable" else None
         finally:
             ctx.close()
         # the link's own rate, same rank, same moment: a raw DMA of the pinned shard to HBM
@@ -519,7 +541,7 @@ def run_host_path(steps: int, warmup: int, rank: int, world: int, local: int, di
          "memory": memory, "steps": steps, **host_path_rate([nbytes] * world, walls, steps),
          "digest_check": check, "numa_node_rank0": node, "copy_threads": s_after["bulk_threads"],
          "staging_numa_node_rank0": s_after["staging_numa_node"], "data_numa_node_rank0": data_node,
-         "raw_pinned_h2d_GiB/s": raw,
+         "raw_pinned_h2d_GiB/s": raw, "data_thp_share": thp,
          "cpu_core_s_per_step_rank0": round(cpu_ns / max(steps, 1) / 1e9, 4)}
     if raw:
         r["frac_of_raw_pinned_h2d"] = round(r["GiB/s"] / raw, 3)
@@ -620,6 +642,8 @@ def main(argv=None) -> int:
     ap.add_argument("--host-path-only", action="store_true",
                     help="only the end-to-end host-memory leg: one JSON line for it (tools/e2e_multi.sh)")
     ap.add_argument("--host-steps", type=int, default=5)
+    ap.add_argument("--host-path-first", action="store_true",
+                    help="run the host-memory leg before the device configs (placement A/B)")
     args = ap.parse_args(argv)
 
     rank, world, local = dist_env()
@@ -679,6 +703,11 @@ def main(argv=None) -> int:
             dist.destroy_process_group()
         return 0
 
+    host_first = None
+    if args.host_path_first and not args.no_host_path:   # before any device config allocates anything
+        host_first = {m: run_host_path(args.host_steps, min(args.warmup, 2), rank, world, local, dist, device, m)
+                      for m in ("pageable", "pinned")}
+        torch.cuda.empty_cache()
     r, bufs, rot = run_config(args.config, args.steps, args.warmup, rank, world, dist, device, args.rotate,
                               streams=args.streams)
     L, cnt, batch_bytes, desc, check = r["L"], r["cnt"], r["batch_bytes"], r["desc"], r["check"]
@@ -758,7 +787,7 @@ def main(argv=None) -> int:
 
     # end to end from host memory, every rank at once (PCIe and host DRAM bound; never `value`)
     host_path = None
-    if not args.no_host_path:
+    if not args.no_host_path and not args.host_path_first:
         del bufs
         torch.cuda.empty_cache()
         host_path = {m: run_host_path(args.host_steps, min(args.warmup, 2), rank, world, local, dist, device, m)
@@ -803,8 +832,10 @@ def main(argv=None) -> int:
             line["stream_probe"] = probe
         if extra:
             line["other_configs"] = extra
-        if host_path:
-            line["host_path"] = host_path
+        if host_path or host_first:
+            line["host_path"] = host_path or host_first
+            if host_first:
+                line["host_path_ran_first"] = True
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         print(json.dumps(line), flush=True)

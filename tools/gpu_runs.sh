@@ -121,6 +121,19 @@ gpu_r4_final() {
 )
 }
 
+# round 4: host leg last (default) vs first in the full bench line (placement / THP A/B)
+gpu_r4_hostorder() {
+(
+  for order in last first last first; do
+    extra=""; [ $order = first ] && extra="--host-path-first"
+    timeout -k 10 400 python3 bench.py --steps 50 --no-cpu-baseline $extra > gpurun_out/r4_hostorder_$order.json 2>> gpurun_out/r4_hostorder.err; rc=$?
+    echo "$order rc=$rc $(python3 -c "import json; d=json.load(open('gpurun_out/r4_hostorder_$order.json'))['host_path']; print({m: (d[m]['GiB/s'], d[m]['numa_node_rank0'], d[m].get('data_thp_share'), d[m]['cpu_core_s_per_step_rank0']) for m in d})")"
+    ok_rc $rc || exit $rc
+  done
+  grep -i AnonHugePages /proc/meminfo; cat /sys/kernel/mm/transparent_hugepage/enabled
+)
+}
+
 # round 3: wire FILL line store (default) — every GPU test first, then the A/B timing three
 # times (the two FILL stores must agree byte for byte every time)
 gpu_r3_fill() {
