@@ -30,6 +30,7 @@ import argparse
 import json
 import math
 import os
+import resource
 import statistics
 import sys
 import time
@@ -432,6 +433,18 @@ def page_node_of(arr) -> int | None:
         return None
 
 
+def cgroup_throttled_us() -> int | None:
+    """The job's cgroup CPU throttling so far (cpu.stat throttled_usec), or None."""
+    try:
+        for line in open("/sys/fs/cgroup/cpu.stat"):
+            k, v = line.split()
+            if k == "throttled_usec":
+                return int(v)
+    except Exception:
+        pass
+    return None
+
+
 def thp_share(arr) -> float | None:
     """Share of the array's mapping backed by transparent huge pages (/proc/self/smaps AnonHugePages
     over Rss of the VMA holding its first byte), or None."""
@@ -513,8 +526,11 @@ def run_host_path(steps: int, warmup: int, rank: int, world: int, local: int, di
                 fl = -max_over_ranks(-flag, dist, device)
                 check = None if fl < 0 else bool(fl == 1.0)
             s_before = ctx.stats()
+            ru0, thr0 = resource.getrusage(resource.RUSAGE_SELF), cgroup_throttled_us()
             wall = timed_region(lambda: ctx.batch_uniform(host, L, L, cnt, ss), steps, warmup, dist, lambda: None)
+            ru1, thr1 = resource.getrusage(resource.RUSAGE_SELF), cgroup_throttled_us()
             s_after = ctx.stats()
+            proc_cpu = (ru1.ru_utime + ru1.ru_stime) - (ru0.ru_utime + ru0.ru_stime)
             data_node = page_node_of(host)
             thp = thp_share(host) if memory == "pageable" else None
         finally:
@@ -542,6 +558,8 @@ def run_host_path(steps: int, warmup: int, rank: int, world: int, local: int, di
          "digest_check": check, "numa_node_rank0": node, "copy_threads": s_after["bulk_threads"],
          "staging_numa_node_rank0": s_after["staging_numa_node"], "data_numa_node_rank0": data_node,
          "raw_pinned_h2d_GiB/s": raw, "data_thp_share": thp,
+         "process_cpu_core_s_per_step_rank0": round(proc_cpu / max(steps + min(warmup, 2), 1), 4),
+         "cgroup_throttled_ms_rank0": None if thr0 is None or thr1 is None else round((thr1 - thr0) / 1e3, 1),
          "cpu_core_s_per_step_rank0": round(cpu_ns / max(steps, 1) / 1e9, 4)}
     if raw:
         r["frac_of_raw_pinned_h2d"] = round(r["GiB/s"] / raw, 3)
