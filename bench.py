@@ -559,6 +559,8 @@ def run_host_path(steps: int, warmup: int, rank: int, world: int, local: int, di
          "staging_numa_node_rank0": s_after["staging_numa_node"], "data_numa_node_rank0": data_node,
          "raw_pinned_h2d_GiB/s": raw, "data_thp_share": thp,
          "process_cpu_core_s_per_step_rank0": round(proc_cpu / max(steps + min(warmup, 2), 1), 4),
+         "copy_ms_per_step_rank0": round((s_after["ns_copy"] - s_before["ns_copy"]) / max(steps + warmup, 1) / 1e6, 3),
+         "wait_ms_per_step_rank0": round((s_after["ns_wait"] - s_before["ns_wait"]) / max(steps + warmup, 1) / 1e6, 3),
          "cgroup_throttled_ms_rank0": None if thr0 is None or thr1 is None else round((thr1 - thr0) / 1e3, 1),
          "cpu_core_s_per_step_rank0": round(cpu_ns / max(steps, 1) / 1e9, 4)}
     if raw:

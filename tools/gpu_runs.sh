@@ -124,10 +124,10 @@ gpu_r4_final() {
 # round 4: host leg last (default) vs first in the full bench line (placement / THP A/B)
 gpu_r4_hostorder() {
 (
-  for order in last first last first; do
+  for order in last first; do
     extra=""; [ $order = first ] && extra="--host-path-first"
     timeout -k 10 400 python3 bench.py --steps 50 --no-cpu-baseline $extra > gpurun_out/r4_hostorder_$order.json 2>> gpurun_out/r4_hostorder.err; rc=$?
-    echo "$order rc=$rc $(python3 -c "import json; d=json.load(open('gpurun_out/r4_hostorder_$order.json'))['host_path']; print({m: (d[m]['GiB/s'], d[m]['numa_node_rank0'], d[m]['cpu_core_s_per_step_rank0'], d[m].get('process_cpu_core_s_per_step_rank0'), d[m].get('cgroup_throttled_ms_rank0')) for m in d})")"
+    echo "$order rc=$rc $(python3 -c "import json; d=json.load(open('gpurun_out/r4_hostorder_$order.json'))['host_path']; print({m: (d[m]['GiB/s'], d[m]['numa_node_rank0'], d[m]['cpu_core_s_per_step_rank0'], d[m].get('copy_ms_per_step_rank0'), d[m].get('wait_ms_per_step_rank0')) for m in d})")"
     ok_rc $rc || exit $rc
   done
   grep -i AnonHugePages /proc/meminfo; cat /sys/kernel/mm/transparent_hugepage/enabled; cat /sys/fs/cgroup/cpu.stat 2>/dev/null | head -6; cat /proc/self/cgroup
