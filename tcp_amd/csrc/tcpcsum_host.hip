@@ -174,10 +174,12 @@ struct tcpcsum_ctx {
     size_t chunk = 0;
     uint32_t flags = 0;
     hipStream_t st[2] = {nullptr, nullptr};
-    hipEvent_t slot_ev[2] = {nullptr, nullptr};
-    bool slot_busy[2] = {false, false};
-    tcpcsum::Pinned slot[2];   // uniform batches: one staged chunk per stream
-    uint8_t* d_slot[2] = {nullptr, nullptr};   // ... and its device copy (uniform_dma)
+    // uniform batches: nslots staged chunks in flight (TCPCSUM_HOST_SLOTS, 2..4), slot s on stream s & 1
+    int nslots = 2;
+    hipEvent_t slot_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    bool slot_busy[4] = {false, false, false, false};
+    tcpcsum::Pinned slot[4];   // one staged chunk each
+    uint8_t* d_slot[4] = {nullptr, nullptr, nullptr, nullptr};   // ... and its device copy (uniform_dma)
     size_t d_slot_bytes = 0;
     tcpcsum::Pinned gath;      // wire batches: packets copied out of pageable memory
     tcpcsum::Pinned ss, res;   // per-segment start values / results, when the caller's are pageable
@@ -543,7 +545,7 @@ int tcpcsum_ctx_create(int device, size_t scratch_bytes, tcpcsum_ctx_t** out) {
     (void)hipGetLastError();
     // pinned staging on the GPU's node too (the copy threads write it, the DMA reads it)
     c->gpu_node = numa ? gpu_node : -1;
-    for (tcpcsum::Pinned* pp : {&c->slot[0], &c->slot[1], &c->gath, &c->ss, &c->res, &c->p_off, &c->p_len, &c->p_out,
+    for (tcpcsum::Pinned* pp : {&c->slot[0], &c->slot[1], &c->slot[2], &c->slot[3], &c->gath, &c->ss, &c->res, &c->p_off, &c->p_len, &c->p_out,
                                 &c->p_stat})
         pp->node = c->gpu_node;
     // never more workers than the node has CPUs this process may use (the caller is one of
@@ -564,9 +566,17 @@ int tcpcsum_ctx_create(int device, size_t scratch_bytes, tcpcsum_ctx_t** out) {
     c->uniform_dma = tcpcsum::env_int("TCPCSUM_HOST_DMA", 1) != 0;
     c->pinned_dma = tcpcsum::env_int("TCPCSUM_HOST_PINNED_DMA", 1) != 0;
     c->stage_blocks = std::max(1, std::min(16, tcpcsum::env_int("TCPCSUM_HOST_STAGE_BLOCKS", 1)));
+    c->nslots = std::max(2, std::min(4, tcpcsum::env_int("TCPCSUM_HOST_SLOTS", 2)));
+    if (!scratch_bytes) c->chunk = (size_t)std::max(1, tcpcsum::env_int("TCPCSUM_HOST_CHUNK_MB", 16)) << 20;
     for (int i = 0; i < 2; ++i) {
         e = hipStreamCreateWithFlags(&c->st[i], hipStreamNonBlocking);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&c->slot_ev[i], hipEventDisableTiming);
+        if (e != hipSuccess) {
+            tcpcsum_ctx_destroy(c);
+            return hip_fail(e);
+        }
+    }
+    for (int i = 0; i < 4; ++i) {
+        e = hipEventCreateWithFlags(&c->slot_ev[i], hipEventDisableTiming);
         if (e != hipSuccess) {
             tcpcsum_ctx_destroy(c);
             return hip_fail(e);
@@ -587,9 +597,11 @@ void tcpcsum_ctx_destroy(tcpcsum_ctx_t* c) {
     for (int i = 0; i < 2; ++i)
         if (c->st[i]) hipStreamSynchronize(c->st[i]);
     if (c->done_ev) hipEventDestroy(c->done_ev);
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < 4; ++i) {
         if (c->d_slot[i]) hipFree(c->d_slot[i]);
         if (c->slot_ev[i]) hipEventDestroy(c->slot_ev[i]);
+    }
+    for (int i = 0; i < 2; ++i) {
         if (c->st[i]) hipStreamDestroy(c->st[i]);
     }
     delete c;   // pinned buffers and copy threads go with it
@@ -683,14 +695,15 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t st
     else if (c->chunk > len) per = (c->chunk - len) / stride + 1;
     if (per > n) per = n;
     const size_t slot_bytes = (size_t)((per - 1) * stride + len) + 16;
+    const int ns = c->nslots;
     auto ensure_hbm_slots = [&]() -> hipError_t {
-        if (slot_bytes <= c->d_slot_bytes) return hipSuccess;
-        for (int i = 0; i < 2; ++i) {
+        if (slot_bytes <= c->d_slot_bytes && c->d_slot[ns - 1]) return hipSuccess;
+        for (int i = 0; i < 4; ++i) {
             if (c->d_slot[i]) (void)hipFree(c->d_slot[i]);
             c->d_slot[i] = nullptr;
         }
         c->d_slot_bytes = 0;
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < ns; ++i) {
             const hipError_t he = hipMalloc(&c->d_slot[i], slot_bytes);
             if (he != hipSuccess) return he;
         }
@@ -709,22 +722,23 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t st
         if (e != hipSuccess) return hip_fail(e);
         uint64_t k = 0;
         for (uint64_t s0 = 0; s0 < n; s0 += per, ++k) {
-            const int s = (int)(k & 1);
+            const int s = (int)(k % (uint64_t)ns);   // slot s on stream s & 1: a slot's next copy
+            hipStream_t sst = c->st[s & 1];          // stays behind its last kernel
             const uint64_t cnt = (n - s0) < per ? (n - s0) : per;
             const size_t bytes = (size_t)((cnt - 1) * stride + len);
             const uint8_t* src = (const uint8_t*)h_base + s0 * stride;
             const size_t mis = (uintptr_t)src & 15u;   // the in-place shape's alignment
-            e = hipMemcpyAsync(c->d_slot[s] + mis, src, bytes, hipMemcpyHostToDevice, c->st[s]);
+            e = hipMemcpyAsync(c->d_slot[s] + mis, src, bytes, hipMemcpyHostToDevice, sst);
             if (e != hipSuccess) return hip_fail(e);
             tcpcsum::launch_uniform(c->d_slot[s] + mis, stride, len, kss ? kss + s0 : nullptr, sum_start, kout + s0,
-                                    cnt, c->st[s], tu);
+                                    cnt, sst, tu);
             rc = check_launch();
             if (rc) return rc;
         }
         e = wait_both(c, expect_ns(span));
         if (e != hipSuccess) return hip_fail(e);
     } else {
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < ns; ++i) {
             e = c->slot[i].ensure(slot_bytes);
             if (e != hipSuccess) return hip_fail(e);
         }
@@ -734,11 +748,12 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t st
         }
         uint64_t k = 0;
         for (uint64_t s0 = 0; s0 < n; s0 += per, ++k) {
-            const int s = (int)(k & 1);
+            const int s = (int)(k % (uint64_t)ns);
+            hipStream_t sst = c->st[s & 1];
             const uint64_t cnt = (n - s0) < per ? (n - s0) : per;
             const size_t bytes = (size_t)((cnt - 1) * stride + len);
             const uint8_t* src = (const uint8_t*)h_base + s0 * stride;
-            if (c->slot_busy[s]) {   // the DMA (or kernel) that last read this slot: chunk k-2
+            if (c->slot_busy[s]) {   // the DMA (or kernel) that last read this slot: chunk k - nslots
                 c->slot_busy[s] = false;
                 const uint64_t t0 = tcpcsum::now_ns();
                 e = hipEventSynchronize(c->slot_ev[s]);
@@ -752,25 +767,24 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t st
             c->stats.bytes_staged += bytes;
             const uint8_t* kin = c->slot[s].d + mis;
             if (c->uniform_dma) {   // pinned -> HBM by the DMA engines, then the kernel reads HBM
-                e = hipMemcpyAsync(c->d_slot[s] + mis, c->slot[s].h + mis, bytes, hipMemcpyHostToDevice, c->st[s]);
+                e = hipMemcpyAsync(c->d_slot[s] + mis, c->slot[s].h + mis, bytes, hipMemcpyHostToDevice, sst);
                 if (e != hipSuccess) return hip_fail(e);
-                e = hipEventRecord(c->slot_ev[s], c->st[s]);
+                e = hipEventRecord(c->slot_ev[s], sst);
                 if (e != hipSuccess) return hip_fail(e);
                 kin = c->d_slot[s] + mis;
             }
-            tcpcsum::launch_uniform(kin, stride, len, kss ? kss + s0 : nullptr, sum_start, kout + s0, cnt, c->st[s],
-                                    tu);
+            tcpcsum::launch_uniform(kin, stride, len, kss ? kss + s0 : nullptr, sum_start, kout + s0, cnt, sst, tu);
             rc = check_launch();
             if (rc) return rc;
             if (!c->uniform_dma) {
-                e = hipEventRecord(c->slot_ev[s], c->st[s]);
+                e = hipEventRecord(c->slot_ev[s], sst);
                 if (e != hipSuccess) return hip_fail(e);
             }
             c->slot_busy[s] = true;
         }
         // the last chunk's DMA and kernel: all earlier chunks have been waited for
         // slot by slot, so what is left is about one chunk's work
-        c->slot_busy[0] = c->slot_busy[1] = false;
+        for (int i = 0; i < 4; ++i) c->slot_busy[i] = false;
         e = wait_both(c, expect_ns(std::min<uint64_t>(span, slot_bytes)));
         if (e != hipSuccess) return hip_fail(e);
     }

@@ -134,6 +134,20 @@ gpu_r4_hostorder() {
 )
 }
 
+# round 4: the pageable pipeline's depth — host leg last in the full bench line, chunk MiB x slots
+gpu_r4_slots() {
+(
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_hostpath.py tests/test_gpu_ptrs.py -q --timeout 120 --timeout-method thread > gpurun_out/r4_slots_tests.log 2>&1; rc=$?
+  echo "tests rc=$rc"; tail -1 gpurun_out/r4_slots_tests.log; ok_rc $rc || exit $rc
+  for cfg in "16 2" "16 4" "64 2" "64 4" "32 4"; do
+    set -- $cfg
+    TCPCSUM_HOST_CHUNK_MB=$1 TCPCSUM_HOST_SLOTS=$2 timeout -k 10 400 python3 bench.py --steps 50 --no-cpu-baseline > gpurun_out/r4_slots_$1_$2.json 2>> gpurun_out/r4_slots.err; rc=$?
+    echo "chunk=$1 slots=$2 rc=$rc $(python3 -c "import json; d=json.load(open('gpurun_out/r4_slots_$1_$2.json'))['host_path']; print({m: (d[m]['GiB/s'], d[m]['numa_node_rank0'], d[m].get('copy_ms_per_step_rank0'), d[m].get('wait_ms_per_step_rank0')) for m in d})")"
+    ok_rc $rc || exit $rc
+  done
+)
+}
+
 # round 3: wire FILL line store (default) — every GPU test first, then the A/B timing three
 # times (the two FILL stores must agree byte for byte every time)
 gpu_r3_fill() {
