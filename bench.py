@@ -474,8 +474,24 @@ def host_path_rate(bytes_per_rank: list, walls: list, steps: int) -> dict:
             "wall_max_s": round(wmax, 6)}
 
 
+def host_context(local: int):
+    """The host leg's context: blocking (sleeping) wait; its staging and HBM slots allocated by one
+    warm batch of two chunks over a pinned buffer and a pageable one, so that, created at the
+    start of the run as an application creates it at start-up, nothing it holds is allocated
+    after the device legs have churned the allocators."""
+    import numpy as np
+    import tcp_amd
+    ctx = tcp_amd.HostContext(local, blocking_wait=True)   # sleep, not spin, while the GPU works
+    warm = 33 << 20   # > 2 chunks of 16 MiB
+    pin = tcp_amd.pinned_empty(warm)
+    pin[:] = 0
+    ctx.batch_uniform(pin, 1500, 1500, warm // 1500, 0)
+    ctx.batch_uniform(np.zeros(warm, np.uint8), 1500, 1500, warm // 1500, 0)
+    return ctx
+
+
 def run_host_path(steps: int, warmup: int, rank: int, world: int, local: int, dist, device,
-                  memory: str = "pageable") -> dict:
+                  memory: str = "pageable", ctx=None) -> dict:
     """The path as north_star states it — starting and ending in host memory (raw-socket buffers) —
     one context per GPU (tcpcsum_ctx_*), every rank at once. Rank r owns its contiguous shard of
     the global 1500-B config (N=8: BASELINE's 8M x 1500 config, Appendix B shard r), held in host
@@ -514,7 +530,9 @@ def run_host_path(steps: int, warmup: int, rank: int, world: int, local: int, di
         del d, dss
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
-        ctx = tcp_amd.HostContext(local, blocking_wait=True)   # sleep, not spin, while the GPU works
+        own_ctx = ctx is None
+        if own_ctx:
+            ctx = tcp_amd.HostContext(local, blocking_wait=True)   # sleep, not spin, while the GPU works
         try:
             res = ctx.batch_uniform(host, L, L, cnt, ss)
             try:
@@ -534,7 +552,8 @@ def run_host_path(steps: int, warmup: int, rank: int, world: int, local: int, di
             data_node = page_node_of(host)
             thp = thp_share(host) if memory == "pageable" else None
         finally:
-            ctx.close()
+            if own_ctx:
+                ctx.close()
         # the link's own rate, same rank, same moment: a raw DMA of the pinned shard to HBM
         # (every rank at once, between barriers), the ceiling both legs are held against
         raw = None
@@ -550,6 +569,7 @@ def run_host_path(steps: int, warmup: int, rank: int, world: int, local: int, di
     finally:
         os.sched_setaffinity(0, saved)
     walls = gather_walls(wall, dist, world)
+    calls = max(steps + warmup, 1)   # the stats and rusage deltas span the warm-up calls too
     cpu_ns = (s_after["ns_cpu_caller"] - s_before["ns_cpu_caller"]) + (s_after["ns_cpu_workers"] - s_before["ns_cpu_workers"])
     r = {"workload": f"{cnt} x {L}-byte segments per GPU in {memory} host memory "
                      f"({'Appendix B shard ' + str(rank) + ' of ' + str(total) if world > 1 else 'Appendix B 1M x 1500'}), "
@@ -558,11 +578,11 @@ def run_host_path(steps: int, warmup: int, rank: int, world: int, local: int, di
          "digest_check": check, "numa_node_rank0": node, "copy_threads": s_after["bulk_threads"],
          "staging_numa_node_rank0": s_after["staging_numa_node"], "data_numa_node_rank0": data_node,
          "raw_pinned_h2d_GiB/s": raw, "data_thp_share": thp,
-         "process_cpu_core_s_per_step_rank0": round(proc_cpu / max(steps + min(warmup, 2), 1), 4),
-         "copy_ms_per_step_rank0": round((s_after["ns_copy"] - s_before["ns_copy"]) / max(steps + warmup, 1) / 1e6, 3),
-         "wait_ms_per_step_rank0": round((s_after["ns_wait"] - s_before["ns_wait"]) / max(steps + warmup, 1) / 1e6, 3),
+         "process_cpu_core_s_per_step_rank0": round(proc_cpu / calls, 4),
+         "copy_ms_per_step_rank0": round((s_after["ns_copy"] - s_before["ns_copy"]) / calls / 1e6, 3),
+         "wait_ms_per_step_rank0": round((s_after["ns_wait"] - s_before["ns_wait"]) / calls / 1e6, 3),
          "cgroup_throttled_ms_rank0": None if thr0 is None or thr1 is None else round((thr1 - thr0) / 1e3, 1),
-         "cpu_core_s_per_step_rank0": round(cpu_ns / max(steps, 1) / 1e9, 4)}
+         "cpu_core_s_per_step_rank0": round(cpu_ns / calls / 1e9, 4)}
     if raw:
         r["frac_of_raw_pinned_h2d"] = round(r["GiB/s"] / raw, 3)
     return r
@@ -657,13 +677,17 @@ def main(argv=None) -> int:
     ap.add_argument("--rotate", type=int, default=0, help="distinct batches to rotate (0 = auto)")
     ap.add_argument("--streams", type=int, default=1, choices=[1, 2],
                     help="2: consecutive launches alternate between two streams (pipelined batches)")
+    ap.add_argument("--other", default="", help=argparse.SUPPRESS)   # A/B: comma list of other configs (+ "wire")
     ap.add_argument("--no-host-path", action="store_true",
                     help="skip the end-to-end host-memory leg (pageable and pinned shards, every rank)")
     ap.add_argument("--host-path-only", action="store_true",
                     help="only the end-to-end host-memory leg: one JSON line for it (tools/e2e_multi.sh)")
     ap.add_argument("--host-steps", type=int, default=5)
-    ap.add_argument("--host-path-first", action="store_true",
-                    help="run the host-memory leg before the device configs (placement A/B)")
+    ap.add_argument("--host-ctx-early", action="store_true",
+                    help="create (and warm) the host leg's context at the start of the run")
+    ap.add_argument("--host-path-first", action="store_true", help=argparse.SUPPRESS)   # the default now
+    ap.add_argument("--host-path-last", action="store_true",
+                    help="run the host-memory leg after the device configs (A/B: DESIGN.md §7, 'order')")
     args = ap.parse_args(argv)
 
     rank, world, local = dist_env()
@@ -723,8 +747,13 @@ def main(argv=None) -> int:
             dist.destroy_process_group()
         return 0
 
+    host_ctx = host_context(local) if (args.host_ctx_early and not args.no_host_path) else None
     host_first = None
-    if args.host_path_first and not args.no_host_path:   # before any device config allocates anything
+    # The host leg runs first, in a process that has not yet allocated and freed the 16 GiB 64k
+    # batch: after that batch, the chunked host pipelines (not a single raw 1.5 GB copy) run
+    # 30-35 % slower for the rest of the process, whichever order the context's own buffers were
+    # allocated in (profiles/r04_host_leg_order.jsonl). --host-path-last for the A/B.
+    if not args.host_path_last and not args.no_host_path:
         host_first = {m: run_host_path(args.host_steps, min(args.warmup, 2), rank, world, local, dist, device, m)
                       for m in ("pageable", "pinned")}
         torch.cuda.empty_cache()
@@ -762,7 +791,7 @@ def main(argv=None) -> int:
         # 2.43-2.47 ms per launch, 2.40 on memory no earlier batch used (tools/order_check.py,
         # profiles/r02_order_check.jsonl) — a property of the allocation, not of the kernel
         for cfg in sorted(CONFIGS, key=lambda c: -CONFIGS[c][0] * CONFIGS[c][1]):
-            if cfg == args.config:
+            if cfg == args.config or (args.other and cfg not in args.other.split(",")):
                 continue
             steps = max(10, min(args.steps, 200 if CONFIGS[cfg][1] < 4096 else 40))
             e, ebufs, _ = run_config(cfg, steps, min(args.warmup, 5), rank, world, dist, device)
@@ -802,15 +831,17 @@ def main(argv=None) -> int:
                     "digest_check": e3["check"], "traffic": load_traffic(cfg + "_multi")}
                 torch.cuda.empty_cache()
         # the reference's own call site on wire packets (context.c:208): FILL and VERIFY in place
-        extra["wire_1500"] = run_wire(max(10, min(args.steps, 100)), min(args.warmup, 5), device)
-        torch.cuda.empty_cache()
+        if not args.other or "wire" in args.other.split(","):
+            extra["wire_1500"] = run_wire(max(10, min(args.steps, 100)), min(args.warmup, 5), device)
+            torch.cuda.empty_cache()
 
     # end to end from host memory, every rank at once (PCIe and host DRAM bound; never `value`)
     host_path = None
-    if not args.no_host_path and not args.host_path_first:
+    if not args.no_host_path and args.host_path_last:
         del bufs
         torch.cuda.empty_cache()
-        host_path = {m: run_host_path(args.host_steps, min(args.warmup, 2), rank, world, local, dist, device, m)
+        host_path = {m: run_host_path(args.host_steps, min(args.warmup, 2), rank, world, local, dist, device, m,
+                                      ctx=host_ctx)
                      for m in ("pageable", "pinned")}
 
     if rank == 0:
@@ -854,8 +885,7 @@ def main(argv=None) -> int:
             line["other_configs"] = extra
         if host_path or host_first:
             line["host_path"] = host_path or host_first
-            if host_first:
-                line["host_path_ran_first"] = True
+            line["host_path_order"] = "before the device configs" if host_first else "after the device configs"
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         print(json.dumps(line), flush=True)

@@ -125,7 +125,7 @@ gpu_r4_final() {
 gpu_r4_hostorder() {
 (
   for order in last first; do
-    extra=""; [ $order = first ] && extra="--host-path-first"
+    extra="--host-path-last"; [ $order = first ] && extra=""
     timeout -k 10 400 python3 bench.py --steps 50 --no-cpu-baseline $extra > gpurun_out/r4_hostorder_$order.json 2>> gpurun_out/r4_hostorder.err; rc=$?
     echo "$order rc=$rc $(python3 -c "import json; d=json.load(open('gpurun_out/r4_hostorder_$order.json'))['host_path']; print({m: (d[m]['GiB/s'], d[m]['numa_node_rank0'], d[m]['cpu_core_s_per_step_rank0'], d[m].get('copy_ms_per_step_rank0'), d[m].get('wait_ms_per_step_rank0')) for m in d})")"
     ok_rc $rc || exit $rc
@@ -143,6 +143,44 @@ gpu_r4_slots() {
     set -- $cfg
     TCPCSUM_HOST_CHUNK_MB=$1 TCPCSUM_HOST_SLOTS=$2 timeout -k 10 400 python3 bench.py --steps 50 --no-cpu-baseline > gpurun_out/r4_slots_$1_$2.json 2>> gpurun_out/r4_slots.err; rc=$?
     echo "chunk=$1 slots=$2 rc=$rc $(python3 -c "import json; d=json.load(open('gpurun_out/r4_slots_$1_$2.json'))['host_path']; print({m: (d[m]['GiB/s'], d[m]['numa_node_rank0'], d[m].get('copy_ms_per_step_rank0'), d[m].get('wait_ms_per_step_rank0')) for m in d})")"
+    ok_rc $rc || exit $rc
+  done
+)
+}
+
+# round 4: host leg last in the full line, its context created late (control) or at the start
+# of the run (--host-ctx-early), and the leg run first — does allocation order explain the
+# pageable slowdown?
+gpu_r4_early() {
+(
+  for v in late early first late2 early2; do
+    case $v in late*) extra="--host-path-last";; early*) extra="--host-path-last --host-ctx-early";; first) extra="";; esac
+    timeout -k 10 400 python3 bench.py --steps 50 --no-cpu-baseline $extra > gpurun_out/r4_early_$v.json 2>> gpurun_out/r4_early.err; rc=$?
+    echo "$v rc=$rc $(python3 -c "import json; d=json.load(open('gpurun_out/r4_early_$v.json'))['host_path']; print({m: (d[m]['GiB/s'], d[m]['numa_node_rank0'], d[m].get('copy_ms_per_step_rank0'), d[m].get('wait_ms_per_step_rank0')) for m in d})")"
+    ok_rc $rc || exit $rc
+  done
+)
+}
+
+# round 4: which device leg leaves the pageable host pipeline slow — the headline alone with
+# many or few steps, host leg last
+gpu_r4_culprit() {
+(
+  for v in "h50:--steps 50" "h2:--steps 2 --warmup 1" "probe2:--steps 2 --warmup 1 --probe" "all2:--steps 2 --warmup 1 --other"; do
+    name=${v%%:*}; a=${v#*:}
+    case $a in *--other) a=${a% --other}; oc="";; *--probe) a=${a% --probe}; oc="--no-other-configs";; *) oc="--no-other-configs --no-probe";; esac
+    timeout -k 10 400 python3 bench.py --no-cpu-baseline --host-path-last $a $oc > gpurun_out/r4_culprit_$name.json 2>> gpurun_out/r4_culprit.err; rc=$?
+    echo "$name rc=$rc $(python3 -c "import json; d=json.load(open('gpurun_out/r4_culprit_$name.json'))['host_path']; print({m: (d[m]['GiB/s'], d[m].get('copy_ms_per_step_rank0'), d[m].get('wait_ms_per_step_rank0')) for m in d})")"
+    ok_rc $rc || exit $rc
+  done
+)
+}
+
+gpu_r4_bisect() {
+(
+  for o in 64k 64 wire; do
+    timeout -k 10 400 python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 --no-probe --host-path-last --other $o > gpurun_out/r4_bisect_$o.json 2>> gpurun_out/r4_bisect.err; rc=$?
+    echo "$o rc=$rc $(python3 -c "import json; d=json.load(open('gpurun_out/r4_bisect_$o.json'))['host_path']; print({m: (d[m]['GiB/s'], d[m].get('copy_ms_per_step_rank0'), d[m].get('wait_ms_per_step_rank0')) for m in d})")"
     ok_rc $rc || exit $rc
   done
 )
