@@ -73,7 +73,7 @@ public:
         }
         if (++batches_ >= kMemoBatches) {
             batches_ = 0;
-            pageable_.clear();
+            forget_pageable();
         }
     }
 
@@ -86,7 +86,7 @@ public:
         uintptr_t rs = 0, re = 0;
         intptr_t delta = 0;
         if (!b_.pinned_extent(p, &rs, &re, &delta)) {
-            if (pageable_.size() >= kPageableMemo) pageable_.clear();
+            if (pageable_.size() >= kPageableMemo) forget_pageable();
             pageable_.insert(pg);
             return kUnmappable;
         }
@@ -96,8 +96,9 @@ public:
         return find(p, e, dev) ? 0 : kUnmappable;
     }
 
-    // Drop the pageable-page memo now (the application has just page-locked
-    // memory it used pageable before, and wants it read in place at once).
+    // Drop the pageable-page memo: every kMemoBatches batches, when it is full,
+    // and on demand (a test that page-locks memory it used pageable before and
+    // wants it read in place at once).
     void forget_pageable() { pageable_.clear(); }
 
     size_t extents() const { return regs_.size(); }
