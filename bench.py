@@ -433,6 +433,44 @@ def page_node_of(arr) -> int | None:
         return None
 
 
+def page_node_shares(arr, samples: int = 512) -> dict | None:
+    """Where a numpy array's pages live: share of `samples` pages spread over it per NUMA node
+    (move_pages with no target nodes reports each page's node), or None."""
+    import ctypes
+    try:
+        libc = ctypes.CDLL(None, use_errno=True)
+        base, nbytes = arr.ctypes.data, arr.nbytes
+        npg = max(1, nbytes // 4096)
+        idx = sorted({i * npg // samples for i in range(min(samples, npg))})
+        pages = (ctypes.c_void_p * len(idx))(*[base + i * 4096 for i in idx])
+        status = (ctypes.c_int * len(idx))()
+        # SYS_move_pages = 279 on x86-64; nodes = NULL: query only
+        if libc.syscall(279, 0, ctypes.c_ulong(len(idx)), pages, None, status, 0) != 0:
+            return None
+        out = {}
+        for st in status:
+            k = str(st) if st >= 0 else "err"
+            out[k] = out.get(k, 0) + 1
+        return {k: round(v / len(idx), 3) for k, v in sorted(out.items())}
+    except Exception:
+        return None
+
+
+def node_free_gib() -> dict | None:
+    """MemFree per NUMA node (sysfs), GiB, or None."""
+    try:
+        import glob
+        out = {}
+        for f in sorted(glob.glob("/sys/devices/system/node/node*/meminfo")):
+            node = f.split("/")[-2][4:]
+            for line in open(f):
+                if "MemFree:" in line:
+                    out[node] = round(int(line.split()[-2]) / (1 << 20), 1)
+        return out or None
+    except Exception:
+        return None
+
+
 def cgroup_throttled_us() -> int | None:
     """The job's cgroup CPU throttling so far (cpu.stat throttled_usec), or None."""
     try:
@@ -523,6 +561,7 @@ def run_host_path(steps: int, warmup: int, rank: int, world: int, local: int, di
         tcp_amd.synth_fill(d, s0 * L, nbytes)
         dss = torch.empty(cnt, dtype=torch.int32, device=device)
         tcp_amd.synth_pseudo(dss, s0, cnt, L)
+        free_before = node_free_gib()
         host = tcp_amd.pinned_empty(nbytes) if memory == "pinned" else np.empty(nbytes, np.uint8)
         host[::4096] = 0   # first touch, page by page, from this node
         torch.from_numpy(host).copy_(d)
@@ -550,6 +589,7 @@ def run_host_path(steps: int, warmup: int, rank: int, world: int, local: int, di
             s_after = ctx.stats()
             proc_cpu = (ru1.ru_utime + ru1.ru_stime) - (ru0.ru_utime + ru0.ru_stime)
             data_node = page_node_of(host)
+            data_nodes = page_node_shares(host)
             thp = thp_share(host) if memory == "pageable" else None
         finally:
             if own_ctx:
@@ -577,7 +617,8 @@ def run_host_path(steps: int, warmup: int, rank: int, world: int, local: int, di
          "memory": memory, "steps": steps, **host_path_rate([nbytes] * world, walls, steps),
          "digest_check": check, "numa_node_rank0": node, "copy_threads": s_after["bulk_threads"],
          "staging_numa_node_rank0": s_after["staging_numa_node"], "data_numa_node_rank0": data_node,
-         "raw_pinned_h2d_GiB/s": raw, "data_thp_share": thp,
+         "raw_pinned_h2d_GiB/s": raw, "data_thp_share": thp, "data_page_node_shares_rank0": data_nodes,
+         "node_free_gib_before_rank0": free_before,
          "process_cpu_core_s_per_step_rank0": round(proc_cpu / calls, 4),
          "copy_ms_per_step_rank0": round((s_after["ns_copy"] - s_before["ns_copy"]) / calls / 1e6, 3),
          "wait_ms_per_step_rank0": round((s_after["ns_wait"] - s_before["ns_wait"]) / calls / 1e6, 3),
