@@ -726,9 +726,9 @@ def main(argv=None) -> int:
     ap.add_argument("--host-steps", type=int, default=5)
     ap.add_argument("--host-ctx-early", action="store_true",
                     help="create (and warm) the host leg's context at the start of the run")
-    ap.add_argument("--host-path-first", action="store_true", help=argparse.SUPPRESS)   # the default now
-    ap.add_argument("--host-path-last", action="store_true",
-                    help="run the host-memory leg after the device configs (A/B: DESIGN.md §7, 'order')")
+    ap.add_argument("--host-path-first", action="store_true",
+                    help="run the host-memory leg before the device configs (A/B: DESIGN.md §7, 'Order')")
+    ap.add_argument("--host-path-last", action="store_true", help=argparse.SUPPRESS)   # the default
     args = ap.parse_args(argv)
 
     rank, world, local = dist_env()
@@ -790,11 +790,10 @@ def main(argv=None) -> int:
 
     host_ctx = host_context(local) if (args.host_ctx_early and not args.no_host_path) else None
     host_first = None
-    # The host leg runs first, in a process that has not yet allocated and freed the 16 GiB 64k
-    # batch: after that batch, the chunked host pipelines (not a single raw 1.5 GB copy) run
-    # 30-35 % slower for the rest of the process, whichever order the context's own buffers were
-    # allocated in (profiles/r04_host_leg_order.jsonl). --host-path-last for the A/B.
-    if not args.host_path_last and not args.no_host_path:
+    # The host leg runs after the device configs; --host-path-first runs it before them (A/B:
+    # with the context's copies and kernels on one stream its rate no longer depends on the
+    # order, DESIGN.md §7 "Order", profiles/r04_host_leg_order.jsonl).
+    if args.host_path_first and not args.no_host_path:
         host_first = {m: run_host_path(args.host_steps, min(args.warmup, 2), rank, world, local, dist, device, m)
                       for m in ("pageable", "pinned")}
         torch.cuda.empty_cache()
@@ -878,7 +877,7 @@ def main(argv=None) -> int:
 
     # end to end from host memory, every rank at once (PCIe and host DRAM bound; never `value`)
     host_path = None
-    if not args.no_host_path and args.host_path_last:
+    if not args.no_host_path and not args.host_path_first:
         del bufs
         torch.cuda.empty_cache()
         host_path = {m: run_host_path(args.host_steps, min(args.warmup, 2), rank, world, local, dist, device, m,

@@ -226,24 +226,27 @@ int tcpcsum_tx_build_dev(const void *d_payload, const tcpcsum_txseg_t *d_segs, u
 
 /* ------------------------------------------------------ host-memory batches
  * The path as the reference sees it: segments start and end in host memory
- * (raw-socket buffers). A context owns one device, two streams, pinned
+ * (raw-socket buffers). A context owns one device, one stream, pinned
  * staging and a few host copy threads (TCPCSUM_HOST_THREADS, default half the
  * CPUs the process may use, at most 8; a staged wire batch of up to 8 MiB
  * copies on TCPCSUM_HOST_WIRE_THREADS of them, default 1 = the calling thread).
  * Host memory is used one of two ways:
  *   - memory its owner page-locked (tcpcsum_host_alloc / hipHostMalloc, or the
  *     application's own hipHostRegister) is read — FILL: written — in place by
- *     the kernel over PCIe;
+ *     the kernel over PCIe (a uniform batch of 32 MiB or more goes to HBM by
+ *     DMA from those pages first, 256 MiB at a time);
  *   - pageable memory is copied by the CPU threads into the context's pinned
- *     staging (uniform batches chunk by chunk, overlapped with the kernel on
- *     the previous chunk; wire batches only the packets' bytes), the kernel
+ *     staging (uniform batches 64 MiB chunk by chunk, each chunk's DMA to HBM
+ *     and kernel overlapped with the copy of the next; wire batches only the packets' bytes), the kernel
  *     reads the staging, and FILL's checks are stored back into the caller's
  *     packets by the CPU. It is never page-locked.
  * All host calls are synchronous: they return when every result is in place. */
 typedef struct tcpcsum_ctx tcpcsum_ctx_t;
 
 /* scratch_bytes: pinned staging per pipeline slot for pageable uniform
- * batches (0 = 16 MiB). */
+ * batches, and the DMA piece for page-locked ones (0 = 64 MiB staging,
+ * 256 MiB DMA pieces; page-locked batches under 32 MiB — two scratch_bytes
+ * when given — are read in place). */
 int tcpcsum_ctx_create(int device, size_t scratch_bytes, tcpcsum_ctx_t **out);
 void tcpcsum_ctx_destroy(tcpcsum_ctx_t *ctx);
 

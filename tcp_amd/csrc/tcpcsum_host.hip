@@ -166,21 +166,35 @@ using tcpcsum::get_tuning;
 using tcpcsum::hip_fail;
 using tcpcsum::require_device;
 
-// Staging chunk per pipeline slot for pageable uniform batches (0 = default).
-constexpr size_t kDefaultChunk = 16u << 20;
+// Staging chunk per pipeline slot for pageable uniform batches, and the DMA chunk
+// for page-locked ones (scratch_bytes, when given, sets both).
+constexpr size_t kDefaultChunk = 64u << 20;
+constexpr size_t kDefaultDmaChunk = 256u << 20;
+// page-locked uniform batches under two of these are read in place over PCIe
+constexpr size_t kDefaultInPlaceChunk = 16u << 20;
 
 struct tcpcsum_ctx {
     int device = 0;
-    size_t chunk = 0;
+    size_t chunk = 0;       // pageable uniform batches: bytes per staged chunk
+    size_t dma_chunk = 0;   // page-locked uniform batches: bytes per DMA to HBM
+    size_t in_place_chunk = 0;   // ... read in place when under two of these
     uint32_t flags = 0;
-    hipStream_t st[2] = {nullptr, nullptr};
-    // uniform batches: nslots staged chunks in flight (TCPCSUM_HOST_SLOTS, 2..4), slot s on stream s & 1
+    // every copy and launch of a context goes to this one stream, in order: two
+    // streams alternating 16 MiB host-to-HBM copies ran at 43.5 GiB/s instead of
+    // 53.3 in some process states (after a 16 GiB device allocation, and on some
+    // boxes from the start), one stream never below 51.2 (tools/dma_state_probe.hip)
+    hipStream_t st = nullptr;
+    // pageable uniform batches: nslots pinned staging chunks in flight
+    // (TCPCSUM_HOST_SLOTS, 2..4); slot_ev[s] is recorded after the last device
+    // work that reads staging slot s, before the copy threads refill it
     int nslots = 2;
     hipEvent_t slot_ev[4] = {nullptr, nullptr, nullptr, nullptr};
     bool slot_busy[4] = {false, false, false, false};
     tcpcsum::Pinned slot[4];   // one staged chunk each
-    uint8_t* d_slot[4] = {nullptr, nullptr, nullptr, nullptr};   // ... and its device copy (uniform_dma)
-    size_t d_slot_bytes = 0;
+    // HBM for the chunk being checksummed (the stream orders each copy behind
+    // the previous chunk's kernel, so one buffer serves every chunk)
+    uint8_t* d_buf = nullptr;
+    size_t d_buf_bytes = 0;
     tcpcsum::Pinned gath;      // wire batches: packets copied out of pageable memory
     tcpcsum::Pinned ss, res;   // per-segment start values / results, when the caller's are pageable
     // per-packet arrays the wire kernels read (addresses, bounds) and write
@@ -313,15 +327,6 @@ hipError_t wait_stream(tcpcsum_ctx* c, hipStream_t st, uint64_t expect_ns) {
 // What a host batch's device work should take: its bytes over PCIe (~50 GB/s,
 // 50 bytes per ns) plus a launch's latency — the sleeping wait's first nap.
 inline uint64_t expect_ns(uint64_t bytes) { return bytes / 50u + 8000u; }
-
-// Both streams drained, waited for once: st[1] waits on st[0]'s last work, and
-// the caller sleeps on st[1] only (the pipelined paths queue on both).
-hipError_t wait_both(tcpcsum_ctx* c, uint64_t expect) {
-    hipError_t e = hipEventRecord(c->slot_ev[0], c->st[0]);
-    if (e == hipSuccess) e = hipStreamWaitEvent(c->st[1], c->slot_ev[0], 0);
-    if (e == hipSuccess) e = wait_stream(c, c->st[1], expect);
-    return e;
-}
 
 // CPU time of the calling thread inside one host call, into stats.ns_cpu_caller.
 struct CallerCpu {
@@ -567,13 +572,17 @@ int tcpcsum_ctx_create(int device, size_t scratch_bytes, tcpcsum_ctx_t** out) {
     c->pinned_dma = tcpcsum::env_int("TCPCSUM_HOST_PINNED_DMA", 1) != 0;
     c->stage_blocks = std::max(1, std::min(16, tcpcsum::env_int("TCPCSUM_HOST_STAGE_BLOCKS", 1)));
     c->nslots = std::max(2, std::min(4, tcpcsum::env_int("TCPCSUM_HOST_SLOTS", 2)));
-    if (!scratch_bytes) c->chunk = (size_t)std::max(1, tcpcsum::env_int("TCPCSUM_HOST_CHUNK_MB", 16)) << 20;
-    for (int i = 0; i < 2; ++i) {
-        e = hipStreamCreateWithFlags(&c->st[i], hipStreamNonBlocking);
-        if (e != hipSuccess) {
-            tcpcsum_ctx_destroy(c);
-            return hip_fail(e);
-        }
+    c->dma_chunk = scratch_bytes ? scratch_bytes : kDefaultDmaChunk;
+    c->in_place_chunk = scratch_bytes ? scratch_bytes : kDefaultInPlaceChunk;
+    if (!scratch_bytes) {
+        c->chunk = (size_t)std::max(1, tcpcsum::env_int("TCPCSUM_HOST_CHUNK_MB", (int)(kDefaultChunk >> 20))) << 20;
+        c->dma_chunk =
+            (size_t)std::max(1, tcpcsum::env_int("TCPCSUM_HOST_DMA_CHUNK_MB", (int)(kDefaultDmaChunk >> 20))) << 20;
+    }
+    e = hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        tcpcsum_ctx_destroy(c);
+        return hip_fail(e);
     }
     for (int i = 0; i < 4; ++i) {
         e = hipEventCreateWithFlags(&c->slot_ev[i], hipEventDisableTiming);
@@ -594,16 +603,12 @@ int tcpcsum_ctx_create(int device, size_t scratch_bytes, tcpcsum_ctx_t** out) {
 void tcpcsum_ctx_destroy(tcpcsum_ctx_t* c) {
     if (!c) return;
     DeviceGuard g(c->device);
-    for (int i = 0; i < 2; ++i)
-        if (c->st[i]) hipStreamSynchronize(c->st[i]);
+    if (c->st) hipStreamSynchronize(c->st);
     if (c->done_ev) hipEventDestroy(c->done_ev);
-    for (int i = 0; i < 4; ++i) {
-        if (c->d_slot[i]) hipFree(c->d_slot[i]);
+    for (int i = 0; i < 4; ++i)
         if (c->slot_ev[i]) hipEventDestroy(c->slot_ev[i]);
-    }
-    for (int i = 0; i < 2; ++i) {
-        if (c->st[i]) hipStreamDestroy(c->st[i]);
-    }
+    if (c->d_buf) hipFree(c->d_buf);
+    if (c->st) hipStreamDestroy(c->st);
     delete c;   // pinned buffers and copy threads go with it
 }
 
@@ -650,15 +655,15 @@ void tcpcsum_host_free(void* p) {
     if (p) hipHostFree(p);
 }
 
-// Page-locked input: small batches (< 2 chunks) are read in place by one launch
-// over PCIe; larger ones go to HBM by DMA straight from the caller's pages,
-// chunk by chunk, alternating between two streams and two HBM slots — every
-// copy and kernel queued at once, stream order keeping a slot's next copy behind
-// its last kernel (TCPCSUM_HOST_PINNED_DMA=0: always in place). Pageable input:
-// chunks alternate between two streams and two pinned staging slots; the copy
-// threads fill slot k&1 with chunk k while the kernel reads chunk k-1 from the
-// other slot. Start values and results use the caller's arrays when those are
-// page-locked, else pinned staging (copied in / out by the CPU).
+// Page-locked input: batches under two 16 MiB pieces are read in place by one
+// launch over PCIe; larger ones go to HBM by DMA straight from the caller's
+// pages in dma_chunk pieces (256 MiB), each copy followed by its kernel on the
+// context's one stream — in-stream order is the only synchronisation
+// (TCPCSUM_HOST_PINNED_DMA=0: always in place). Pageable input: the copy threads
+// fill pinned staging slot k % nslots with chunk k (64 MiB) while the stream
+// copies chunk k-1 to HBM and checksums it; a slot is refilled once the DMA that
+// read it has finished. Start values and results use the caller's arrays when
+// those are page-locked, else pinned staging (copied in / out by the CPU).
 int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t stride, uint32_t len,
                                const uint32_t* h_sum_start, uint32_t sum_start, uint16_t* h_out, uint64_t n) {
     if (!c) return TCPCSUM_EINVAL;
@@ -689,69 +694,68 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t st
         kout = (uint16_t*)c->res.d;
     }
     const size_t span = (size_t)((n - 1) * stride + len);
-    // segments per chunk: (cnt-1)*stride + len <= chunk (at least one segment)
-    uint64_t per = 1;
-    if (stride == 0) per = n;
-    else if (c->chunk > len) per = (c->chunk - len) / stride + 1;
-    if (per > n) per = n;
-    const size_t slot_bytes = (size_t)((per - 1) * stride + len) + 16;
-    const int ns = c->nslots;
-    auto ensure_hbm_slots = [&]() -> hipError_t {
-        if (slot_bytes <= c->d_slot_bytes && c->d_slot[ns - 1]) return hipSuccess;
-        for (int i = 0; i < 4; ++i) {
-            if (c->d_slot[i]) (void)hipFree(c->d_slot[i]);
-            c->d_slot[i] = nullptr;
-        }
-        c->d_slot_bytes = 0;
-        for (int i = 0; i < ns; ++i) {
-            const hipError_t he = hipMalloc(&c->d_slot[i], slot_bytes);
-            if (he != hipSuccess) return he;
-        }
-        c->d_slot_bytes = slot_bytes;
-        return hipSuccess;
+    // segments per piece of at most `bytes` (at least one segment)
+    auto per_piece = [&](size_t bytes) -> uint64_t {
+        uint64_t per = 1;
+        if (stride == 0) per = n;
+        else if (bytes > len) per = (bytes - len) / stride + 1;
+        return per > n ? n : per;
     };
+    auto piece_bytes = [&](uint64_t cnt) { return (size_t)((cnt - 1) * stride + len); };
+    auto ensure_hbm = [&](size_t bytes) -> hipError_t {
+        bytes += 16;   // the piece keeps its start's alignment mod 16
+        if (bytes <= c->d_buf_bytes) return hipSuccess;
+        if (c->d_buf) {
+            (void)hipStreamSynchronize(c->st);
+            (void)hipFree(c->d_buf);
+        }
+        c->d_buf = nullptr;
+        c->d_buf_bytes = 0;
+        const hipError_t he = hipMalloc(&c->d_buf, bytes);
+        if (he == hipSuccess) c->d_buf_bytes = bytes;
+        return he;
+    };
+    const uint64_t per = per_piece(c->chunk);
     const uint8_t* zb = (const uint8_t*)pinned_dev_ptr(h_base, span);
-    if (zb && (!c->pinned_dma || per * 2 > n)) {
-        tcpcsum::launch_uniform(zb, stride, len, kss, sum_start, kout, n, c->st[0], tu);
+    if (zb && (!c->pinned_dma || per_piece(c->in_place_chunk) * 2 > n)) {
+        tcpcsum::launch_uniform(zb, stride, len, kss, sum_start, kout, n, c->st, tu);
         rc = check_launch();
         if (rc) return rc;
-        e = wait_stream(c, c->st[0], expect_ns(span));
+        e = wait_stream(c, c->st, expect_ns(span));
         if (e != hipSuccess) return hip_fail(e);
-    } else if (zb) {   // page-locked, large: DMA from the caller's pages, every chunk queued up front
-        e = ensure_hbm_slots();
+    } else if (zb) {   // page-locked, large: DMA from the caller's pages, every piece queued at once
+        const uint64_t dper = per_piece(c->dma_chunk);
+        e = ensure_hbm(piece_bytes(dper));
         if (e != hipSuccess) return hip_fail(e);
-        uint64_t k = 0;
-        for (uint64_t s0 = 0; s0 < n; s0 += per, ++k) {
-            const int s = (int)(k % (uint64_t)ns);   // slot s on stream s & 1: a slot's next copy
-            hipStream_t sst = c->st[s & 1];          // stays behind its last kernel
-            const uint64_t cnt = (n - s0) < per ? (n - s0) : per;
-            const size_t bytes = (size_t)((cnt - 1) * stride + len);
+        for (uint64_t s0 = 0; s0 < n; s0 += dper) {
+            const uint64_t cnt = (n - s0) < dper ? (n - s0) : dper;
             const uint8_t* src = (const uint8_t*)h_base + s0 * stride;
             const size_t mis = (uintptr_t)src & 15u;   // the in-place shape's alignment
-            e = hipMemcpyAsync(c->d_slot[s] + mis, src, bytes, hipMemcpyHostToDevice, sst);
+            e = hipMemcpyAsync(c->d_buf + mis, src, piece_bytes(cnt), hipMemcpyHostToDevice, c->st);
             if (e != hipSuccess) return hip_fail(e);
-            tcpcsum::launch_uniform(c->d_slot[s] + mis, stride, len, kss ? kss + s0 : nullptr, sum_start, kout + s0,
-                                    cnt, sst, tu);
+            tcpcsum::launch_uniform(c->d_buf + mis, stride, len, kss ? kss + s0 : nullptr, sum_start, kout + s0, cnt,
+                                    c->st, tu);
             rc = check_launch();
             if (rc) return rc;
         }
-        e = wait_both(c, expect_ns(span));
+        e = wait_stream(c, c->st, expect_ns(span));
         if (e != hipSuccess) return hip_fail(e);
     } else {
+        const int ns = c->nslots;
+        const size_t slot_bytes = piece_bytes(per) + 16;
         for (int i = 0; i < ns; ++i) {
             e = c->slot[i].ensure(slot_bytes);
             if (e != hipSuccess) return hip_fail(e);
         }
         if (c->uniform_dma) {
-            e = ensure_hbm_slots();
+            e = ensure_hbm(piece_bytes(per));
             if (e != hipSuccess) return hip_fail(e);
         }
         uint64_t k = 0;
         for (uint64_t s0 = 0; s0 < n; s0 += per, ++k) {
             const int s = (int)(k % (uint64_t)ns);
-            hipStream_t sst = c->st[s & 1];
             const uint64_t cnt = (n - s0) < per ? (n - s0) : per;
-            const size_t bytes = (size_t)((cnt - 1) * stride + len);
+            const size_t bytes = piece_bytes(cnt);
             const uint8_t* src = (const uint8_t*)h_base + s0 * stride;
             if (c->slot_busy[s]) {   // the DMA (or kernel) that last read this slot: chunk k - nslots
                 c->slot_busy[s] = false;
@@ -767,25 +771,24 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t st
             c->stats.bytes_staged += bytes;
             const uint8_t* kin = c->slot[s].d + mis;
             if (c->uniform_dma) {   // pinned -> HBM by the DMA engines, then the kernel reads HBM
-                e = hipMemcpyAsync(c->d_slot[s] + mis, c->slot[s].h + mis, bytes, hipMemcpyHostToDevice, sst);
+                e = hipMemcpyAsync(c->d_buf + mis, c->slot[s].h + mis, bytes, hipMemcpyHostToDevice, c->st);
                 if (e != hipSuccess) return hip_fail(e);
-                e = hipEventRecord(c->slot_ev[s], sst);
+                e = hipEventRecord(c->slot_ev[s], c->st);
                 if (e != hipSuccess) return hip_fail(e);
-                kin = c->d_slot[s] + mis;
+                kin = c->d_buf + mis;
             }
-            tcpcsum::launch_uniform(kin, stride, len, kss ? kss + s0 : nullptr, sum_start, kout + s0, cnt, sst, tu);
+            tcpcsum::launch_uniform(kin, stride, len, kss ? kss + s0 : nullptr, sum_start, kout + s0, cnt, c->st, tu);
             rc = check_launch();
             if (rc) return rc;
             if (!c->uniform_dma) {
-                e = hipEventRecord(c->slot_ev[s], sst);
+                e = hipEventRecord(c->slot_ev[s], c->st);
                 if (e != hipSuccess) return hip_fail(e);
             }
             c->slot_busy[s] = true;
         }
-        // the last chunk's DMA and kernel: all earlier chunks have been waited for
-        // slot by slot, so what is left is about one chunk's work
+        // what is left is about the last chunk's DMA and kernel
         for (int i = 0; i < 4; ++i) c->slot_busy[i] = false;
-        e = wait_both(c, expect_ns(std::min<uint64_t>(span, slot_bytes)));
+        e = wait_stream(c, c->st, expect_ns(std::min<uint64_t>(span, slot_bytes)));
         if (e != hipSuccess) return hip_fail(e);
     }
     if (out_staged) par_copy(c, h_out, c->res.h, n * sizeof(uint16_t));
@@ -811,7 +814,7 @@ int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t* c, void* h_pkts, size_t region_bytes,
     std::lock_guard<std::mutex> lk(c->mu);
     CallerCpu cpu(c);
     DeviceGuard g(c->device);
-    hipStream_t st = c->st[0];
+    hipStream_t st = c->st;
     c->stats.batches++;
     int rc = ensure_pkt_arrays(c, n);
     if (rc) return rc;
@@ -876,7 +879,7 @@ int tcpcsum_ipv4_batch_ptrs_host(tcpcsum_ctx_t* c, void* const* h_pkts, const ui
     std::lock_guard<std::mutex> lk(c->mu);
     CallerCpu cpu(c);
     DeviceGuard g(c->device);
-    hipStream_t st = c->st[0];
+    hipStream_t st = c->st;
     c->stats.batches++;
     int rc = ensure_pkt_arrays(c, n);
     if (rc) return rc;

@@ -146,7 +146,7 @@ def test_staging_on_the_gpus_numa_node(dev):
 @pytest.mark.parametrize("offset,stride,length", [(0, 1500, 1500), (3, 1501, 1499), (16, 4096, 4000), (1, 64, 64)])
 def test_uniform_host_pinned_dma_chunks(dev, offset, stride, length):
     """Page-locked input of two chunks or more goes to HBM by DMA straight from the caller's pages,
-    chunk by chunk on two streams (1 MiB chunks here, so a 6 MiB batch takes six); every segment
+    piece by piece on the context's stream (1 MiB pieces here, so a 6 MiB batch takes six); every segment
     matches the oracle, and so does the in-place path the same batch takes with
     TCPCSUM_HOST_PINNED_DMA=0 (read at context creation)."""
     import os

@@ -186,6 +186,34 @@ gpu_r4_bisect() {
 )
 }
 
+# round 4: after the 64k batch, which part of the pageable pipeline is slow — DMA to HBM or the
+# kernel reading staging over PCIe; 4 slots; HIP's own event waits spinning or yielding
+gpu_r4_dma() {
+(
+  for v in "dflt:" "nodma:TCPCSUM_HOST_DMA=0" "slots4:TCPCSUM_HOST_SLOTS=4" "nocache:PYTORCH_NO_HIP_MEMORY_CACHING=1"; do
+    name=${v%%:*}; e=${v#*:}
+    env $e timeout -k 10 300 python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 --no-probe --host-path-last --other 64k > gpurun_out/r4_dma_$name.json 2>> gpurun_out/r4_dma.err; rc=$?
+    echo "$name rc=$rc $(python3 -c "import json; d=json.load(open('gpurun_out/r4_dma_$name.json'))['host_path']; print({m: (d[m]['GiB/s'], d[m].get('copy_ms_per_step_rank0'), d[m].get('wait_ms_per_step_rank0'), d[m].get('raw_pinned_h2d_GiB/s')) for m in d})")"
+    ok_rc $rc || exit $rc
+  done
+)
+}
+
+# round 4: the uniform host paths on one stream (64 MiB staging, 256 MiB DMA pieces) — every
+# GPU test, then the host leg first (default), last after the 64k batch, and last after all
+gpu_r4_onestream() {
+(
+  timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/r4_onestream_tests.log 2>&1; rc=$?
+  echo "tests rc=$rc"; grep -E "passed|failed" gpurun_out/r4_onestream_tests.log | tail -1; grep FAILED gpurun_out/r4_onestream_tests.log | head; ok_rc $rc || exit $rc
+  for v in "first:--steps 50" "last64k:--steps 2 --warmup 1 --no-probe --host-path-last --other 64k" "lastall:--steps 50 --host-path-last"; do
+    name=${v%%:*}; a=${v#*:}
+    timeout -k 10 400 python3 bench.py --no-cpu-baseline $a > gpurun_out/r4_onestream_$name.json 2>> gpurun_out/r4_onestream.err; rc=$?
+    echo "$name rc=$rc $(python3 -c "import json; D=json.load(open('gpurun_out/r4_onestream_$name.json')); d=D['host_path']; print(D['value'], {m: (d[m]['GiB/s'], d[m].get('copy_ms_per_step_rank0'), d[m].get('wait_ms_per_step_rank0'), d[m].get('raw_pinned_h2d_GiB/s'), d[m]['cpu_core_s_per_step_rank0']) for m in d})")"
+    ok_rc $rc || exit $rc
+  done
+)
+}
+
 # round 3: wire FILL line store (default) — every GPU test first, then the A/B timing three
 # times (the two FILL stores must agree byte for byte every time)
 gpu_r3_fill() {
