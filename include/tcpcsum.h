@@ -236,15 +236,16 @@ int tcpcsum_tx_build_dev(const void *d_payload, const tcpcsum_txseg_t *d_segs, u
  *     the kernel over PCIe (a uniform batch of 32 MiB or more goes to HBM by
  *     DMA from those pages first, 256 MiB at a time);
  *   - pageable memory is copied by the CPU threads into the context's pinned
- *     staging (uniform batches 64 MiB chunk by chunk, each chunk's DMA to HBM
- *     and kernel overlapped with the copy of the next; wire batches only the packets' bytes), the kernel
- *     reads the staging, and FILL's checks are stored back into the caller's
+ *     staging (uniform batches chunk by chunk — 16, 32, 64, then 128 MiB —
+ *     each chunk's DMA to HBM and kernel overlapped with the copy of the
+ *     next; wire batches only the packets' bytes), the kernel reads the
+ *     staging, and FILL's checks are stored back into the caller's
  *     packets by the CPU. It is never page-locked.
  * All host calls are synchronous: they return when every result is in place. */
 typedef struct tcpcsum_ctx tcpcsum_ctx_t;
 
 /* scratch_bytes: pinned staging per pipeline slot for pageable uniform
- * batches, and the DMA piece for page-locked ones (0 = 64 MiB staging,
+ * batches, and the DMA piece for page-locked ones (0 = 128 MiB staging,
  * 256 MiB DMA pieces; page-locked batches under 32 MiB — two scratch_bytes
  * when given — are read in place). */
 int tcpcsum_ctx_create(int device, size_t scratch_bytes, tcpcsum_ctx_t **out);

@@ -168,7 +168,7 @@ using tcpcsum::require_device;
 
 // Staging chunk per pipeline slot for pageable uniform batches, and the DMA chunk
 // for page-locked ones (scratch_bytes, when given, sets both).
-constexpr size_t kDefaultChunk = 64u << 20;
+constexpr size_t kDefaultChunk = 128u << 20;
 constexpr size_t kDefaultDmaChunk = 256u << 20;
 // page-locked uniform batches under two of these are read in place over PCIe
 constexpr size_t kDefaultInPlaceChunk = 16u << 20;
@@ -660,7 +660,7 @@ void tcpcsum_host_free(void* p) {
 // pages in dma_chunk pieces (256 MiB), each copy followed by its kernel on the
 // context's one stream — in-stream order is the only synchronisation
 // (TCPCSUM_HOST_PINNED_DMA=0: always in place). Pageable input: the copy threads
-// fill pinned staging slot k % nslots with chunk k (64 MiB) while the stream
+// fill pinned staging slot k % nslots with chunk k (16, 32, 64, then 128 MiB) while the stream
 // copies chunk k-1 to HBM and checksums it; a slot is refilled once the DMA that
 // read it has finished. Start values and results use the caller's arrays when
 // those are page-locked, else pinned staging (copied in / out by the CPU).
@@ -752,9 +752,14 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t st
             if (e != hipSuccess) return hip_fail(e);
         }
         uint64_t k = 0;
-        for (uint64_t s0 = 0; s0 < n; s0 += per, ++k) {
+        // chunks ramp up from chunk / 8, doubling: the first copy, which nothing
+        // overlaps, is short, and the later DMAs are long (per-copy overhead)
+        size_t want = std::max<size_t>(c->chunk / 8, 1);
+        for (uint64_t s0 = 0, pk = 0; s0 < n; s0 += pk, ++k) {
             const int s = (int)(k % (uint64_t)ns);
-            const uint64_t cnt = (n - s0) < per ? (n - s0) : per;
+            pk = std::min<uint64_t>(per_piece(want), per);
+            want = std::min(want * 2, c->chunk);
+            const uint64_t cnt = (n - s0) < pk ? (n - s0) : pk;
             const size_t bytes = piece_bytes(cnt);
             const uint8_t* src = (const uint8_t*)h_base + s0 * stride;
             if (c->slot_busy[s]) {   // the DMA (or kernel) that last read this slot: chunk k - nslots

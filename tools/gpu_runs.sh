@@ -203,12 +203,12 @@ gpu_r4_dma() {
 # GPU test, then the host leg first (default), last after the 64k batch, and last after all
 gpu_r4_onestream() {
 (
-  timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/r4_onestream_tests.log 2>&1; rc=$?
-  echo "tests rc=$rc"; grep -E "passed|failed" gpurun_out/r4_onestream_tests.log | tail -1; grep FAILED gpurun_out/r4_onestream_tests.log | head; ok_rc $rc || exit $rc
+  timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/${R4OS:-r4_onestream}_tests.log 2>&1; rc=$?
+  echo "tests rc=$rc"; grep -E "passed|failed" gpurun_out/${R4OS:-r4_onestream}_tests.log | tail -1; grep FAILED gpurun_out/${R4OS:-r4_onestream}_tests.log | head; ok_rc $rc || exit $rc
   for v in "first:--steps 50" "last64k:--steps 2 --warmup 1 --no-probe --host-path-last --other 64k" "lastall:--steps 50 --host-path-last"; do
     name=${v%%:*}; a=${v#*:}
-    timeout -k 10 400 python3 bench.py --no-cpu-baseline $a > gpurun_out/r4_onestream_$name.json 2>> gpurun_out/r4_onestream.err; rc=$?
-    echo "$name rc=$rc $(python3 -c "import json; D=json.load(open('gpurun_out/r4_onestream_$name.json')); d=D['host_path']; print(D['value'], {m: (d[m]['GiB/s'], d[m].get('copy_ms_per_step_rank0'), d[m].get('wait_ms_per_step_rank0'), d[m].get('raw_pinned_h2d_GiB/s'), d[m]['cpu_core_s_per_step_rank0']) for m in d})")"
+    timeout -k 10 400 python3 bench.py --no-cpu-baseline $a > gpurun_out/${R4OS:-r4_onestream}_$name.json 2>> gpurun_out/r4_onestream.err; rc=$?
+    echo "$name rc=$rc $(python3 -c "import json; D=json.load(open('gpurun_out/${R4OS:-r4_onestream}_$name.json')); d=D['host_path']; print(D['value'], {m: (d[m]['GiB/s'], d[m].get('copy_ms_per_step_rank0'), d[m].get('wait_ms_per_step_rank0'), d[m].get('raw_pinned_h2d_GiB/s'), d[m]['cpu_core_s_per_step_rank0']) for m in d})")"
     ok_rc $rc || exit $rc
   done
 )
