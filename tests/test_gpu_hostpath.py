@@ -167,3 +167,55 @@ def test_uniform_host_pinned_dma_chunks(dev, offset, stride, length):
             assert np.array_equal(ctx.batch_uniform(buf, stride, length, n, ss, offset=offset), want)
     finally:
         os.environ.pop("TCPCSUM_HOST_PINNED_DMA", None)
+
+
+@pytest.mark.parametrize("env", [{}, {"TCPCSUM_HOST_SLOTS": "3"}, {"TCPCSUM_HOST_DMA": "0"},
+                                 {"TCPCSUM_HOST_SLOTS": "4", "TCPCSUM_HOST_DMA": "0"}],
+                         ids=["default", "slots3", "nodma", "slots4_nodma"])
+def test_uniform_host_pageable_pipeline_variants(dev, env):
+    """Pageable input through the staging pipeline on the context's one stream: chunks ramp up
+    from scratch/8 (128 KiB here) to scratch (1 MiB), staged in 2-4 slots, each moved to HBM by
+    DMA (or read over PCIe with TCPCSUM_HOST_DMA=0) while the next is copied; a slot is refilled
+    only after the work that read it. Every segment matches the oracle, twice in a row."""
+    import os
+    import tcp_amd
+    rng = np.random.default_rng(len(env) * 11 + 5)
+    buf = rng.integers(0, 256, 6 << 20, dtype=np.uint8)
+    for offset, stride, length in [(3, 1501, 1499), (0, 64, 64), (16, 70000, 65536)]:
+        n = (buf.size - offset - length) // stride + 1
+        ss = rng.integers(0, 393211, n, dtype=np.uint32)
+        want = oracle.batch_uniform(buf, stride, length, n, ss, offset=offset)
+        old = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        try:
+            with tcp_amd.HostContext(0, scratch_bytes=1 << 20) as ctx:
+                for _ in range(2):
+                    assert np.array_equal(ctx.batch_uniform(buf, stride, length, n, ss, offset=offset), want)
+                assert ctx.stats()["bytes_staged"] > 0
+        finally:
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+
+
+@pytest.mark.parametrize("memory", ["pageable", "pinned"])
+def test_uniform_host_default_pieces_large(dev, memory):
+    """The default context on batches larger than its pieces: 300 MB pageable (staged chunks of
+    16, 32, 64, 128, 128 MiB ...) and 600 MB page-locked (DMA pieces of 256 MiB from the caller's
+    pages), 1500-B segments at an odd start, against the oracle."""
+    import tcp_amd
+    rng = np.random.default_rng(21 if memory == "pinned" else 22)
+    nbytes = (600 if memory == "pinned" else 300) * 1000 * 1000
+    buf = tcp_amd.pinned_empty(nbytes) if memory == "pinned" else np.empty(nbytes, np.uint8)
+    buf[:] = np.frombuffer(rng.bytes(nbytes), np.uint8)
+    offset, stride, length = 5, 1500, 1500
+    n = (nbytes - offset - length) // stride + 1
+    ss = rng.integers(0, 393211, n, dtype=np.uint32)
+    want = oracle.batch_uniform(buf, stride, length, n, ss, offset=offset)
+    with tcp_amd.HostContext(0) as ctx:
+        got = ctx.batch_uniform(buf, stride, length, n, ss, offset=offset)
+        staged = ctx.stats()["bytes_staged"]
+    assert np.array_equal(got, want)
+    assert (staged == 0) if memory == "pinned" else (staged >= n * length)
