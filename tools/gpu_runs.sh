@@ -214,6 +214,21 @@ gpu_r4_onestream() {
 )
 }
 
+# round 4: DMA piece size for page-locked uniform batches (HBM the context holds), and the
+# pageable chunk cap, interleaved twice — host leg only
+gpu_r4_pieces() {
+(
+  for rep in 1 2; do
+    for cfg in "256 128" "1024 128" "512 256"; do
+      set -- $cfg
+      TCPCSUM_HOST_DMA_CHUNK_MB=$1 TCPCSUM_HOST_CHUNK_MB=$2 timeout -k 10 200 python3 bench.py --host-path-only --host-steps 10 > gpurun_out/r4_pieces_$1_$2_rep$rep.json 2>> gpurun_out/r4_pieces.err; rc=$?
+      echo "dma=$1 chunk=$2 rep=$rep rc=$rc $(python3 -c "import json; d=json.load(open('gpurun_out/r4_pieces_$1_$2_rep$rep.json'))['host_path']; print({m: (d[m]['GiB/s'], d[m].get('raw_pinned_h2d_GiB/s'), d[m]['cpu_core_s_per_step_rank0']) for m in d})")"
+      ok_rc $rc || exit $rc
+    done
+  done
+)
+}
+
 # round 3: wire FILL line store (default) — every GPU test first, then the A/B timing three
 # times (the two FILL stores must agree byte for byte every time)
 gpu_r3_fill() {
