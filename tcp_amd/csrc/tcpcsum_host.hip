@@ -8,13 +8,18 @@
 // Which host memory a kernel touches, and how:
 //   * memory its owner page-locked — tcpcsum_host_alloc / hipHostMalloc, or a
 //     hipHostRegister of the application's own — is read in place by the
-//     kernel over PCIe (zero-copy), and FILL stores the checks there;
+//     kernel over PCIe (zero-copy), and FILL stores the checks there; a bulk
+//     uniform batch (32 MiB or more) is DMA'd to HBM from those pages instead;
 //   * pageable memory is never page-locked and never handed to a HIP copy.
 //     CPU threads copy its bytes into the context's own pinned staging —
-//     uniform batches chunk by chunk, wire batches packet by packet (only the
-//     packets, not the slack between them) — which the kernel reads over PCIe;
-//     FILL results go back as 2-byte CPU stores at TCP+16 (and IP+10), exactly
-//     where context.c:208 puts them.
+//     uniform batches chunk by chunk (then DMA'd to HBM), wire batches packet
+//     by packet (only the packets, not the slack between them, read by the
+//     kernel over PCIe); FILL results go back as 2-byte CPU stores at TCP+16
+//     (and IP+10), exactly where context.c:208 puts them.
+//
+// Every copy and launch of a context goes to its one stream: host-to-HBM copies
+// alternating over two streams fell to 43.5 GiB/s in some process states, one
+// stream holds 51-53 (tools/dma_state_probe.hip).
 //
 // The library page-locks only memory it allocates itself (round 4). Rounds 2
 // and 3 page-locked pageable heap memory — per call (round 2), then on request

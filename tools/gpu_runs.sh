@@ -229,6 +229,25 @@ gpu_r4_pieces() {
 )
 }
 
+# round 4, last: the final rehearsal at HEAD plus the seam's default and pinned-pool latency /
+# core-us beside the reference's one-core checksum
+gpu_r4_final2() {
+(
+  gpu_r4_final || exit $?
+  O=gpurun_out/r4final
+  for v in "cpu:cpu:" "staged:gpu:" "pinned:gpu:pinned"; do
+    IFS=: read name mode extra <<< "$v"
+    if [ $mode = gpu ]; then
+      env -u TCPCSUM_PRELOAD_TX LD_PRELOAD=$PWD/tcp_amd/libtcpcsum_preload.so TCPCSUM_PRELOAD_ANY_SOCKET=1 TCPCSUM_PRELOAD_TX=fill \
+        timeout -k 10 120 tools/mmsg_bench gpu 300 $extra > $O/seam_$name.json 2> $O/seam_$name.err; rc=$?
+    else
+      timeout -k 10 120 tools/mmsg_bench cpu 300 > $O/seam_$name.json 2> $O/seam_$name.err; rc=$?
+    fi
+    echo "seam $name rc=$rc $(cat $O/seam_$name.json)"; ok_rc $rc || exit $rc
+  done
+)
+}
+
 # round 3: wire FILL line store (default) — every GPU test first, then the A/B timing three
 # times (the two FILL stores must agree byte for byte every time)
 gpu_r3_fill() {
