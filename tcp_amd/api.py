@@ -427,9 +427,10 @@ def pinned_empty(nbytes: int, dtype=np.uint8) -> np.ndarray:
 
 
 class HostContext:
-    """tcpcsum_ctx_t: host-memory batches, synchronous. Memory its owner page-locked (pinned_empty /
-    tcpcsum_host_alloc) is read in place; pageable memory is copied into the context's pinned staging
-    and never page-locked. ``blocking_wait`` (TCPCSUM_CTX_BLOCKING_WAIT): sleep, not spin, while the
+    """tcpcsum_ctx_t: host-memory batches, synchronous, on one stream. Memory its owner page-locked
+    (pinned_empty / tcpcsum_host_alloc) is read in place (a uniform batch of 32 MiB or more: DMA'd to
+    HBM from those pages in 256 MiB pieces); pageable memory is copied into the context's pinned
+    staging and never page-locked. ``blocking_wait`` (TCPCSUM_CTX_BLOCKING_WAIT): sleep, not spin, while the
     device works."""
 
     def __init__(self, device: int = 0, scratch_bytes: int = 0, blocking_wait: bool = False):
