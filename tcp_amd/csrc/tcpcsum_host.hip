@@ -234,6 +234,19 @@ struct tcpcsum_ctx {
 
 namespace {
 
+// A host call that returns early on an error may have queued copies and kernels
+// that still read or write the caller's memory: drain the stream before the
+// caller gets control back (and may free that memory). Disarmed once the call
+// has waited for its work.
+struct DrainOnError {
+    hipStream_t st;
+    bool done = false;
+    explicit DrainOnError(hipStream_t s) : st(s) {}
+    ~DrainOnError() {
+        if (!done && st) (void)hipStreamSynchronize(st);
+    }
+};
+
 struct DeviceGuard {
     int prev = -1;
     explicit DeviceGuard(int dev) {
@@ -677,6 +690,7 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t st
     std::lock_guard<std::mutex> lk(c->mu);
     CallerCpu cpu(c);
     DeviceGuard g(c->device);
+    DrainOnError drain(c->st);
     const tcpcsum::Tuning tu = c->tune;
     c->stats.batches++;
     hipError_t e;
@@ -728,6 +742,7 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t st
         if (rc) return rc;
         e = wait_stream(c, c->st, expect_ns(span));
         if (e != hipSuccess) return hip_fail(e);
+        drain.done = true;
     } else if (zb) {   // page-locked, large: DMA from the caller's pages, every piece queued at once
         const uint64_t dper = per_piece(c->dma_chunk);
         e = ensure_hbm(piece_bytes(dper));
@@ -745,6 +760,7 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t st
         }
         e = wait_stream(c, c->st, expect_ns(span));
         if (e != hipSuccess) return hip_fail(e);
+        drain.done = true;
     } else {
         const int ns = c->nslots;
         const size_t slot_bytes = piece_bytes(per) + 16;
@@ -800,6 +816,7 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t st
         for (int i = 0; i < 4; ++i) c->slot_busy[i] = false;
         e = wait_stream(c, c->st, expect_ns(std::min<uint64_t>(span, slot_bytes)));
         if (e != hipSuccess) return hip_fail(e);
+        drain.done = true;
     }
     if (out_staged) par_copy(c, h_out, c->res.h, n * sizeof(uint16_t));
     return TCPCSUM_OK;
@@ -825,6 +842,7 @@ int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t* c, void* h_pkts, size_t region_bytes,
     CallerCpu cpu(c);
     DeviceGuard g(c->device);
     hipStream_t st = c->st;
+    DrainOnError drain(st);
     c->stats.batches++;
     int rc = ensure_pkt_arrays(c, n);
     if (rc) return rc;
@@ -870,6 +888,7 @@ int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t* c, void* h_pkts, size_t region_bytes,
     if (rc) return rc;
     e = wait_stream(c, st, expect_ns(std::min<uint64_t>((uint64_t)n * std::min<uint64_t>(cap, 1500u), region_bytes)));
     if (e != hipSuccess) return hip_fail(e);
+    drain.done = true;
     if (fill && !c->g_idx.empty())
         write_back_checks(c, zst ? h_status : c->p_stat.h, (mode & TCPCSUM_IPV4_IPHDR) != 0);
     if (h_out && !zout) memcpy(h_out, c->p_out.h, n * sizeof(uint16_t));
@@ -890,6 +909,7 @@ int tcpcsum_ipv4_batch_ptrs_host(tcpcsum_ctx_t* c, void* const* h_pkts, const ui
     CallerCpu cpu(c);
     DeviceGuard g(c->device);
     hipStream_t st = c->st;
+    DrainOnError drain(st);
     c->stats.batches++;
     int rc = ensure_pkt_arrays(c, n);
     if (rc) return rc;
@@ -938,6 +958,7 @@ int tcpcsum_ipv4_batch_ptrs_host(tcpcsum_ctx_t* c, void* const* h_pkts, const ui
     if (rc) return rc;
     hipError_t e = wait_stream(c, st, expect_ns(foot + c->stats.bytes_staged - staged_before));
     if (e != hipSuccess) return hip_fail(e);
+    drain.done = true;
     if ((mode & TCPCSUM_IPV4_VERIFY) == 0 && !c->g_idx.empty())
         write_back_checks(c, zst ? h_status : c->p_stat.h, (mode & TCPCSUM_IPV4_IPHDR) != 0);
     if (h_out && !zout) memcpy(h_out, c->p_out.h, n * sizeof(uint16_t));
