@@ -228,6 +228,7 @@ struct tcpcsum_ctx {
     bool stage_one_pass = true;   // wire staging laid out by bounds, one pass (TCPCSUM_HOST_STAGE_PASSES=2: by lengths)
     bool uniform_dma = true;   // staged uniform chunks go to HBM by DMA (TCPCSUM_HOST_DMA=0: kernel reads them over PCIe)
     bool pinned_dma = true;    // large page-locked uniform batches go to HBM by DMA (TCPCSUM_HOST_PINNED_DMA=0: in place)
+    bool slot_sleep = true;    // BLOCKING_WAIT also sleeps in staging-slot waits (TCPCSUM_HOST_SLOT_SLEEP=0: spin)
     tcpcsum_ctx_stats_t stats{};
     std::mutex mu;
 };
@@ -296,12 +297,40 @@ void par_copy(tcpcsum_ctx* c, void* dst, const void* src, size_t n, bool nt = fa
     c->stats.ns_copy += tcpcsum::now_ns() - t0;
 }
 
+// Sleep until ev has completed: a first nap of nap_ns, then a poll every
+// c->poll_ns, doubling up to max_step_ns (1 us timer slack on this thread while
+// it sleeps, restored after).
+hipError_t sleep_on_event(tcpcsum_ctx* c, hipEvent_t ev, uint64_t nap_ns, uint64_t max_step_ns) {
+    const int slack = prctl(PR_GET_TIMERSLACK, 0, 0, 0, 0);
+    bool slack_set = false;
+    uint64_t step = std::min<uint64_t>(c->poll_ns, max_step_ns);
+    hipError_t e;
+    for (;;) {
+        e = hipEventQuery(ev);
+        if (e != hipErrorNotReady) break;
+        (void)hipGetLastError();   // not ready is not an error for us
+        if (!slack_set && slack > 0) {
+            prctl(PR_SET_TIMERSLACK, 1000, 0, 0, 0);
+            slack_set = true;
+        }
+        uint64_t ns = nap_ns;
+        if (!ns) {
+            ns = step;
+            step = std::min<uint64_t>(step * 2, max_step_ns);
+        }
+        nap_ns = 0;
+        timespec ts{(time_t)(ns / 1000000000u), (long)(ns % 1000000000u)};
+        nanosleep(&ts, nullptr);
+    }
+    if (slack_set) prctl(PR_SET_TIMERSLACK, (unsigned long)slack, 0, 0, 0);
+    return e;
+}
+
 // Wait for everything queued on st, timed into stats.ns_wait: hipStreamSynchronize
 // (HIP spins: the waiting thread burns a core for the kernel's whole length), or
 // with TCPCSUM_CTX_BLOCKING_WAIT a poll of the stream's completion event between
 // sleeps — first for 3/4 of expect_ns (what the queued work should take: the
-// caller's estimate from its bytes), then every poll_ns, doubling up to 100 us
-// (1 us timer slack on this thread for the wait, restored after). A
+// caller's estimate from its bytes), then every poll_ns, doubling up to 100 us. A
 // hipEventBlockingSync event did not help: the runtime waits on its signal
 // actively for about a batch kernel's length, and the thread used as much CPU as
 // with hipStreamSynchronize (48.7 vs 48.5 us per 1024-packet in-place batch,
@@ -311,33 +340,23 @@ hipError_t wait_stream(tcpcsum_ctx* c, hipStream_t st, uint64_t expect_ns) {
     hipError_t e;
     if (c->flags & TCPCSUM_CTX_BLOCKING_WAIT) {
         e = hipEventRecord(c->done_ev, st);
-        const int slack = prctl(PR_GET_TIMERSLACK, 0, 0, 0, 0);
-        bool slack_set = false;
-        uint64_t nap = expect_ns - expect_ns / 4;
-        if (nap > 50000000u) nap = 50000000u;
-        uint64_t step = c->poll_ns;
-        while (e == hipSuccess) {
-            e = hipEventQuery(c->done_ev);
-            if (e != hipErrorNotReady) break;
-            (void)hipGetLastError();   // not ready is not an error for us
-            e = hipSuccess;
-            if (!slack_set && slack > 0) {
-                prctl(PR_SET_TIMERSLACK, 1000, 0, 0, 0);
-                slack_set = true;
-            }
-            uint64_t ns = nap;
-            if (!ns) {
-                ns = step;
-                step = std::min<uint64_t>(step * 2, 100000u);
-            }
-            nap = 0;
-            timespec ts{(time_t)(ns / 1000000000u), (long)(ns % 1000000000u)};
-            nanosleep(&ts, nullptr);
-        }
-        if (slack_set) prctl(PR_SET_TIMERSLACK, (unsigned long)slack, 0, 0, 0);
+        if (e == hipSuccess)
+            e = sleep_on_event(c, c->done_ev, std::min<uint64_t>(expect_ns - expect_ns / 4, 50000000u), 100000u);
     } else {
         e = hipStreamSynchronize(st);
     }
+    c->stats.ns_wait += tcpcsum::now_ns() - t0;
+    return e;
+}
+
+// Wait for a staging slot's event (the DMA that last read the slot), timed into
+// stats.ns_wait: spinning in hipEventSynchronize, or with
+// TCPCSUM_CTX_BLOCKING_WAIT polling between sleeps of at most 20 us (no first
+// nap: how much of that DMA is left when the copy threads get here varies).
+hipError_t wait_slot(tcpcsum_ctx* c, hipEvent_t ev) {
+    const uint64_t t0 = tcpcsum::now_ns();
+    const hipError_t e = ((c->flags & TCPCSUM_CTX_BLOCKING_WAIT) && c->slot_sleep) ? sleep_on_event(c, ev, 0, 20000u)
+                                                                                   : hipEventSynchronize(ev);
     c->stats.ns_wait += tcpcsum::now_ns() - t0;
     return e;
 }
@@ -588,6 +607,7 @@ int tcpcsum_ctx_create(int device, size_t scratch_bytes, tcpcsum_ctx_t** out) {
     c->stage_one_pass = tcpcsum::env_int("TCPCSUM_HOST_STAGE_PASSES", 1) == 1;
     c->uniform_dma = tcpcsum::env_int("TCPCSUM_HOST_DMA", 1) != 0;
     c->pinned_dma = tcpcsum::env_int("TCPCSUM_HOST_PINNED_DMA", 1) != 0;
+    c->slot_sleep = tcpcsum::env_int("TCPCSUM_HOST_SLOT_SLEEP", 1) != 0;
     c->stage_blocks = std::max(1, std::min(16, tcpcsum::env_int("TCPCSUM_HOST_STAGE_BLOCKS", 1)));
     c->nslots = std::max(2, std::min(4, tcpcsum::env_int("TCPCSUM_HOST_SLOTS", 2)));
     c->dma_chunk = scratch_bytes ? scratch_bytes : kDefaultDmaChunk;
@@ -785,9 +805,7 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t st
             const uint8_t* src = (const uint8_t*)h_base + s0 * stride;
             if (c->slot_busy[s]) {   // the DMA (or kernel) that last read this slot: chunk k - nslots
                 c->slot_busy[s] = false;
-                const uint64_t t0 = tcpcsum::now_ns();
-                e = hipEventSynchronize(c->slot_ev[s]);
-                c->stats.ns_wait += tcpcsum::now_ns() - t0;
+                e = wait_slot(c, c->slot_ev[s]);
                 if (e != hipSuccess) return hip_fail(e);
             }
             // keep the start's alignment mod 16, so the kernel shape matches what the

@@ -248,6 +248,20 @@ gpu_r4_final2() {
 )
 }
 
+# round 4: staging-slot waits sleeping (default with the blocking wait) vs spinning, host leg
+# only, interleaved four times
+gpu_r4_slotwait() {
+(
+  for rep in 1 2 3 4; do
+    for sl in 1 0; do
+      TCPCSUM_HOST_SLOT_SLEEP=$sl timeout -k 10 200 python3 bench.py --host-path-only --host-steps 10 > gpurun_out/r4_slotwait_s${sl}_rep$rep.json 2>> gpurun_out/r4_slotwait.err; rc=$?
+      echo "sleep=$sl rep=$rep rc=$rc $(python3 -c "import json; d=json.load(open('gpurun_out/r4_slotwait_s${sl}_rep$rep.json'))['host_path']['pageable']; print(d['GiB/s'], d['cpu_core_s_per_step_rank0'], d['copy_ms_per_step_rank0'], d['wait_ms_per_step_rank0'])")"
+      ok_rc $rc || exit $rc
+    done
+  done
+)
+}
+
 # round 3: wire FILL line store (default) — every GPU test first, then the A/B timing three
 # times (the two FILL stores must agree byte for byte every time)
 gpu_r3_fill() {
