@@ -229,7 +229,8 @@ int tcpcsum_tx_build_dev(const void *d_payload, const tcpcsum_txseg_t *d_segs, u
  * (raw-socket buffers). A context owns one device, one stream, pinned
  * staging and a few host copy threads (TCPCSUM_HOST_THREADS, default half the
  * CPUs the process may use, at most 8; a staged wire batch of up to 8 MiB
- * copies on TCPCSUM_HOST_WIRE_THREADS of them, default 1 = the calling thread).
+ * copies on TCPCSUM_HOST_WIRE_THREADS of them, default 1 = the calling thread,
+ * a bulk uniform copy on TCPCSUM_HOST_BULK_THREADS, default 4).
  * Host memory is used one of two ways:
  *   - memory its owner page-locked (tcpcsum_host_alloc / hipHostMalloc, or the
  *     application's own hipHostRegister) is read — FILL: written — in place by

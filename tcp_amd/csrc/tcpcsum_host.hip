@@ -218,6 +218,12 @@ struct tcpcsum_ctx {
     // threads a staged wire batch copies on, the caller included (TCPCSUM_HOST_WIRE_THREADS):
     // a releaseSend batch is ~1.5 MB, where extra threads cost more CPU than they save time
     int wire_threads = 1;
+    // threads a bulk copy (uniform staging chunks, per-segment arrays) runs on, the caller
+    // included (TCPCSUM_HOST_BULK_THREADS, default 4; 0 = every copy thread): the DMA to
+    // HBM bounds the pageable pipeline, and 4 threads copy 1.5 GB in ~14.5 ms beside its
+    // ~28 ms at the rate 8 reach, with 0.060 instead of 0.087 core-s
+    // (profiles/r04_host_bulk_threads_ab.jsonl)
+    int bulk_threads = 4;
     int stage_threads = 1;   // the current staged batch's: wire_threads, or all for a large batch
     int stage_blocks = 1;    // a small single-threaded staged batch copied and launched in this many blocks
     // TCPCSUM_CTX_BLOCKING_WAIT: wait for the device by polling this event between
@@ -291,9 +297,10 @@ void par_copy(tcpcsum_ctx* c, void* dst, const void* src, size_t n, bool nt = fa
     const uint8_t* s = (const uint8_t*)src;
     const uint64_t t0 = tcpcsum::now_ns();
     if (nt)
-        c->pool->run(n, kGrain, [&](size_t lo, size_t hi) { tcpcsum::copy_nt(d + lo, s + lo, hi - lo); });
+        c->pool->run(n, kGrain, [&](size_t lo, size_t hi) { tcpcsum::copy_nt(d + lo, s + lo, hi - lo); },
+                     c->bulk_threads);
     else
-        c->pool->run(n, kGrain, [&](size_t lo, size_t hi) { memcpy(d + lo, s + lo, hi - lo); });
+        c->pool->run(n, kGrain, [&](size_t lo, size_t hi) { memcpy(d + lo, s + lo, hi - lo); }, c->bulk_threads);
     c->stats.ns_copy += tcpcsum::now_ns() - t0;
 }
 
@@ -601,7 +608,8 @@ int tcpcsum_ctx_create(int device, size_t scratch_bytes, tcpcsum_ctx_t** out) {
     }
     c->wire_threads = std::max(1, std::min(c->pool->threads(), tcpcsum::env_int("TCPCSUM_HOST_WIRE_THREADS", 1)));
     c->stats.copy_threads = (uint64_t)c->wire_threads;
-    c->stats.bulk_threads = (uint64_t)c->pool->threads();
+    c->bulk_threads = std::max(0, std::min(c->pool->threads(), tcpcsum::env_int("TCPCSUM_HOST_BULK_THREADS", 4)));
+    c->stats.bulk_threads = (uint64_t)(c->bulk_threads ? c->bulk_threads : c->pool->threads());
     c->nt_copy = tcpcsum::env_int("TCPCSUM_HOST_NT", 1) != 0;
     c->poll_ns = (uint64_t)std::max(1, tcpcsum::env_int("TCPCSUM_HOST_POLL_US", 5)) * 1000u;
     c->stage_one_pass = tcpcsum::env_int("TCPCSUM_HOST_STAGE_PASSES", 1) == 1;

@@ -262,6 +262,20 @@ gpu_r4_slotwait() {
 )
 }
 
+# round 4: how many threads the pageable uniform path copies on (the DMA, not the copy, is
+# the bound), host leg only, interleaved twice
+gpu_r4_bulk() {
+(
+  for rep in 1 2; do
+    for t in 2 3 4 0; do
+      TCPCSUM_HOST_BULK_THREADS=$t timeout -k 10 200 python3 bench.py --host-path-only --host-steps 10 > gpurun_out/r4_bulk_t${t}_rep$rep.json 2>> gpurun_out/r4_bulk.err; rc=$?
+      echo "threads=$t rep=$rep rc=$rc $(python3 -c "import json; d=json.load(open('gpurun_out/r4_bulk_t${t}_rep$rep.json'))['host_path']['pageable']; print(d['GiB/s'], d['cpu_core_s_per_step_rank0'], d['copy_ms_per_step_rank0'], d['wait_ms_per_step_rank0'], d['copy_threads'])")"
+      ok_rc $rc || exit $rc
+    done
+  done
+)
+}
+
 # round 3: wire FILL line store (default) — every GPU test first, then the A/B timing three
 # times (the two FILL stores must agree byte for byte every time)
 gpu_r3_fill() {
