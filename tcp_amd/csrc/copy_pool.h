@@ -235,7 +235,15 @@ inline bool numa_node_cpus(const char* device_pci_bus, cpu_set_t* out, int* node
 // destination lines into the cache (read-for-ownership) nor evict the source
 // stream's own working set. Ends with sfence: streaming stores are weakly
 // ordered, and the piece must be globally visible before the launch.
+inline void copy_stream(uint8_t* d, const uint8_t* s, size_t n);
 inline void copy_nt(uint8_t* d, const uint8_t* s, size_t n) {
+    copy_stream(d, s, n);
+    _mm_sfence();
+}
+
+// copy_nt without the closing sfence, for a thread that copies many pieces and
+// fences once after the last.
+inline void copy_stream(uint8_t* d, const uint8_t* s, size_t n) {
     size_t h = (16u - ((uintptr_t)d & 15u)) & 15u;
     if (h > n) h = n;
     memcpy(d, s, h);
@@ -254,7 +262,6 @@ inline void copy_nt(uint8_t* d, const uint8_t* s, size_t n) {
         _mm_stream_si128((__m128i*)(d + i + 48), e);
     }
     memcpy(d + k, s + k, n - k);
-    _mm_sfence();
 }
 
 }  // namespace tcpcsum

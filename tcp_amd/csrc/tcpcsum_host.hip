@@ -234,7 +234,12 @@ struct tcpcsum_ctx {
     bool stage_one_pass = true;   // wire staging laid out by bounds, one pass (TCPCSUM_HOST_STAGE_PASSES=2: by lengths)
     bool uniform_dma = true;   // staged uniform chunks go to HBM by DMA (TCPCSUM_HOST_DMA=0: kernel reads them over PCIe)
     bool pinned_dma = true;    // large page-locked uniform batches go to HBM by DMA (TCPCSUM_HOST_PINNED_DMA=0: in place)
-    bool slot_sleep = true;    // BLOCKING_WAIT also sleeps in staging-slot waits (TCPCSUM_HOST_SLOT_SLEEP=0: spin)
+    bool slot_sleep = true;
+    // wire staging with streaming stores, each packet from a 64-B line of its own, one
+    // fence per copy job (TCPCSUM_HOST_WIRE_NT=0: plain memcpy from 16-B starts). The
+    // seam's 1024 x 1500-B batch: 102-112 instead of 119-171 us, 65-75 instead of
+    // 72-102 core-us (profiles/r04_wire_nt_ab.jsonl)
+    bool wire_nt = true;    // BLOCKING_WAIT also sleeps in staging-slot waits (TCPCSUM_HOST_SLOT_SLEEP=0: spin)
     tcpcsum_ctx_stats_t stats{};
     std::mutex mu;
 };
@@ -422,10 +427,11 @@ int stage_packets(tcpcsum_ctx* c, uint64_t* k_off, uint32_t* k_len, size_t* stag
     *staged_bytes = 0;
     if (!m) return TCPCSUM_OK;
     const uint64_t t0 = tcpcsum::now_ns();
+    const size_t am = c->wire_nt ? 63u : 15u;   // each packet's staging start: 64-B line or 16 B
     size_t span = 0;
     for (size_t k = 0; k < m; ++k) {
         c->g_off[k] = span;
-        span += ((size_t)c->g_len[k] + 15u) & ~(size_t)15u;
+        span += ((size_t)c->g_len[k] + am) & ~am;
     }
     const bool by_bound = span <= kStageByBound && c->stage_one_pass;
     // small (releaseSend-sized) batches copy on wire_threads; large ones on every copy thread
@@ -437,7 +443,7 @@ int stage_packets(tcpcsum_ctx* c, uint64_t* k_off, uint32_t* k_len, size_t* stag
         span = 0;
         for (size_t k = 0; k < m; ++k) {
             c->g_off[k] = span;
-            span += ((size_t)c->g_len[k] + 15u) & ~(size_t)15u;
+            span += ((size_t)c->g_len[k] + am) & ~am;
         }
     }
     hipError_t e = c->gath.ensure(span ? span : 16);
@@ -452,15 +458,18 @@ int stage_packets(tcpcsum_ctx* c, uint64_t* k_off, uint32_t* k_len, size_t* stag
         size_t b = 0;
         for (size_t k = lo; k < hi; ++k) {
             if (by_bound) c->g_len[k] = copy_len(c->g_src[k], c->g_len[k]);
-            // plain memcpy: streaming stores (copy_nt, with its sfence per packet) made a
-            // 1024 x 1500-B staged batch 4.6 x slower on one thread (618 vs 135 us,
-            // profiles/r04_e2e_first.jsonl) — they pay off only for the uniform path's
-            // 256 KiB pieces
-            memcpy(gh + c->g_off[k], c->g_src[k], c->g_len[k]);
+            // streaming stores from 64-B starts, fenced once per job: with an sfence per
+            // packet and 16-B starts (copy_nt) they had made a 1024 x 1500-B staged batch
+            // 4.6 x slower on one thread (618 vs 135 us, profiles/r04_e2e_first.jsonl)
+            if (c->wire_nt)
+                tcpcsum::copy_stream(gh + c->g_off[k], c->g_src[k], c->g_len[k]);
+            else
+                memcpy(gh + c->g_off[k], c->g_src[k], c->g_len[k]);
             k_off[c->g_idx[k]] = (uint64_t)(uintptr_t)(gd + c->g_off[k]);
             k_len[c->g_idx[k]] = c->g_len[k];
             b += c->g_len[k];
         }
+        if (c->wire_nt) _mm_sfence();   // this thread's streaming stores, before the launch
         copied.fetch_add(b, std::memory_order_relaxed);
     }, c->stage_threads);
     c->stats.ns_copy += tcpcsum::now_ns() - t0;
@@ -616,6 +625,7 @@ int tcpcsum_ctx_create(int device, size_t scratch_bytes, tcpcsum_ctx_t** out) {
     c->uniform_dma = tcpcsum::env_int("TCPCSUM_HOST_DMA", 1) != 0;
     c->pinned_dma = tcpcsum::env_int("TCPCSUM_HOST_PINNED_DMA", 1) != 0;
     c->slot_sleep = tcpcsum::env_int("TCPCSUM_HOST_SLOT_SLEEP", 1) != 0;
+    c->wire_nt = tcpcsum::env_int("TCPCSUM_HOST_WIRE_NT", 1) != 0;
     c->stage_blocks = std::max(1, std::min(16, tcpcsum::env_int("TCPCSUM_HOST_STAGE_BLOCKS", 1)));
     c->nslots = std::max(2, std::min(4, tcpcsum::env_int("TCPCSUM_HOST_SLOTS", 2)));
     c->dma_chunk = scratch_bytes ? scratch_bytes : kDefaultDmaChunk;

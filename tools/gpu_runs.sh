@@ -276,6 +276,23 @@ gpu_r4_bulk() {
 )
 }
 
+# round 4: staged wire batches through the sendmmsg seam with plain memcpy (default) vs
+# streaming stores from 64-B starts (TCPCSUM_HOST_WIRE_NT=1), interleaved four times; the
+# seam tests with the streaming variant first
+gpu_r4_wirent() {
+(
+  TCPCSUM_HOST_WIRE_NT=1 timeout -k 10 300 python -u -m pytest tests/test_seam.py tests/test_gpu_ptrs.py tests/test_plumbing.py -q --timeout 120 --timeout-method thread > gpurun_out/r4_wirent_tests.log 2>&1; rc=$?
+  echo "tests(nt) rc=$rc"; grep -E "passed|failed" gpurun_out/r4_wirent_tests.log | tail -1; [ $rc -eq 0 ] || exit $rc
+  for rep in 1 2 3 4; do
+    for nt in 0 1; do
+      env LD_PRELOAD=$PWD/tcp_amd/libtcpcsum_preload.so TCPCSUM_PRELOAD_ANY_SOCKET=1 TCPCSUM_PRELOAD_TX=fill TCPCSUM_HOST_WIRE_NT=$nt \
+        timeout -k 10 120 tools/mmsg_bench gpu 300 > gpurun_out/r4_wirent_nt${nt}_rep$rep.json 2>> gpurun_out/r4_wirent.err; rc=$?
+      echo "nt=$nt rep=$rep rc=$rc $(cat gpurun_out/r4_wirent_nt${nt}_rep$rep.json)"; [ $rc -eq 0 ] || exit $rc
+    done
+  done
+)
+}
+
 # round 3: wire FILL line store (default) — every GPU test first, then the A/B timing three
 # times (the two FILL stores must agree byte for byte every time)
 gpu_r3_fill() {
