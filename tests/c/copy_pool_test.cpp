@@ -59,19 +59,24 @@ int main() {
             for (size_t i = lo; i < hi; ++i) out[i] = (uint32_t)(i * 2654435761u);
         });
         for (size_t i = 0; i < out.size(); ++i) EXPECT(out[i] == (uint32_t)(i * 2654435761u));
-        // the streaming-store copy, every head / tail alignment
+        // the streaming-store copy, every destination head / tail alignment, source at
+        // an aligned and an odd offset (wire staging: 64-B destination starts, packets
+        // anywhere in the caller's buffers)
         std::vector<uint8_t> src(4096 + 64), dst(4096 + 64);
         for (size_t i = 0; i < src.size(); ++i) src[i] = (uint8_t)(i * 7 + 3);
-        for (size_t a = 0; a < 16; ++a)
-            for (size_t len : {(size_t)0, (size_t)1, (size_t)63, (size_t)64, (size_t)65, (size_t)1500, (size_t)4000}) {
-                std::fill(dst.begin(), dst.end(), 0);
-                pool.run(len, 256, [&](size_t lo, size_t hi) {
-                    tcpcsum::copy_nt(dst.data() + a + lo, src.data() + lo, hi - lo);
-                });
-                EXPECT(std::equal(src.begin(), src.begin() + len, dst.begin() + a));
-                EXPECT(std::all_of(dst.begin(), dst.begin() + a, [](uint8_t v) { return v == 0; }));
-                EXPECT(std::all_of(dst.begin() + a + len, dst.end(), [](uint8_t v) { return v == 0; }));
-            }
+        for (size_t b : {(size_t)0, (size_t)5})
+            for (size_t a = 0; a < 16; ++a)
+                for (size_t len : {(size_t)0, (size_t)1, (size_t)63, (size_t)64, (size_t)65, (size_t)1500, (size_t)4000}) {
+                    std::fill(dst.begin(), dst.end(), 0);
+                    pool.run(len, 256, [&](size_t lo, size_t hi) {
+                        if (lo & 1024) tcpcsum::copy_nt(dst.data() + a + lo, src.data() + b + lo, hi - lo);
+                        else tcpcsum::copy_stream(dst.data() + a + lo, src.data() + b + lo, hi - lo);
+                        _mm_sfence();
+                    });
+                    EXPECT(std::equal(src.begin() + b, src.begin() + b + len, dst.begin() + a));
+                    EXPECT(std::all_of(dst.begin(), dst.begin() + a, [](uint8_t v) { return v == 0; }));
+                    EXPECT(std::all_of(dst.begin() + a + len, dst.end(), [](uint8_t v) { return v == 0; }));
+                }
     }   // teardown with idle workers
     {
         tcpcsum::CopyPool unused(4, 0);   // workers never started
