@@ -295,17 +295,19 @@ void* pinned_dev_ptr(const void* p, size_t bytes = 1) {
     return a.devicePointer;
 }
 
-// memcpy on the context's copy threads (pieces of 256 KiB); nt: streaming stores.
-void par_copy(tcpcsum_ctx* c, void* dst, const void* src, size_t n, bool nt = false) {
+// memcpy on the context's copy threads (pieces of 256 KiB); nt: streaming stores;
+// threads: how many take part, the caller included (-1: bulk_threads, 0: all).
+void par_copy(tcpcsum_ctx* c, void* dst, const void* src, size_t n, bool nt = false, int threads = -1) {
+    if (threads < 0) threads = c->bulk_threads;
     constexpr size_t kGrain = 256u << 10;
     uint8_t* d = (uint8_t*)dst;
     const uint8_t* s = (const uint8_t*)src;
     const uint64_t t0 = tcpcsum::now_ns();
     if (nt)
         c->pool->run(n, kGrain, [&](size_t lo, size_t hi) { tcpcsum::copy_nt(d + lo, s + lo, hi - lo); },
-                     c->bulk_threads);
+                     threads);
     else
-        c->pool->run(n, kGrain, [&](size_t lo, size_t hi) { memcpy(d + lo, s + lo, hi - lo); }, c->bulk_threads);
+        c->pool->run(n, kGrain, [&](size_t lo, size_t hi) { memcpy(d + lo, s + lo, hi - lo); }, threads);
     c->stats.ns_copy += tcpcsum::now_ns() - t0;
 }
 
@@ -814,6 +816,11 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t st
         // chunks ramp up from chunk / 8, doubling: the first copy, which nothing
         // overlaps, is short, and the later DMAs are long (per-copy overhead)
         size_t want = std::max<size_t>(c->chunk / 8, 1);
+        // bulk_threads copy while the DMA is the bound; once a full chunk's DMA has
+        // finished before the threads come back for its slot, the copy is the bound
+        // (a slow host, or few threads): every copy thread from then on
+        int copy_threads = c->bulk_threads;
+        bool slot_full[4] = {false, false, false, false};
         for (uint64_t s0 = 0, pk = 0; s0 < n; s0 += pk, ++k) {
             const int s = (int)(k % (uint64_t)ns);
             pk = std::min<uint64_t>(per_piece(want), per);
@@ -823,13 +830,18 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t st
             const uint8_t* src = (const uint8_t*)h_base + s0 * stride;
             if (c->slot_busy[s]) {   // the DMA (or kernel) that last read this slot: chunk k - nslots
                 c->slot_busy[s] = false;
+                if (copy_threads != 0 && slot_full[s] && pk == per) {
+                    if (hipEventQuery(c->slot_ev[s]) == hipSuccess) copy_threads = 0;
+                    else (void)hipGetLastError();   // not ready: the DMA is still the bound
+                }
                 e = wait_slot(c, c->slot_ev[s]);
                 if (e != hipSuccess) return hip_fail(e);
             }
+            slot_full[s] = pk == per;
             // keep the start's alignment mod 16, so the kernel shape matches what the
             // same batch gets in place
             const size_t mis = (uintptr_t)src & 15u;
-            par_copy(c, c->slot[s].h + mis, src, bytes, c->nt_copy);
+            par_copy(c, c->slot[s].h + mis, src, bytes, c->nt_copy, copy_threads);
             c->stats.bytes_staged += bytes;
             const uint8_t* kin = c->slot[s].d + mis;
             if (c->uniform_dma) {   // pinned -> HBM by the DMA engines, then the kernel reads HBM

@@ -293,6 +293,21 @@ gpu_r4_wirent() {
 )
 }
 
+# round 4: the pageable copy's escalation to every copy thread once the copy, not the DMA, is
+# the bound — default (4 threads) vs forced 1 and 2 threads, host leg only
+gpu_r4_escal() {
+(
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_hostpath.py tests/test_gpu_parity.py -q --timeout 120 --timeout-method thread > gpurun_out/r4_escal_tests.log 2>&1; rc=$?
+  echo "tests rc=$rc"; grep -E "passed|failed" gpurun_out/r4_escal_tests.log | tail -1; [ $rc -eq 0 ] || exit $rc
+  for v in dflt1:4 bulk1:1 dflt2:4 bulk2:2; do
+    n=${v%%:*}; t=${v#*:}
+    TCPCSUM_HOST_BULK_THREADS=$t timeout -k 10 200 python3 bench.py --host-path-only --host-steps 10 > gpurun_out/r4_escal_$n.json 2>> gpurun_out/r4_escal.err; rc=$?
+    echo "$n threads=$t rc=$rc $(python3 -c "import json; d=json.load(open('gpurun_out/r4_escal_$n.json'))['host_path']['pageable']; print(d['GiB/s'], d['cpu_core_s_per_step_rank0'], d['copy_ms_per_step_rank0'], d['wait_ms_per_step_rank0'])")"
+    ok_rc $rc || exit $rc
+  done
+)
+}
+
 # round 3: wire FILL line store (default) — every GPU test first, then the A/B timing three
 # times (the two FILL stores must agree byte for byte every time)
 gpu_r3_fill() {
