@@ -170,8 +170,9 @@ def test_uniform_host_pinned_dma_chunks(dev, offset, stride, length):
 
 
 @pytest.mark.parametrize("env", [{}, {"TCPCSUM_HOST_SLOTS": "3"}, {"TCPCSUM_HOST_DMA": "0"},
-                                 {"TCPCSUM_HOST_SLOTS": "4", "TCPCSUM_HOST_DMA": "0"}],
-                         ids=["default", "slots3", "nodma", "slots4_nodma"])
+                                 {"TCPCSUM_HOST_SLOTS": "4", "TCPCSUM_HOST_DMA": "0"},
+                                 {"TCPCSUM_HOST_BULK_THREADS": "1"}, {"TCPCSUM_HOST_SLOT_SLEEP": "0"}],
+                         ids=["default", "slots3", "nodma", "slots4_nodma", "bulk1_escalates", "slot_spin"])
 def test_uniform_host_pageable_pipeline_variants(dev, env):
     """Pageable input through the staging pipeline on the context's one stream: chunks ramp up
     from scratch/8 (128 KiB here) to scratch (1 MiB), staged in 2-4 slots, each moved to HBM by
@@ -188,7 +189,7 @@ def test_uniform_host_pageable_pipeline_variants(dev, env):
         old = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
         try:
-            with tcp_amd.HostContext(0, scratch_bytes=1 << 20) as ctx:
+            with tcp_amd.HostContext(0, scratch_bytes=1 << 20, blocking_wait=True) as ctx:
                 for _ in range(2):
                     assert np.array_equal(ctx.batch_uniform(buf, stride, length, n, ss, offset=offset), want)
                 assert ctx.stats()["bytes_staged"] > 0
@@ -219,3 +220,36 @@ def test_uniform_host_default_pieces_large(dev, memory):
         staged = ctx.stats()["bytes_staged"]
     assert np.array_equal(got, want)
     assert (staged == 0) if memory == "pinned" else (staged >= n * length)
+
+
+@pytest.mark.parametrize("nt", ["1", "0"], ids=["stream_stores", "memcpy"])
+@pytest.mark.parametrize("mode", ["fill", "verify"])
+def test_wire_staging_store_kinds(dev, nt, mode):
+    """Pageable wire batches staged with streaming stores from 64-B starts (default) or plain
+    memcpy from 16-B starts (TCPCSUM_HOST_WIRE_NT=0): the loop's 1024 x 32 KiB layout by
+    pointer, and a region with odd offsets, against the oracle; FILL's checks land in the
+    caller's packets."""
+    import os
+    import tcp_amd
+    from tests.packets import build_batch
+    rng = np.random.default_rng(31 if nt == "1" else 32)
+    region, off, _ = build_batch(rng, 700, malformed=True, odd_offsets=True)
+    ref = region.copy()
+    m = tcp_amd.IPV4_FILL if mode == "fill" else tcp_amd.IPV4_VERIFY
+    if mode == "verify":
+        oracle.ipv4_batch(ref, off, 32768, tcp_amd.IPV4_FILL)   # checks in place, then verify
+        region[:] = ref
+    want_out, want_st = oracle.ipv4_batch(ref, off, 32768, m)
+    old = os.environ.get("TCPCSUM_HOST_WIRE_NT")
+    os.environ["TCPCSUM_HOST_WIRE_NT"] = nt
+    try:
+        with tcp_amd.HostContext(0, blocking_wait=True) as ctx:
+            out, st = ctx.ipv4_batch(region, off, 32768, m)
+            assert ctx.stats()["pkts_staged"] > 0
+    finally:
+        if old is None:
+            os.environ.pop("TCPCSUM_HOST_WIRE_NT", None)
+        else:
+            os.environ["TCPCSUM_HOST_WIRE_NT"] = old
+    assert np.array_equal(st, want_st) and np.array_equal(out, want_out)
+    assert np.array_equal(region, ref)
