@@ -308,6 +308,20 @@ gpu_r4_escal() {
 )
 }
 
+# round 4: the recvmmsg side — 1024 packets over UDP loopback, one recvmmsg timed: plain, under
+# the interposer (RX=drop: GPU verify), and plain + CPU verify per packet; twice
+gpu_r4_rx() {
+(
+  for rep in 1 2; do
+    timeout -k 10 120 tools/mmsg_bench rx 300 > gpurun_out/r4_rx_plain_$rep.json 2>> gpurun_out/r4_rx.err || exit $?
+    env LD_PRELOAD=$PWD/tcp_amd/libtcpcsum_preload.so TCPCSUM_PRELOAD_ANY_SOCKET=1 TCPCSUM_PRELOAD_TX=off TCPCSUM_PRELOAD_RX=drop \
+      timeout -k 10 120 tools/mmsg_bench rx 300 > gpurun_out/r4_rx_gpu_$rep.json 2>> gpurun_out/r4_rx.err || exit $?
+    timeout -k 10 120 tools/mmsg_bench rxcpu 300 > gpurun_out/r4_rx_cpu_$rep.json 2>> gpurun_out/r4_rx.err || exit $?
+    for v in plain gpu cpu; do echo "$v rep=$rep $(cat gpurun_out/r4_rx_${v}_$rep.json)"; done
+  done
+)
+}
+
 # round 3: wire FILL line store (default) — every GPU test first, then the A/B timing three
 # times (the two FILL stores must agree byte for byte every time)
 gpu_r3_fill() {

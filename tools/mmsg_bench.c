@@ -16,6 +16,15 @@
  *   mmsg_bench gpu <iters> pinned   the out-buffers carved from one tcpcsum_host_alloc
  *                            pool instead (INTEGRATION.md level 2: loop.c:180-183
  *                            allocating page-locked memory): filled in place
+ *   mmsg_bench rx <iters>    the recvmmsg side (loop.c:22-25): 1024 finished packets sent
+ *                            as UDP datagrams over loopback, then ONE recvmmsg of all
+ *                            1024 into the loop's 32 KiB malloc'd in-buffers is timed —
+ *                            under the interposer with TCPCSUM_PRELOAD_RX=drop (verify
+ *                            on the GPU; the count returned = segments that verify),
+ *                            or without it (plain: the syscall alone)
+ *   mmsg_bench rxcpu <iters> the same recvmmsg, then the CPU verify of every segment
+ *                            (csum_continue over pseudo header + segment == 0, -O2):
+ *                            what verifying on one core would cost the loop
  *
  * Prints one JSON line: first-call and steady-state (min / median) latency
  * per 1024-packet batch, the CPU time the whole process spent per batch
@@ -88,8 +97,93 @@ static int cmp_d(const void *a, const void *b) {
     return x < y ? -1 : x > y;
 }
 
+/* csum_continue over the pseudo header and the whole segment, check included: 0 when
+ * the segment verifies (the rx check, context.c:121-145 applied to a received packet) */
+static int cpu_verify(const uint8_t *ip, unsigned len) {
+    uint32_t sa, da;
+    memcpy(&sa, ip + 12, 4);
+    memcpy(&da, ip + 16, 4);
+    const unsigned tl = len - 20;
+    return tcpcsum_continue(tcpcsum_pseudo(sa, da, htons((uint16_t) tl)), (const char *) ip + 20, (int) tl) == 0;
+}
+
+static int rx_main(int cpu_verify_mode, int iters) {
+    static uint8_t *outb[NPKT], *inb[NPKT];
+    static struct iovec tiov[NPKT], riov[NPKT];
+    static struct mmsghdr tv[NPKT], rv[NPKT];
+    for (int i = 0; i < NPKT; ++i) {
+        outb[i] = malloc(SLOT);
+        inb[i] = malloc(SLOT);
+        memset(inb[i], 0, SLOT);
+        build(outb[i], i);
+        const uint16_t c = cpu_check(outb[i]);
+        memcpy(outb[i] + 36, &c, 2);
+        tiov[i].iov_base = outb[i];
+        tiov[i].iov_len = 20 + 24 + PAYLOAD;
+        tv[i].msg_hdr.msg_iov = &tiov[i];
+        tv[i].msg_hdr.msg_iovlen = 1;
+        riov[i].iov_base = inb[i];
+        riov[i].iov_len = SLOT;
+        rv[i].msg_hdr.msg_iov = &riov[i];
+        rv[i].msg_hdr.msg_iovlen = 1;
+    }
+    const int rx = socket(AF_INET, SOCK_DGRAM, 0), tx = socket(AF_INET, SOCK_DGRAM, 0);
+    int big = 32 << 20;
+    setsockopt(rx, SOL_SOCKET, SO_RCVBUF, &big, sizeof big);
+    setsockopt(tx, SOL_SOCKET, SO_SNDBUF, &big, sizeof big);
+    struct sockaddr_in a = {0};
+    a.sin_family = AF_INET;
+    a.sin_addr.s_addr = htonl(0x7F000001u);
+    if (bind(rx, (struct sockaddr *) &a, sizeof a) != 0) { perror("bind"); return 2; }
+    socklen_t al = sizeof a;
+    getsockname(rx, (struct sockaddr *) &a, &al);
+    if (connect(tx, (struct sockaddr *) &a, sizeof a) != 0) { perror("connect"); return 2; }
+    double *t = malloc(sizeof(double) * (size_t) iters), *c = malloc(sizeof(double) * (size_t) iters);
+    int short_batches = 0, bad = 0, kept_last = 0;
+    for (int k = 0; k < iters; ++k) {
+        int sent = 0;
+        while (sent < NPKT) {
+            const int r = sendmmsg(tx, tv + sent, (unsigned) (NPKT - sent), 0);
+            if (r <= 0) { perror("sendmmsg"); return 3; }
+            sent += r;
+        }
+        usleep(2000);   /* every datagram queued before the timed call */
+        for (int i = 0; i < NPKT; ++i) riov[i].iov_base = inb[i], riov[i].iov_len = SLOT;
+        const double c0 = cpu_us();
+        const double t0 = now_us();
+        const int r = recvmmsg(rx, rv, NPKT, MSG_DONTWAIT, NULL);
+        int ok = r;
+        if (cpu_verify_mode && r > 0) {
+            ok = 0;
+            for (int i = 0; i < r; ++i) ok += cpu_verify((const uint8_t *) riov[i].iov_base, rv[i].msg_len);
+        }
+        t[k] = now_us() - t0;
+        c[k] = cpu_us() - c0;
+        if (r != NPKT) ++short_batches;
+        if (ok != NPKT) ++bad;
+        kept_last = ok;
+        /* drain anything left (a short batch) so the next iteration starts empty */
+        while (recvmmsg(rx, rv, NPKT, MSG_DONTWAIT, NULL) > 0) {}
+    }
+    const double first = t[0];
+    qsort(t + 1, (size_t) (iters - 1), sizeof(double), cmp_d);
+    qsort(c + 1, (size_t) (iters - 1), sizeof(double), cmp_d);
+    double csum = 0;
+    for (int k = 1; k < iters; ++k) csum += c[k];
+    printf("{\"path\": \"%s\", \"batch\": \"1024 x 1500-B packets received into separate 32 KiB malloc'd buffers "
+           "(loop.c:22-25, 180-183), UDP over loopback\", \"first_us\": %.1f, \"min_us\": %.1f, "
+           "\"median_us\": %.1f, \"cpu_us_median\": %.1f, \"cpu_us_mean\": %.1f, \"iters\": %d, "
+           "\"short_batches\": %d, \"batches_not_all_verified\": %d, \"verified_last\": %d}\n",
+           cpu_verify_mode ? "recvmmsg + cpu verify per packet (-O2)" : "recvmmsg (interposed when LD_PRELOAD is set)",
+           first, t[1], t[1 + (iters - 1) / 2], c[1 + (iters - 1) / 2], csum / (iters - 1), iters, short_batches, bad,
+           kept_last);
+    return 0;
+}
+
 int main(int argc, char **argv) {
-    if (argc < 3) { fprintf(stderr, "usage: %s gpu|cpu iters [pinned]\n", argv[0]); return 2; }
+    if (argc < 3) { fprintf(stderr, "usage: %s gpu|cpu|rx|rxcpu iters [pinned]\n", argv[0]); return 2; }
+    if (!strcmp(argv[1], "rx") || !strcmp(argv[1], "rxcpu"))
+        return rx_main(!strcmp(argv[1], "rxcpu"), atoi(argv[2]) > 1 ? atoi(argv[2]) : 2);
     const int gpu = !strcmp(argv[1], "gpu");
     const int iters = atoi(argv[2]) > 1 ? atoi(argv[2]) : 2;
     const int pinned = argc > 3 && !strcmp(argv[3], "pinned");
