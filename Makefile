@@ -46,7 +46,7 @@ $(LIB): $(OBJDIR)/tcpcsum_kernels.o $(OBJDIR)/tcpcsum_api.o $(OBJDIR)/tcpcsum_ho
 	mv $@.tmp $@
 
 # LD_PRELOAD seam library (sendmmsg / recvmmsg interposer) over the C ABI
-$(PRELOAD): tcp_amd/csrc/preload_mmsg.c tcp_amd/csrc/rx_compact.h include/tcpcsum.h $(LIB)
+$(PRELOAD): tcp_amd/csrc/preload_mmsg.c tcp_amd/csrc/preload_arena.h tcp_amd/csrc/rx_compact.h include/tcpcsum.h $(LIB)
 	$(CC) -O2 -fPIC -shared -Wall -Wextra -Iinclude -o $@ $< -Ltcp_amd -ltcpcsum -ldl -lpthread -Wl,-rpath,'$$ORIGIN'
 
 oracle: oracle/build/liboracle.so oracle/build/liboracle_O0.so

@@ -306,6 +306,26 @@ def run_config(config: str, steps: int, warmup: int, rank: int, world: int, dist
     return r, bufs, rot
 
 
+def time_probe(bufs, nbytes: int, steps: int, device) -> float:
+    """Average ms of the read-only probe (k_probe: the kernels' access shape, every byte read once)
+    over the same rotation of batches a config's kernel was timed on, HIP events on the stream."""
+    import torch
+    import tcp_amd
+    pout = torch.zeros(tcp_amd.api.PROBE_SLOTS, dtype=torch.int64, device=device)
+    nb = (nbytes // 16) * 16
+    for _ in range(3):
+        tcp_amd.stream_probe(bufs[0], nb, pout, tune=(0, 0, -1, 0))
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    pe0, pe1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    pe0.record(stream)
+    for i in range(steps):
+        tcp_amd.stream_probe(bufs[i % len(bufs)], nb, pout, tune=(0, 0, -1, 0))
+    pe1.record(stream)
+    torch.cuda.synchronize()
+    return pe0.elapsed_time(pe1) / steps
+
+
 def run_wire(steps: int, warmup: int, device) -> dict:
     """The reference's own operation on wire packets, device-resident, beside the headline:
     1M IPv4/TCP packets of 1500 B (1480 TCP bytes) framed as context.c:169-206 frames them, one
@@ -343,7 +363,22 @@ def run_wire(steps: int, warmup: int, device) -> dict:
     # FILL and VERIFY interleaved over 5 rounds (3 untimed + `steps` timed launches each), median
     # per mode: the first window after the build runs slow on some boxes (0.29 vs 0.245 ms VERIFY,
     # tools/wire_fresh.py), which one window per mode would report as the kernel's rate
-    modes = (("fill", tcp_amd.IPV4_FILL), ("verify", tcp_amd.IPV4_VERIFY))
+    # Beside them, the same box's ceilings for their traffic, over the same region: the read-only
+    # probe (every line read, as VERIFY) and the write-back probe (every line read and one whole
+    # 128-B line per 1536-B slot written back through, bytes unchanged — the FILL's HBM traffic
+    # without its arithmetic; TCPCSUM_TUNE_PROBE_WRITE, period 12 lines)
+    pout = torch.zeros(tcp_amd.api.PROBE_SLOTS, dtype=torch.int64, device=device)
+    probe_rw = tcp_amd.make_tuning(0, 0, slot // 128, tcp_amd.TUNE_PROBE_WRITE)
+    modes = (("fill", tcp_amd.IPV4_FILL), ("verify", tcp_amd.IPV4_VERIFY), ("copy_probe", None),
+             ("read_probe", None))
+
+    def launch(name, mode):
+        if name == "copy_probe":
+            tcp_amd.stream_probe(reg, n * slot, pout, tune=probe_rw)
+        elif name == "read_probe":
+            tcp_amd.stream_probe(reg, n * slot, pout, tune=(0, 0, -1, 0))
+        else:
+            tcp_amd.ipv4_batch(reg, doff, n, slot, mode, out, sta)
     times = {name: [] for name, _ in modes}
     fill_ok = verify_ok = True
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -355,23 +390,33 @@ def run_wire(steps: int, warmup: int, device) -> dict:
     for _ in range(5):
         for name, mode in modes:
             for _ in range(3):
-                tcp_amd.ipv4_batch(reg, doff, n, slot, mode, out, sta)
+                launch(name, mode)
             e0.record(stream)
             for _ in range(steps):
-                tcp_amd.ipv4_batch(reg, doff, n, slot, mode, out, sta)
+                launch(name, mode)
             e1.record(stream)
             torch.cuda.synchronize()
             times[name].append(e0.elapsed_time(e1) / steps)
             if name == "fill":
                 fill_ok = fill_ok and bool(torch.equal(out, built)) and bool((sta == tcp_amd.PKT_OK).all())
-            else:
+            elif name == "verify":
                 verify_ok = verify_ok and bool((out == 0).all()) and bool((sta == tcp_amd.PKT_OK).all())
     for name, _ in modes:
         ms = statistics.median(times[name])
+        if name.endswith("probe"):
+            moved = n * slot + (n * 128 if name == "copy_probe" else 0)
+            res[name] = {"avg_ms": round(ms, 5), "ms_rounds": [round(t, 4) for t in times[name]],
+                         "bytes_moved_per_launch": moved, "GB/s": round(moved / (ms * 1e-3) / 1e9, 1)}
+            continue
         gbs = n * tcp_len / (ms * 1e-3) / 1e9
         res[name] = {"kernel_avg_ms": round(ms, 5), "kernel_ms_rounds": [round(t, 4) for t in times[name]],
                      "achieved_GB/s": round(gbs, 1), "roofline_frac": round(gbs / HBM_PEAK_GBS, 4)}
+    res["copy_probe"]["what"] = ("k_probe<16,WR>: every line of the 1.61 GB region read, one 128-B line per "
+                                 "1536-B slot written back through (sc0 sc1), bytes unchanged")
+    res["read_probe"]["what"] = "k_probe<16>: every line of the region read"
     res["fill_over_verify"] = round(res["fill"]["kernel_avg_ms"] / res["verify"]["kernel_avg_ms"], 3)
+    res["fill_over_copy_probe"] = round(res["fill"]["kernel_avg_ms"] / res["copy_probe"]["avg_ms"], 3)
+    res["verify_over_read_probe"] = round(res["verify"]["kernel_avg_ms"] / res["read_probe"]["avg_ms"], 3)
     # HBM bytes actually moved (committed PMC pass: whole 128-B lines read, FILL's check lines
     # written back whole) per launch time — the FILL is a read+write stream, whose measured
     # ceiling is a plain copy's ~6.1 TB/s (tools/copy_probe.hip), not the 8 TB/s read peak
@@ -385,6 +430,10 @@ def run_wire(steps: int, warmup: int, device) -> dict:
         res["traffic_source"] = "profiles/traffic.json wire_fill_1Mx1500 (rocprofv3 --pmc, round 4)"
     except Exception:
         pass
+    # the write-back probe rewrote the lines it read: the packets are still the builder's
+    tcp_amd.ipv4_batch(reg, doff, n, slot, tcp_amd.IPV4_VERIFY, out, sta)
+    torch.cuda.synchronize()
+    verify_ok = verify_ok and bool((out == 0).all()) and bool((sta == tcp_amd.PKT_OK).all())
     res["check"] = fill_ok and verify_ok
     return res
 
@@ -514,13 +563,15 @@ def host_path_rate(bytes_per_rank: list, walls: list, steps: int) -> dict:
 
 def host_context(local: int):
     """The host leg's context: blocking (sleeping) wait; its staging and HBM slots allocated by one
-    warm batch of two chunks over a pinned buffer and a pageable one, so that, created at the
-    start of the run as an application creates it at start-up, nothing it holds is allocated
-    after the device legs have churned the allocators."""
+    warm batch past two full staging chunks (2 x 128 MiB) over a pinned buffer and a pageable one,
+    so that, created at the start of the run as an application creates it at start-up, nothing it
+    holds is allocated after the device legs have churned the allocators."""
     import numpy as np
     import tcp_amd
     ctx = tcp_amd.HostContext(local, blocking_wait=True)   # sleep, not spin, while the GPU works
-    warm = 33 << 20   # > 2 chunks of 16 MiB
+    # the pageable ramp is 16, 32, 64 then 128 MiB chunks: past 2 full chunks both staging slots
+    # reach their full size; pinned batches past 2 x 16 MiB take the DMA path (256 MiB pieces)
+    warm = (16 + 32 + 64 + 128 + 128) << 20
     pin = tcp_amd.pinned_empty(warm)
     pin[:] = 0
     ctx.batch_uniform(pin, 1500, 1500, warm // 1500, 0)
@@ -609,6 +660,10 @@ def run_host_path(steps: int, warmup: int, rank: int, world: int, local: int, di
     finally:
         os.sched_setaffinity(0, saved)
     walls = gather_walls(wall, dist, world)
+    # every rank's cgroup CPU throttling over its timed region (a rank's cgroup may be the job's:
+    # then they all report the same counter's growth)
+    thr = None if thr0 is None or thr1 is None else round((thr1 - thr0) / 1e3, 1)
+    throttled = gather_walls(thr, dist, world)
     calls = max(steps + warmup, 1)   # the stats and rusage deltas span the warm-up calls too
     cpu_ns = (s_after["ns_cpu_caller"] - s_before["ns_cpu_caller"]) + (s_after["ns_cpu_workers"] - s_before["ns_cpu_workers"])
     r = {"workload": f"{cnt} x {L}-byte segments per GPU in {memory} host memory "
@@ -622,7 +677,9 @@ def run_host_path(steps: int, warmup: int, rank: int, world: int, local: int, di
          "process_cpu_core_s_per_step_rank0": round(proc_cpu / calls, 4),
          "copy_ms_per_step_rank0": round((s_after["ns_copy"] - s_before["ns_copy"]) / calls / 1e6, 3),
          "wait_ms_per_step_rank0": round((s_after["ns_wait"] - s_before["ns_wait"]) / calls / 1e6, 3),
-         "cgroup_throttled_ms_rank0": None if thr0 is None or thr1 is None else round((thr1 - thr0) / 1e3, 1),
+         "cgroup_throttled_ms_per_rank": throttled,
+         "copy_threads_per_rank": gather_walls(s_after["bulk_threads"], dist, world),
+         "local_world_size": int(os.environ.get("LOCAL_WORLD_SIZE", "1")),
          "cpu_core_s_per_step_rank0": round(cpu_ns / calls / 1e9, 4)}
     if raw:
         r["frac_of_raw_pinned_h2d"] = round(r["GiB/s"] / raw, 3)
@@ -805,21 +862,9 @@ def main(argv=None) -> int:
 
     probe = None
     if world == 1 and not args.no_probe:
-        pout = torch.zeros(tcp_amd.api.PROBE_SLOTS, dtype=torch.int64, device=device)
-        tcp_amd.set_tuning(0, 0, -1, 0)
-        nb = (batch_bytes // 16) * 16
-        for _ in range(3):
-            tcp_amd.stream_probe(bufs[0], nb, pout)
-        torch.cuda.synchronize()
-        pe0, pe1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        pe0.record(stream)
-        for i in range(args.steps):
-            tcp_amd.stream_probe(bufs[i % rot], nb, pout)
-        pe1.record(stream)
-        torch.cuda.synchronize()
-        pms = pe0.elapsed_time(pe1) / args.steps
+        pms = time_probe(bufs[:rot], batch_bytes, args.steps, device)
         probe = {"kernel": "k_probe (read-only 16-B stream, same access shape)", "avg_ms": round(pms, 5),
-                 "GB/s": round(nb / (pms * 1e-3) / 1e9, 1),
+                 "GB/s": round((batch_bytes // 16) * 16 / (pms * 1e-3) / 1e9, 1),
                  "headline_kernel_over_probe": round(kernel_ms / pms, 4)}
 
     # the other single-GPU BASELINE configs (parity configs, reported beside the
@@ -834,7 +879,10 @@ def main(argv=None) -> int:
             if cfg == args.config or (args.other and cfg not in args.other.split(",")):
                 continue
             steps = max(10, min(args.steps, 200 if CONFIGS[cfg][1] < 4096 else 40))
-            e, ebufs, _ = run_config(cfg, steps, min(args.warmup, 5), rank, world, dist, device)
+            e, ebufs, erot = run_config(cfg, steps, min(args.warmup, 5), rank, world, dist, device)
+            # the read-only probe over the same rotation, same box, same moment: the config's own
+            # ceiling (for 64 B: a 64 MiB launch's ramp and drain bound the probe as well)
+            epms = time_probe(ebufs[:erot], e["batch_bytes"], steps, device) if not args.no_probe else None
             del ebufs
             gbs = e["batch_bytes"] / (e["kernel_ms"] * 1e-3) / 1e9
             extra[cfg] = {"workload": e["desc"], "GiB/s": round(e["batch_bytes"] * steps / e["wall_max"] / (1 << 30), 2),
@@ -842,6 +890,10 @@ def main(argv=None) -> int:
                           "roofline_frac": round(gbs / HBM_PEAK_GBS, 4), "steps": steps,
                           "rotating_batches": e["rot"], "digest_check": e["check"],
                           "traffic": load_traffic(cfg)}
+            if epms:
+                extra[cfg]["stream_probe"] = {"avg_ms": round(epms, 5),
+                                              "GB/s": round(e["batch_bytes"] / (epms * 1e-3) / 1e9, 1),
+                                              "kernel_over_probe": round(e["kernel_ms"] / epms, 4)}
             torch.cuda.empty_cache()
             if CONFIGS[cfg][1] < 4096:
                 # small segments: the per-launch ramp is a large share of a launch; the same

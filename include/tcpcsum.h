@@ -329,7 +329,9 @@ int tcpcsum_synth_pseudo_dev(uint32_t *d_sum_start, uint64_t seg0, uint64_t n, u
 
 /* Read-only streaming probe: the chip's practical HBM read ceiling for the
  * checksum kernels' access pattern (16-B non-temporal loads, each wave
- * reading contiguous 1 KiB per instruction), reported beside them.
+ * reading contiguous 1 KiB per instruction), reported beside them. With
+ * TCPCSUM_TUNE_PROBE_WRITE it also writes lines back (the wire FILL's ceiling);
+ * d_src is then written (its bytes unchanged) and must be writable.
  * d_partials: TCPCSUM_PROBE_SLOTS u64 entries; on completion the sum over the
  * first *n_partials entries equals the sum of the lo16+hi16 halves of every
  * u32 word of d_src. nbytes multiple of 16, d_src 16-B aligned. */
@@ -370,6 +372,9 @@ int tcpcsum_plan_uniform(uint64_t base, uint64_t stride, uint32_t len, uint64_t 
 #define TCPCSUM_TUNE_TX_WT_STORE 1024  /* builder: payload stores written through (sc0 sc1 buffer stores) */
 /* wire FILL: the 64-B block holding the checks written through instead of the 128-B line */
 #define TCPCSUM_TUNE_FILL_HALF 2048
+/* stream probe: also write back through (sc0 sc1) every shape-th 128-B line it reads, bytes
+ * unchanged (shape 0: every 12th) — the wire FILL's traffic on 1536-B slots, without its work */
+#define TCPCSUM_TUNE_PROBE_WRITE 4096
 /* 0 if *tune is a valid tuning (NULL counts as valid), else TCPCSUM_EINVAL. */
 int tcpcsum_tuning_check(const tcpcsum_tuning_t *tune);
 

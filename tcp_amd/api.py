@@ -8,9 +8,12 @@ that both use the one HIP runtime already in the process (torch ships a
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
+import sys
 import threading
+import weakref
 from typing import Optional
 
 import numpy as np
@@ -23,7 +26,7 @@ except Exception:  # pragma: no cover - torch is always present in this image
 __all__ = [
     "DESC_DTYPE", "TXSEG_DTYPE", "IPV4_FILL", "IPV4_VERIFY", "IPV4_IPHDR", "PKT_OK", "PKT_SKIPPED",
     "PKT_IPHDR_BAD", "PKT_CSUM_PARTIAL", "CTX_BLOCKING_WAIT", "TUNE_WIRE_CACHED", "TUNE_WIN16", "TUNE_TX_NT_STORE", "TUNE_FILL_DWORD", "TUNE_FILL_U16",
-    "TUNE_TX_WT_STORE", "TUNE_FILL_HALF",
+    "TUNE_TX_WT_STORE", "TUNE_FILL_HALF", "TUNE_PROBE_WRITE",
     "TcpCsumError", "Tuning", "HostContext", "lib", "lib_path", "device_check", "build_info", "make_tuning", "set_tuning",
     "get_tuning", "plan_uniform", "getPseudoHeaderSum", "csum_continue", "batch_uniform", "batch_uniform_multi",
     "ubatches", "batch_desc",
@@ -73,6 +76,32 @@ class TcpCsumError(RuntimeError):
 
 _lib = None
 _lock = threading.Lock()
+
+# Teardown. Contexts still open when the interpreter exits are closed by an
+# atexit hook — their stream drained and copy threads joined while the HIP runtime is still up
+# (torch, imported first, registered its own hooks earlier, so they run after this one). From
+# then on no finalizer calls into HIP: pinned blocks still referenced are left to the OS, since
+# their hipHostFree could otherwise run during interpreter shutdown, after the runtime's own
+# static destructors.
+_live_contexts: "weakref.WeakSet[HostContext]" = weakref.WeakSet()
+_exiting = False
+
+
+def _close_at_exit() -> None:
+    global _exiting
+    for ctx in list(_live_contexts):
+        try:
+            ctx.close()
+        except Exception:
+            pass
+    _exiting = True
+
+
+atexit.register(_close_at_exit)
+
+
+def _finalizer_may_call_hip() -> bool:
+    return not _exiting and not sys.is_finalizing()
 
 c_u8p = ctypes.POINTER(ctypes.c_uint8)
 c_u16p = ctypes.POINTER(ctypes.c_uint16)
@@ -206,6 +235,7 @@ PROBE_SLOTS = 8192
 TUNE_PIPE_ON, TUNE_PIPE_OFF, TUNE_NT_ON, TUNE_NT_OFF = 1, 2, 4, 8
 TUNE_WIRE_CACHED, TUNE_WIN16 = 32, 64   # wire kernel variants (tcpcsum.h)
 TUNE_TX_NT_STORE, TUNE_FILL_DWORD, TUNE_FILL_U16, TUNE_TX_WT_STORE, TUNE_FILL_HALF = 128, 256, 512, 1024, 2048
+TUNE_PROBE_WRITE = 4096   # stream probe: write back every shape-th 128-B line (the wire FILL's traffic)
 
 
 # The C library holds no tuning state: every device call takes an explicit
@@ -410,9 +440,9 @@ class _Pinned:
 
     def __del__(self):
         try:
-            if self.ptr:
+            if self.ptr and _finalizer_may_call_hip():
                 lib().tcpcsum_host_free(self.ptr)
-                self.ptr = None
+            self.ptr = None
         except Exception:
             pass
 
@@ -435,8 +465,10 @@ class HostContext:
 
     def __init__(self, device: int = 0, scratch_bytes: int = 0, blocking_wait: bool = False):
         h = vp()
+        self._h = vp()
         _check(lib().tcpcsum_ctx_create(device, scratch_bytes, ctypes.byref(h)), "tcpcsum_ctx_create")
         self._h = h
+        _live_contexts.add(self)
         if blocking_wait:
             self.set_flags(CTX_BLOCKING_WAIT)
 
@@ -465,7 +497,8 @@ class HostContext:
 
     def __del__(self):
         try:
-            self.close()
+            if _finalizer_may_call_hip():
+                self.close()
         except Exception:
             pass
 

@@ -170,9 +170,13 @@ private:
     std::atomic<bool> quit_{false};
 };
 
-// Host threads for staging copies: TCPCSUM_HOST_THREADS, else half the CPUs
-// this process may use (the affinity mask, capped by a cgroup CPU quota), 1..8.
-int default_copy_threads() {
+// Host threads for staging copies: TCPCSUM_HOST_THREADS, else from the CPUs this
+// process may use (the affinity mask, capped by a cgroup CPU quota): half of them
+// (1..8) for a process alone on its node; when LOCAL_WORLD_SIZE (torch.distributed.run's
+// ranks on this node, which share that quota) is k > 1, the rank's 1/k share of them
+// (1..8), so k ranks copying at once fit the CPUs the job has instead of
+// oversubscribing the quota and being throttled.
+inline int default_copy_threads() {
     if (const char* e = getenv("TCPCSUM_HOST_THREADS")) {
         const int v = atoi(e);
         if (v >= 1) return std::min(v, 64);
@@ -189,6 +193,9 @@ int default_copy_threads() {
         }
         fclose(f);
     }
+    int ranks = 1;
+    if (const char* e = getenv("LOCAL_WORLD_SIZE")) ranks = std::max(1, atoi(e));
+    if (ranks > 1) return std::max(1, std::min(8, cpus / ranks));
     return std::max(1, std::min(8, cpus / 2));
 }
 

@@ -33,6 +33,27 @@
  *   TCPCSUM_PRELOAD_WAIT=spin    wait for the GPU in HIP's spin (default: block,
  *                                TCPCSUM_CTX_BLOCKING_WAIT — the thread sleeps
  *                                while the kernel runs)
+ *   TCPCSUM_PRELOAD_DEVICE=<k>   the GPU this process's batches run on (default 0):
+ *                                one loop process per GPU on a multi-GPU node
+ *   TCPCSUM_PRELOAD_POOL=<prog>  zero copy with loop.c unedited: malloc(32 KiB) —
+ *                                the loop's 2 x 1024 packet buffers, loop.c:180-183 —
+ *                                is served from one page-locked block the library
+ *                                allocates itself (tcpcsum_host_alloc, 64 MiB) before
+ *                                main runs, so both seams read and fill the loop's
+ *                                buffers in place (preload_arena.h). Every other
+ *                                allocation, and any past the first 2048 of that
+ *                                size, goes to libc; free / realloc /
+ *                                malloc_usable_size route arena pointers back here.
+ *                                <prog> is the loop's executable name ("stress"), or
+ *                                1 for whatever process loads the interposer. The pool
+ *                                initialises HIP in a constructor, and a process that
+ *                                has done so must not exec: name the program, or put
+ *                                LD_PRELOAD on the loop binary itself, never on a
+ *                                wrapper (timeout, a shell). The process that takes the
+ *                                pool removes the variable from its environment before
+ *                                HIP starts, so its children do not inherit it. A
+ *                                forked child must not touch arena buffers
+ *                                (page-locked memory is not inherited).
  *
  * Buffers the application page-locked (tcpcsum_host_alloc for its out-buffer
  * pool, loop.c:180-183 — INTEGRATION.md level 2 — or its own hipHostRegister)
@@ -52,14 +73,23 @@
  * with a 127/8 source arriving on any other interface is a martian and dropped
  * by the kernel) — and (with IPHDR) its IPv4 header checksum verifies. A
  * forged or corrupted segment from anywhere else whose check word happens to
- * equal the un-complemented pseudo-header fold is therefore rejected.
+ * equal the un-complemented pseudo-header fold is therefore rejected. That
+ * argument holds for AF_INET sockets on hosts without route_localnet (which
+ * lets 127/8 in on other interfaces; kube-proxy sets it) only: for any other
+ * socket family (AF_PACKET sees frames before the martian filter) or when any
+ * interface has net.ipv4.conf.*.route_localnet=1 (read once, at the first
+ * call), there is no exception and a CHECKSUM_PARTIAL segment counts as failed.
  * Messages that are not IPv4/TCP are passed through untouched (the reference
  * filters them itself, loop.c:319). IPv4/TCP messages the library cannot
  * verify — truncated (tot_len past the bytes received), bad IHL or lengths —
  * are counted as skipped; in drop mode they are dropped, since they would
- * reach the application's TCP handler unverified.
+ * reach the application's TCP handler unverified. A message with several
+ * iovecs (the reference uses one, loop.c:187-188) is checked from its first
+ * iovec when that holds the whole packet; otherwise it is skipped and, in drop
+ * mode, passed through unverified (a scatter read the library cannot see whole).
  */
 #define _GNU_SOURCE
+#include <dirent.h>
 #include <dlfcn.h>
 #include <errno.h>
 #include <pthread.h>
@@ -69,12 +99,15 @@
 #include <string.h>
 #include <sys/socket.h>
 #include <sys/types.h>
+#include <unistd.h>
 
+#include "preload_arena.h"
 #include "rx_compact.h"
 #include "tcpcsum.h"
 
 typedef int (*sendmmsg_fn)(int, struct mmsghdr *, unsigned int, int);
 typedef int (*recvmmsg_fn)(int, struct mmsghdr *, unsigned int, int, struct timespec *);
+typedef size_t (*usable_fn)(void *);
 
 enum { MODE_OFF = 0, MODE_FILL = 1, MODE_VERIFY = 2, MODE_DROP = 3 };
 
@@ -88,13 +121,95 @@ static pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;
 static pthread_once_t g_once = PTHREAD_ONCE_INIT;
 static sendmmsg_fn real_sendmmsg;
 static recvmmsg_fn real_recvmmsg;
-static int g_tx = MODE_FILL, g_rx = MODE_OFF, g_iphdr, g_any, g_stats;
+static int g_tx = MODE_FILL, g_rx = MODE_OFF, g_iphdr, g_any, g_stats, g_device, g_localnet;
 static tcpcsum_ctx_t *g_ctx;
 static int g_ctx_failed;
 static uint16_t *g_out;     /* pinned: the kernel writes results straight here */
 static uint8_t *g_status;
 static struct tcpcsum_preload_stats g_st;
 
+/* ------------------------------------------------------------------ the arena
+ * TCPCSUM_PRELOAD_POOL=1: malloc(kPoolBlock) served from page-locked memory the
+ * library owns (preload_arena.h). t_guard: this thread is inside the library
+ * (the constructor's HIP start-up, a GPU batch) — its allocations of the block
+ * size are the runtime's, not the loop's, and go to libc. */
+enum { kPoolBlock = 1024 * 32 };   /* loop.c:181-182 */
+static arena_t g_arena = ARENA_INIT;
+static __thread int t_guard __attribute__((tls_model("initial-exec")));
+static int g_pool_asked, g_pool_failed;
+
+extern void *__libc_malloc(size_t);
+extern void __libc_free(void *);
+extern void *__libc_realloc(void *, size_t);
+
+static const arena_libc_t k_libc = {__libc_malloc, __libc_free, __libc_realloc};
+
+void *malloc(size_t n) {
+    return arena_route_malloc(&g_arena, n, t_guard, &k_libc);
+}
+
+void free(void *p) {
+    arena_route_free(&g_arena, p, &k_libc);
+}
+
+void *realloc(void *p, size_t n) {
+    return arena_route_realloc(&g_arena, p, n, &k_libc);
+}
+
+/* glibc's reallocarray calls its own realloc internally, which must never see an
+ * arena pointer */
+void *reallocarray(void *p, size_t nmemb, size_t size) {
+    size_t n;
+    if (__builtin_mul_overflow(nmemb, size, &n)) {
+        errno = ENOMEM;
+        return NULL;
+    }
+    return realloc(p, n);
+}
+
+size_t malloc_usable_size(void *p) {
+    if (arena_owns(&g_arena, p)) return arena_block(&g_arena);
+    static usable_fn real_usable;
+    usable_fn f = __atomic_load_n(&real_usable, __ATOMIC_ACQUIRE);
+    if (!f) {
+        f = (usable_fn) dlsym(RTLD_NEXT, "malloc_usable_size");
+        __atomic_store_n(&real_usable, f, __ATOMIC_RELEASE);
+    }
+    return f ? f(p) : 0;
+}
+
+/* Before main: the pool's page-locked block, so HIP never starts inside a malloc
+ * call. Dependencies' constructors (the HIP runtime's) have run by now. */
+/* TCPCSUM_PRELOAD_POOL names the process the pool is for: "1" any process that
+ * loads the interposer, else the basename of its executable ("stress") — so a
+ * wrapper the preload also reaches (timeout, a shell) neither consumes the
+ * variable nor starts HIP. */
+static int pool_wanted(const char *v) {
+    if (!v || !*v || !strcmp(v, "0")) return 0;
+    if (!strcmp(v, "1")) return 1;
+    char exe[4096];
+    const ssize_t n = readlink("/proc/self/exe", exe, sizeof exe - 1);
+    if (n <= 0) return 0;
+    exe[n] = 0;
+    const char *base = strrchr(exe, '/');
+    return !strcmp(base ? base + 1 : exe, v);
+}
+
+__attribute__((constructor)) static void pool_ctor(void) {
+    if (!pool_wanted(getenv("TCPCSUM_PRELOAD_POOL"))) return;
+    g_pool_asked = 1;
+    unsetenv("TCPCSUM_PRELOAD_POOL");   /* children (an exec'd shell, say) never start HIP for it */
+    t_guard = 1;
+    void *mem = tcpcsum_host_alloc((size_t) kPoolBlock * ARENA_MAX_BLOCKS);
+    t_guard = 0;
+    if (!mem || arena_publish(&g_arena, mem, kPoolBlock, ARENA_MAX_BLOCKS)) {
+        g_pool_failed = 1;
+        fprintf(stderr, "tcpcsum_preload: TCPCSUM_PRELOAD_POOL: no page-locked pool (%s); the loop's buffers stay "
+                        "malloc'd and are copied into staging\n", mem ? "publish failed" : tcpcsum_strerror(TCPCSUM_ENOMEM));
+    }
+}
+
+/* ------------------------------------------------------------------ seams */
 static int env_mode(const char *name, int dflt) {
     const char *v = getenv(name);
     if (!v) return dflt;
@@ -110,10 +225,32 @@ static int env_flag(const char *name) {
     return v && atoi(v);
 }
 
+/* Whether any interface has net.ipv4.conf.<if>.route_localnet = 1 ("all" included):
+ * 127/8 may then arrive on interfaces other than lo. */
+static int any_route_localnet(void) {
+    DIR *d = opendir("/proc/sys/net/ipv4/conf");
+    if (!d) return 0;
+    int any = 0;
+    for (struct dirent *e; !any && (e = readdir(d));) {
+        if (e->d_name[0] == '.' || !strcmp(e->d_name, "lo")) continue;
+        char path[320];
+        snprintf(path, sizeof path, "/proc/sys/net/ipv4/conf/%s/route_localnet", e->d_name);
+        FILE *f = fopen(path, "r");
+        if (!f) continue;
+        int v = 0;
+        if (fscanf(f, "%d", &v) == 1 && v) any = 1;
+        fclose(f);
+    }
+    closedir(d);
+    return any;
+}
+
 static void print_stats(void) {
     if (!g_stats) return;
     tcpcsum_ctx_stats_t cs;
     memset(&cs, 0, sizeof cs);
+    uint64_t served = 0, released = 0, full = 0;
+    arena_counters(&g_arena, &served, &released, &full);
     pthread_mutex_lock(&g_mu);
     if (g_ctx) tcpcsum_ctx_get_stats(g_ctx, &cs);
     pthread_mutex_unlock(&g_mu);
@@ -121,13 +258,16 @@ static void print_stats(void) {
             "tcpcsum_preload: tx batches=%llu packets=%llu filled=%llu verified=%llu verify_failed=%llu "
             "skipped=%llu | rx batches=%llu packets=%llu verified=%llu verify_failed=%llu skipped=%llu "
             "partial=%llu dropped=%llu | errors=%llu | ctx in_place=%llu staged=%llu copy_threads=%llu "
-            "cpu_caller_us=%llu cpu_workers_us=%llu\n",
+            "cpu_caller_us=%llu cpu_workers_us=%llu | pool on=%d served=%llu released=%llu full=%llu "
+            "device=%d localnet=%d\n",
             g_st.tx_batches, g_st.tx_packets, g_st.tx_filled, g_st.tx_verified, g_st.tx_verify_failed,
             g_st.tx_skipped, g_st.rx_batches, g_st.rx_packets, g_st.rx_verified, g_st.rx_verify_failed,
             g_st.rx_skipped, g_st.rx_partial, g_st.rx_dropped, g_st.errors,
             (unsigned long long) cs.pkts_in_place, (unsigned long long) cs.pkts_staged,
             (unsigned long long) cs.copy_threads, (unsigned long long) (cs.ns_cpu_caller / 1000),
-            (unsigned long long) (cs.ns_cpu_workers / 1000));
+            (unsigned long long) (cs.ns_cpu_workers / 1000), arena_base(&g_arena) != NULL,
+            (unsigned long long) served, (unsigned long long) released, (unsigned long long) full, g_device,
+            g_localnet);
 }
 
 static void init_once(void) {
@@ -139,9 +279,15 @@ static void init_once(void) {
     g_iphdr = env_flag("TCPCSUM_PRELOAD_IPHDR");
     g_any = env_flag("TCPCSUM_PRELOAD_ANY_SOCKET");
     g_stats = env_flag("TCPCSUM_PRELOAD_STATS");
+    const char *dv = getenv("TCPCSUM_PRELOAD_DEVICE");
+    g_device = dv && *dv ? atoi(dv) : 0;
+    g_localnet = g_rx != MODE_OFF && any_route_localnet();
+    if (g_localnet)
+        fprintf(stderr, "tcpcsum_preload: route_localnet is set on this host: CHECKSUM_PARTIAL segments get no "
+                        "loopback exception\n");
     if (env_flag("TCPCSUM_PRELOAD_INPLACE"))
         fprintf(stderr, "tcpcsum_preload: TCPCSUM_PRELOAD_INPLACE is gone (ABI v4): buffers from "
-                        "tcpcsum_host_alloc are filled in place, all others are copied\n");
+                        "tcpcsum_host_alloc (or TCPCSUM_PRELOAD_POOL=1) are filled in place, all others are copied\n");
     atexit(print_stats);
 }
 
@@ -152,19 +298,21 @@ void tcpcsum_preload_get_stats(struct tcpcsum_preload_stats *out) {
     pthread_mutex_unlock(&g_mu);
 }
 
+static int sock_opt(int fd, int opt) {
+    int v = -1;
+    socklen_t len = sizeof v;
+    return getsockopt(fd, SOL_SOCKET, opt, &v, &len) == 0 ? v : -1;
+}
+
 static int wants_fd(int fd) {
-    if (g_any) return 1;
-    int type = 0;
-    socklen_t len = sizeof type;
-    if (getsockopt(fd, SOL_SOCKET, SO_TYPE, &type, &len) != 0) return 0;
-    return type == SOCK_RAW;
+    return g_any || sock_opt(fd, SO_TYPE) == SOCK_RAW;
 }
 
 /* g_mu held. */
 static int ensure_ctx(void) {
     if (g_ctx_failed) return -1;
     if (!g_ctx) {
-        int rc = tcpcsum_ctx_create(0, 0, &g_ctx);
+        int rc = tcpcsum_ctx_create(g_device, 0, &g_ctx);
         const char *w = getenv("TCPCSUM_PRELOAD_WAIT");
         if (!rc && !(w && !strcmp(w, "spin"))) rc = tcpcsum_ctx_set_flags(g_ctx, TCPCSUM_CTX_BLOCKING_WAIT);
         if (!rc) {
@@ -173,8 +321,8 @@ static int ensure_ctx(void) {
             if (!g_out || !g_status) rc = TCPCSUM_ENOMEM;
         }
         if (rc) {
-            fprintf(stderr, "tcpcsum_preload: GPU checksum path unavailable (%s); refusing to send/accept "
-                            "packets with unchecked checksums\n", tcpcsum_strerror(rc));
+            fprintf(stderr, "tcpcsum_preload: GPU checksum path unavailable on device %d (%s); refusing to "
+                            "send/accept packets with unchecked checksums\n", g_device, tcpcsum_strerror(rc));
             g_ctx_failed = 1;
             tcpcsum_ctx_destroy(g_ctx);
             g_ctx = NULL;
@@ -196,15 +344,17 @@ static int loopback_pair(const uint8_t *p) {
 }
 
 /* g_mu held. Whether message k of a finished batch is kept (rx drop), and its
- * accounting. p / len: its bytes as the GPU batch saw them. */
-static int account(int k, int fill, int is_tx, const uint8_t *p, uint32_t len) {
+ * accounting. p / len: its bytes as the GPU batch saw them; multi: it had several
+ * iovecs; partial_ok: the socket may claim the loopback CHECKSUM_PARTIAL exception. */
+static int account(int k, int fill, int is_tx, const uint8_t *p, uint32_t len, int multi, int partial_ok) {
     const int skipped = (g_status[k] & TCPCSUM_PKT_SKIPPED) != 0;
     if (skipped) {
         if (is_tx) g_st.tx_skipped++; else g_st.rx_skipped++;
         /* an IPv4/TCP segment that could not be verified (truncated, bad IHL or
-         * lengths) is not passed on unverified in drop mode; anything else is
-         * not TCP and goes through (the reference filters it, loop.c:319) */
-        return !(g_rx == MODE_DROP && !is_tx && is_ipv4_tcp(p, len));
+         * lengths) is not passed on unverified in drop mode; a scatter read
+         * (several iovecs, the first not holding the packet) and anything that is
+         * not TCP go through (the reference filters the latter, loop.c:319) */
+        return !(g_rx == MODE_DROP && !is_tx && !multi && is_ipv4_tcp(p, len));
     }
     if (fill) {
         g_st.tx_filled++;
@@ -212,39 +362,32 @@ static int account(int k, int fill, int is_tx, const uint8_t *p, uint32_t len) {
     }
     /* CHECKSUM_PARTIAL segments (checksum left to offload, Linux loopback;
      * SURVEY.md §4.5) are counted apart, not as corrupt — on 127/8 only */
-    const int partial = (g_status[k] & TCPCSUM_PKT_CSUM_PARTIAL) != 0 && loopback_pair(p);
+    const int partial = partial_ok && (g_status[k] & TCPCSUM_PKT_CSUM_PARTIAL) != 0 && loopback_pair(p);
     const int bad = (g_out[k] != 0 && !partial) || (g_status[k] & TCPCSUM_PKT_IPHDR_BAD);
     if (is_tx) { g_st.tx_verified++; if (bad) g_st.tx_verify_failed++; }
     else { g_st.rx_verified++; if (bad) g_st.rx_verify_failed++; if (partial) g_st.rx_partial++; }
     return !bad;
 }
 
-/* Checksum a batch of <= 1024 messages on the GPU (one iov_base per message:
- * the reference's layout, loop.c:53-54; other messages are SKIPPED). lens:
- * each message's byte count (iov_len for tx, msg_len for rx). fill: store the
- * checks in the caller's buffers. keep (nullable): per message, whether it
- * passed. Returns 0, or -1 with errno set. */
+/* Checksum a batch of <= 1024 messages on the GPU, each from its first iovec
+ * (one iov_base per message: the reference's layout, loop.c:53-54). lens: the
+ * bytes of that iovec worth reading (iov_len for tx, msg_len bounded by iov_len
+ * for rx); a packet longer than that is SKIPPED. fill: store the checks in the
+ * caller's buffers. keep (nullable): per message, whether it passed. partial_ok:
+ * see account(). Returns 0, or -1 with errno set. */
 static int gpu_batch(struct mmsghdr *vec, unsigned int vlen, const unsigned int *lens, int fill, int is_tx,
-                     unsigned char *keep) {
+                     unsigned char *keep, int partial_ok) {
     void *ptrs[1024];
     uint32_t plen[1024];
-    const uint8_t *head[1024];   /* the message's first bytes, to tell IPv4/TCP from the rest */
-    uint32_t hlen[1024];
     for (unsigned int i = 0; i < vlen; ++i) {
         const struct msghdr *h = &vec[i].msg_hdr;
-        const int one = h->msg_iovlen == 1;
-        ptrs[i] = one ? h->msg_iov[0].iov_base : NULL;
-        plen[i] = one ? lens[i] : 0;   /* < 20 bytes: SKIPPED, nothing read */
-        head[i] = h->msg_iovlen >= 1 && h->msg_iov ? (const uint8_t *) h->msg_iov[0].iov_base : NULL;
-        hlen[i] = 0;
-        if (head[i]) {
-            const size_t cap = h->msg_iov[0].iov_len;
-            const unsigned int got = is_tx ? (unsigned int) cap : vec[i].msg_len;
-            hlen[i] = (uint32_t) (got < cap ? got : cap);
-        }
+        ptrs[i] = h->msg_iovlen >= 1 && h->msg_iov ? h->msg_iov[0].iov_base : NULL;
+        plen[i] = ptrs[i] ? lens[i] : 0;   /* < 20 bytes: SKIPPED, nothing read */
     }
     pthread_mutex_lock(&g_mu);
+    t_guard = 1;
     if (ensure_ctx()) {
+        t_guard = 0;
         g_st.errors++;
         pthread_mutex_unlock(&g_mu);
         errno = ENXIO;
@@ -252,6 +395,7 @@ static int gpu_batch(struct mmsghdr *vec, unsigned int vlen, const unsigned int 
     }
     int mode = (fill ? TCPCSUM_IPV4_FILL : TCPCSUM_IPV4_VERIFY) | (g_iphdr ? TCPCSUM_IPV4_IPHDR : 0);
     int rc = tcpcsum_ipv4_batch_ptrs_host(g_ctx, ptrs, plen, vlen, mode, g_out, g_status);
+    t_guard = 0;
     if (rc) {
         g_st.errors++;
         pthread_mutex_unlock(&g_mu);
@@ -260,11 +404,24 @@ static int gpu_batch(struct mmsghdr *vec, unsigned int vlen, const unsigned int 
         return -1;
     }
     for (unsigned int i = 0; i < vlen; ++i) {
-        const int ok = account((int) i, fill, is_tx, head[i], hlen[i]);
+        const int ok = account((int) i, fill, is_tx, (const uint8_t *) ptrs[i], plen[i], vec[i].msg_hdr.msg_iovlen > 1,
+                               partial_ok);
         if (keep) keep[i] = (unsigned char) ok;
     }
     pthread_mutex_unlock(&g_mu);
     return 0;
+}
+
+/* The readable bytes of message m's first iovec: iov_len (tx), or what was received
+ * into it (rx: msg_len — with MSG_TRUNC a raw or UDP socket reports the datagram's
+ * real length there, which may exceed the buffer). */
+static unsigned int first_iov_bytes(const struct mmsghdr *m, int is_tx) {
+    const struct msghdr *h = &m->msg_hdr;
+    if (h->msg_iovlen < 1 || !h->msg_iov) return 0;
+    const size_t cap = h->msg_iov[0].iov_len;
+    const size_t got = is_tx ? cap : m->msg_len;
+    const size_t n = got < cap ? got : cap;
+    return n > 0xFFFFFFFFu ? 0xFFFFFFFFu : (unsigned int) n;
 }
 
 int sendmmsg(int fd, struct mmsghdr *vec, unsigned int vlen, int flags) {
@@ -274,11 +431,8 @@ int sendmmsg(int fd, struct mmsghdr *vec, unsigned int vlen, int flags) {
         unsigned int done = 0;
         while (done < vlen) {   /* GPU batches of <= 1024 messages */
             unsigned int cnt = vlen - done < 1024 ? vlen - done : 1024;
-            for (unsigned int i = 0; i < cnt; ++i) {
-                const struct msghdr *h = &vec[done + i].msg_hdr;
-                lens[i] = h->msg_iovlen == 1 ? (unsigned int) h->msg_iov[0].iov_len : 0;
-            }
-            if (gpu_batch(vec + done, cnt, lens, g_tx == MODE_FILL, 1, NULL)) return -1;
+            for (unsigned int i = 0; i < cnt; ++i) lens[i] = first_iov_bytes(&vec[done + i], 1);
+            if (gpu_batch(vec + done, cnt, lens, g_tx == MODE_FILL, 1, NULL, 0)) return -1;
             pthread_mutex_lock(&g_mu);
             g_st.tx_batches++;
             g_st.tx_packets += cnt;
@@ -297,16 +451,12 @@ int recvmmsg(int fd, struct mmsghdr *vec, unsigned int vlen, int flags, struct t
         unsigned char keep[1024];
         unsigned int done = 0, kept = 0;
         const int by_entry = g_rx == MODE_DROP && rx_by_entry(vec, (unsigned int) r);
+        /* the loopback CHECKSUM_PARTIAL exception: AF_INET sockets, no route_localnet */
+        const int partial_ok = !g_localnet && sock_opt(fd, SO_DOMAIN) == AF_INET;
         while (done < (unsigned int) r) {
             unsigned int cnt = (unsigned int) r - done < 1024 ? (unsigned int) r - done : 1024;
-            /* the bytes received, never past the buffer: with MSG_TRUNC in flags a
-             * raw or UDP socket reports the datagram's real length in msg_len */
-            for (unsigned int i = 0; i < cnt; ++i) {
-                const struct msghdr *h = &vec[done + i].msg_hdr;
-                const unsigned int cap = h->msg_iovlen == 1 ? (unsigned int) h->msg_iov[0].iov_len : 0;
-                lens[i] = vec[done + i].msg_len < cap ? vec[done + i].msg_len : cap;
-            }
-            if (gpu_batch(vec + done, cnt, lens, 0, 0, keep)) return -1;
+            for (unsigned int i = 0; i < cnt; ++i) lens[i] = first_iov_bytes(&vec[done + i], 0);
+            if (gpu_batch(vec + done, cnt, lens, 0, 0, keep, partial_ok)) return -1;
             if (g_rx == MODE_DROP) {
                 /* stable partition by swaps: passing messages move to the front in
                  * arrival order; failing ones end up behind them, still in the

@@ -98,6 +98,16 @@ inline int env_int(const char* name, int dflt) {
     return e && *e ? atoi(e) : dflt;
 }
 
+// The switch of a measured-and-rejected or A/B-only variant of the host pipeline:
+// read from the environment in measurement builds only (-DTCPCSUM_MEASUREMENT_BUILD=1);
+// a product library takes the measured default, and the variable's name is not even
+// in its binary. tcpcsum_build_info() lists the runtime knobs a build reads.
+#if TCPCSUM_MEASUREMENT_BUILD
+#define TCPCSUM_MEAS_KNOB(name, dflt) tcpcsum::env_int(name, dflt)
+#else
+#define TCPCSUM_MEAS_KNOB(name, dflt) (dflt)
+#endif
+
 // NUMA node of the (touched) host page at p, or -1.
 inline int page_node(const void* p) {
     int node = -1;
@@ -133,11 +143,15 @@ struct Pinned {
     Pinned(const Pinned&) = delete;
     Pinned& operator=(const Pinned&) = delete;
     ~Pinned() { release(); }
-    // grow to at least `need` bytes; the caller knows no kernel is using it
+    // grow to at least `need` bytes; the caller knows no kernel is using it. Doubling
+    // (small per-batch arrays grow a few times), but never past `need` rounded up to
+    // 2 MiB: a 128 MiB staging slot is 128 MiB, not the next power of two
     hipError_t ensure(size_t need) {
         if (need <= bytes) return hipSuccess;
         size_t nb = bytes ? bytes : 4096;
         while (nb < need) nb *= 2;
+        const size_t k2m = (size_t)2 << 20;
+        nb = std::min(nb, (need + k2m - 1) / k2m * k2m);
         release();
         void* p = nullptr;
         hipError_t e = host_malloc_on(&p, nb, node);
@@ -190,7 +204,7 @@ struct tcpcsum_ctx {
     // boxes from the start), one stream never below 51.2 (tools/dma_state_probe.hip)
     hipStream_t st = nullptr;
     // pageable uniform batches: nslots pinned staging chunks in flight
-    // (TCPCSUM_HOST_SLOTS, 2..4); slot_ev[s] is recorded after the last device
+    // (2; measurement builds: TCPCSUM_HOST_SLOTS, 2..4); slot_ev[s] is recorded after the last device
     // work that reads staging slot s, before the copy threads refill it
     int nslots = 2;
     hipEvent_t slot_ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -215,31 +229,31 @@ struct tcpcsum_ctx {
     tcpcsum::PinnedLookup<tcpcsum::HipHostBackend> pinned{backend};
     std::unique_ptr<tcpcsum::CopyPool> pool;
     int gpu_node = -1;   // the GPU's NUMA node, where the staging is allocated (-1: unknown / off)
-    // threads a staged wire batch copies on, the caller included (TCPCSUM_HOST_WIRE_THREADS):
-    // a releaseSend batch is ~1.5 MB, where extra threads cost more CPU than they save time
+    // threads a staged wire batch copies on, the caller included (1): a releaseSend batch
+    // is ~1.5 MB, where extra threads cost more CPU than they save time
     int wire_threads = 1;
     // threads a bulk copy (uniform staging chunks, per-segment arrays) runs on, the caller
-    // included (TCPCSUM_HOST_BULK_THREADS, default 4; 0 = every copy thread): the DMA to
-    // HBM bounds the pageable pipeline, and 4 threads copy 1.5 GB in ~14.5 ms beside its
-    // ~28 ms at the rate 8 reach, with 0.060 instead of 0.087 core-s
-    // (profiles/r04_host_bulk_threads_ab.jsonl)
+    // included (4, at most the pool's): the DMA to HBM bounds the pageable pipeline, and 4
+    // threads copy 1.5 GB in ~14.5 ms beside its ~28 ms at the rate 8 reach, with 0.060
+    // instead of 0.087 core-s (profiles/r04_host_bulk_threads_ab.jsonl)
     int bulk_threads = 4;
     int stage_threads = 1;   // the current staged batch's: wire_threads, or all for a large batch
-    int stage_blocks = 1;    // a small single-threaded staged batch copied and launched in this many blocks
     // TCPCSUM_CTX_BLOCKING_WAIT: wait for the device by polling this event between
     // short sleeps instead of HIP's spin in hipStreamSynchronize
     hipEvent_t done_ev = nullptr;
-    uint64_t poll_ns = 5000;     // first sleep between polls after the expected time (TCPCSUM_HOST_POLL_US, default 5)
-    bool nt_copy = true;   // streaming stores for the uniform chunks (TCPCSUM_HOST_NT=0: plain memcpy)
-    bool stage_one_pass = true;   // wire staging laid out by bounds, one pass (TCPCSUM_HOST_STAGE_PASSES=2: by lengths)
-    bool uniform_dma = true;   // staged uniform chunks go to HBM by DMA (TCPCSUM_HOST_DMA=0: kernel reads them over PCIe)
-    bool pinned_dma = true;    // large page-locked uniform batches go to HBM by DMA (TCPCSUM_HOST_PINNED_DMA=0: in place)
-    bool slot_sleep = true;
+    // The product's choices below; measurement builds can flip each (the TCPCSUM_HOST_*
+    // name in brackets) for A/B runs:
+    uint64_t poll_ns = 5000;     // first sleep between polls after the expected time (POLL_US)
+    bool nt_copy = true;   // streaming stores for the uniform chunks (NT=0: plain memcpy)
+    bool stage_one_pass = true;   // wire staging laid out by bounds, one pass (STAGE_PASSES=2: by lengths)
+    bool uniform_dma = true;   // staged uniform chunks go to HBM by DMA (DMA=0: kernel reads them over PCIe)
+    bool pinned_dma = true;    // large page-locked uniform batches go to HBM by DMA (PINNED_DMA=0: in place)
+    bool slot_sleep = true;    // BLOCKING_WAIT also sleeps in staging-slot waits (SLOT_SLEEP=0: spin)
     // wire staging with streaming stores, each packet from a 64-B line of its own, one
-    // fence per copy job (TCPCSUM_HOST_WIRE_NT=0: plain memcpy from 16-B starts). The
-    // seam's 1024 x 1500-B batch: 102-112 instead of 119-171 us, 65-75 instead of
-    // 72-102 core-us (profiles/r04_wire_nt_ab.jsonl)
-    bool wire_nt = true;    // BLOCKING_WAIT also sleeps in staging-slot waits (TCPCSUM_HOST_SLOT_SLEEP=0: spin)
+    // fence per copy job (WIRE_NT=0: plain memcpy from 16-B starts). The seam's 1024 x
+    // 1500-B batch: 102-112 instead of 119-171 us, 65-75 instead of 72-102 core-us
+    // (profiles/r04_wire_nt_ab.jsonl)
+    bool wire_nt = true;
     tcpcsum_ctx_stats_t stats{};
     std::mutex mu;
 };
@@ -481,56 +495,6 @@ int stage_packets(tcpcsum_ctx* c, uint64_t* k_off, uint32_t* k_len, size_t* stag
     return TCPCSUM_OK;
 }
 
-// Single-threaded staging of a small batch in B blocks (TCPCSUM_HOST_STAGE_BLOCKS): the
-// packets of block b are copied, then the kernel over packet indices [n*b/B, n*(b+1)/B)
-// is queued, so block b's kernel runs over PCIe while block b+1 is copied. Returns
-// -1 when the batch does not qualify (the caller stages it in one piece).
-int stage_and_launch_blocks(tcpcsum_ctx* c, uint64_t n, uint32_t in_cap, uint64_t in_foot, int mode,
-                            uint16_t* kout, uint8_t* kst, hipStream_t st, const tcpcsum::Tuning& tu) {
-    const size_t m = c->g_idx.size();
-    const int B = c->stage_blocks;
-    if (B <= 1 || m == 0 || n < (uint64_t)B * 16u || !c->stage_one_pass) return -1;
-    size_t span = 0;
-    uint32_t cap = in_cap;
-    for (size_t k = 0; k < m; ++k) {
-        c->g_off[k] = span;
-        span += ((size_t)c->g_len[k] + 15u) & ~(size_t)15u;
-        cap = std::max(cap, c->g_len[k]);
-    }
-    if (span > kSmallStage || c->wire_threads != 1) return -1;
-    const uint64_t t0 = tcpcsum::now_ns();
-    hipError_t e = c->gath.ensure(span ? span : 16);
-    if (e != hipSuccess) {
-        tcpcsum::note_hip_error((int)e);
-        return TCPCSUM_ENOMEM;
-    }
-    uint64_t* k_off = (uint64_t*)c->p_off.h;
-    uint32_t* k_len = (uint32_t*)c->p_len.h;
-    size_t k = 0, copied = 0;
-    uint64_t ns_launch = 0;
-    for (int b = 0; b < B; ++b) {
-        const uint64_t i0 = n * (uint64_t)b / (uint64_t)B, i1 = n * (uint64_t)(b + 1) / (uint64_t)B;
-        for (; k < m && c->g_idx[k] < i1; ++k) {
-            c->g_len[k] = copy_len(c->g_src[k], c->g_len[k]);
-            memcpy(c->gath.h + c->g_off[k], c->g_src[k], c->g_len[k]);
-            k_off[c->g_idx[k]] = (uint64_t)(uintptr_t)(c->gath.d + c->g_off[k]);
-            k_len[c->g_idx[k]] = c->g_len[k];
-            copied += c->g_len[k];
-        }
-        const uint64_t l0 = tcpcsum::now_ns();
-        tcpcsum::launch_ipv4(nullptr, (const uint64_t*)c->p_off.d + i0, (const uint32_t*)c->p_len.d + i0, i1 - i0,
-                             cap, ~0ull, (in_foot + span) * (i1 - i0) / n, mode, kout + i0, kst + i0, nullptr, st, tu);
-        const int rc = check_launch();
-        if (rc) return rc;
-        ns_launch += tcpcsum::now_ns() - l0;
-    }
-    c->stats.ns_copy += tcpcsum::now_ns() - t0 - ns_launch;
-    c->stats.pkts_staged += m;
-    c->stats.bytes_staged += copied;
-    c->stage_threads = 1;
-    return TCPCSUM_OK;
-}
-
 // Stage the packets in g_* and launch the wire kernel over all n packets on
 // st (k_off / k_len of the packets read in place already set; in_cap /
 // in_foot their largest length and sum). One launch after the copies: queueing
@@ -541,8 +505,6 @@ int stage_and_launch_blocks(tcpcsum_ctx* c, uint64_t n, uint32_t in_cap, uint64_
 // the copies (profiles/r03_hostpath_sweep_wire_split.jsonl).
 int stage_and_launch(tcpcsum_ctx* c, uint64_t n, uint32_t in_cap, uint64_t in_foot, int mode, uint16_t* kout,
                      uint8_t* kst, hipStream_t st, const tcpcsum::Tuning& tu) {
-    const int rb = stage_and_launch_blocks(c, n, in_cap, in_foot, mode, kout, kst, st, tu);
-    if (rb != -1) return rb;
     size_t staged = 0;
     int rc = stage_packets(c, (uint64_t*)c->p_off.h, (uint32_t*)c->p_len.h, &staged);
     if (rc) return rc;
@@ -617,25 +579,24 @@ int tcpcsum_ctx_create(int device, size_t scratch_bytes, tcpcsum_ctx_t** out) {
         delete c;
         return TCPCSUM_ENOMEM;
     }
-    c->wire_threads = std::max(1, std::min(c->pool->threads(), tcpcsum::env_int("TCPCSUM_HOST_WIRE_THREADS", 1)));
+    c->wire_threads = std::max(1, std::min(c->pool->threads(), TCPCSUM_MEAS_KNOB("TCPCSUM_HOST_WIRE_THREADS", 1)));
     c->stats.copy_threads = (uint64_t)c->wire_threads;
-    c->bulk_threads = std::max(0, std::min(c->pool->threads(), tcpcsum::env_int("TCPCSUM_HOST_BULK_THREADS", 4)));
+    c->bulk_threads = std::max(0, std::min(c->pool->threads(), TCPCSUM_MEAS_KNOB("TCPCSUM_HOST_BULK_THREADS", 4)));
     c->stats.bulk_threads = (uint64_t)(c->bulk_threads ? c->bulk_threads : c->pool->threads());
-    c->nt_copy = tcpcsum::env_int("TCPCSUM_HOST_NT", 1) != 0;
-    c->poll_ns = (uint64_t)std::max(1, tcpcsum::env_int("TCPCSUM_HOST_POLL_US", 5)) * 1000u;
-    c->stage_one_pass = tcpcsum::env_int("TCPCSUM_HOST_STAGE_PASSES", 1) == 1;
-    c->uniform_dma = tcpcsum::env_int("TCPCSUM_HOST_DMA", 1) != 0;
-    c->pinned_dma = tcpcsum::env_int("TCPCSUM_HOST_PINNED_DMA", 1) != 0;
-    c->slot_sleep = tcpcsum::env_int("TCPCSUM_HOST_SLOT_SLEEP", 1) != 0;
-    c->wire_nt = tcpcsum::env_int("TCPCSUM_HOST_WIRE_NT", 1) != 0;
-    c->stage_blocks = std::max(1, std::min(16, tcpcsum::env_int("TCPCSUM_HOST_STAGE_BLOCKS", 1)));
-    c->nslots = std::max(2, std::min(4, tcpcsum::env_int("TCPCSUM_HOST_SLOTS", 2)));
+    c->nt_copy = TCPCSUM_MEAS_KNOB("TCPCSUM_HOST_NT", 1) != 0;
+    c->poll_ns = (uint64_t)std::max(1, TCPCSUM_MEAS_KNOB("TCPCSUM_HOST_POLL_US", 5)) * 1000u;
+    c->stage_one_pass = TCPCSUM_MEAS_KNOB("TCPCSUM_HOST_STAGE_PASSES", 1) == 1;
+    c->uniform_dma = TCPCSUM_MEAS_KNOB("TCPCSUM_HOST_DMA", 1) != 0;
+    c->pinned_dma = TCPCSUM_MEAS_KNOB("TCPCSUM_HOST_PINNED_DMA", 1) != 0;
+    c->slot_sleep = TCPCSUM_MEAS_KNOB("TCPCSUM_HOST_SLOT_SLEEP", 1) != 0;
+    c->wire_nt = TCPCSUM_MEAS_KNOB("TCPCSUM_HOST_WIRE_NT", 1) != 0;
+    c->nslots = std::max(2, std::min(4, TCPCSUM_MEAS_KNOB("TCPCSUM_HOST_SLOTS", 2)));
     c->dma_chunk = scratch_bytes ? scratch_bytes : kDefaultDmaChunk;
     c->in_place_chunk = scratch_bytes ? scratch_bytes : kDefaultInPlaceChunk;
     if (!scratch_bytes) {
-        c->chunk = (size_t)std::max(1, tcpcsum::env_int("TCPCSUM_HOST_CHUNK_MB", (int)(kDefaultChunk >> 20))) << 20;
+        c->chunk = (size_t)std::max(1, TCPCSUM_MEAS_KNOB("TCPCSUM_HOST_CHUNK_MB", (int)(kDefaultChunk >> 20))) << 20;
         c->dma_chunk =
-            (size_t)std::max(1, tcpcsum::env_int("TCPCSUM_HOST_DMA_CHUNK_MB", (int)(kDefaultDmaChunk >> 20))) << 20;
+            (size_t)std::max(1, TCPCSUM_MEAS_KNOB("TCPCSUM_HOST_DMA_CHUNK_MB", (int)(kDefaultDmaChunk >> 20))) << 20;
     }
     e = hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking);
     if (e != hipSuccess) {
@@ -662,12 +623,13 @@ void tcpcsum_ctx_destroy(tcpcsum_ctx_t* c) {
     if (!c) return;
     DeviceGuard g(c->device);
     if (c->st) hipStreamSynchronize(c->st);
+    c->pool.reset();   // the copy threads are joined here, before any HIP object goes
     if (c->done_ev) hipEventDestroy(c->done_ev);
     for (int i = 0; i < 4; ++i)
         if (c->slot_ev[i]) hipEventDestroy(c->slot_ev[i]);
     if (c->d_buf) hipFree(c->d_buf);
     if (c->st) hipStreamDestroy(c->st);
-    delete c;   // pinned buffers and copy threads go with it
+    delete c;   // pinned buffers go with it
 }
 
 int tcpcsum_ctx_set_tuning(tcpcsum_ctx_t* c, const tcpcsum_tuning_t* tune) {
@@ -774,7 +736,8 @@ int tcpcsum_batch_uniform_host(tcpcsum_ctx_t* c, const void* h_base, uint64_t st
         if (he == hipSuccess) c->d_buf_bytes = bytes;
         return he;
     };
-    const uint64_t per = per_piece(c->chunk);
+    // a staging slot holds a piece plus its start's misalignment (16 B) within `chunk`
+    const uint64_t per = per_piece(c->chunk > 32 ? c->chunk - 16 : c->chunk);
     const uint8_t* zb = (const uint8_t*)pinned_dev_ptr(h_base, span);
     if (zb && (!c->pinned_dma || per_piece(c->in_place_chunk) * 2 > n)) {
         tcpcsum::launch_uniform(zb, stride, len, kss, sum_start, kout, n, c->st, tu);

@@ -37,6 +37,22 @@
     (TCPCSUM_TUNING_VARIANTS != 0 || TCPCSUM_TX_KNOCKOUT != 0 || TCPCSUM_WIRE_WAVES != 1 || TCPCSUM_TX_WAVES != 1)
 #error "tuning / knock-out / waves knobs are for measurement builds only (-DTCPCSUM_MEASUREMENT_BUILD=1), never a product library"
 #endif
+// Environment variables a context reads at creation (tcpcsum_build_info "runtime_knobs"):
+// a product library reads the deployment ones only — copy threads, their NUMA pinning
+// and spin, and the launcher's rank count on the node (copy_pool.h); a measurement build
+// also reads the switches of the host pipeline's A/B variants (tcpcsum_host.hip,
+// TCPCSUM_MEAS_KNOB), which a product library never sees.
+#define TCPCSUM_PRODUCT_RUNTIME_KNOBS \
+    "\"TCPCSUM_HOST_THREADS\", \"TCPCSUM_HOST_NUMA\", \"TCPCSUM_HOST_SPIN_US\", \"LOCAL_WORLD_SIZE\""
+#if TCPCSUM_MEASUREMENT_BUILD
+#define TCPCSUM_RUNTIME_KNOBS_JSON TCPCSUM_PRODUCT_RUNTIME_KNOBS \
+    ", \"TCPCSUM_HOST_WIRE_THREADS\", \"TCPCSUM_HOST_BULK_THREADS\", \"TCPCSUM_HOST_NT\", " \
+    "\"TCPCSUM_HOST_POLL_US\", \"TCPCSUM_HOST_STAGE_PASSES\", \"TCPCSUM_HOST_DMA\", " \
+    "\"TCPCSUM_HOST_PINNED_DMA\", \"TCPCSUM_HOST_SLOT_SLEEP\", \"TCPCSUM_HOST_WIRE_NT\", " \
+    "\"TCPCSUM_HOST_SLOTS\", \"TCPCSUM_HOST_CHUNK_MB\", \"TCPCSUM_HOST_DMA_CHUNK_MB\""
+#else
+#define TCPCSUM_RUNTIME_KNOBS_JSON TCPCSUM_PRODUCT_RUNTIME_KNOBS
+#endif
 // Hash of the sources the library was compiled from (the Makefile passes it).
 #ifndef TCPCSUM_SRC_HASH
 #define TCPCSUM_SRC_HASH "unknown"

@@ -918,6 +918,31 @@ __device__ __forceinline__ void stg_wt16(uint8_t* p, u32x4 v) {
     }
 }
 
+// 16 bytes at the 16-B aligned p, written through, relative to a wave-uniform
+// base: a kernel argument, or a readfirstlane taken in converged code before the
+// (divergent) store branch — stg_wt16 builds its base from the first active lane
+// inside the branch, a readfirstlane pair and the descriptor per store. A lane
+// outside [base, base + 4 GiB) takes a default-policy store (same bytes).
+__device__ __forceinline__ void stg_wt16_at(uint8_t* p, u32x4 v, uint64_t base) {
+    const uint64_t a = (uint64_t)(uintptr_t)p;
+    const uint64_t rel = a - base;
+    if (a >= base && rel <= 0xFFFFFF00ull) {
+        const __amdgpu_buffer_rsrc_t r =
+            __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>((uintptr_t)base), 0, -1, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)(uint32_t)rel, 0, kCpolSc0Sc1);
+    } else {
+        *(gptr<u32x4>)(p) = v;
+    }
+}
+
+// The write-through base for a wave whose stores land near addr (any lane's, taken
+// where the wave is converged): 2 GiB below it, so the window covers addr +- 2 GiB.
+__device__ __forceinline__ uint64_t wt_base_near(uint64_t addr) {
+    const uint64_t first = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(addr >> 32)) << 32) |
+                           (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)addr);
+    return first > 0x80000000ull ? first - 0x80000000ull : 0ull;
+}
+
 // A native u16 at p, written through: a lone 2-byte store per packet in the
 // middle of a read stream costs less that way (tools/fill_store_probe.hip: +62
 // vs +72 us per 1M stores).
@@ -1074,6 +1099,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(wire_waves(
             }
         }
     };
+    // FILL's line stores go out written through relative to a wave-uniform base
+    // (stg_wt16_at): the region's start (rounded down to its 128-B window) when the
+    // whole region lies within 4 GiB of it — a kernel argument, no per-store setup —
+    // else 2 GiB below the tile's first packet, taken once per tile where the wave
+    // is converged, not inside the divergent store branch.
+    const bool region_base = !PL && limit <= 0xFFFFFE00ull;
+    uint64_t wt_base = region_base ? ((uint64_t)(uintptr_t)pkts & ~(uint64_t)127u) : 0u;
+    const __amdgpu_buffer_rsrc_t wt_rsrc =
+        __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>((uintptr_t)wt_base), 0, -1, 0x00020000);
     auto process = [&](int u, uint64_t i) -> IpDone {
         IpDone d;
         d.w = false;
@@ -1230,7 +1264,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(wire_waves(
                     u32x4 x = v[u][0];
                     if (idx == (cpos >> 4)) patch(x, cpos, (uint32_t)d.c);
                     if (iphdr && idx == (ipos >> 4)) patch(x, ipos, (uint32_t)ic_fill);
-                    stg_wt16(ip - m + (uint64_t)idx * 16u, x);
+                    uint8_t* dst = ip - m + (uint64_t)idx * 16u;
+                    if (region_base)   // wave-uniform: every line of the region is in the window
+                        __builtin_amdgcn_raw_buffer_store_b128(
+                            x, wt_rsrc, (int)(uint32_t)((uint64_t)(uintptr_t)dst - wt_base), 0, kCpolSc0Sc1);
+                    else
+                        stg_wt16_at(dst, x, wt_base);
                 }
                 d.fill = false;   // stored
             }
@@ -1266,6 +1305,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(wire_waves(
     load_off(t);
     for (; t < ntiles; t += nwaves) {
         issue(t);
+        if constexpr (!VER) {   // converged here: the line stores' base for this tile
+            if (!region_base) wt_base = wt_base_near((uint64_t)(uintptr_t)p[0].ip);
+        }
         // the next tile's offsets, in flight while this tile is summed
         load_off(t + nwaves);
 #pragma unroll
@@ -1726,9 +1768,15 @@ __global__ __launch_bounds__(256) void k_synth_pseudo(uint32_t* __restrict__ ss,
 // contiguous 1 KiB per load instruction, C in flight per lane), summed so it
 // cannot be dead-code eliminated. One plain store of a per-block partial at
 // the end (no atomics: 2048 same-address atomics cost ~25 us on this chip).
-template <int C>
+//
+// WR (TCPCSUM_TUNE_PROBE_WRITE): also write back, through (sc0 sc1, as the wire
+// FILL's line store), every `period`-th 128-B line it read — the bytes unchanged.
+// With period 12 over 1536-B slots that is the wire FILL's HBM traffic (every line
+// read, one whole line written per packet) without its arithmetic: the ceiling the
+// FILL is held to.
+template <int C, bool WR>
 __global__ __launch_bounds__(256) void k_probe(const uint8_t* __restrict__ src, uint64_t nchunks,
-                                               uint64_t* __restrict__ partials) {
+                                               uint64_t* __restrict__ partials, uint32_t period) {
     __shared__ uint64_t wsum[4];
     const int lane = threadIdx.x & 63;
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
@@ -1745,6 +1793,14 @@ __global__ __launch_bounds__(256) void k_probe(const uint8_t* __restrict__ src, 
 #pragma unroll
         for (int k = 0; k < C; ++k) w += chunk_w<M16>(v[k], 0u, 0u);
         acc += w;
+        if constexpr (WR) {
+#pragma unroll
+            for (int k = 0; k < C; ++k) {
+                const uint64_t idx = t * (64 * C) + (uint64_t)(k * 64 + lane);
+                if (idx < nchunks && (idx >> 3) % period == 0u)
+                    stg_wt16_at(const_cast<uint8_t*>(src) + idx * 16u, v[k], (uint64_t)(uintptr_t)src);
+            }
+        }
     }
     acc = group_sum64<64>(acc);
     if (lane == 0) wsum[threadIdx.x >> 6] = acc;
@@ -2340,9 +2396,16 @@ int launch_probe(const uint8_t* src, uint64_t nbytes, uint64_t* partials, hipStr
     const uint64_t nchunks = nbytes / 16;
     const int unroll = tu.unroll ? tu.unroll : 2;
     const unsigned g = grid_for((nchunks + 64 * 8 * unroll - 1) / (64 * 8 * unroll), max_blocks);
-    if (unroll <= 1) hipLaunchKernelGGL(k_probe<8>, dim3(g), dim3(256), 0, s, src, nchunks, partials);
-    else if (unroll == 2) hipLaunchKernelGGL(k_probe<16>, dim3(g), dim3(256), 0, s, src, nchunks, partials);
-    else hipLaunchKernelGGL(k_probe<32>, dim3(g), dim3(256), 0, s, src, nchunks, partials);
+    if (tu.flags & TCPCSUM_TUNE_PROBE_WRITE) {   // the wire FILL's traffic: shape = line period
+        const uint32_t period = tu.shape > 0 ? (uint32_t)tu.shape : 12u;
+        if (unroll <= 1) hipLaunchKernelGGL((k_probe<8, true>), dim3(g), dim3(256), 0, s, src, nchunks, partials, period);
+        else if (unroll == 2) hipLaunchKernelGGL((k_probe<16, true>), dim3(g), dim3(256), 0, s, src, nchunks, partials, period);
+        else hipLaunchKernelGGL((k_probe<32, true>), dim3(g), dim3(256), 0, s, src, nchunks, partials, period);
+        return (int)g;
+    }
+    if (unroll <= 1) hipLaunchKernelGGL((k_probe<8, false>), dim3(g), dim3(256), 0, s, src, nchunks, partials, 1u);
+    else if (unroll == 2) hipLaunchKernelGGL((k_probe<16, false>), dim3(g), dim3(256), 0, s, src, nchunks, partials, 1u);
+    else hipLaunchKernelGGL((k_probe<32, false>), dim3(g), dim3(256), 0, s, src, nchunks, partials, 1u);
     return (int)g;
 }
 

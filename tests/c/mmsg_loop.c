@@ -3,10 +3,11 @@
  * does (loop.c:27-94 releaseSend, loop.c:22-25 fetchPackageBatch), over UDP
  * loopback so no root is needed. Run under LD_PRELOAD=libtcpcsum_preload.so.
  *
- *   mmsg_loop <npkts> <out-file> [cpu-checks | corrupt | trunc | forge | plain] [pinned]
+ *   mmsg_loop <npkts> <out-file> [cpu-checks | corrupt | trunc | forge | plain] [pinned | iov2]
  *
- * Builds npkts IPv4/TCP packets in separate 32 KiB malloc'd buffers (as
- * loop.c:180-183 allocates them) with the reference's framing
+ * Allocates the loop's buffers as loop.c:180-183 does (1024 in-buffers and 1024
+ * out-buffers, 32 KiB each, malloc'd alternately), builds npkts IPv4/TCP
+ * packets, packet i in outBuffer[i % 1024] as it is queued, with the reference's framing
  * (context.c:169-206): check = 0, or — with "cpu-checks" — the check the
  * reference's CPU path would store (tcpcsum_continue == csum_continue,
  * context.c:208). "corrupt": CPU checks, then one TCP header byte (the
@@ -21,10 +22,15 @@
  * every 7th packet at i % 7 == 5 a genuine-looking one with both addresses
  * in 127/8 (daddr 127.x.y.z). "pinned": the out-buffers are carved from one
  * tcpcsum_host_alloc pool (INTEGRATION.md level 2: loop.c:180-183 allocating
- * its pool page-locked), so the interposer fills them in place.
+ * its pool page-locked), so the interposer fills them in place. "iov2": every
+ * message is received into two iovecs (the first 800 bytes of an in-buffer,
+ * then the rest): a packet the first holds whole is verified, a longer one is
+ * a scatter read the interposer passes through unverified. Under
+ * TCPCSUM_PRELOAD_POOL=1 the interposer serves the loop's 2048 mallocs from its
+ * page-locked arena and both seams run in place.
  * Under TCPCSUM_PRELOAD_RX=drop the receiver expects exactly the packets the
- * mode makes unverifiable to go missing (corrupt / forge: i % 7 == 3; trunc:
- * those longer than 600 bytes). Sends them with sendmmsg in batches
+ * mode makes unverifiable to go missing (corrupt / forge: i % 7 == 3, with iov2
+ * only those of at most 800 bytes; trunc: those longer than 600 bytes). Sends them with sendmmsg in batches
  * of <= 1024 and receives them with recvmmsg. Writes to <out-file>: for every
  * packet u32 length + the bytes as built, then u32 length + the bytes as
  * received (length 0: never received). Exit 0 on success; 3 if sendmmsg
@@ -39,10 +45,13 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/socket.h>
+#include <sys/time.h>
 #include <time.h>
 #include <unistd.h>
 
 #include "tcpcsum.h"
+
+enum { NBUF = 1024, SLOT = 1024 * 32, IOV2_FIRST = 800 };   /* loop.c:180-183 */
 
 static uint64_t rng = 0x9E3779B97F4A7C15ull;
 static uint32_t next32(void) {
@@ -89,16 +98,17 @@ static size_t build(uint8_t *b, int i, int cpu_checks, int corrupt, int forge) {
 }
 
 int main(int argc, char **argv) {
-    if (argc < 3) { fprintf(stderr, "usage: %s npkts out [cpu-checks|corrupt|trunc|forge|plain] [pinned]\n", argv[0]); return 2; }
+    if (argc < 3) { fprintf(stderr, "usage: %s npkts out [cpu-checks|corrupt|trunc|forge|plain] [pinned|iov2]\n", argv[0]); return 2; }
     int n = atoi(argv[1]);
     int corrupt = argc > 3 && !strcmp(argv[3], "corrupt");
     int trunc = argc > 3 && !strcmp(argv[3], "trunc");
     int forge = argc > 3 && !strcmp(argv[3], "forge");
     int pinned = argc > 4 && !strcmp(argv[4], "pinned");
+    int iov2 = argc > 4 && !strcmp(argv[4], "iov2");
     int cpu_checks = corrupt || trunc || forge || (argc > 3 && !strcmp(argv[3], "cpu-checks"));
     const char *rxm = getenv("TCPCSUM_PRELOAD_RX");
     const int rx_drop = rxm && !strcmp(rxm, "drop");
-    const size_t rx_cap = trunc ? 600 : 32768;
+    const size_t rx_cap = trunc ? 600 : SLOT;
     FILE *f = fopen(argv[2], "wb");
     if (!f || n <= 0) return 2;
     int rx = socket(AF_INET, SOCK_DGRAM, 0), tx = socket(AF_INET, SOCK_DGRAM, 0);
@@ -107,30 +117,42 @@ int main(int argc, char **argv) {
     if (bind(rx, (struct sockaddr *) &a, sizeof a)) { perror("bind"); return 2; }
     socklen_t al = sizeof a;
     getsockname(rx, (struct sockaddr *) &a, &al);
-    uint8_t **out = calloc((size_t) n, sizeof *out), **in = calloc((size_t) n, sizeof *in);
-    size_t *olen = calloc((size_t) n, sizeof *olen), *ilen = calloc((size_t) n, sizeof *ilen);
-    uint8_t **orig = calloc((size_t) n, sizeof *orig);
+    /* a receive that finds nothing for 3 s returns EAGAIN instead of blocking for ever
+     * (recvmmsg's own timeout is checked only after a datagram arrives): under rx drop
+     * the rest of the burst was dropped */
+    struct timeval rto = {3, 0};
+    setsockopt(rx, SOL_SOCKET, SO_RCVTIMEO, &rto, sizeof rto);
+    /* the loop's packet buffers, exactly as loop.c:180-183 allocates them: 1024
+     * in-buffers and 1024 out-buffers of 32 KiB, malloc'd alternately. "pinned"
+     * carves the out-buffers from one tcpcsum_host_alloc block instead. */
+    static uint8_t *buffer[NBUF], *outBuffer[NBUF];
     uint8_t *pool = NULL;
     if (pinned) {
-        pool = (uint8_t *) tcpcsum_host_alloc((size_t) n * 32768);
+        pool = (uint8_t *) tcpcsum_host_alloc((size_t) NBUF * SLOT);
         if (!pool) { fprintf(stderr, "tcpcsum_host_alloc failed\n"); return 2; }
     }
-    for (int i = 0; i < n; ++i) {
-        out[i] = pinned ? pool + (size_t) i * 32768 : malloc(32768);
-        in[i] = malloc(32768);
-        olen[i] = build(out[i], i, cpu_checks, corrupt, forge);
-        orig[i] = malloc(olen[i]);
-        memcpy(orig[i], out[i], olen[i]);
+    for (int i = 0; i < NBUF; ++i) {
+        buffer[i] = malloc(SLOT);
+        outBuffer[i] = pinned ? pool + (size_t) i * SLOT : malloc(SLOT);
+        if (!buffer[i] || !outBuffer[i]) return 2;
     }
+    /* what was built and what arrived, per packet, at their own sizes */
+    uint8_t **orig = calloc((size_t) n, sizeof *orig), **in = calloc((size_t) n, sizeof *in);
+    size_t *olen = calloc((size_t) n, sizeof *olen), *ilen = calloc((size_t) n, sizeof *ilen);
     int drops_only = 0;
     enum { B = 64 };   /* stay below the default socket receive buffer per burst */
     struct mmsghdr mv[B];
-    struct iovec iv[B];
+    struct iovec iv[2 * B];
     for (int s0 = 0; s0 < n; s0 += B) {
         int cnt = n - s0 < B ? n - s0 : B;
         memset(mv, 0, sizeof mv);
-        for (int k = 0; k < cnt; ++k) {
-            iv[k].iov_base = out[s0 + k]; iv[k].iov_len = olen[s0 + k];
+        for (int k = 0; k < cnt; ++k) {   /* packet i goes out of outBuffer[i % 1024], as queued */
+            const int i = s0 + k;
+            uint8_t *ob = outBuffer[i % NBUF];
+            olen[i] = build(ob, i, cpu_checks, corrupt, forge);
+            orig[i] = malloc(olen[i]);
+            memcpy(orig[i], ob, olen[i]);
+            iv[k].iov_base = ob; iv[k].iov_len = olen[i];
             mv[k].msg_hdr.msg_iov = &iv[k]; mv[k].msg_hdr.msg_iovlen = 1;
             mv[k].msg_hdr.msg_name = &a; mv[k].msg_hdr.msg_namelen = sizeof a;
         }
@@ -142,28 +164,42 @@ int main(int argc, char **argv) {
         }
         int want = cnt;   /* under rx drop: the packets this mode makes unverifiable never arrive */
         if (rx_drop)
-            for (int k = 0; k < cnt; ++k)
-                want -= ((corrupt || forge) && (s0 + k) % 7 == 3) || (trunc && olen[s0 + k] > rx_cap);
-        static uint8_t scratch[B][32768];
+            for (int k = 0; k < cnt; ++k) {
+                const int i = s0 + k;
+                /* iov2: a packet longer than the first iovec is a scatter read, passed unverified */
+                const int whole = !iov2 || olen[i] <= IOV2_FIRST;
+                want -= ((corrupt || forge) && i % 7 == 3 && whole) || (trunc && olen[i] > rx_cap);
+            }
         int got = 0;
         while (got < want) {
             memset(mv, 0, sizeof mv);
-            for (int k = 0; k < cnt - got; ++k) {
-                iv[k].iov_base = scratch[k]; iv[k].iov_len = rx_cap;
-                mv[k].msg_hdr.msg_iov = &iv[k]; mv[k].msg_hdr.msg_iovlen = 1;
+            for (int k = 0; k < cnt - got; ++k) {   /* into the loop's in-buffers (loop.c:186-189) */
+                if (iov2) {
+                    iv[2 * k].iov_base = buffer[k]; iv[2 * k].iov_len = IOV2_FIRST;
+                    iv[2 * k + 1].iov_base = buffer[k] + IOV2_FIRST; iv[2 * k + 1].iov_len = rx_cap - IOV2_FIRST;
+                    mv[k].msg_hdr.msg_iov = &iv[2 * k]; mv[k].msg_hdr.msg_iovlen = 2;
+                } else {
+                    iv[k].iov_base = buffer[k]; iv[k].iov_len = rx_cap;
+                    mv[k].msg_hdr.msg_iov = &iv[k]; mv[k].msg_hdr.msg_iovlen = 1;
+                }
             }
             struct timespec to = {5, 0};
             int r = recvmmsg(rx, mv, (unsigned) (cnt - got), MSG_WAITFORONE | (trunc ? MSG_TRUNC : 0), &to);
+            if (r < 0 && rx_drop && (errno == EAGAIN || errno == EWOULDBLOCK)) break;   /* more dropped than expected */
             if (r < 0) { fprintf(stderr, "recvmmsg: %s\n", strerror(errno)); return 4; }
             if (r == 0 && !rx_drop) return 5;
             for (int k = 0; k < r; ++k) {
                 /* which packet: daddr = 10.x.y.z carries its index. Read through the
                  * iovec array by position, as the reference does (getIpPacket,
-                 * loop.c:96-100: loop->iovecs[index]), not through mv[k].msg_iov */
-                const uint8_t *b = (const uint8_t *) iv[k].iov_base;
+                 * loop.c:96-100: loop->iovecs[index]), not through mv[k].msg_iov;
+                 * a receive with several iovecs per message is reordered by vector
+                 * entries, so it is read through the vector */
+                const uint8_t *b = iov2 ? (const uint8_t *) mv[k].msg_hdr.msg_iov[0].iov_base
+                                        : (const uint8_t *) iv[k].iov_base;
                 const size_t held = mv[k].msg_len < rx_cap ? mv[k].msg_len : rx_cap;
                 const int idx = held >= 20 ? (b[17] << 16) | (b[18] << 8) | b[19] : -1;   /* 24-bit index */
                 if (idx < s0 || idx >= s0 + cnt || ilen[idx]) { fprintf(stderr, "unexpected message\n"); return 5; }
+                in[idx] = malloc(held);
                 memcpy(in[idx], b, held);
                 ilen[idx] = held;
             }
@@ -179,9 +215,14 @@ int main(int argc, char **argv) {
         uint32_t l = (uint32_t) olen[i];
         fwrite(&l, 4, 1, f); fwrite(orig[i], 1, l, f);
         l = (uint32_t) ilen[i];
-        fwrite(&l, 4, 1, f); fwrite(in[i], 1, l, f);
+        fwrite(&l, 4, 1, f);
+        if (l) fwrite(in[i], 1, l, f);
     }
     fclose(f);
+    for (int i = 0; i < NBUF; ++i) {   /* the buffers go back the way they came */
+        free(buffer[i]);
+        if (!pinned) free(outBuffer[i]);
+    }
     printf("ok %d\n", n);
     return 0;
 }

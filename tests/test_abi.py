@@ -69,10 +69,25 @@ def test_library_is_a_product_build_of_this_tree():
     assert info["abi"] == api.lib().tcpcsum_abi_version() and info["arch"] == "gfx950"
     assert info["knobs"] == {"TCPCSUM_MEASUREMENT_BUILD": 0, "TCPCSUM_TUNING_VARIANTS": 0, "TCPCSUM_TX_KNOCKOUT": 0,
                              "TCPCSUM_WIRE_WAVES": 1, "TCPCSUM_TX_WAVES": 1}
+    # the only environment a product context reads
+    assert info["runtime_knobs"] == ["TCPCSUM_HOST_THREADS", "TCPCSUM_HOST_NUMA", "TCPCSUM_HOST_SPIN_US",
+                                     "LOCAL_WORLD_SIZE"]
     # the Makefile hashes the same files in the same order
     mk = open(os.path.join(REPO, "Makefile")).read()
     listed = re.search(r"HASH_SRCS := (.*?)\nSRC_HASH", mk, re.S).group(1).replace("\\", " ").split()
     assert tuple(listed) == provenance.HASH_SRCS
+
+
+def test_product_library_does_not_contain_retired_knobs():
+    """the host pipeline's A/B switches (measured and rejected, or kept for A/B runs)
+    are read by measurement builds only — the product library's binary does not even hold their
+    names, so no application environment can change the product path through them."""
+    blob = open(api.lib_path(), "rb").read()
+    for name in ("STAGE_BLOCKS", "STAGE_PASSES", "WIRE_NT", "DMA", "SLOT_SLEEP", "SLOTS", "CHUNK_MB",
+                 "DMA_CHUNK_MB", "WIRE_THREADS", "BULK_THREADS", "NT", "POLL_US", "PINNED_DMA"):
+        assert b"TCPCSUM_HOST_" + name.encode() not in blob, name
+    for kept in (b"TCPCSUM_HOST_THREADS", b"TCPCSUM_HOST_NUMA", b"TCPCSUM_HOST_SPIN_US", b"LOCAL_WORLD_SIZE"):
+        assert kept in blob
 
 
 def test_product_build_refuses_measurement_knobs(tmp_path):
@@ -150,7 +165,7 @@ def test_argument_errors_need_no_device():
     for bad in (T(-1, 0, -1, 0), T(0, 3, -1, 0), T(0, 0, 14, 0), T(0, 0, -2, 0),
                 T(0, 0, -1, 3),      # PIPE_ON | PIPE_OFF
                 T(0, 0, -1, 12),     # NT_ON | NT_OFF
-                T(0, 0, -1, 4096)):
+                T(0, 0, -1, 8192)):   # past the last TCPCSUM_TUNE_* bit
         assert L.tcpcsum_tuning_check(ctypes.byref(bad)) == api.EINVAL
         # every entry point rejects it before touching anything else (n == 0 included)
         assert L.tcpcsum_batch_uniform_dev(None, 0, 0, None, 0, None, 0, None, ctypes.byref(bad)) == api.EINVAL

@@ -232,14 +232,11 @@ def test_round3_fault_sequence_in_process(dev):
         assert ctx.stats()["pkts_in_place"] == 3 * 64
 
 
-@pytest.mark.parametrize("blocks", ["1", "3"])
-def test_ipv4_ptrs_host_pinned_and_mixed(dev, blocks, monkeypatch):
+def test_ipv4_ptrs_host_pinned_and_mixed(dev):
     """Packets in page-locked memory (tcpcsum_host_alloc) are used through their existing mapping
     (no registration, no copy); pageable buffers in the same batch are staged; NULL and short
-    messages are SKIPPED. blocks=3 (TCPCSUM_HOST_STAGE_BLOCKS): the staged packets copied and
-    launched in three blocks of packet indices, each block's kernel queued before the next is copied."""
+    messages are SKIPPED."""
     import tcp_amd
-    monkeypatch.setenv("TCPCSUM_HOST_STAGE_BLOCKS", blocks)
     rng = np.random.default_rng(12)
     pinned = tcp_amd.pinned_empty(64 * 2048)
     pinned[:] = 0
@@ -315,18 +312,15 @@ def test_ipv4_region_host_pool(dev, memory):
         assert np.array_equal(u, oracle.batch_uniform(region, 1501, 1499, u.size, 777))
 
 
-@pytest.mark.parametrize("passes", ["1", "2"])
-def test_ipv4_region_host_staging_large_bounds(dev, passes, monkeypatch):
+def test_ipv4_region_host_staging_large_bounds(dev):
     """A pageable region whose packets' readable bounds add up past the one-pass staging limit
     (64 MiB: 1400 packets in 32 KiB slots with cap 65535, so each bound is up to 64 KiB): the copy
-    threads read every packet's tot_len first and pack the copies by it (two passes). With
-    TCPCSUM_HOST_STAGE_PASSES=2 (read once, at context creation) a small batch takes the same
-    two-pass route. Results, statuses and the caller's bytes match the oracle either way."""
+    threads read every packet's tot_len first and pack the copies by it (two passes). Results,
+    statuses and the caller's bytes match the oracle."""
     import tcp_amd
     from tests.packets import build_batch
-    monkeypatch.setenv("TCPCSUM_HOST_STAGE_PASSES", passes)
     rng = np.random.default_rng(31)
-    n = 1400 if passes == "1" else 300
+    n = 1400
     region, off, _ = build_batch(rng, n, slot=32768, malformed=True)
     ref = region.copy()
     for mode in (tcp_amd.IPV4_FILL | tcp_amd.IPV4_IPHDR, tcp_amd.IPV4_VERIFY | tcp_amd.IPV4_IPHDR):

@@ -27,7 +27,8 @@ def _ensure_built():
         subprocess.run(["make", "-C", REPO, "tests/c/mmsg_loop", "tcp_amd/libtcpcsum_preload.so"], check=True)
 
 
-def run_loop(tmp_path, n, env_extra, cpu_checks=False, corrupt=False, trunc=False, forge=False, pinned=False):
+def run_loop(tmp_path, n, env_extra, cpu_checks=False, corrupt=False, trunc=False, forge=False, pinned=False,
+             iov2=False):
     _ensure_built()
     out = tmp_path / "mm.bin"
     env = {k: v for k, v in os.environ.items() if not k.startswith("TCPCSUM_PRELOAD")}
@@ -35,7 +36,7 @@ def run_loop(tmp_path, n, env_extra, cpu_checks=False, corrupt=False, trunc=Fals
     env.update(env_extra)
     mode = ("trunc" if trunc else "corrupt" if corrupt else "forge" if forge else
             "cpu-checks" if cpu_checks else "plain")
-    args = [EXE, str(n), str(out), mode] + (["pinned"] if pinned else [])
+    args = [EXE, str(n), str(out), mode] + (["pinned"] if pinned else ["iov2"] if iov2 else [])
     r = subprocess.run(args, env=env, capture_output=True, text=True, timeout=120)
     pkts = []
     if r.returncode == 0:
@@ -50,12 +51,31 @@ def run_loop(tmp_path, n, env_extra, cpu_checks=False, corrupt=False, trunc=Fals
             pos += 4 + li
             pkts.append((built, got))
     stats = {}
-    m = re.search(r"tcpcsum_preload: (.*)", r.stderr)
+    m = re.search(r"tcpcsum_preload: (tx batches=.*)", r.stderr)
     if m:
-        for side, body in zip(("tx", "rx", "all", "ctx"), m.group(1).split("|")[:4]):
+        for side, body in zip(("tx", "rx", "all", "ctx", "pool"), m.group(1).split("|")[:5]):
             for k, v in re.findall(r"(\w+)=(\d+)", body):
                 stats[f"{side}_{k}"] = int(v)
     return r, pkts, stats
+
+
+def route_localnet_any() -> bool:
+    """Whether any interface but lo has net.ipv4.conf.<if>.route_localnet = 1 (as the interposer
+    reads it): 127/8 may then arrive on other interfaces."""
+    base = "/proc/sys/net/ipv4/conf"
+    try:
+        names = os.listdir(base)
+    except OSError:
+        return False
+    for name in names:
+        if name == "lo":
+            continue
+        try:
+            if int(open(os.path.join(base, name, "route_localnet")).read().strip() or 0):
+                return True
+        except (OSError, ValueError):
+            pass
+    return False
 
 
 def oracle_fill(pkt: bytes, mode=0) -> bytes:
@@ -69,6 +89,33 @@ def test_passthrough_when_off(tmp_path):
     assert r.returncode == 0, r.stderr
     assert len(pkts) == 150 and all(b == g for b, g in pkts)
     assert stats["tx_packets"] == 0
+
+
+def test_pool_request_without_gpu_falls_back_to_libc(tmp_path):
+    """TCPCSUM_PRELOAD_POOL=1 where no page-locked memory can be had: the constructor says so, every
+    malloc goes to libc (the loop still runs, free() of its buffers included), nothing is served."""
+    import tcp_amd
+    if tcp_amd.device_check()[0] == 0:
+        pytest.skip("a GPU is present")
+    r, pkts, stats = run_loop(tmp_path, 1500, {"TCPCSUM_PRELOAD_TX": "off", "TCPCSUM_PRELOAD_POOL": "1"})
+    assert r.returncode == 0, r.stderr
+    assert "TCPCSUM_PRELOAD_POOL: no page-locked pool" in r.stderr
+    assert len(pkts) == 1500 and all(b == g for b, g in pkts)
+    assert stats["pool_on"] == 0 and stats["pool_served"] == 0
+
+
+@pytest.mark.parametrize("name,tried", [("mmsg_loop", True), ("stress", False), ("0", False)])
+def test_pool_only_for_the_named_program(tmp_path, name, tried):
+    """TCPCSUM_PRELOAD_POOL=<executable name>: only that program takes the pool (and starts HIP for it);
+    a wrapper or any other program the preload reaches leaves it alone. Here without a GPU, so the
+    named program's attempt fails loudly and falls back; the others never try."""
+    import tcp_amd
+    if tcp_amd.device_check()[0] == 0:
+        pytest.skip("a GPU is present")
+    r, pkts, stats = run_loop(tmp_path, 300, {"TCPCSUM_PRELOAD_TX": "off", "TCPCSUM_PRELOAD_POOL": name})
+    assert r.returncode == 0, r.stderr
+    assert ("TCPCSUM_PRELOAD_POOL: no page-locked pool" in r.stderr) == tried
+    assert stats["pool_on"] == 0 and len(pkts) == 300
 
 
 def test_fails_loudly_without_gpu(tmp_path):
@@ -97,6 +144,67 @@ def test_tx_fill_on_gpu(tmp_path, pinned):
     # tx packets in the pinned pool go in place; rx scratch buffers (and malloc'd tx buffers) are staged
     assert (stats["ctx_in_place"] == 3000) == pinned
     assert stats["ctx_staged"] == (3000 if pinned else 6000)
+
+
+@pytest.mark.gpu
+def test_pool_zero_copy_loop_unedited(tmp_path):
+    """TCPCSUM_PRELOAD_POOL=1 with mmsg_loop's plain mallocs (loop.c:180-183 unedited):
+    the interposer serves the loop's 2 x 1024 32-KiB buffers from its own page-locked arena, so every
+    tx packet is filled and every rx packet verified in place — nothing staged — and each received
+    packet is the oracle's FILL of what was built."""
+    n = 3000
+    r, pkts, stats = run_loop(tmp_path, n, {"TCPCSUM_PRELOAD_TX": "fill", "TCPCSUM_PRELOAD_RX": "verify",
+                                            "TCPCSUM_PRELOAD_POOL": "mmsg_loop"})
+    assert r.returncode == 0, r.stderr
+    assert len(pkts) == n
+    for built, got in pkts:
+        assert got == oracle_fill(built)
+    assert stats["pool_on"] == 1 and stats["pool_served"] == 2048 and stats["pool_full"] == 0
+    assert stats["pool_released"] == 2048                      # the loop's free()s came back to the arena
+    assert stats["tx_filled"] == n and stats["rx_verified"] == n and stats["rx_verify_failed"] == 0
+    assert stats["ctx_in_place"] == 2 * n and stats["ctx_staged"] == 0
+
+
+@pytest.mark.gpu
+def test_pool_rx_drop_in_place(tmp_path):
+    """rx drop on the arena's in-buffers: the corrupted segments (every 7th) never reach the caller,
+    the rest arrive byte-identical; verified in place, nothing staged."""
+    n = 2100
+    r, pkts, stats = run_loop(tmp_path, n, {"TCPCSUM_PRELOAD_TX": "off", "TCPCSUM_PRELOAD_RX": "drop",
+                                            "TCPCSUM_PRELOAD_POOL": "1"}, corrupt=True)
+    assert r.returncode == 0, r.stderr
+    bad = 0
+    for i, (built, got) in enumerate(pkts):
+        if i % 7 == 3:
+            assert got == b""
+            bad += 1
+        else:
+            assert got == built
+    assert stats["rx_verify_failed"] == bad and stats["rx_dropped"] == bad
+    assert stats["ctx_in_place"] == n and stats["ctx_staged"] == 0
+
+
+@pytest.mark.gpu
+def test_rx_drop_multi_iov_messages(tmp_path):
+    """a message received into two iovecs (800 bytes, then the rest) is verified from its
+    first iovec when that holds the whole packet — corrupted ones are dropped — and otherwise passed
+    through unverified (a scatter read), counted as skipped, never silently dropped."""
+    n = 1400
+    r, pkts, stats = run_loop(tmp_path, n, {"TCPCSUM_PRELOAD_TX": "off", "TCPCSUM_PRELOAD_RX": "drop"},
+                              corrupt=True, iov2=True)
+    assert r.returncode == 0, r.stderr
+    dropped = whole = 0
+    for i, (built, got) in enumerate(pkts):
+        fits = len(built) <= 800
+        whole += fits
+        if i % 7 == 3 and fits:
+            assert got == b""
+            dropped += 1
+        else:
+            assert got == built
+    assert 0 < whole < n
+    assert stats["rx_dropped"] == dropped and stats["rx_verify_failed"] == dropped
+    assert stats["rx_skipped"] == n - whole and stats["rx_verified"] == whole
 
 
 @pytest.mark.gpu
@@ -158,6 +266,10 @@ def test_rx_drop_forged_checksum_partial(tmp_path):
                               forge=True)
     assert r.returncode == 0, r.stderr
     assert len(pkts) == n
+    # with route_localnet set on any interface (kube-proxy does), 127/8 is no proof of lo:
+    # the exception is off and the 127/8 partial segments are dropped as well
+    localnet = route_localnet_any()
+    assert stats["pool_localnet"] == int(localnet)
     forged = loop = 0
     for i, (built, got) in enumerate(pkts):
         region = np.frombuffer(built + b"\0" * 16, np.uint8).copy()
@@ -168,12 +280,13 @@ def test_rx_drop_forged_checksum_partial(tmp_path):
             forged += 1
         elif i % 7 == 5:
             assert built[12] == 127 and built[16] == 127 and st[0] & 4
-            assert got == built
+            assert got == (b"" if localnet else built)
             loop += 1
         else:
             assert st[0] == 0 and v[0] == 0 and got == built
-    assert stats["rx_verified"] == n and stats["rx_verify_failed"] == forged and stats["rx_dropped"] == forged
-    assert stats["rx_partial"] == loop
+    failed = forged + (loop if localnet else 0)
+    assert stats["rx_verified"] == n and stats["rx_verify_failed"] == failed and stats["rx_dropped"] == failed
+    assert stats["rx_partial"] == (0 if localnet else loop)
 
 
 @pytest.mark.gpu
@@ -248,7 +361,7 @@ def run_raw(tmp_path, n, env_extra, cpu=False):
             pos += 4 + li
             pkts.append((built, got))
     stats = {}
-    m = re.search(r"tcpcsum_preload: (.*)", r.stderr)
+    m = re.search(r"tcpcsum_preload: (tx batches=.*)", r.stderr)
     if m:
         for side, body in zip(("tx", "rx"), m.group(1).split("|")[:2]):
             for k, v in re.findall(r"(\w+)=(\d+)", body):

@@ -1,0 +1,66 @@
+#!/usr/bin/env bash
+# Round-5 GPU runs (one function per experiment; outputs under gpurun_out/r5/):
+#   bash tools/r5_runs.sh <function> [args]
+# Every GPU step runs under its own timeout and the steps are chained: the first
+# failure ends the call.
+set -o pipefail
+O=gpurun_out/r5
+mkdir -p $O
+PRE=$PWD/tcp_amd/libtcpcsum_preload.so
+
+ok_rc() { [ "$1" = 0 ]; }
+
+# GPU tests of the files named (default: all), one pytest process
+tests() {
+  timeout -k 10 900 python3 -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu "${@:-tests}" \
+    > $O/gputest.txt 2>&1; rc=$?
+  tail -5 $O/gputest.txt; return $rc
+}
+
+# the sendmmsg / recvmmsg seam per 1024 x 1500-B batch: reference CPU checksum; staged (loop.c's
+# malloc'd buffers); TCPCSUM_PRELOAD_POOL=mmsg_bench (the same mallocs served from the interposer's
+# page-locked arena, loop.c unedited); level 2 (out-buffers carved from tcpcsum_host_alloc by the
+# application). rx: plain recvmmsg, rx drop staged / pool, CPU verify. Interleaved, $1 rounds.
+seam() {
+  local reps=${1:-3}
+  for rep in $(seq 1 $reps); do
+    for v in "cpu:cpu::" "staged:gpu::" "pool:gpu::mmsg_bench" "pinned:gpu:pinned:"; do
+      IFS=: read name mode extra pool <<< "$v"
+      if [ $mode = gpu ]; then
+        # LD_PRELOAD on the measured program only (env execs it), never on timeout
+        timeout -k 10 120 env LD_PRELOAD=$PRE TCPCSUM_PRELOAD_ANY_SOCKET=1 TCPCSUM_PRELOAD_TX=fill \
+          TCPCSUM_PRELOAD_STATS=1 TCPCSUM_PRELOAD_POOL=${pool:-0} tools/mmsg_bench gpu 300 $extra \
+          > $O/seam_${name}_$rep.json 2> $O/seam_${name}_$rep.err; rc=$?
+      else
+        timeout -k 10 120 tools/mmsg_bench cpu 300 > $O/seam_${name}_$rep.json 2> $O/seam_${name}_$rep.err; rc=$?
+      fi
+      echo "seam $name rep=$rep rc=$rc $(cat $O/seam_${name}_$rep.json) $(grep -o 'in_place=[0-9]* staged=[0-9]*' $O/seam_${name}_$rep.err)"
+      ok_rc $rc || return $rc
+    done
+    for v in "rxplain:rx:" "rxdrop_staged:rx:gpu" "rxdrop_pool:rx:pool" "rxcpu:rxcpu:"; do
+      IFS=: read name mode how <<< "$v"
+      if [ -n "$how" ]; then
+        local poolenv=TCPCSUM_PRELOAD_POOL=0
+        [ "$how" = pool ] && poolenv=TCPCSUM_PRELOAD_POOL=mmsg_bench
+        timeout -k 10 120 env LD_PRELOAD=$PRE TCPCSUM_PRELOAD_ANY_SOCKET=1 TCPCSUM_PRELOAD_TX=off \
+          TCPCSUM_PRELOAD_RX=drop TCPCSUM_PRELOAD_STATS=1 $poolenv \
+          tools/mmsg_bench $mode 300 > $O/seam_${name}_$rep.json 2> $O/seam_${name}_$rep.err; rc=$?
+      else
+        timeout -k 10 120 tools/mmsg_bench $mode 300 > $O/seam_${name}_$rep.json 2> $O/seam_${name}_$rep.err; rc=$?
+      fi
+      echo "seam $name rep=$rep rc=$rc $(cat $O/seam_${name}_$rep.json) $(grep -o 'in_place=[0-9]* staged=[0-9]*' $O/seam_${name}_$rep.err)"
+      ok_rc $rc || return $rc
+    done
+  done
+}
+
+# wire FILL / VERIFY: the in-tree library against the round-3 and round-4 builds
+# (tools/ab_build.sh), interleaved in one process, byte-identity checked
+wire_ab() {
+  WIRE_AB_ONLY=${WIRE_AB_ONLY:-1Mx1500_slots1536,1Mx1500_packed,128Kx9000_slots9216} WIRE_AB_ROUNDS=${1:-5} \
+    timeout -k 10 400 python3 -u tools/wire_lib_ab.py tcp_amd/ab/libtcpcsum_wire_r3.so tcp_amd/ab/libtcpcsum_wire_r4.so \
+    > $O/wire_ab.jsonl 2> $O/wire_ab.err; rc=$?
+  cat $O/wire_ab.jsonl; return $rc
+}
+
+"$@"
