@@ -24,7 +24,7 @@
  *   arena_release  return a block; p must be a block's start and in use — anything
  *                  else is heap corruption in the caller and aborts, as glibc's
  *                  free() does for an invalid or double-freed pointer
- *   arena_route_*  what the interposer's malloc / free / realloc do: arena blocks
+ *   arena_route_*  what the interposer's malloc / calloc / free / realloc do: arena blocks
  *                  here, everything else to the allocator underneath (libc's)
  */
 #pragma once
@@ -140,6 +140,18 @@ static inline void *arena_route_malloc(arena_t *a, size_t n, int guard, const ar
         if (p) return p;
     }
     return l->malloc(n);
+}
+
+/* calloc: a zeroed block when nmemb * size is exactly the block size (a compiler may
+ * turn the loop's malloc + memset into calloc), else underneath. */
+static inline void *arena_route_calloc(arena_t *a, size_t nmemb, size_t size, int guard,
+                                       void *(*under)(size_t, size_t)) {
+    size_t n;
+    if (!guard && !__builtin_mul_overflow(nmemb, size, &n) && n && n == arena_block(a)) {
+        void *p = arena_alloc(a, n);
+        if (p) return memset(p, 0, n);
+    }
+    return under(nmemb, size);
 }
 
 static inline void arena_route_free(arena_t *a, void *p, const arena_libc_t *l) {

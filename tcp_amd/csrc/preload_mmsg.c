@@ -42,7 +42,9 @@
  *                                main runs, so both seams read and fill the loop's
  *                                buffers in place (preload_arena.h). Every other
  *                                allocation, and any past the first 2048 of that
- *                                size, goes to libc; free / realloc /
+ *                                size, goes to libc (calloc of exactly 32 KiB is
+ *                                served too, zeroed: a compiler may turn malloc +
+ *                                memset into it); free / realloc / reallocarray /
  *                                malloc_usable_size route arena pointers back here.
  *                                <prog> is the loop's executable name ("stress"), or
  *                                1 for whatever process loads the interposer. The pool
@@ -141,11 +143,16 @@ static int g_pool_asked, g_pool_failed;
 extern void *__libc_malloc(size_t);
 extern void __libc_free(void *);
 extern void *__libc_realloc(void *, size_t);
+extern void *__libc_calloc(size_t, size_t);
 
 static const arena_libc_t k_libc = {__libc_malloc, __libc_free, __libc_realloc};
 
 void *malloc(size_t n) {
     return arena_route_malloc(&g_arena, n, t_guard, &k_libc);
+}
+
+void *calloc(size_t nmemb, size_t size) {
+    return arena_route_calloc(&g_arena, nmemb, size, t_guard, __libc_calloc);
 }
 
 void free(void *p) {

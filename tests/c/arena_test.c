@@ -129,12 +129,15 @@ int main(void) {
         CHECK(buf[i] == mem + (size_t) i * BLK);        /* address order */
     }
     extra = arena_route_malloc(&A, BLK, 0, &L);        /* the 2049th: libc */
+    void *cz = arena_route_calloc(&A, 8, BLK / 8, 0, calloc);   /* full: calloc falls through too */
+    CHECK(cz && !arena_owns(&A, cz));
+    free(cz);
     CHECK(extra && !arena_owns(&A, extra));
     void *small = arena_route_malloc(&A, 100, 0, &L);
     CHECK(small && !arena_owns(&A, small));
     uint64_t served, released, full;
     arena_counters(&A, &served, &released, &full);
-    CHECK(served == NBLK && released == 0 && full == 1);
+    CHECK(served == NBLK && released == 0 && full == 2);   /* the 2049th malloc and the calloc */
     arena_route_free(&A, extra, &L);
     arena_route_free(&A, small, &L);
 
@@ -148,6 +151,15 @@ int main(void) {
     CHECK(arena_route_malloc(&A, BLK, 0, &L) == buf[7]);   /* the freed block is reused first */
     CHECK(arena_route_realloc(&A, buf[9], 0, &L) == NULL);
     CHECK(arena_route_malloc(&A, BLK, 0, &L) == buf[9]);
+    /* calloc of exactly a block: the block, zeroed (it held 0xab); other sizes underneath */
+    memset(buf[11], 0xab, BLK);
+    arena_route_free(&A, buf[11], &L);
+    uint8_t *c = arena_route_calloc(&A, BLK / 16, 16, 0, calloc);
+    CHECK(c == buf[11]);
+    for (size_t k = 0; k < BLK; ++k) CHECK(c[k] == 0);
+    void *c2 = arena_route_calloc(&A, 3, BLK, 0, calloc);
+    CHECK(c2 && !arena_owns(&A, c2));
+    free(c2);
     void *r = arena_route_realloc(&A, NULL, BLK, &L);     /* realloc(NULL, n) is malloc underneath */
     CHECK(r && !arena_owns(&A, r));
     free(r);

@@ -63,4 +63,32 @@ wire_ab() {
   cat $O/wire_ab.jsonl; return $rc
 }
 
+# the default bench line (driver form), plus $@ extra bench.py flags
+bench() {
+  timeout -k 10 900 python3 -u bench.py "$@" > $O/bench.json 2> $O/bench.err; rc=$?
+  tail -c 600 $O/bench.err; python3 - << 'PY'
+import json
+d = json.load(open("gpurun_out/r5/bench.json"))
+print("value", d["value"], "frac", d["roofline"]["frac"], "probe", d.get("stream_probe"))
+oc = d.get("other_configs", {})
+for k, v in oc.items():
+    if k == "wire_1500":
+        print(k, {m: v[m].get("kernel_avg_ms", v[m].get("avg_ms")) for m in ("fill", "verify", "copy_probe", "read_probe")},
+              "fill/verify", v["fill_over_verify"], "fill/copy_probe", v["fill_over_copy_probe"], "check", v["check"])
+    else:
+        print(k, v["kernel_avg_ms"], v["roofline_frac"], v.get("stream_probe"), v.get("multi_batch", {}).get("roofline_frac"))
+for m, v in (d.get("host_path") or {}).items():
+    print("host", m, v["GiB/s"], v.get("raw_pinned_h2d_GiB/s"), v["cpu_core_s_per_step_rank0"], v["cgroup_throttled_ms_per_rank"],
+          v["copy_threads_per_rank"], v["digest_check"])
+print("cpu", d.get("cpu_baseline", {}).get("value"), "digest", d["digest_check"])
+PY
+  return $rc
+}
+
+# write-back probe shapes beside the wire FILL / VERIFY (tools/probe_rw_sweep.py)
+probe_rw() {
+  timeout -k 10 300 python3 -u tools/probe_rw_sweep.py > $O/probe_rw.jsonl 2> $O/probe_rw.err; rc=$?
+  cat $O/probe_rw.jsonl; return $rc
+}
+
 "$@"
