@@ -228,9 +228,12 @@ int tcpcsum_tx_build_dev(const void *d_payload, const tcpcsum_txseg_t *d_segs, u
  * The path as the reference sees it: segments start and end in host memory
  * (raw-socket buffers). A context owns one device, one stream, pinned
  * staging and a few host copy threads (TCPCSUM_HOST_THREADS, default half the
- * CPUs the process may use, at most 8; a staged wire batch of up to 8 MiB
- * copies on TCPCSUM_HOST_WIRE_THREADS of them, default 1 = the calling thread,
- * a bulk uniform copy on TCPCSUM_HOST_BULK_THREADS, default 4).
+ * CPUs the process may use, at most 8 — or, with LOCAL_WORLD_SIZE = k > 1 ranks
+ * sharing the node's CPU quota, the rank's 1/k share; a staged wire batch of up
+ * to 8 MiB copies on the calling thread alone, a bulk uniform copy on at most 4).
+ * tcpcsum_ctx_destroy drains the stream and joins the copy threads before it
+ * frees the context's HIP objects: call it while the HIP runtime is up (before
+ * exit), as the Python front end's atexit hook does for contexts left open.
  * Host memory is used one of two ways:
  *   - memory its owner page-locked (tcpcsum_host_alloc / hipHostMalloc, or the
  *     application's own hipHostRegister) is read — FILL: written — in place by

@@ -2268,12 +2268,12 @@ void launch_ipv4(uint8_t* pkts, const uint64_t* off, const uint32_t* plen, uint6
     // turn) the lane-group kernels, one speculative round trip per packet. Large
     // batches of 1-1.5 KiB packets take 4-chunk rounds (fewer registers, more
     // waves: 1024-B slots 0.226 -> 0.173 ms VERIFY, 1536-B 0.250 -> 0.242 than
-    // one 12-chunk round; tools/wire_mtu_sweep.sh)
+    // one 12-chunk round; profiles/r02_wire_mtu_sweep.jsonl)
     // Large batches of 1.5-5 KiB packets (the cap, or the mean footprint when
     // smaller, sizes them) keep 4- or 6-chunk rounds: 2 KiB slots VERIFY 0.549 ->
     // 0.314 ms and FILL 0.578 -> 0.402 against one 96-chunk round per lane group
     // (32,3); 3 KiB -19 % / -11 %, 4.5 KiB -7 % / -7 % with (16,6); 9 KiB jumbo
-    // slots alike across shapes and keep (32,3) (tools/wire_big_sweep.sh,
+    // slots alike across shapes and keep (32,3) (profiles/r02_wire_big_sweep.jsonl,
     // profiles/r02_wire_big_sweep.jsonl)
     const uint64_t nsz = mean && ((mean + 15u) >> 4) < nch ? (mean + 15u) >> 4 : nch;
     if (sh < 0 || sh > 9) {
@@ -2299,7 +2299,7 @@ void launch_ipv4(uint8_t* pkts, const uint64_t* off, const uint32_t* plen, uint6
         if (auto_shape)
             while (spw > 1 && (n + spw - 1) / spw < 4096u) spw >>= 1;
         // one tile per wave by default (4M packed 84-B packets 0.116 -> 0.112 ms
-        // against 8192 blocks; tools/lb_sweep.sh)
+        // against 8192 blocks; profiles/r02_lb_grid_sweep.jsonl)
         const dim3 grid(grid_for((n + spw - 1) / spw, tu.max_blocks > 0 ? tu.max_blocks : 1 << 24));
         if (sh == 8 && plen)
             hipLaunchKernelGGL((k_ipv4_lb<4, true>), grid, dim3(256), 0, s, pkts, off, plen, n, cap, limit, mode, out,
