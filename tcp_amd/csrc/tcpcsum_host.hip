@@ -864,7 +864,7 @@ int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t* c, void* h_pkts, size_t region_bytes,
     const bool fill = (mode & TCPCSUM_IPV4_VERIFY) == 0;
     // zero-copy over PCIe: 16-lane groups, 512 B per round (more waves with
     // reads in flight) beat the HBM-tuned MTU shape — 1024 x 1500-B FILL
-    // batch 49 vs 59 us on MI355X (tools/e2e.py --sweep)
+    // batch 49 vs 59 us on MI355X (profiles/r02_e2e_ptrs_sweep.jsonl)
     tcpcsum::Tuning tu = c->tune;
     if (tu.shape < 0 && n < 65536u) tu.shape = 3;
     hipError_t e;

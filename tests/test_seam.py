@@ -208,6 +208,22 @@ def test_rx_drop_multi_iov_messages(tmp_path):
 
 
 @pytest.mark.gpu
+def test_preload_device_choice(tmp_path):
+    """TCPCSUM_PRELOAD_DEVICE (one loop process per GPU): device 0 named explicitly
+    fills every packet; a device this box does not have makes the interposer refuse loudly (ENXIO,
+    naming the device) instead of falling back to another GPU or to unchecked packets."""
+    import torch
+    r, pkts, stats = run_loop(tmp_path, 400, {"TCPCSUM_PRELOAD_TX": "fill", "TCPCSUM_PRELOAD_DEVICE": "0"})
+    assert r.returncode == 0, r.stderr
+    assert all(got == oracle_fill(built) for built, got in pkts)
+    assert stats["pool_device"] == 0 and stats["tx_filled"] == 400
+    missing = torch.cuda.device_count()
+    r, _, stats = run_loop(tmp_path, 10, {"TCPCSUM_PRELOAD_TX": "fill", "TCPCSUM_PRELOAD_DEVICE": str(missing)})
+    assert r.returncode == 3 and "No such device or address" in r.stderr
+    assert f"unavailable on device {missing}" in r.stderr
+
+
+@pytest.mark.gpu
 def test_tx_verify_live_parity_with_cpu_checks(tmp_path):
     """Checks written by the reference's CPU path (tcpcsum_continue == csum_continue) verify on the GPU."""
     r, pkts, stats = run_loop(tmp_path, 2000, {"TCPCSUM_PRELOAD_TX": "verify"}, cpu_checks=True)

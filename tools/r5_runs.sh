@@ -91,4 +91,21 @@ probe_rw() {
   cat $O/probe_rw.jsonl; return $rc
 }
 
+# bench.py at N ranks on this one GPU (TCPCSUM_BENCH_SHARE_DEVICE=1): the launcher, barriers,
+# every rank's shard digest, per-rank throttling and copy-thread budget — not the scaling
+shared() {
+  local n=${1:-8}
+  TCPCSUM_BENCH_SHARE_DEVICE=1 timeout -k 10 900 python3 -u bench.py --gpus $n --steps ${2:-20} --warmup 3 \
+    > $O/bench_n${n}_shared.json 2> $O/bench_n${n}_shared.err; rc=$?
+  tail -c 400 $O/bench_n${n}_shared.err; python3 - $n << 'PY'
+import json, sys
+d = json.load(open(f"gpurun_out/r5/bench_n{sys.argv[1]}_shared.json"))
+print("n", d["n_gpus"], "value", d["value"], "digest", d["digest_check"])
+for m, v in (d.get("host_path") or {}).items():
+    print("host", m, v["GiB/s"], v["per_rank_GiB/s"], "throttled", v["cgroup_throttled_ms_per_rank"],
+          "threads", v["copy_threads_per_rank"], "lws", v["local_world_size"], "digest", v["digest_check"])
+PY
+  return $rc
+}
+
 "$@"
