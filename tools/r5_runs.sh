@@ -108,4 +108,17 @@ PY
   return $rc
 }
 
+# 1M x 64-B batches: launch shapes of the uniform kernel beside the probe (tools/sweep.py)
+sweep64() {
+  timeout -k 10 600 python3 -u tools/sweep.py --config 64 --rounds 3 --steps 100 --probe \
+    --blocks 512,1024,2048,4096,8192,16384,0 --unrolls 1,2,4,8 --shapes -1,0,1,10,11 \
+    > $O/sweep64.jsonl 2> $O/sweep64.err; rc=$?
+  python3 -c "
+import json
+rows = [json.loads(l) for l in open('$O/sweep64.jsonl')]
+for r in sorted((r for r in rows if 'med_ms' in r), key=lambda r: r['med_ms'])[:8]: print(r)
+print([r for r in rows if 'probe_med_ms' in r or (r.get('shape') == -1 and r.get('max_blocks') == 0 and r.get('unroll') == 1)])
+"; return $rc
+}
+
 "$@"
