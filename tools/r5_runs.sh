@@ -111,7 +111,7 @@ PY
 # 1M x 64-B batches: launch shapes of the uniform kernel beside the probe (tools/sweep.py)
 sweep64() {
   timeout -k 10 600 python3 -u tools/sweep.py --config 64 --rounds 3 --steps 100 --probe \
-    --blocks 512,1024,2048,4096,8192,16384,0 --unrolls 1,2,4,8 --shapes -1,0,1,10,11 \
+    --blocks 512,1024,2048,4096,8192,16384,0 --unrolls 1,2,4,8 --shapes=-1,0,1,10,11 \
     > $O/sweep64.jsonl 2> $O/sweep64.err; rc=$?
   python3 -c "
 import json
