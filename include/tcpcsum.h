@@ -313,7 +313,10 @@ int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t *ctx, void *h_pkts, size_t region_byte
  * readable bytes (results and status as tcpcsum_ipv4_batch_ptrs_dev). A
  * packet inside one page-locked allocation (tcpcsum_host_alloc, the
  * application's own hipHostRegister) is read and FILLed in place; any other is
- * copied into staging and its check stored back. */
+ * copied into staging and its check stored back. Host batches store exactly the
+ * 2-byte check (and, with IPHDR, the 2-byte IP header checksum) into the caller's
+ * packets, as context.c:208 does; device batches may write the check's whole 128-B
+ * line back (the bytes they read, check patched in), see TCPCSUM_TUNE_FILL_U16. */
 int tcpcsum_ipv4_batch_ptrs_host(tcpcsum_ctx_t *ctx, void *const *h_pkts, const uint32_t *h_lens, uint64_t n,
                                  int mode, uint16_t *h_out, uint8_t *h_status);
 

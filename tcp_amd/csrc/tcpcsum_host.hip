@@ -241,6 +241,10 @@ struct tcpcsum_ctx {
     // TCPCSUM_CTX_BLOCKING_WAIT: wait for the device by polling this event between
     // short sleeps instead of HIP's spin in hipStreamSynchronize
     hipEvent_t done_ev = nullptr;
+    // the sleeping wait's prediction: observed / expected device time (x1024) of this
+    // context's batches, [0] releaseSend-sized (expected < 1 ms), [1] bulk; start at
+    // 3/4, round 4's fixed first nap
+    uint32_t wait_ratio[2] = {768u, 768u};
     // The product's choices below; measurement builds can flip each (the TCPCSUM_HOST_*
     // name in brackets) for A/B runs:
     uint64_t poll_ns = 5000;     // first sleep between polls after the expected time (POLL_US)
@@ -326,14 +330,17 @@ void par_copy(tcpcsum_ctx* c, void* dst, const void* src, size_t n, bool nt = fa
 }
 
 // Sleep until ev has completed: a first nap of nap_ns, then a poll every
-// c->poll_ns, doubling up to max_step_ns (1 us timer slack on this thread while
-// it sleeps, restored after).
-hipError_t sleep_on_event(tcpcsum_ctx* c, hipEvent_t ev, uint64_t nap_ns, uint64_t max_step_ns) {
+// c->poll_ns — at that fixed step until the clock passes fixed_until_ns, then
+// doubling up to max_step_ns (1 us timer slack on this thread while it sleeps,
+// restored after).
+hipError_t sleep_on_event(tcpcsum_ctx* c, hipEvent_t ev, uint64_t nap_ns, uint64_t max_step_ns,
+                          uint64_t fixed_until_ns = 0, int* sleeps = nullptr) {
     const int slack = prctl(PR_GET_TIMERSLACK, 0, 0, 0, 0);
     bool slack_set = false;
     uint64_t step = std::min<uint64_t>(c->poll_ns, max_step_ns);
     hipError_t e;
-    for (;;) {
+    int n = 0;   // sleeps taken before the event was seen complete
+    for (;; ++n) {
         e = hipEventQuery(ev);
         if (e != hipErrorNotReady) break;
         (void)hipGetLastError();   // not ready is not an error for us
@@ -344,32 +351,53 @@ hipError_t sleep_on_event(tcpcsum_ctx* c, hipEvent_t ev, uint64_t nap_ns, uint64
         uint64_t ns = nap_ns;
         if (!ns) {
             ns = step;
-            step = std::min<uint64_t>(step * 2, max_step_ns);
+            if (tcpcsum::now_ns() >= fixed_until_ns) step = std::min<uint64_t>(step * 2, max_step_ns);
         }
         nap_ns = 0;
         timespec ts{(time_t)(ns / 1000000000u), (long)(ns % 1000000000u)};
         nanosleep(&ts, nullptr);
     }
     if (slack_set) prctl(PR_SET_TIMERSLACK, (unsigned long)slack, 0, 0, 0);
+    if (sleeps) *sleeps = n;
     return e;
 }
 
 // Wait for everything queued on st, timed into stats.ns_wait: hipStreamSynchronize
 // (HIP spins: the waiting thread burns a core for the kernel's whole length), or
 // with TCPCSUM_CTX_BLOCKING_WAIT a poll of the stream's completion event between
-// sleeps — first for 3/4 of expect_ns (what the queued work should take: the
-// caller's estimate from its bytes), then every poll_ns, doubling up to 100 us. A
-// hipEventBlockingSync event did not help: the runtime waits on its signal
-// actively for about a batch kernel's length, and the thread used as much CPU as
-// with hipStreamSynchronize (48.7 vs 48.5 us per 1024-packet in-place batch,
-// profiles/r04_e2e_first.jsonl).
+// sleeps. A hipEventBlockingSync event did not help: the runtime waits on its
+// signal actively for about a batch kernel's length, and the thread used as much
+// CPU as with hipStreamSynchronize (48.7 vs 48.5 us per 1024-packet in-place
+// batch, profiles/r04_e2e_first.jsonl).
+//
+// The sleeping wait predicts when the work ends: expect_ns (the caller's estimate
+// from its bytes) times a ratio this context learns per size class. It naps until
+// the prediction, then polls every poll_ns until twice the prediction, then backs
+// off. When the work was already done at the end of the nap, the nap may have been
+// too long: the ratio shrinks by 1/32. When it took polls, the ratio moves an
+// eighth of the way to what the wait took (at most one poll interval late). A wake
+// that comes late (a busy host) therefore never lengthens the next nap. Round 4
+// napped 3/4 of the estimate and then polled at 5, 10, 20, 40 us, so a releaseSend
+// batch done at 64 us was seen at 104 us (profiles/r05_host_fill_ab.jsonl, r05_wait_ab.jsonl).
 hipError_t wait_stream(tcpcsum_ctx* c, hipStream_t st, uint64_t expect_ns) {
     const uint64_t t0 = tcpcsum::now_ns();
     hipError_t e;
     if (c->flags & TCPCSUM_CTX_BLOCKING_WAIT) {
         e = hipEventRecord(c->done_ev, st);
-        if (e == hipSuccess)
-            e = sleep_on_event(c, c->done_ev, std::min<uint64_t>(expect_ns - expect_ns / 4, 50000000u), 100000u);
+        if (e == hipSuccess) {
+            uint32_t& ratio = c->wait_ratio[expect_ns < 1000000u ? 0 : 1];   // predicted / expected, x1024
+            const uint64_t pred = std::min<uint64_t>(expect_ns * ratio / 1024u, 200000000u);
+            int sleeps = 0;
+            e = sleep_on_event(c, c->done_ev, pred, 100000u, t0 + 2 * pred, &sleeps);
+            const uint64_t took = tcpcsum::now_ns() - t0;
+            if (e == hipSuccess && expect_ns) {
+                if (sleeps <= 1)   // done by the end of the nap: try a shorter one
+                    ratio -= ratio / 32u;
+                else
+                    ratio = (uint32_t)((ratio * 7u + std::min<uint64_t>(took * 1024u / expect_ns, 8192u)) / 8u);
+                ratio = std::max<uint32_t>(ratio, 128u);
+            }
+        }
     } else {
         e = hipStreamSynchronize(st);
     }
@@ -532,6 +560,23 @@ void write_back_checks(tcpcsum_ctx* c, const uint8_t* status, bool iphdr) {
         }
     }, c->stage_threads);
     c->stats.ns_copy += tcpcsum::now_ns() - t0;
+}
+
+// Launch shape and FILL store of a host wire batch (tcpcsum_ipv4_batch_host /
+// _ptrs_host) unless the context's tuning says otherwise:
+//   * 16-lane groups, 512 B per round, for latency-bound batches read over PCIe:
+//     more waves with reads in flight beat the HBM-tuned MTU shape — 1024 x
+//     1500-B FILL batch 49 vs 59 us (profiles/r02_e2e_ptrs_sweep.jsonl);
+//   * the plain 2-byte check store, exactly the bytes context.c:208 writes. The
+//     whole-line write-back that pays in HBM (whole lines instead of partial ones)
+//     buys nothing over PCIe: 1024 x 1500-B in-place FILL 67.4-70.1 vs 68.2-68.4 us
+//     (profiles/r05_host_fill_ab.jsonl, r05_wait_ab.jsonl).
+tcpcsum::Tuning host_wire_tuning(const tcpcsum_ctx* c, uint64_t n) {
+    tcpcsum::Tuning tu = c->tune;
+    if (tu.shape < 0 && n < 65536u) tu.shape = 3;
+    if (!(tu.flags & (TCPCSUM_TUNE_FILL_DWORD | TCPCSUM_TUNE_FILL_U16 | TCPCSUM_TUNE_FILL_HALF)))
+        tu.flags |= TCPCSUM_TUNE_FILL_U16;
+    return tu;
 }
 
 }  // namespace
@@ -862,11 +907,7 @@ int tcpcsum_ipv4_batch_host(tcpcsum_ctx_t* c, void* h_pkts, size_t region_bytes,
     uint16_t* kout = zout ? zout : (uint16_t*)c->p_out.d;
     uint8_t* kst = zst ? zst : c->p_stat.d;
     const bool fill = (mode & TCPCSUM_IPV4_VERIFY) == 0;
-    // zero-copy over PCIe: 16-lane groups, 512 B per round (more waves with
-    // reads in flight) beat the HBM-tuned MTU shape — 1024 x 1500-B FILL
-    // batch 49 vs 59 us on MI355X (profiles/r02_e2e_ptrs_sweep.jsonl)
-    tcpcsum::Tuning tu = c->tune;
-    if (tu.shape < 0 && n < 65536u) tu.shape = 3;
+    const tcpcsum::Tuning tu = host_wire_tuning(c, n);
     hipError_t e;
     uint8_t* zp = (uint8_t*)pinned_dev_ptr(h_pkts, region_bytes);
     c->g_idx.clear();
@@ -961,10 +1002,7 @@ int tcpcsum_ipv4_batch_ptrs_host(tcpcsum_ctx_t* c, void* const* h_pkts, const ui
     c->stats.pkts_in_place += in_place;
     uint16_t* zout = h_out ? (uint16_t*)pinned_dev_ptr(h_out, n * sizeof(uint16_t)) : nullptr;
     uint8_t* zst = h_status ? (uint8_t*)pinned_dev_ptr(h_status, n) : nullptr;
-    // zero-copy over PCIe: the 16-lane group shape for latency-bound batches
-    // (as tcpcsum_ipv4_batch_host on a pinned pool)
-    tcpcsum::Tuning tu = c->tune;
-    if (tu.shape < 0 && n < 65536u) tu.shape = 3;
+    const tcpcsum::Tuning tu = host_wire_tuning(c, n);
     rc = stage_and_launch(c, n, cap, foot, mode, zout ? zout : (uint16_t*)c->p_out.d, zst ? zst : c->p_stat.d, st, tu);
     if (rc) return rc;
     hipError_t e = wait_stream(c, st, expect_ns(foot + c->stats.bytes_staged - staged_before));

@@ -121,4 +121,32 @@ print([r for r in rows if 'probe_med_ms' in r or (r.get('shape') == -1 and r.get
 "; return $rc
 }
 
+# in-place host FILL of one releaseSend batch: store shape x kernel shape (tools/host_fill_ab.py)
+host_fill() {
+  timeout -k 10 300 python3 -u tools/host_fill_ab.py > $O/host_fill.jsonl 2> $O/host_fill.err; rc=$?
+  cat $O/host_fill.jsonl; return $rc
+}
+
+# A/B of the in-tree library against tcp_amd/ab/$1/libtcpcsum.so on the seam (pool, staged) and
+# the in-place host FILL, interleaved $2 times (the old library through LD_LIBRARY_PATH /
+# TCPCSUM_LIB: mmsg_bench and the preload find libtcpcsum.so by RUNPATH, which it precedes)
+lib_ab() {
+  local old=$PWD/tcp_amd/ab/$1 reps=${2:-3}
+  for rep in $(seq 1 $reps); do
+    for which in new old; do
+      local lp="" tl=""
+      [ $which = old ] && lp=$old && tl=$old/libtcpcsum.so
+      for v in pool staged; do
+        local pool=0; [ $v = pool ] && pool=mmsg_bench
+        timeout -k 10 120 env LD_LIBRARY_PATH=$lp LD_PRELOAD=$PRE TCPCSUM_PRELOAD_ANY_SOCKET=1 \
+          TCPCSUM_PRELOAD_TX=fill TCPCSUM_PRELOAD_STATS=1 TCPCSUM_PRELOAD_POOL=$pool tools/mmsg_bench gpu 300 \
+          > $O/libab_${which}_${v}_$rep.json 2> $O/libab_${which}_${v}_$rep.err || return $?
+        echo "$which $v rep=$rep $(python3 -c "import json; d=json.load(open('$O/libab_${which}_${v}_$rep.json')); print(d['median_us'], d['min_us'], d['cpu_us_median'], d['checks_match_cpu'])") $(grep -o 'in_place=[0-9]*' $O/libab_${which}_${v}_$rep.err)"
+      done
+      env ${tl:+TCPCSUM_LIB=$tl} ROUNDS=2 timeout -k 10 200 python3 -u tools/host_fill_ab.py > $O/libab_${which}_hostfill_$rep.jsonl 2>> $O/libab.err || return $?
+      echo "$which hostfill rep=$rep $(head -2 $O/libab_${which}_hostfill_$rep.jsonl | tr '\n' ' ')"
+    done
+  done
+}
+
 "$@"
