@@ -2010,6 +2010,14 @@ UniformPlan plan_uniform(uintptr_t b, uint64_t stride, uint32_t len, uint64_t n,
         // loop (1M x 1500 B 0.2248 -> 0.2186 ms = 7.19 TB/s, 256 B -3 %, 576 B -7 %;
         // 4-8 KiB segments keep their grids; profiles/r02_grid_sweep.jsonl)
         p.max_blocks = 1 << 24;
+        // header-only segments (<= 4 chunks, 16-B aligned) in large batches: eight in
+        // flight per lane group on 1024 workgroups that loop, not one tile per wave —
+        // 1M x 64 B 12.28 vs 12.48 us and 12.21 vs 12.42 on two boxes, the best of 140
+        // shapes both times (profiles/r05_sweep64_shapes.jsonl, r05_sweep64_confirm.jsonl)
+        if (p.shape == 0 && p.mode == M16 && n >= (1u << 19) && !tu.unroll) {
+            p.unroll = 8;
+            p.max_blocks = 1024;
+        }
     } else if (p.shape == 9 && tu.max_blocks <= 0 && (p.mode != M16 || len < 12288u)) {
         // one wave per segment: segments of one round (jumbo frames, 8-12 KiB)
         // and the dword-masked path want more waves than the 64 KiB config's

@@ -149,4 +149,26 @@ lib_ab() {
   done
 }
 
+# the round's one rehearsal: every GPU test, smoke(), the default bench line, a rocprofv3
+# kernel trace of the bench, and PMC passes (FETCH_SIZE of the headline; WRITE_SIZE and
+# FETCH_SIZE of the wire FILL / VERIFY / write-back probe), each pass its own run
+final() {
+  export TMPDIR=/tmp
+  tests || return $?
+  cp $O/gputest.txt $O/gputest_final.txt
+  timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 || { cat $O/smoke.txt; return 1; }
+  tail -3 $O/smoke.txt
+  bench || return $?
+  cp $O/bench.json $O/bench_final.json
+  timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o bench -- \
+    python3 bench.py --no-host-path --no-cpu-baseline > $O/bench_under_rocprof.json 2> $O/rocprof.err || return $?
+  timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_h -o fetch -- \
+    python3 bench.py --steps 50 --no-other-configs --no-host-path --no-cpu-baseline > $O/pmc_h.json 2> $O/pmc_h.err || return $?
+  timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_w -o write -- \
+    python3 tools/wire_fill_pmc.py > $O/pmc_w.txt 2> $O/pmc_w.err || return $?
+  timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_f -o fetch -- \
+    python3 tools/wire_fill_pmc.py > $O/pmc_f.txt 2> $O/pmc_f.err || return $?
+  find $O/prof $O/pmc_h $O/pmc_w $O/pmc_f -name "*.csv" | head -20
+}
+
 "$@"

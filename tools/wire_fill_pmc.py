@@ -3,7 +3,9 @@
 1M x 1500-B packets in 1536-B slots (device), 10 FILLs with the 2-byte store
 (TCPCSUM_TUNE_FILL_U16), then 10 FILLs with the default line store, then 10
 VERIFYs — in that order, so the rows of a rocprofv3 --pmc run (same kernel
-name for all three) are told apart by dispatch order.
+name for all three) are told apart by dispatch order — then 10 launches of the
+write-back probe over the same region (k_probe<8, true>: exactly 1M x 1536 B
+read and 1M x 128 B written through), the counters' calibration.
 
   rocprofv3 --pmc WRITE_SIZE --output-format csv -d DIR -o p -- python3 tools/wire_fill_pmc.py
 """
@@ -40,6 +42,11 @@ def main():
         tcp_amd.ipv4_batch(reg, off, n, slot, 1, out, st)
     torch.cuda.synchronize()
     assert bool((out == 0).all().item())
+    # calibration: the write-back probe moves exactly 1M x 1536 B read + 1M x 128 B written
+    pout = torch.zeros(tcp_amd.api.PROBE_SLOTS, dtype=torch.int64, device=dev)
+    for _ in range(10):
+        tcp_amd.stream_probe(reg, n * slot, pout, tune=(8192, 1, slot // 128, tcp_amd.TUNE_PROBE_WRITE))
+    torch.cuda.synchronize()
     print("ok")
 
 
