@@ -2013,7 +2013,9 @@ UniformPlan plan_uniform(uintptr_t b, uint64_t stride, uint32_t len, uint64_t n,
         // header-only segments (<= 4 chunks, 16-B aligned) in large batches: eight in
         // flight per lane group on 1024 workgroups that loop, not one tile per wave —
         // 1M x 64 B 12.28 vs 12.48 us and 12.21 vs 12.42 on two boxes, the best of 140
-        // shapes both times (profiles/r05_sweep64_shapes.jsonl, r05_sweep64_confirm.jsonl)
+        // shapes both times; as bench.py's headline config, alternating fresh processes,
+        // 12.60-12.65 vs 12.71-12.81 us (profiles/r05_sweep64_shapes.jsonl,
+        // r05_sweep64_confirm.jsonl, r05_ab64_bench_form.jsonl)
         if (p.shape == 0 && p.mode == M16 && n >= (1u << 19) && !tu.unroll) {
             p.unroll = 8;
             p.max_blocks = 1024;
