@@ -131,14 +131,13 @@ static uint8_t *g_status;
 static struct tcpcsum_preload_stats g_st;
 
 /* ------------------------------------------------------------------ the arena
- * TCPCSUM_PRELOAD_POOL=1: malloc(kPoolBlock) served from page-locked memory the
+ * TCPCSUM_PRELOAD_POOL: malloc(kPoolBlock) served from page-locked memory the
  * library owns (preload_arena.h). t_guard: this thread is inside the library
  * (the constructor's HIP start-up, a GPU batch) — its allocations of the block
  * size are the runtime's, not the loop's, and go to libc. */
 enum { kPoolBlock = 1024 * 32 };   /* loop.c:181-182 */
 static arena_t g_arena = ARENA_INIT;
 static __thread int t_guard __attribute__((tls_model("initial-exec")));
-static int g_pool_asked, g_pool_failed;
 
 extern void *__libc_malloc(size_t);
 extern void __libc_free(void *);
@@ -185,8 +184,6 @@ size_t malloc_usable_size(void *p) {
     return f ? f(p) : 0;
 }
 
-/* Before main: the pool's page-locked block, so HIP never starts inside a malloc
- * call. Dependencies' constructors (the HIP runtime's) have run by now. */
 /* TCPCSUM_PRELOAD_POOL names the process the pool is for: "1" any process that
  * loads the interposer, else the basename of its executable ("stress") — so a
  * wrapper the preload also reaches (timeout, a shell) neither consumes the
@@ -202,15 +199,15 @@ static int pool_wanted(const char *v) {
     return !strcmp(base ? base + 1 : exe, v);
 }
 
+/* Before main: the pool's page-locked block, so HIP never starts inside a malloc
+ * call. Dependencies' constructors (the HIP runtime's) have run by now. */
 __attribute__((constructor)) static void pool_ctor(void) {
     if (!pool_wanted(getenv("TCPCSUM_PRELOAD_POOL"))) return;
-    g_pool_asked = 1;
     unsetenv("TCPCSUM_PRELOAD_POOL");   /* children (an exec'd shell, say) never start HIP for it */
     t_guard = 1;
     void *mem = tcpcsum_host_alloc((size_t) kPoolBlock * ARENA_MAX_BLOCKS);
     t_guard = 0;
     if (!mem || arena_publish(&g_arena, mem, kPoolBlock, ARENA_MAX_BLOCKS)) {
-        g_pool_failed = 1;
         fprintf(stderr, "tcpcsum_preload: TCPCSUM_PRELOAD_POOL: no page-locked pool (%s); the loop's buffers stay "
                         "malloc'd and are copied into staging\n", mem ? "publish failed" : tcpcsum_strerror(TCPCSUM_ENOMEM));
     }
