@@ -90,6 +90,17 @@
  * iovec when that holds the whole packet; otherwise it is skipped and, in drop
  * mode, passed through unverified (a scatter read the library cannot see whole).
  */
+/*
+ * Built twice (Makefile): as the LD_PRELOAD library above, and with
+ * -DTCPCSUM_WRAP as tcp_amd/libtcpcsum_wrap.a for the link-time seam SURVEY.md
+ * §8(b)(ii) names — link the loop with
+ *     -Wl,--wrap=sendmmsg,--wrap=recvmmsg  (+ ,--wrap=malloc,--wrap=calloc,--wrap=free,--wrap=realloc
+ *                                           for TCPCSUM_PRELOAD_POOL: all four, or none)
+ *     tcp_amd/libtcpcsum_wrap.a -ltcpcsum -ldl -lpthread
+ * and the same entry points become __wrap_sendmmsg / __wrap_recvmmsg (the real
+ * calls __real_*). Its arena then serves only the wrapped objects' own mallocs —
+ * the loop's, never the HIP runtime's. The environment variables are the same.
+ */
 #define _GNU_SOURCE
 #include <dirent.h>
 #include <dlfcn.h>
@@ -144,24 +155,41 @@ extern void __libc_free(void *);
 extern void *__libc_realloc(void *, size_t);
 extern void *__libc_calloc(size_t, size_t);
 
-static const arena_libc_t k_libc = {__libc_malloc, __libc_free, __libc_realloc};
+#ifdef TCPCSUM_WRAP
+/* link-time seam: the wrapped objects' calls land here, the rest of the process
+ * (HIP included) keeps libc's allocator untouched */
+#define SEAM(fn) __wrap_##fn
+#define UNDER(fn) __real_##fn
+void *__real_malloc(size_t);
+void __real_free(void *);
+void *__real_realloc(void *, size_t);
+void *__real_calloc(size_t, size_t);
+int __real_sendmmsg(int, struct mmsghdr *, unsigned int, int);
+int __real_recvmmsg(int, struct mmsghdr *, unsigned int, int, struct timespec *);
+#else
+#define SEAM(fn) fn
+#define UNDER(fn) __libc_##fn
+#endif
 
-void *malloc(size_t n) {
+static const arena_libc_t k_libc = {UNDER(malloc), UNDER(free), UNDER(realloc)};
+
+void *SEAM(malloc)(size_t n) {
     return arena_route_malloc(&g_arena, n, t_guard, &k_libc);
 }
 
-void *calloc(size_t nmemb, size_t size) {
-    return arena_route_calloc(&g_arena, nmemb, size, t_guard, __libc_calloc);
+void *SEAM(calloc)(size_t nmemb, size_t size) {
+    return arena_route_calloc(&g_arena, nmemb, size, t_guard, UNDER(calloc));
 }
 
-void free(void *p) {
+void SEAM(free)(void *p) {
     arena_route_free(&g_arena, p, &k_libc);
 }
 
-void *realloc(void *p, size_t n) {
+void *SEAM(realloc)(void *p, size_t n) {
     return arena_route_realloc(&g_arena, p, n, &k_libc);
 }
 
+#ifndef TCPCSUM_WRAP
 /* glibc's reallocarray calls its own realloc internally, which must never see an
  * arena pointer */
 void *reallocarray(void *p, size_t nmemb, size_t size) {
@@ -183,6 +211,7 @@ size_t malloc_usable_size(void *p) {
     }
     return f ? f(p) : 0;
 }
+#endif
 
 /* TCPCSUM_PRELOAD_POOL names the process the pool is for: "1" any process that
  * loads the interposer, else the basename of its executable ("stress") — so a
@@ -275,8 +304,13 @@ static void print_stats(void) {
 }
 
 static void init_once(void) {
+#ifdef TCPCSUM_WRAP
+    real_sendmmsg = __real_sendmmsg;
+    real_recvmmsg = __real_recvmmsg;
+#else
     real_sendmmsg = (sendmmsg_fn) dlsym(RTLD_NEXT, "sendmmsg");
     real_recvmmsg = (recvmmsg_fn) dlsym(RTLD_NEXT, "recvmmsg");
+#endif
     g_tx = env_mode("TCPCSUM_PRELOAD_TX", MODE_FILL);
     if (g_tx == MODE_DROP) g_tx = MODE_VERIFY;   /* never drop what the application sends */
     g_rx = env_mode("TCPCSUM_PRELOAD_RX", MODE_OFF);
@@ -428,7 +462,7 @@ static unsigned int first_iov_bytes(const struct mmsghdr *m, int is_tx) {
     return n > 0xFFFFFFFFu ? 0xFFFFFFFFu : (unsigned int) n;
 }
 
-int sendmmsg(int fd, struct mmsghdr *vec, unsigned int vlen, int flags) {
+int SEAM(sendmmsg)(int fd, struct mmsghdr *vec, unsigned int vlen, int flags) {
     pthread_once(&g_once, init_once);
     if (g_tx != MODE_OFF && vlen && vec && wants_fd(fd)) {
         unsigned int lens[1024];
@@ -447,7 +481,7 @@ int sendmmsg(int fd, struct mmsghdr *vec, unsigned int vlen, int flags) {
     return real_sendmmsg(fd, vec, vlen, flags);
 }
 
-int recvmmsg(int fd, struct mmsghdr *vec, unsigned int vlen, int flags, struct timespec *timeout) {
+int SEAM(recvmmsg)(int fd, struct mmsghdr *vec, unsigned int vlen, int flags, struct timespec *timeout) {
     pthread_once(&g_once, init_once);
     int r = real_recvmmsg(fd, vec, vlen, flags, timeout);
     if (r > 0 && g_rx != MODE_OFF && wants_fd(fd)) {

@@ -19,24 +19,29 @@ import oracle
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EXE = os.path.join(REPO, "tests", "c", "mmsg_loop")
+EXE_WRAP = os.path.join(REPO, "tests", "c", "mmsg_loop_wrap")   # the seam linked in (-Wl,--wrap=...)
 PRELOAD = os.path.join(REPO, "tcp_amd", "libtcpcsum_preload.so")
 
 
 def _ensure_built():
-    if not (os.path.exists(EXE) and os.path.exists(PRELOAD)):
-        subprocess.run(["make", "-C", REPO, "tests/c/mmsg_loop", "tcp_amd/libtcpcsum_preload.so"], check=True)
+    if not (os.path.exists(EXE) and os.path.exists(PRELOAD) and os.path.exists(EXE_WRAP)):
+        subprocess.run(["make", "-C", REPO, "tests/c/mmsg_loop", "tests/c/mmsg_loop_wrap",
+                        "tcp_amd/libtcpcsum_preload.so"], check=True)
 
 
 def run_loop(tmp_path, n, env_extra, cpu_checks=False, corrupt=False, trunc=False, forge=False, pinned=False,
-             iov2=False):
+             iov2=False, wrap=False):
+    """Run mmsg_loop under the LD_PRELOAD interposer, or (wrap) its build with the seam linked in."""
     _ensure_built()
     out = tmp_path / "mm.bin"
-    env = {k: v for k, v in os.environ.items() if not k.startswith("TCPCSUM_PRELOAD")}
-    env.update({"LD_PRELOAD": PRELOAD, "TCPCSUM_PRELOAD_ANY_SOCKET": "1", "TCPCSUM_PRELOAD_STATS": "1"})
+    env = {k: v for k, v in os.environ.items() if not k.startswith("TCPCSUM_PRELOAD") and k != "LD_PRELOAD"}
+    env.update({"TCPCSUM_PRELOAD_ANY_SOCKET": "1", "TCPCSUM_PRELOAD_STATS": "1"})
+    if not wrap:
+        env["LD_PRELOAD"] = PRELOAD
     env.update(env_extra)
     mode = ("trunc" if trunc else "corrupt" if corrupt else "forge" if forge else
             "cpu-checks" if cpu_checks else "plain")
-    args = [EXE, str(n), str(out), mode] + (["pinned"] if pinned else ["iov2"] if iov2 else [])
+    args = [EXE_WRAP if wrap else EXE, str(n), str(out), mode] + (["pinned"] if pinned else ["iov2"] if iov2 else [])
     r = subprocess.run(args, env=env, capture_output=True, text=True, timeout=120)
     pkts = []
     if r.returncode == 0:
@@ -118,6 +123,19 @@ def test_pool_only_for_the_named_program(tmp_path, name, tried):
     assert stats["pool_on"] == 0 and len(pkts) == 300
 
 
+def test_wrap_seam_passthrough_and_refusal(tmp_path):
+    """The link-time form (-Wl,--wrap=sendmmsg,recvmmsg,malloc,calloc,free,realloc against
+    tcp_amd/libtcpcsum_wrap.a): with TX off every packet goes through untouched; without a GPU,
+    FILL refuses loudly (ENXIO) exactly as the preload does."""
+    import tcp_amd
+    r, pkts, stats = run_loop(tmp_path, 150, {"TCPCSUM_PRELOAD_TX": "off"}, wrap=True)
+    assert r.returncode == 0, r.stderr
+    assert len(pkts) == 150 and all(b == g for b, g in pkts) and stats["tx_packets"] == 0
+    if tcp_amd.device_check()[0] != 0:
+        r, _, _ = run_loop(tmp_path, 10, {"TCPCSUM_PRELOAD_TX": "fill"}, wrap=True)
+        assert r.returncode == 3 and "No such device or address" in r.stderr
+
+
 def test_fails_loudly_without_gpu(tmp_path):
     import tcp_amd
     if tcp_amd.device_check()[0] == 0:
@@ -163,6 +181,25 @@ def test_pool_zero_copy_loop_unedited(tmp_path):
     assert stats["pool_released"] == 2048                      # the loop's free()s came back to the arena
     assert stats["tx_filled"] == n and stats["rx_verified"] == n and stats["rx_verify_failed"] == 0
     assert stats["ctx_in_place"] == 2 * n and stats["ctx_staged"] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pool", ["0", "mmsg_loop_wrap"])
+def test_wrap_seam_on_gpu(tmp_path, pool):
+    """The seam linked in at build time (-Wl,--wrap=..., tcp_amd/libtcpcsum_wrap.a), no LD_PRELOAD:
+    every packet filled on the GPU equals the oracle's FILL and verifies on receive. With the pool, the
+    wrapped mallocs of the loop's 2 x 1024 buffers come from the arena and both seams run in place —
+    while the HIP runtime's own allocations never pass through the wrap at all."""
+    n = 2500
+    r, pkts, stats = run_loop(tmp_path, n, {"TCPCSUM_PRELOAD_TX": "fill", "TCPCSUM_PRELOAD_RX": "verify",
+                                            "TCPCSUM_PRELOAD_POOL": pool}, wrap=True)
+    assert r.returncode == 0, r.stderr
+    assert len(pkts) == n and all(got == oracle_fill(built) for built, got in pkts)
+    assert stats["tx_filled"] == n and stats["rx_verified"] == n and stats["rx_verify_failed"] == 0
+    if pool != "0":
+        assert stats["pool_served"] == 2048 and stats["ctx_in_place"] == 2 * n and stats["ctx_staged"] == 0
+    else:
+        assert stats["pool_on"] == 0 and stats["ctx_staged"] == 2 * n
 
 
 @pytest.mark.gpu
