@@ -33,8 +33,14 @@
 #ifndef TCPCSUM_TX_WAVES
 #define TCPCSUM_TX_WAVES 1
 #endif
+//   TCPCSUM_LINE_CPOL        cache-policy bits of the 16-B line stores (wire FILL, write-back
+//                            probe): 17 = sc0|sc1, written through (the product's)
+#ifndef TCPCSUM_LINE_CPOL
+#define TCPCSUM_LINE_CPOL 17
+#endif
 #if !TCPCSUM_MEASUREMENT_BUILD && \
-    (TCPCSUM_TUNING_VARIANTS != 0 || TCPCSUM_TX_KNOCKOUT != 0 || TCPCSUM_WIRE_WAVES != 1 || TCPCSUM_TX_WAVES != 1)
+    (TCPCSUM_TUNING_VARIANTS != 0 || TCPCSUM_TX_KNOCKOUT != 0 || TCPCSUM_WIRE_WAVES != 1 || TCPCSUM_TX_WAVES != 1 || \
+     TCPCSUM_LINE_CPOL != 17)
 #error "tuning / knock-out / waves knobs are for measurement builds only (-DTCPCSUM_MEASUREMENT_BUILD=1), never a product library"
 #endif
 // Environment variables a context reads at creation (tcpcsum_build_info "runtime_knobs"):

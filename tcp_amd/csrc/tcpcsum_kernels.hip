@@ -889,7 +889,7 @@ __device__ __forceinline__ void store_u16(uint8_t* p, uint16_t v) {
 // exactly global_store_{byte,short} sc0 sc1 on gfx950 (the memory model's
 // system-scope store: no wait, no fence); a 16-byte one is a raw buffer store
 // with cache policy sc0|sc1 (CPol bits 1 | 16).
-constexpr int kCpolSc0Sc1 = 1 | 16;
+constexpr int kCpolSc0Sc1 = TCPCSUM_LINE_CPOL;   // 1 | 16 (measurement builds may change it)
 
 template <class T>
 __device__ __forceinline__ void stg_wt(uint8_t* p, T v) {

@@ -68,7 +68,7 @@ def test_library_is_a_product_build_of_this_tree():
     info = provenance.check_product_build()
     assert info["abi"] == api.lib().tcpcsum_abi_version() and info["arch"] == "gfx950"
     assert info["knobs"] == {"TCPCSUM_MEASUREMENT_BUILD": 0, "TCPCSUM_TUNING_VARIANTS": 0, "TCPCSUM_TX_KNOCKOUT": 0,
-                             "TCPCSUM_WIRE_WAVES": 1, "TCPCSUM_TX_WAVES": 1}
+                             "TCPCSUM_WIRE_WAVES": 1, "TCPCSUM_TX_WAVES": 1, "TCPCSUM_LINE_CPOL": 17}
     # the only environment a product context reads
     assert info["runtime_knobs"] == ["TCPCSUM_HOST_THREADS", "TCPCSUM_HOST_NUMA", "TCPCSUM_HOST_SPIN_US",
                                      "LOCAL_WORLD_SIZE"]
@@ -100,7 +100,7 @@ def test_product_build_refuses_measurement_knobs(tmp_path):
         pytest.skip("no hipcc")
     ok = subprocess.run(base, capture_output=True, text=True)
     assert ok.returncode == 0, ok.stderr
-    for knob in ("-DTCPCSUM_TX_KNOCKOUT=8", "-DTCPCSUM_WIRE_WAVES=5", "-DTCPCSUM_TUNING_VARIANTS=1"):
+    for knob in ("-DTCPCSUM_TX_KNOCKOUT=8", "-DTCPCSUM_WIRE_WAVES=5", "-DTCPCSUM_TUNING_VARIANTS=1", "-DTCPCSUM_LINE_CPOL=2"):
         bad = subprocess.run(base + [knob], capture_output=True, text=True)
         assert bad.returncode != 0 and "measurement builds only" in bad.stderr, knob
         meas = subprocess.run(base + [knob, "-DTCPCSUM_MEASUREMENT_BUILD=1"], capture_output=True, text=True)

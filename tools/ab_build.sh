@@ -1,10 +1,12 @@
 #!/usr/bin/env bash
 # Build the library as it was at a git revision, for same-process A/B runs against
 # the in-tree build (tools/wire_lib_ab.py, tools/lb_ab.py ...):
-#   bash tools/ab_build.sh <rev> <name>   ->  tcp_amd/ab/libtcpcsum_<name>.so
+#   bash tools/ab_build.sh <rev> <name> [extra compiler flags]  ->  tcp_amd/ab/libtcpcsum_<name>.so
+# Extra flags set measurement knobs, e.g. -DTCPCSUM_MEASUREMENT_BUILD=1 -DTCPCSUM_LINE_CPOL=2.
 # (CPU only: hipcc cross-compiles gfx950 here; the .so travels with the tree.)
 set -euo pipefail
-rev=$1; name=$2
+rev=$1; name=$2; shift 2
+extra=("$@")
 src=$(mktemp -d)
 trap 'rm -rf "$src"' EXIT
 git archive "$rev" tcp_amd/csrc include | tar -x -C "$src"
@@ -12,7 +14,7 @@ mkdir -p tcp_amd/ab
 objs=()
 for f in "$src"/tcp_amd/csrc/*.hip; do
   o="$src/$(basename "$f" .hip).o"
-  /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wno-unused-value -Wno-unused-result -I"$src/include" -c "$f" -o "$o" &
+  /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wno-unused-value -Wno-unused-result "${extra[@]}" -I"$src/include" -c "$f" -o "$o" &
   objs+=("$o")
 done
 for f in "$src"/tcp_amd/csrc/*.c; do
