@@ -169,6 +169,10 @@ final() {
   timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_f -o fetch -- \
     python3 tools/wire_fill_pmc.py > $O/pmc_f.txt 2> $O/pmc_f.err || return $?
   find $O/prof $O/pmc_h $O/pmc_w $O/pmc_f -name "*.csv" | head -20
+  # last: round 4's exit-time SIGSEGV record (gpurun_out/r4_hostprof.err) — the same command again
+  timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $O/hostprof -o h -- \
+    python3 bench.py --host-path-only --host-steps 5 > $O/hostprof.json 2> $O/hostprof.err
+  echo "hostprof rc=$?"
 }
 
 "$@"
