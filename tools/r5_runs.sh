@@ -175,4 +175,15 @@ final() {
   echo "hostprof rc=$?"
 }
 
+# round 4's exit-time SIGSEGV under rocprofv3 --memory-copy-trace, with the process's address map
+# saved at exit (tools/maps_at_exit.py) so the faulting frames can be resolved to libraries
+hostprof_maps() {
+  export TMPDIR=/tmp MAPS_OUT=$O/maps_at_exit.txt
+  timeout -k 10 300 rocprofv3 ${@:---kernel-trace --memory-copy-trace} --output-format csv -d $O/hostprof2 -o h -- \
+    python3 tools/maps_at_exit.py bench.py --host-path-only --host-steps 5 > $O/hostprof2.json 2> $O/hostprof2.err
+  local rc=$?
+  cp /proc/self/maps $O/maps_shell.txt 2>/dev/null
+  echo "hostprof rc=$rc"; tail -20 $O/hostprof2.err
+}
+
 "$@"
