@@ -119,7 +119,8 @@ const char* tcpcsum_build_info(void) {
         ", \"TCPCSUM_TX_KNOCKOUT\": " TCPCSUM_STR(TCPCSUM_TX_KNOCKOUT)
         ", \"TCPCSUM_WIRE_WAVES\": " TCPCSUM_STR(TCPCSUM_WIRE_WAVES)
         ", \"TCPCSUM_TX_WAVES\": " TCPCSUM_STR(TCPCSUM_TX_WAVES)
-        ", \"TCPCSUM_LINE_CPOL\": " TCPCSUM_STR(TCPCSUM_LINE_CPOL) "}"
+        ", \"TCPCSUM_LINE_CPOL\": " TCPCSUM_STR(TCPCSUM_LINE_CPOL)
+        ", \"TCPCSUM_LOAD_CPOL\": " TCPCSUM_STR(TCPCSUM_LOAD_CPOL) "}"
         ", \"runtime_knobs\": [" TCPCSUM_RUNTIME_KNOBS_JSON "]}";
     return info;
 }

@@ -38,9 +38,15 @@
 #ifndef TCPCSUM_LINE_CPOL
 #define TCPCSUM_LINE_CPOL 17
 #endif
+//   TCPCSUM_LOAD_CPOL        >= 0: the uniform kernel's segment loads become buffer loads with
+//                            these cache-policy bits (batches under 4 GiB only); -1: global
+//                            loads, non-temporal (the product's)
+#ifndef TCPCSUM_LOAD_CPOL
+#define TCPCSUM_LOAD_CPOL -1
+#endif
 #if !TCPCSUM_MEASUREMENT_BUILD && \
     (TCPCSUM_TUNING_VARIANTS != 0 || TCPCSUM_TX_KNOCKOUT != 0 || TCPCSUM_WIRE_WAVES != 1 || TCPCSUM_TX_WAVES != 1 || \
-     TCPCSUM_LINE_CPOL != 17)
+     TCPCSUM_LINE_CPOL != 17 || TCPCSUM_LOAD_CPOL != -1)
 #error "tuning / knock-out / waves knobs are for measurement builds only (-DTCPCSUM_MEASUREMENT_BUILD=1), never a product library"
 #endif
 // Environment variables a context reads at creation (tcpcsum_build_info "runtime_knobs"):

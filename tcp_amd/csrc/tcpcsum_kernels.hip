@@ -196,7 +196,17 @@ struct UniformTile {
 #pragma unroll
             for (int k = 0; k < C; ++k) {
                 const uint32_t idx = (uint32_t)(k * G + gl);
+#if TCPCSUM_LOAD_CPOL >= 0   // measurement builds: buffer loads with chosen cache-policy bits
+                const uint8_t* b0 = reinterpret_cast<const uint8_t*>((uintptr_t)base & ~(uintptr_t)15u);
+                const __amdgpu_buffer_rsrc_t rs =
+                    __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(b0), 0, -1, 0x00020000);
+                v[u][k] = (live && idx < nch)
+                              ? __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(uint32_t)(a0 - b0) + (int)(idx * 16u), 0,
+                                                                       TCPCSUM_LOAD_CPOL)
+                              : u32x4{0u, 0u, 0u, 0u};
+#else
                 v[u][k] = (live && idx < nch) ? ldq<NT>(a0 + (uint64_t)idx * 16u) : u32x4{0u, 0u, 0u, 0u};
+#endif
             }
         }
     }
