@@ -10,6 +10,7 @@
 
 #include <cstdio>
 #include <set>
+#include <string>
 #include <vector>
 
 static int fails = 0;
@@ -90,6 +91,28 @@ int main() {
         for (int rep = 0; rep < 10; ++rep) exactly_once(pinned, 10000, 16);
         cpu_set_t none;
         EXPECT(!tcpcsum::numa_node_cpus("no-such-bus", &none));   // no device: no pinning
+    }
+    {   // copy threads per context: TCPCSUM_HOST_THREADS, else half the usable CPUs (1..8) alone,
+        // or the rank's 1/LOCAL_WORLD_SIZE share of them (1..8) beside co-located ranks
+        unsetenv("TCPCSUM_HOST_THREADS");
+        unsetenv("LOCAL_WORLD_SIZE");
+        const int alone = tcpcsum::default_copy_threads();
+        EXPECT(alone >= 1 && alone <= 8);
+        cpu_set_t set;
+        EXPECT(sched_getaffinity(0, sizeof set, &set) == 0);
+        const int cpus = CPU_COUNT(&set);   // this container has no cgroup quota below its mask
+        for (int k : {2, 4, 8, 64}) {
+            setenv("LOCAL_WORLD_SIZE", std::to_string(k).c_str(), 1);
+            const int share = tcpcsum::default_copy_threads();
+            EXPECT(share >= 1 && share <= 8 && share <= std::max(1, cpus / k));
+        }
+        setenv("LOCAL_WORLD_SIZE", "1", 1);
+        EXPECT(tcpcsum::default_copy_threads() == alone);
+        setenv("TCPCSUM_HOST_THREADS", "3", 1);   // explicit: wins over the share
+        setenv("LOCAL_WORLD_SIZE", "8", 1);
+        EXPECT(tcpcsum::default_copy_threads() == 3);
+        unsetenv("TCPCSUM_HOST_THREADS");
+        unsetenv("LOCAL_WORLD_SIZE");
     }
     std::printf(fails ? "copy_pool_test: %d failures\n" : "copy_pool_test: OK\n", fails);
     return fails ? 1 : 0;

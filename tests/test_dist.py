@@ -49,7 +49,7 @@ def _worker(rank, world, port, total, seg_len, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,total", [(2, 4096), (2, 4097), (3, 1000)])
+@pytest.mark.parametrize("world,total", [(2, 4096), (2, 4097), (3, 1000), (8, 8192)])
 def test_sharded_equals_unsharded_gloo(world, total):
     import torch.multiprocessing as mp
 
