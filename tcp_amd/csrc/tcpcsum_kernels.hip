@@ -248,7 +248,13 @@ __global__ __launch_bounds__(256) void k_uniform(const uint8_t* __restrict__ bas
     const int q = lane / G, gl = lane % G;
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
     const uint64_t ntiles = (n + Tile::SPT - 1) / Tile::SPT;
+#if TCPCSUM_XCD_REMAP   // measurement builds: tiles XCD by XCD
+    const uint32_t nb = gridDim.x, bx = blockIdx.x;
+    const uint64_t blk = (nb % 8u == 0u) ? (uint64_t)(bx % 8u) * (nb / 8u) + bx / 8u : (uint64_t)bx;
+    const uint64_t wave = blk * 4u + (threadIdx.x >> 6);
+#else
     const uint64_t wave = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
+#endif
     uint64_t t = wave;
     if constexpr (!PIPE) {
         Tile a;
