@@ -17,6 +17,8 @@
  * nothing is owned, nothing is served).
  *
  *   arena_publish  hand the arena its memory (once; readers see all of it or none)
+ *   arena_close    serve no more blocks (a forked child: the page-locked memory is
+ *                  the parent's); blocks already out are still owned and released
  *   arena_alloc    a free block when size == block, else NULL (caller falls through
  *                  to libc); NULL too when every block is taken
  *   arena_owns     whether p lies inside the arena (free / realloc / usable-size
@@ -46,10 +48,11 @@ typedef struct {
     uint16_t free_idx[ARENA_MAX_BLOCKS];
     uint8_t in_use[ARENA_MAX_BLOCKS];
     uint64_t served, released, full;   /* counters (under mu) */
+    int closed;               /* arena_close: nothing more is served */
     pthread_mutex_t mu;
 } arena_t;
 
-#define ARENA_INIT {NULL, NULL, 0, 0, 0, 0, {0}, {0}, 0, 0, 0, PTHREAD_MUTEX_INITIALIZER}
+#define ARENA_INIT {NULL, NULL, 0, 0, 0, 0, {0}, {0}, 0, 0, 0, 0, PTHREAD_MUTEX_INITIALIZER}
 
 static inline uint8_t *arena_base(const arena_t *a) {
     return __atomic_load_n(&a->base, __ATOMIC_ACQUIRE);
@@ -71,6 +74,10 @@ static inline int arena_publish(arena_t *a, void *mem, size_t block, uint32_t nb
     return 0;
 }
 
+static inline void arena_close(arena_t *a) {
+    __atomic_store_n(&a->closed, 1, __ATOMIC_RELEASE);
+}
+
 static inline int arena_owns(const arena_t *a, const void *p) {
     const uint8_t *b = arena_base(a);
     return b && (const uint8_t *) p >= b && (const uint8_t *) p < a->end;
@@ -83,7 +90,7 @@ static inline size_t arena_block(const arena_t *a) {
 
 static inline void *arena_alloc(arena_t *a, size_t size) {
     uint8_t *b = arena_base(a);
-    if (!b || size != a->block) return NULL;
+    if (!b || size != a->block || __atomic_load_n(&a->closed, __ATOMIC_ACQUIRE)) return NULL;
     pthread_mutex_lock(&a->mu);
     uint32_t idx;
     if (a->nfree) {

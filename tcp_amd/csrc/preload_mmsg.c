@@ -53,9 +53,12 @@
  *                                LD_PRELOAD on the loop binary itself, never on a
  *                                wrapper (timeout, a shell). The process that takes the
  *                                pool removes the variable from its environment before
- *                                HIP starts, so its children do not inherit it. A
- *                                forked child must not touch arena buffers
- *                                (page-locked memory is not inherited).
+ *                                HIP starts, so its children do not inherit it.
+ *   fork: a child of a process whose interposer started HIP (the pool, or a GPU batch)
+ *   has no GPU path — HIP does not survive fork — so its seams fail with ENXIO; its
+ *   mallocs go to libc (the arena is closed in the child), and it must not touch the
+ *   parent's arena buffers (page-locked memory need not be inherited), though freeing
+ *   them is allowed (bookkeeping only).
  *
  * Buffers the application page-locked (tcpcsum_host_alloc for its out-buffer
  * pool, loop.c:180-183 — INTEGRATION.md level 2 — or its own hipHostRegister)
@@ -137,6 +140,7 @@ static recvmmsg_fn real_recvmmsg;
 static int g_tx = MODE_FILL, g_rx = MODE_OFF, g_iphdr, g_any, g_stats, g_device, g_localnet;
 static tcpcsum_ctx_t *g_ctx;
 static int g_ctx_failed;
+static int g_forked;        /* a forked child of a process that had started HIP */
 static uint16_t *g_out;     /* pinned: the kernel writes results straight here */
 static uint8_t *g_status;
 static struct tcpcsum_preload_stats g_st;
@@ -242,6 +246,37 @@ __attribute__((constructor)) static void pool_ctor(void) {
     }
 }
 
+/* fork: the handlers hold the interposer's locks across it, so the child never
+ * inherits one taken mid-update; the child then gives up the GPU path and the arena
+ * if the parent had started HIP for them. */
+static void fork_prepare(void) {
+    pthread_mutex_lock(&g_mu);
+    pthread_mutex_lock(&g_arena.mu);
+}
+
+static void fork_parent(void) {
+    pthread_mutex_unlock(&g_arena.mu);
+    pthread_mutex_unlock(&g_mu);
+}
+
+static void fork_child(void) {
+    pthread_mutex_unlock(&g_arena.mu);
+    if (g_ctx || arena_base(&g_arena)) {
+        arena_close(&g_arena);
+        g_ctx = NULL;   /* the parent's: not usable, not destroyable here */
+        g_out = NULL;
+        g_status = NULL;
+        g_ctx_failed = 1;
+        g_forked = 1;
+        g_stats = 0;    /* the counters are the parent's */
+    }
+    pthread_mutex_unlock(&g_mu);
+}
+
+__attribute__((constructor)) static void fork_ctor(void) {
+    pthread_atfork(fork_prepare, fork_parent, fork_child);
+}
+
 /* ------------------------------------------------------------------ seams */
 static int env_mode(const char *name, int dflt) {
     const char *v = getenv(name);
@@ -329,6 +364,11 @@ static void init_once(void) {
     atexit(print_stats);
 }
 
+/* Exported for tests: whether p is one of the pool's blocks. */
+int tcpcsum_preload_pool_owns(const void *p) {
+    return arena_owns(&g_arena, p);
+}
+
 /* Exported for tests / the application: a copy of the counters. */
 void tcpcsum_preload_get_stats(struct tcpcsum_preload_stats *out) {
     pthread_mutex_lock(&g_mu);
@@ -348,6 +388,11 @@ static int wants_fd(int fd) {
 
 /* g_mu held. */
 static int ensure_ctx(void) {
+    if (g_forked == 1) {
+        fprintf(stderr, "tcpcsum_preload: forked child of a process that started HIP: no GPU path here; refusing to "
+                        "send/accept packets with unchecked checksums\n");
+        g_forked = 2;   /* said once */
+    }
     if (g_ctx_failed) return -1;
     if (!g_ctx) {
         int rc = tcpcsum_ctx_create(g_device, 0, &g_ctx);

@@ -248,13 +248,16 @@ __global__ __launch_bounds__(256) void k_uniform(const uint8_t* __restrict__ bas
     const int q = lane / G, gl = lane % G;
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
     const uint64_t ntiles = (n + Tile::SPT - 1) / Tile::SPT;
-#if TCPCSUM_XCD_REMAP   // measurement builds: tiles XCD by XCD
+    // XCD-aware tile order (one tile per wave, a whole number of XCD rounds): workgroups are
+    // dispatched to the 8 XCDs round-robin, so block b takes tile run (b % 8) * B/8 + b / 8 and
+    // each XCD sweeps one contiguous eighth of the batch (TCPCSUM_XCD_REMAP). 1M x 1500 B: 0.34
+    // and 0.38 % faster in two A/Bs, HBM bytes unchanged (profiles/r05_xcd_remap_ab.jsonl).
+    // Grid-stride launches keep block order: remapped, 1M x 64 B on 1024 looping workgroups
+    // ran 14.8 instead of 12.6 us.
     const uint32_t nb = gridDim.x, bx = blockIdx.x;
-    const uint64_t blk = (nb % 8u == 0u) ? (uint64_t)(bx % 8u) * (nb / 8u) + bx / 8u : (uint64_t)bx;
+    const bool xcd_order = TCPCSUM_XCD_REMAP && nb % 8u == 0u && (uint64_t)nb * 4u >= ntiles;
+    const uint64_t blk = xcd_order ? (uint64_t)(bx % 8u) * (nb / 8u) + bx / 8u : (uint64_t)bx;
     const uint64_t wave = blk * 4u + (threadIdx.x >> 6);
-#else
-    const uint64_t wave = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
-#endif
     uint64_t t = wave;
     if constexpr (!PIPE) {
         Tile a;

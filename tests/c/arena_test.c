@@ -10,7 +10,9 @@
  *     grow moves underneath with the contents, size 0 frees);
  *   * churn from 8 threads: no block is handed out twice (each holder's tag
  *     survives until it frees), counters balance;
- *   * an interior or double free aborts, as glibc's free() does.
+ *   * an interior or double free aborts, as glibc's free() does;
+ *   * closed (a forked child): nothing more is served, blocks already out are still
+ *     owned and released.
  */
 #define _GNU_SOURCE
 #include <assert.h>
@@ -179,6 +181,24 @@ int main(void) {
     for (int t = 0; t < THREADS; ++t) pthread_join(th[t], NULL);
     arena_counters(&A, &served, &released, &full);
     CHECK(served == released && full > 1);   /* churn ran the arena full: the rest fell through */
+
+    /* closed: blocks out before stay the arena's, nothing new is served */
+    void *k = arena_route_malloc(&A, BLK, 0, &L);
+    CHECK(arena_owns(&A, k));
+    arena_close(&A);
+    void *after = arena_route_malloc(&A, BLK, 0, &L);
+    void *afterc = arena_route_calloc(&A, 1, BLK, 0, calloc);
+    CHECK(after && !arena_owns(&A, after) && afterc && !arena_owns(&A, afterc));
+    free(after);
+    free(afterc);
+    CHECK(arena_route_realloc(&A, k, 64, &L) == k);       /* still a block: shrink keeps it */
+    arena_route_free(&A, k, &L);
+    void *again = arena_route_malloc(&A, BLK, 0, &L);     /* the freed block is not served again */
+    CHECK(again && again != k && !arena_owns(&A, again));
+    free(again);
+    uint64_t s2, r2, f2;
+    arena_counters(&A, &s2, &r2, &f2);
+    CHECK(s2 == served + 1 && r2 == released + 1);
     printf("arena_test: served=%llu full=%llu OK\n", (unsigned long long) served, (unsigned long long) full);
     free(mem);
     return 0;

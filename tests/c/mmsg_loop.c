@@ -3,7 +3,7 @@
  * does (loop.c:27-94 releaseSend, loop.c:22-25 fetchPackageBatch), over UDP
  * loopback so no root is needed. Run under LD_PRELOAD=libtcpcsum_preload.so.
  *
- *   mmsg_loop <npkts> <out-file> [cpu-checks | corrupt | trunc | forge | plain] [pinned | iov2]
+ *   mmsg_loop <npkts> <out-file> [cpu-checks | corrupt | trunc | forge | plain] [pinned | iov2 | fork]
  *
  * Allocates the loop's buffers as loop.c:180-183 does (1024 in-buffers and 1024
  * out-buffers, 32 KiB each, malloc'd alternately), builds npkts IPv4/TCP
@@ -27,14 +27,19 @@
  * then the rest): a packet the first holds whole is verified, a longer one is
  * a scatter read the interposer passes through unverified. Under
  * TCPCSUM_PRELOAD_POOL=1 the interposer serves the loop's 2048 mallocs from its
- * page-locked arena and both seams run in place.
+ * page-locked arena and both seams run in place. "fork": after the run, a forked
+ * child mallocs and writes a 32 KiB buffer, frees one of the parent's, sends one
+ * packet through the seam, and prints "fork child parent_owned=<0|1|-1>
+ * child_owned=<..> send=<r> errno=<e>" (owned: whether the interposer's pool holds
+ * the block, -1 without the interposer); the parent waits for it (exit 6 if it failed).
  * Under TCPCSUM_PRELOAD_RX=drop the receiver expects exactly the packets the
  * mode makes unverifiable to go missing (corrupt / forge: i % 7 == 3, with iov2
  * only those of at most 800 bytes; trunc: those longer than 600 bytes). Sends them with sendmmsg in batches
  * of <= 1024 and receives them with recvmmsg. Writes to <out-file>: for every
  * packet u32 length + the bytes as built, then u32 length + the bytes as
  * received (length 0: never received). Exit 0 on success; 3 if sendmmsg
- * failed (errno printed); 4 if recvmmsg failed; 5 if a packet went missing.
+ * failed (errno printed); 4 if recvmmsg failed; 5 if a packet went missing;
+ * 6 if the fork child failed.
  */
 #define _GNU_SOURCE
 #include <arpa/inet.h>
@@ -46,12 +51,16 @@
 #include <string.h>
 #include <sys/socket.h>
 #include <sys/time.h>
+#include <sys/wait.h>
 #include <time.h>
 #include <unistd.h>
 
 #include "tcpcsum.h"
 
 enum { NBUF = 1024, SLOT = 1024 * 32, IOV2_FIRST = 800 };   /* loop.c:180-183 */
+
+/* the interposer's (preload or --wrap build); absent when the loop runs without it */
+extern int tcpcsum_preload_pool_owns(const void *p) __attribute__((weak));
 
 static uint64_t rng = 0x9E3779B97F4A7C15ull;
 static uint32_t next32(void) {
@@ -98,13 +107,14 @@ static size_t build(uint8_t *b, int i, int cpu_checks, int corrupt, int forge) {
 }
 
 int main(int argc, char **argv) {
-    if (argc < 3) { fprintf(stderr, "usage: %s npkts out [cpu-checks|corrupt|trunc|forge|plain] [pinned|iov2]\n", argv[0]); return 2; }
+    if (argc < 3) { fprintf(stderr, "usage: %s npkts out [cpu-checks|corrupt|trunc|forge|plain] [pinned|iov2|fork]\n", argv[0]); return 2; }
     int n = atoi(argv[1]);
     int corrupt = argc > 3 && !strcmp(argv[3], "corrupt");
     int trunc = argc > 3 && !strcmp(argv[3], "trunc");
     int forge = argc > 3 && !strcmp(argv[3], "forge");
     int pinned = argc > 4 && !strcmp(argv[4], "pinned");
     int iov2 = argc > 4 && !strcmp(argv[4], "iov2");
+    int forkm = argc > 4 && !strcmp(argv[4], "fork");
     int cpu_checks = corrupt || trunc || forge || (argc > 3 && !strcmp(argv[3], "cpu-checks"));
     const char *rxm = getenv("TCPCSUM_PRELOAD_RX");
     const int rx_drop = rxm && !strcmp(rxm, "drop");
@@ -219,6 +229,38 @@ int main(int argc, char **argv) {
         if (l) fwrite(in[i], 1, l, f);
     }
     fclose(f);
+    if (forkm) {
+        fflush(NULL);
+        const pid_t pid = fork();
+        if (pid < 0) return 6;
+        if (pid == 0) {
+            const int parent_owned = tcpcsum_preload_pool_owns ? tcpcsum_preload_pool_owns(buffer[0]) : -1;
+            uint8_t *p = malloc(SLOT);   /* the loop's size: the child's own memory */
+            if (!p) _exit(7);
+            memset(p, 0x5a, SLOT);
+            const int child_owned = tcpcsum_preload_pool_owns ? tcpcsum_preload_pool_owns(p) : -1;
+            free(p);
+            free(buffer[0]);             /* a parent's block: freeing it is allowed */
+            uint8_t *q = malloc(2048);
+            if (!q) _exit(7);
+            struct iovec civ = {q, build(q, 1, 0, 0, 0)};
+            struct mmsghdr cm;
+            memset(&cm, 0, sizeof cm);
+            cm.msg_hdr.msg_iov = &civ; cm.msg_hdr.msg_iovlen = 1;
+            cm.msg_hdr.msg_name = &a; cm.msg_hdr.msg_namelen = sizeof a;
+            errno = 0;
+            const int r = sendmmsg(tx, &cm, 1, 0);
+            printf("fork child parent_owned=%d child_owned=%d send=%d errno=%d\n", parent_owned, child_owned, r,
+                   r < 0 ? errno : 0);
+            fflush(stdout);
+            _exit(0);
+        }
+        int st = 0;
+        if (waitpid(pid, &st, 0) != pid || !WIFEXITED(st) || WEXITSTATUS(st) != 0) {
+            fprintf(stderr, "fork child failed: status 0x%x\n", st);
+            return 6;
+        }
+    }
     for (int i = 0; i < NBUF; ++i) {   /* the buffers go back the way they came */
         free(buffer[i]);
         if (!pinned) free(outBuffer[i]);

@@ -5,6 +5,7 @@ tests/c/mmsg_loop builds packets with the reference's framing in separate
 (no root needed). With TCPCSUM_PRELOAD_TX=fill every received packet must equal
 the oracle's FILL of the packet as built (check computed per context.c:208).
 """
+import errno
 import json
 import os
 import re
@@ -30,7 +31,7 @@ def _ensure_built():
 
 
 def run_loop(tmp_path, n, env_extra, cpu_checks=False, corrupt=False, trunc=False, forge=False, pinned=False,
-             iov2=False, wrap=False):
+             iov2=False, wrap=False, fork=False):
     """Run mmsg_loop under the LD_PRELOAD interposer, or (wrap) its build with the seam linked in."""
     _ensure_built()
     out = tmp_path / "mm.bin"
@@ -41,7 +42,8 @@ def run_loop(tmp_path, n, env_extra, cpu_checks=False, corrupt=False, trunc=Fals
     env.update(env_extra)
     mode = ("trunc" if trunc else "corrupt" if corrupt else "forge" if forge else
             "cpu-checks" if cpu_checks else "plain")
-    args = [EXE_WRAP if wrap else EXE, str(n), str(out), mode] + (["pinned"] if pinned else ["iov2"] if iov2 else [])
+    args = [EXE_WRAP if wrap else EXE, str(n), str(out), mode] + (
+        ["pinned"] if pinned else ["iov2"] if iov2 else ["fork"] if fork else [])
     r = subprocess.run(args, env=env, capture_output=True, text=True, timeout=120)
     pkts = []
     if r.returncode == 0:
@@ -136,6 +138,22 @@ def test_wrap_seam_passthrough_and_refusal(tmp_path):
         assert r.returncode == 3 and "No such device or address" in r.stderr
 
 
+def fork_child_line(r):
+    m = re.search(r"fork child parent_owned=(-?\d+) child_owned=(-?\d+) send=(-?\d+) errno=(\d+)", r.stdout)
+    assert m, (r.stdout, r.stderr)
+    return tuple(int(x) for x in m.groups())
+
+
+@pytest.mark.parametrize("wrap", [False, True])
+def test_fork_child_of_a_process_without_hip(tmp_path, wrap):
+    """A forked child of a loop whose interposer never started HIP (TX off, no pool): its mallocs are
+    libc's, freeing a parent's buffer is fine, and its sendmmsg goes straight through."""
+    r, pkts, stats = run_loop(tmp_path, 200, {"TCPCSUM_PRELOAD_TX": "off"}, wrap=wrap, fork=True)
+    assert r.returncode == 0, r.stderr
+    assert len(pkts) == 200 and all(b == g for b, g in pkts)
+    assert fork_child_line(r) == (0, 0, 1, 0)
+
+
 def test_fails_loudly_without_gpu(tmp_path):
     import tcp_amd
     if tcp_amd.device_check()[0] == 0:
@@ -200,6 +218,25 @@ def test_wrap_seam_on_gpu(tmp_path, pool):
         assert stats["pool_served"] == 2048 and stats["ctx_in_place"] == 2 * n and stats["ctx_staged"] == 0
     else:
         assert stats["pool_on"] == 0 and stats["ctx_staged"] == 2 * n
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wrap", [False, True])
+def test_pool_fork_child(tmp_path, wrap):
+    """fork() in a loop whose interposer holds the pool and a GPU context: the child's malloc(32 KiB)
+    comes from libc (the arena is closed in the child), it may free a parent's arena buffer, and its
+    sendmmsg fails with ENXIO (HIP does not survive fork) instead of sending an unchecked packet. The
+    parent runs on unharmed and prints its counters once."""
+    n = 1200
+    pool = "mmsg_loop_wrap" if wrap else "mmsg_loop"
+    r, pkts, stats = run_loop(tmp_path, n, {"TCPCSUM_PRELOAD_TX": "fill", "TCPCSUM_PRELOAD_POOL": pool},
+                              wrap=wrap, fork=True)
+    assert r.returncode == 0, r.stderr
+    assert len(pkts) == n and all(got == oracle_fill(built) for built, got in pkts)
+    assert fork_child_line(r) == (1, 0, -1, errno.ENXIO)
+    assert "forked child of a process that started HIP" in r.stderr
+    assert r.stderr.count("tcpcsum_preload: tx batches=") == 1
+    assert stats["pool_served"] == 2048 and stats["pool_released"] == 2048 and stats["ctx_staged"] == 0
 
 
 @pytest.mark.gpu
