@@ -415,7 +415,7 @@ def run_wire(steps: int, warmup: int, device) -> dict:
                      "achieved_GB/s": round(gbs, 1), "roofline_frac": round(gbs / HBM_PEAK_GBS, 4)}
     res["copy_probe"]["what"] = ("k_probe<8,WR>, 8192 workgroups: every line of the 1.61 GB region read, one "
                                  "128-B line per 1536-B slot written back through (sc0 sc1), bytes unchanged")
-    res["read_probe"]["what"] = "k_probe<16>: every line of the region read"
+    res["read_probe"]["what"] = "k_probe<4>, one 4 KiB tile per wave in XCD order: every line of the region read"
     res["fill_over_verify"] = round(res["fill"]["kernel_avg_ms"] / res["verify"]["kernel_avg_ms"], 3)
     res["fill_over_copy_probe"] = round(res["fill"]["kernel_avg_ms"] / res["copy_probe"]["avg_ms"], 3)
     res["verify_over_read_probe"] = round(res["verify"]["kernel_avg_ms"] / res["read_probe"]["avg_ms"], 3)
@@ -865,7 +865,8 @@ def main(argv=None) -> int:
     probe = None
     if world == 1 and not args.no_probe:
         pms = time_probe(bufs[:rot], batch_bytes, args.steps, device)
-        probe = {"kernel": "k_probe (read-only 16-B stream, same access shape)", "avg_ms": round(pms, 5),
+        probe = {"kernel": "k_probe<4> (read-only 16-B stream: one 4 KiB tile per wave, XCD order, as the plan)",
+                 "avg_ms": round(pms, 5),
                  "GB/s": round((batch_bytes // 16) * 16 / (pms * 1e-3) / 1e9, 1),
                  "headline_kernel_over_probe": round(kernel_ms / pms, 4)}
 

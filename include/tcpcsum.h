@@ -335,12 +335,14 @@ int tcpcsum_synth_pseudo_dev(uint32_t *d_sum_start, uint64_t seg0, uint64_t n, u
 
 /* Read-only streaming probe: the chip's practical HBM read ceiling for the
  * checksum kernels' access pattern (16-B non-temporal loads, each wave
- * reading contiguous 1 KiB per instruction), reported beside them. With
- * TCPCSUM_TUNE_PROBE_WRITE it also writes lines back (the wire FILL's ceiling);
- * d_src is then written (its bytes unchanged) and must be writable.
- * d_partials: TCPCSUM_PROBE_SLOTS u64 entries; on completion the sum over the
- * first *n_partials entries equals the sum of the lo16+hi16 halves of every
- * u32 word of d_src. nbytes multiple of 16, d_src 16-B aligned. */
+ * reading contiguous 1 KiB per instruction; by default one 4 KiB tile per
+ * wave, tiles in XCD order, as the uniform kernel's plan), reported beside
+ * them. With TCPCSUM_TUNE_PROBE_WRITE it also writes lines back (the wire
+ * FILL's ceiling); d_src is then written (its bytes unchanged) and must be
+ * writable. d_partials: TCPCSUM_PROBE_SLOTS u64 entries; the launch ADDS into
+ * the first *n_partials of them (workgroup b into slot b % TCPCSUM_PROBE_SLOTS),
+ * so when they were zero, their sum on completion is the sum of the lo16+hi16
+ * halves of every u32 word of d_src. nbytes multiple of 16, d_src 16-B aligned. */
 #define TCPCSUM_PROBE_SLOTS 8192
 int tcpcsum_stream_probe_dev(const void *d_src, uint64_t nbytes, uint64_t *d_partials,
                              int *n_partials, void *stream, const tcpcsum_tuning_t *tune);

@@ -414,7 +414,8 @@ def synth_pseudo(dst, seg0: int, n: int, seg_len: int, stream=None) -> None:
 
 def stream_probe(src, nbytes: int, partials, stream=None, tune=None) -> int:
     """Launch the read-only probe; ``partials`` is a device int64 tensor of >= PROBE_SLOTS.
-    Returns how many leading partials the launch writes (their sum = lo16+hi16 word sum)."""
+    The launch adds into the leading partials and returns how many: zeroed first, their sum is
+    the lo16+hi16 word sum."""
     if partials.numel() < PROBE_SLOTS:
         raise ValueError("partials needs PROBE_SLOTS entries")
     n = ctypes.c_int()

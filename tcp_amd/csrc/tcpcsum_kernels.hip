@@ -159,6 +159,22 @@ __device__ __forceinline__ uint64_t combine(uint64_t start, uint64_t W, uint64_t
     return odd_start ? start + O + 256ull * (W - 256ull * O) : start + W;
 }
 
+// ---------------------------------------------------------------- XCD order
+// Workgroups are dispatched to the 8 XCDs round-robin (workgroup b on XCD b % 8). When a
+// launch gives every unit of work (a wave tile, or a segment per workgroup) its own
+// workgroup slot — nb >= units_per_block-rounded need — and its grid is a whole number
+// of XCD rounds, workgroup b takes block-run (b % 8) * nb/8 + b / 8 instead of b: each
+// XCD then sweeps one contiguous eighth of the batch through its own L2 and the HBM
+// channels see eight long streams instead of an interleave of small tiles
+// (TCPCSUM_XCD_REMAP; measured per kernel). Grid-stride launches keep
+// block order (remapped, the 64-B config's 1024 looping workgroups ran 14.8 instead of
+// 12.6 us, profiles/r05_xcd_remap_ab.jsonl).
+__device__ __forceinline__ uint64_t xcd_block(uint64_t blocks_needed) {
+    const uint32_t nb = gridDim.x, bx = blockIdx.x;
+    const bool remap = TCPCSUM_XCD_REMAP && nb % 8u == 0u && (uint64_t)nb >= blocks_needed;
+    return remap ? (uint64_t)(bx % 8u) * (nb / 8u) + bx / 8u : (uint64_t)bx;
+}
+
 // ---------------------------------------------------------------- uniform
 // Segment i at base + i*stride, all of length len; n segments.
 // G lanes per segment, C chunk loads per lane per segment (G*C >= chunks a
@@ -248,16 +264,10 @@ __global__ __launch_bounds__(256) void k_uniform(const uint8_t* __restrict__ bas
     const int q = lane / G, gl = lane % G;
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
     const uint64_t ntiles = (n + Tile::SPT - 1) / Tile::SPT;
-    // XCD-aware tile order (one tile per wave, a whole number of XCD rounds): workgroups are
-    // dispatched to the 8 XCDs round-robin, so block b takes tile run (b % 8) * B/8 + b / 8 and
-    // each XCD sweeps one contiguous eighth of the batch (TCPCSUM_XCD_REMAP). 1M x 1500 B: 0.34
-    // and 0.38 % faster in two A/Bs, HBM bytes unchanged (profiles/r05_xcd_remap_ab.jsonl).
-    // Grid-stride launches keep block order: remapped, 1M x 64 B on 1024 looping workgroups
-    // ran 14.8 instead of 12.6 us.
-    const uint32_t nb = gridDim.x, bx = blockIdx.x;
-    const bool xcd_order = TCPCSUM_XCD_REMAP && nb % 8u == 0u && (uint64_t)nb * 4u >= ntiles;
-    const uint64_t blk = xcd_order ? (uint64_t)(bx % 8u) * (nb / 8u) + bx / 8u : (uint64_t)bx;
-    const uint64_t wave = blk * 4u + (threadIdx.x >> 6);
+    // tiles XCD by XCD (xcd_block): 1M x 1500 B 0.34 / 0.38 % faster at eight segments in
+    // flight, HBM bytes unchanged (profiles/r05_xcd_remap_ab.jsonl); with it smaller tiles
+    // win (plan_uniform)
+    const uint64_t wave = xcd_block((ntiles + 3) / 4) * 4u + (threadIdx.x >> 6);
     uint64_t t = wave;
     if constexpr (!PIPE) {
         Tile a;
@@ -311,7 +321,8 @@ __global__ __launch_bounds__(256) void k_uniform_multi(UniformMultiArgs args) {
     const int q = lane / G, gl = lane % G;
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
     const uint64_t ntiles = (n + Tile::SPT - 1) / Tile::SPT;
-    for (uint64_t t = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6); t < ntiles; t += nwaves) {
+    // XCD order within the row (a row of nb % 8 == 0 workgroups starts on XCD 0)
+    for (uint64_t t = xcd_block((ntiles + 3) / 4) * 4u + (threadIdx.x >> 6); t < ntiles; t += nwaves) {
         Tile a;
         a.load(t, base, stride, len, e.ss, e.ss0, n, q, gl);
         a.finish(t, base, stride, len, e.out, n, q, gl);
@@ -330,7 +341,7 @@ __global__ __launch_bounds__(256) void k_uniform_long(const uint8_t* __restrict_
                                                       uint16_t* __restrict__ out, uint64_t n) {
     const int lane = threadIdx.x & 63;
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
-    uint64_t seg = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
+    uint64_t seg = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);   // block order (xcd_block: unmeasured here)
     if (seg >= n) return;
     uint32_t r = 0;
     uint64_t W = 0, O = 0;
@@ -411,6 +422,8 @@ __global__ __launch_bounds__(256) void k_uniform_split(const uint8_t* __restrict
                                                        uint16_t* __restrict__ out, uint64_t n) {
     __shared__ uint64_t part[4][2];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    // block order: XCD order measured 3.8 % slower at 12300 B, even at 8192 / 9000 B
+    // (profiles/r05_xcd_kernels_ab.jsonl)
     for (uint64_t seg = blockIdx.x; seg < n; seg += gridDim.x) {
         const uint8_t* p = base + seg * stride;
         const uint32_t m = (uint32_t)((uintptr_t)p & 15u);
@@ -476,7 +489,7 @@ __global__ __launch_bounds__(256) void k_flat(const uint8_t* __restrict__ base, 
     const uint64_t ntiles = (n + spt - 1) / spt;
     const uint32_t bm = (uint32_t)((uintptr_t)base & 15u);
     const uint8_t* b0 = base - bm;   // 16-B aligned
-    for (uint64_t t = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6); t < ntiles; t += nwaves) {
+    for (uint64_t t = xcd_block((ntiles + 3) / 4) * 4u + (threadIdx.x >> 6); t < ntiles; t += nwaves) {
         const uint64_t s_first = t * spt;
         const uint32_t nseg = (uint32_t)((n - s_first) < spt ? (n - s_first) : spt);
         const uint64_t tbase = s_first * (uint64_t)stride + bm;        // tile's first byte, from b0
@@ -547,6 +560,7 @@ __global__ __launch_bounds__(256) void k_desc(const uint8_t* __restrict__ base,
     const int q = lane / G, gl = lane % G;
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
     const uint64_t ntiles = (n + SPT - 1) / SPT;
+    // block order: XCD order inconclusive on ragged batches (profiles/r05_xcd_kernels_ab.jsonl)
     uint64_t t = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
     // one 16-B load per descriptor; slots past n read zeros (len 0)
     auto load_desc = [&](uint64_t tile, u32x4 (&dst)[U]) {
@@ -833,7 +847,7 @@ __global__ __launch_bounds__(256) void k_desc_lb(const uint8_t* __restrict__ bas
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
     const uint64_t ntiles = (n + spw - 1) / spw;
-    for (uint64_t t = (uint64_t)blockIdx.x * 4u + wv; t < ntiles; t += nwaves) {
+    for (uint64_t t = (uint64_t)blockIdx.x * 4u + wv; t < ntiles; t += nwaves) {   // block order, as k_desc
         const uint64_t seg = t * spw + (uint64_t)lane;
         const bool mine = (uint32_t)lane < spw && seg < n;
         const u32x4 d = ldg<u32x4>(zsel(mine, reinterpret_cast<const uint8_t*>(desc + seg)));
@@ -1059,7 +1073,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(wire_waves(
     const uint64_t ntiles = (n + SPT - 1) / SPT;
     constexpr bool verify = VER;
     const bool iphdr = (mode & TCPCSUM_IPV4_IPHDR) != 0;
-    uint64_t t = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
+    // XCD order for MTU-size packets: 1536 / 2048-B slots and packed 1500-B packets VERIFY
+    // -2.4 / -3.4 / -2.4 %, FILL -1..-2 % where it moved; 9216-B jumbo slots VERIFY +3 %, so
+    // batches whose cap passes 4 KiB keep block order (profiles/r05_xcd_kernels_ab.jsonl)
+    uint64_t t = xcd_block(cap <= 4096u ? (ntiles + 3) / 4 : ~0ull) * 4u + (threadIdx.x >> 6);
     // offsets of packet i and of packet i + 1 (0 past the end: no bound)
     uint64_t on[U], on1[U];
     uint32_t pn[U];
@@ -1354,6 +1371,8 @@ __global__ __launch_bounds__(256) void k_ipv4_lb(uint8_t* __restrict__ pkts, con
     const uint64_t ntiles = (n + spw - 1) / spw;
     const bool verify = (mode & TCPCSUM_IPV4_VERIFY) != 0;
     const bool iphdr = (mode & TCPCSUM_IPV4_IPHDR) != 0;
+    // block order: XCD order measured 1 % slower on 2M packed 576-B packets
+    // (profiles/r05_xcd_kernels_ab.jsonl)
     for (uint64_t t = (uint64_t)blockIdx.x * 4u + wv; t < ntiles; t += nwaves) {
         const uint64_t i = t * spw + (uint64_t)lane;
         const bool live = (uint32_t)lane < spw && i < n;
@@ -1662,6 +1681,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TCPCSUM_TX_
     const int q0 = lane / G, gl = lane % G;
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
     const uint64_t ntiles = (n + SPT - 1) / SPT;
+    // block order: XCD order measured no faster (0.6200 vs 0.6198 ms, 1M x 1456-B payloads;
+    // profiles/r05_xcd_kernels_ab.jsonl)
     uint64_t t = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
     TxRec rn[U];
 #pragma unroll
@@ -1784,9 +1805,11 @@ __global__ __launch_bounds__(256) void k_synth_pseudo(uint32_t* __restrict__ ss,
 
 // ---------------------------------------------------------------- probe
 // Read-only stream with the checksum kernels' access shape (each wave reads
-// contiguous 1 KiB per load instruction, C in flight per lane), summed so it
-// cannot be dead-code eliminated. One plain store of a per-block partial at
-// the end (no atomics: 2048 same-address atomics cost ~25 us on this chip).
+// contiguous 1 KiB per load instruction, C in flight per lane; by default one
+// 4 KiB tile per wave in XCD order, as the uniform kernel's plan), summed so it
+// cannot be dead-code eliminated. Each block adds its partial into slot
+// blockIdx % kProbeSlots (one atomic per block; a few per slot at most — 2048
+// same-address atomics would cost ~25 us on this chip).
 //
 // WR (TCPCSUM_TUNE_PROBE_WRITE): also write back, through (sc0 sc1, as the wire
 // FILL's line store), every `period`-th 128-B line it read — the bytes unchanged.
@@ -1801,7 +1824,7 @@ __global__ __launch_bounds__(256) void k_probe(const uint8_t* __restrict__ src, 
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
     const uint64_t ntiles = (nchunks + 64 * C - 1) / (64 * C);
     uint64_t acc = 0;
-    for (uint64_t t = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6); t < ntiles; t += nwaves) {
+    for (uint64_t t = xcd_block((ntiles + 3) / 4) * 4u + (threadIdx.x >> 6); t < ntiles; t += nwaves) {
         u32x4 v[C];
 #pragma unroll
         for (int k = 0; k < C; ++k) {
@@ -1824,7 +1847,10 @@ __global__ __launch_bounds__(256) void k_probe(const uint8_t* __restrict__ src, 
     acc = group_sum64<64>(acc);
     if (lane == 0) wsum[threadIdx.x >> 6] = acc;
     __syncthreads();
-    if (threadIdx.x == 0) partials[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    // a grid wider than the slots folds into them: a handful of vector atomics per slot
+    if (threadIdx.x == 0)
+        atomicAdd((unsigned long long*)&partials[blockIdx.x % (uint32_t)kProbeSlots],
+                  (unsigned long long)(wsum[0] + wsum[1] + wsum[2] + wsum[3]));
 }
 
 }  // namespace tcpcsum
@@ -1838,9 +1864,16 @@ namespace {
 // workgroups at most 2^24 - 1 of them (the kernels grid-stride past that).
 constexpr uint64_t kMaxGrid = (1u << 24) - 1u;
 
+// A grid that covers the work is rounded up to whole XCD rounds, so the kernels can take
+// their tiles XCD by XCD (xcd_block): at most 7 idle workgroups.
+inline uint64_t xcd_rounds(uint64_t blocks) {
+    return (blocks + 7u) & ~(uint64_t)7u;
+}
+
 inline unsigned grid_for(uint64_t waves_needed, int max_blocks) {
     uint64_t blocks = (waves_needed + 3) / 4;
     if (blocks < 1) blocks = 1;
+    if (blocks < (uint64_t)max_blocks) blocks = xcd_rounds(blocks);
     if (blocks > (uint64_t)max_blocks) blocks = (uint64_t)max_blocks;
     if (blocks > kMaxGrid) blocks = kMaxGrid;
     return (unsigned)blocks;
@@ -1887,7 +1920,8 @@ void launch_split(const uint8_t* base, uint64_t stride, uint32_t len, const uint
     int C = unroll <= 1 ? 4 : unroll == 2 ? 8 : unroll == 4 ? 16 : 32;
     while (C > 4 && 256u * (uint64_t)(C / 2) >= nch) C /= 2;
     const uint32_t rounds = (uint32_t)((nch + 256u * C - 1) / (256u * C));
-    uint64_t gb = n < (uint64_t)max_blocks ? n : (uint64_t)max_blocks;
+    uint64_t gb = n < (uint64_t)max_blocks ? xcd_rounds(n) : (uint64_t)max_blocks;
+    if (gb > (uint64_t)max_blocks) gb = (uint64_t)max_blocks;
     if (gb > kMaxGrid) gb = kMaxGrid;
     const unsigned g = (unsigned)gb;
 #define TC_S(CC)                                                                                             \
@@ -2023,21 +2057,27 @@ UniformPlan plan_uniform(uintptr_t b, uint64_t stride, uint32_t len, uint64_t n,
     // 1-5 %, profiles/r02_grid_m1.jsonl)
     if (p.mode == M1) {
         if (!tu.unroll && p.shape != 9 && p.unroll > 4) p.unroll = 4;
+        // (one tile per wave in XCD order, as below, loses here: 99 B +8 %, 577 B +11 %,
+        // 1499 / 3001 B +1 %, profiles/r05_plan_ab.jsonl)
         if (tu.max_blocks <= 0) p.max_blocks = 16384;
-    } else if (p.shape <= 5 && tu.max_blocks <= 0) {
-        // segments of up to 1.5 KiB, 4-B aligned: one tile per wave, no grid-stride
-        // loop (1M x 1500 B 0.2248 -> 0.2186 ms = 7.19 TB/s, 256 B -3 %, 576 B -7 %;
-        // 4-8 KiB segments keep their grids; profiles/r02_grid_sweep.jsonl)
+    } else if (p.shape <= 8 && tu.max_blocks <= 0) {
+        // Lane-group shapes, 4-B aligned: one tile per wave (no grid-stride loop), the
+        // tiles taken XCD by XCD (k_uniform), and a tile of at most ~4.5 KiB of the
+        // batch — the most segments in flight per group (1..8) whose span fits. Under
+        // the XCD order smaller tiles stream faster; a sweep of every unroll and grid at
+        // ten sizes picked exactly this tile (profiles/r05_tile_sweep_xcd.jsonl), and
+        // against the round-5 plan before it (eight in flight; 1024 looping workgroups
+        // for 64 B), same process: 1M x 1500 B 0.2189 -> 0.2089 ms, 64 B -3 %, 128 B
+        // -2 %, 256 B -4 %, 512 / 1024 B -3 %, 2048 / 3000 B -7 %, 4096 B -4 %, 6000 B -3 %
+        // (profiles/r05_plan_ab.jsonl). Before the XCD order, eight in flight won
+        // (profiles/r02_grid_sweep.jsonl).
         p.max_blocks = 1 << 24;
-        // header-only segments (<= 4 chunks, 16-B aligned) in large batches: eight in
-        // flight per lane group on 1024 workgroups that loop, not one tile per wave —
-        // 1M x 64 B 12.28 vs 12.48 us and 12.21 vs 12.42 on two boxes, the best of 140
-        // shapes both times; as bench.py's headline config, alternating fresh processes,
-        // 12.60-12.65 vs 12.71-12.81 us (profiles/r05_sweep64_shapes.jsonl,
-        // r05_sweep64_confirm.jsonl, r05_ab64_bench_form.jsonl)
-        if (p.shape == 0 && p.mode == M16 && n >= (1u << 19) && !tu.unroll) {
-            p.unroll = 8;
-            p.max_blocks = 1024;
+        if (!tu.unroll) {
+            static const uint32_t kGroupsPerWave[9] = {16, 8, 4, 2, 1, 2, 1, 1, 1};
+            const uint64_t span = (uint64_t)kGroupsPerWave[p.shape] * (stride > len ? stride : len);
+            int u = 8;
+            while (u > 1 && span * (uint64_t)u > 4608u) u >>= 1;
+            p.unroll = u;
         }
     } else if (p.shape == 9 && tu.max_blocks <= 0 && (p.mode != M16 || len < 12288u)) {
         // one wave per segment: segments of one round (jumbo frames, 8-12 KiB)
@@ -2126,11 +2166,13 @@ static void launch_multi_mode(int shape, int unroll, const UniformMultiArgs& a, 
 void launch_uniform_multi(const tcpcsum_ubatch_t* b, uint32_t k, hipStream_t s, const Tuning& tu) {
     UniformMultiArgs a;
     uint32_t m = 0;
-    int mode = M16, shape = -1;
+    int mode = M16, shape = -1, unroll = 8, max_blocks = 0;
     bool one = true;
     for (uint32_t i = 0; i < k; ++i) {
         if (b[i].n == 0) continue;
         const UniformPlan p = plan_uniform((uintptr_t)b[i].d_base, b[i].stride, b[i].len, b[i].n, tu);
+        unroll = std::min(unroll, p.unroll);            // the smallest tile any batch's plan takes
+        max_blocks = std::max(max_blocks, p.max_blocks);
         const bool lane_group = p.shape <= 8 || p.shape == 10 || p.shape == 11;
         if (!lane_group || (shape >= 0 && (shape > 8 || p.shape > 8) && shape != p.shape)) one = false;
         mode = std::max(mode, p.mode);
@@ -2146,17 +2188,13 @@ void launch_uniform_multi(const tcpcsum_ubatch_t* b, uint32_t k, hipStream_t s, 
                                b[i].d_out, b[i].n, s, tu);
         return;
     }
-    // the single-batch defaults for this shape and mode (plan_uniform)
-    int unroll = kShapeUnroll[shape];
-    int max_blocks = kShapeBlocks[shape];
+    // the single-batch plans' launch shape (plan_uniform: one tile per wave for lane-group
+    // shapes); the byte-granular mode any batch forces keeps its own (<= 4 in flight, 16384
+    // workgroups)
     if (mode == M1) {
-        unroll = std::min(unroll, 4);
-        max_blocks = 16384;
-    } else if (shape <= 5) {
-        max_blocks = 1 << 24;   // one tile per wave
+        if (!tu.unroll) unroll = std::min(unroll, 4);
+        max_blocks = tu.max_blocks > 0 ? tu.max_blocks : 16384;
     }
-    if (tu.unroll) unroll = tu.unroll;
-    if (tu.max_blocks > 0) max_blocks = tu.max_blocks;
     if (mode == M16) launch_multi_mode<M16>(shape, unroll, a, m, s, max_blocks);
     else if (mode == M4) launch_multi_mode<M4>(shape, unroll, a, m, s, max_blocks);
     else launch_multi_mode<M1>(shape, unroll, a, m, s, max_blocks);
@@ -2421,21 +2459,33 @@ void launch_synth_pseudo(uint32_t* ss, uint64_t seg0, uint64_t n, uint32_t seg_l
 }
 
 int launch_probe(const uint8_t* src, uint64_t nbytes, uint64_t* partials, hipStream_t s, const Tuning& tu) {
-    const int max_blocks = tu.max_blocks > 0 ? (tu.max_blocks < kProbeSlots ? tu.max_blocks : kProbeSlots) : 512;
+    // chunks per lane per wave tile, C: by unroll 0 / 1 / 2 / >= 4 -> 4 (the default: one 4 KiB
+    // tile per wave, the uniform plan's tile) / 8 / 16 / 32; a read-only probe also takes
+    // shape 2 or 3 as C (tile-size sweeps)
+    const bool wr = (tu.flags & TCPCSUM_TUNE_PROBE_WRITE) != 0;
+    int C = tu.unroll == 0 ? 4 : tu.unroll == 1 ? 8 : tu.unroll == 2 ? 16 : 32;
+    if (!wr && (tu.shape == 2 || tu.shape == 3)) C = tu.shape;
+    const int max_blocks = tu.max_blocks > 0 ? tu.max_blocks : (1 << 24);
     const uint64_t nchunks = nbytes / 16;
-    const int unroll = tu.unroll ? tu.unroll : 2;
-    const unsigned g = grid_for((nchunks + 64 * 8 * unroll - 1) / (64 * 8 * unroll), max_blocks);
-    if (tu.flags & TCPCSUM_TUNE_PROBE_WRITE) {   // the wire FILL's traffic: shape = line period
-        const uint32_t period = tu.shape > 0 ? (uint32_t)tu.shape : 12u;
-        if (unroll <= 1) hipLaunchKernelGGL((k_probe<8, true>), dim3(g), dim3(256), 0, s, src, nchunks, partials, period);
-        else if (unroll == 2) hipLaunchKernelGGL((k_probe<16, true>), dim3(g), dim3(256), 0, s, src, nchunks, partials, period);
-        else hipLaunchKernelGGL((k_probe<32, true>), dim3(g), dim3(256), 0, s, src, nchunks, partials, period);
-        return (int)g;
+    const unsigned g = grid_for((nchunks + 64u * C - 1) / (64u * C), max_blocks);
+    const int used = (int)(g < (unsigned)kProbeSlots ? g : (unsigned)kProbeSlots);
+    // write-back probe: the wire FILL's traffic, shape = line period
+    const uint32_t period = wr ? (tu.shape > 0 ? (uint32_t)tu.shape : 12u) : 1u;
+#define TC_P(CC)                                                                                              \
+    do {                                                                                                      \
+        if (wr) hipLaunchKernelGGL((k_probe<CC, true>), dim3(g), dim3(256), 0, s, src, nchunks, partials, period); \
+        else hipLaunchKernelGGL((k_probe<CC, false>), dim3(g), dim3(256), 0, s, src, nchunks, partials, period);   \
+    } while (0)
+    switch (C) {
+        case 2: hipLaunchKernelGGL((k_probe<2, false>), dim3(g), dim3(256), 0, s, src, nchunks, partials, 1u); break;
+        case 3: hipLaunchKernelGGL((k_probe<3, false>), dim3(g), dim3(256), 0, s, src, nchunks, partials, 1u); break;
+        case 4: TC_P(4); break;
+        case 8: TC_P(8); break;
+        case 16: TC_P(16); break;
+        default: TC_P(32); break;
     }
-    if (unroll <= 1) hipLaunchKernelGGL((k_probe<8, false>), dim3(g), dim3(256), 0, s, src, nchunks, partials, 1u);
-    else if (unroll == 2) hipLaunchKernelGGL((k_probe<16, false>), dim3(g), dim3(256), 0, s, src, nchunks, partials, 1u);
-    else hipLaunchKernelGGL((k_probe<32, false>), dim3(g), dim3(256), 0, s, src, nchunks, partials, 1u);
-    return (int)g;
+#undef TC_P
+    return used;
 }
 
 }  // namespace tcpcsum

@@ -286,13 +286,27 @@ def test_stream_probe_sums(dev):
     d = to_dev(host.view(np.uint8), dev)
     parts = torch.zeros(tcp_amd.api.PROBE_SLOTS, dtype=torch.int64, device=dev)
     want = int((host & 0xFFFF).astype(np.uint64).sum() + (host >> 16).astype(np.uint64).sum())
+    # default (one 4 KiB tile per wave: 64 workgroups here), small and wide grids; the launch adds
+    # into the slots, so they are zeroed first
     for blocks, unroll in ((0, 0), (7, 1), (3000, 4)):
         tcp_amd.set_tuning(blocks, unroll, -1, 0)
+        parts.zero_()
         try:
             k = tcp_amd.stream_probe(d, host.nbytes, parts)
         finally:
             tcp_amd.set_tuning(0, 0, -1, 0)
         assert int(parts[:k].sum().item()) == want
+    # 192 MiB: 12288 workgroups by default, more than the slots (partials fold into slot
+    # blockIdx % PROBE_SLOTS); the expected sum from torch on the device
+    g = torch.Generator(device=dev).manual_seed(9)
+    w = torch.randint(0, 2**32, (48 << 20,), dtype=torch.int64, device=dev, generator=g)
+    want = int(((w & 0xFFFF) + (w >> 16)).sum().item())
+    d = w.to(torch.int32)   # the same u32 words, two's complement
+    del w
+    parts.zero_()
+    k = tcp_amd.stream_probe(d, d.numel() * 4, parts)
+    assert k == tcp_amd.api.PROBE_SLOTS
+    assert int(parts.sum().item()) == want
 
 
 def test_nondefault_stream(dev):

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--flags", default="0", help="TCPCSUM_TUNE_* bits: 1 pipe on, 2 pipe off, 4 nt on, 8 nt off")
     ap.add_argument("--probe", action="store_true")
     ap.add_argument("--rot", type=int, default=0, help="rotating input buffers (0: enough for >= 1 GiB in total)")
+    ap.add_argument("--probe-shapes", default="0:0:-1", help="probe max_blocks:unroll:shape triples, with --probe")
     args = ap.parse_args()
     import torch
     import tcp_amd
@@ -60,7 +61,8 @@ def main():
                 for u in [int(x) for x in args.unrolls.split(",")]:
                     variants.append((b, u, sh, fl))
     times = {v: [] for v in variants}
-    ptimes = []
+    ptimes = {}
+    pshapes = [tuple(int(y) for y in (x + ":-1").split(":")[:3]) for x in args.probe_shapes.split(",")]
     st = torch.cuda.current_stream()
     for rnd in range(args.rounds):
         for v in variants:
@@ -76,14 +78,15 @@ def main():
             times[v].append(e0.elapsed_time(e1) / args.steps)
         if args.probe:
             po = torch.zeros(tcp_amd.api.PROBE_SLOTS, dtype=torch.int64, device=dev)
-            tcp_amd.set_tuning(0, 0, -1, 0)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(st)
-            for i in range(args.steps):
-                tcp_amd.stream_probe(bufs[i % rot], (nbytes // 16) * 16, po)
-            e1.record(st)
-            torch.cuda.synchronize()
-            ptimes.append(e0.elapsed_time(e1) / args.steps)
+            for ps in pshapes:
+                tcp_amd.set_tuning(ps[0], ps[1], ps[2], 0)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(st)
+                for i in range(args.steps):
+                    tcp_amd.stream_probe(bufs[i % rot], (nbytes // 16) * 16, po)
+                e1.record(st)
+                torch.cuda.synchronize()
+                ptimes.setdefault(ps, []).append(e0.elapsed_time(e1) / args.steps)
     tcp_amd.set_tuning(0, 0, -1, 0)
     res = []
     for v in variants:
@@ -91,9 +94,10 @@ def main():
         res.append({"max_blocks": v[0], "unroll": v[1], "shape": v[2], "flags": v[3], "med_ms": round(med, 5), "min_ms": round(mn, 5),
                     "GB/s_med": round(nbytes / med / 1e6, 1), "GB/s_best": round(nbytes / mn / 1e6, 1)})
         print(json.dumps({"config": args.config, **res[-1]}), flush=True)
-    if ptimes:
-        med = statistics.median(ptimes)
-        print(json.dumps({"config": args.config, "probe_med_ms": round(med, 5), "probe_GB/s": round(nbytes / med / 1e6, 1)}))
+    for ps, ts in ptimes.items():
+        med = statistics.median(ts)
+        print(json.dumps({"config": args.config, "probe_max_blocks": ps[0], "probe_unroll": ps[1], "probe_shape": ps[2],
+                          "probe_med_ms": round(med, 5), "probe_GB/s": round(nbytes / med / 1e6, 1)}))
 
 
 if __name__ == "__main__":

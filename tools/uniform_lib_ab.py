@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Uniform kernel (tcpcsum_batch_uniform_dev) A/B: the in-tree library against other builds
 (tools/ab_build.sh, e.g. measurement builds of TCPCSUM_LOAD_CPOL), interleaved in one process on
-the same Appendix B batches (bench.py's headline and 64-B configs, rotating buffers), HIP events on
-the launch stream. Every build's results must equal the in-tree build's. JSON lines.
+the same Appendix B batches (bench.py's headline and 64-B configs, rotating buffers; AB_LENS=a,b,...
+adds ~1.5 GB batches of those segment lengths), HIP events on the launch stream. Every build's results must equal the in-tree build's. JSON lines.
 
   python tools/uniform_lib_ab.py tcp_amd/ab/libtcpcsum_X.so ...
 """
@@ -29,7 +29,10 @@ def main():
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream()
     rounds = int(os.environ.get("AB_ROUNDS", "5"))
-    for name, n, L, rot, steps in (("1Mx1500", 1 << 20, 1500, 2, 50), ("1Mx64", 1 << 20, 64, 32, 200)):
+    cases = [("1Mx1500", 1 << 20, 1500, 2, 50), ("1Mx64", 1 << 20, 64, 32, 200)]
+    for L in [int(x) for x in os.environ.get("AB_LENS", "").split(",") if x]:   # more sizes, ~1.5 GB each
+        cases.append((f"len{L}", 1572864000 // L, L, 2, 30))
+    for name, n, L, rot, steps in cases:
         bufs, sss = [], []
         for r in range(rot):
             d = torch.empty(n * L, dtype=torch.uint8, device=dev)

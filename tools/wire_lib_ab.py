@@ -54,7 +54,9 @@ def main():
              ("1Mx2000_slots2048", np.arange(n, dtype=np.uint64) * 2048, np.full(n, 1980, np.uint32), n * 2048, 2048),
              ("1Mx1500_packed", np.arange(n, dtype=np.uint64) * 1500, np.full(n, 1480, np.uint32), n * 1500, 1536),
              ("128Kx9000_slots9216", np.arange(n // 8, dtype=np.uint64) * 9216, np.full(n // 8, 8980, np.uint32),
-              (n // 8) * 9216, 9216)]
+              (n // 8) * 9216, 9216),
+             ("2Mx576_packed", np.arange(2 * n, dtype=np.uint64) * 576, np.full(2 * n, 556, np.uint32), 2 * n * 576,
+              576)]   # small packets: the balanced kernel (k_ipv4_lb)
     only = os.environ.get("WIRE_AB_ONLY")
     rounds = int(os.environ.get("WIRE_AB_ROUNDS", "5"))
     for name, offs, tl, rb, cap in works:
