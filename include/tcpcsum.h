@@ -340,7 +340,7 @@ int tcpcsum_synth_pseudo_dev(uint32_t *d_sum_start, uint64_t seg0, uint64_t n, u
  * them. With TCPCSUM_TUNE_PROBE_WRITE it also writes lines back (the wire
  * FILL's ceiling); d_src is then written (its bytes unchanged) and must be
  * writable. d_partials: TCPCSUM_PROBE_SLOTS u64 entries; the launch ADDS into
- * the first *n_partials of them (workgroup b into slot b % TCPCSUM_PROBE_SLOTS),
+ * the first *n_partials of them (wave w into slot w % TCPCSUM_PROBE_SLOTS),
  * so when they were zero, their sum on completion is the sum of the lo16+hi16
  * halves of every u32 word of d_src. nbytes multiple of 16, d_src 16-B aligned. */
 #define TCPCSUM_PROBE_SLOTS 8192

@@ -121,7 +121,8 @@ const char* tcpcsum_build_info(void) {
         ", \"TCPCSUM_TX_WAVES\": " TCPCSUM_STR(TCPCSUM_TX_WAVES)
         ", \"TCPCSUM_LINE_CPOL\": " TCPCSUM_STR(TCPCSUM_LINE_CPOL)
         ", \"TCPCSUM_LOAD_CPOL\": " TCPCSUM_STR(TCPCSUM_LOAD_CPOL)
-        ", \"TCPCSUM_XCD_REMAP\": " TCPCSUM_STR(TCPCSUM_XCD_REMAP) "}"
+        ", \"TCPCSUM_XCD_REMAP\": " TCPCSUM_STR(TCPCSUM_XCD_REMAP)
+        ", \"TCPCSUM_XCD_CHUNK\": " TCPCSUM_STR(TCPCSUM_XCD_CHUNK) "}"
         ", \"runtime_knobs\": [" TCPCSUM_RUNTIME_KNOBS_JSON "]}";
     return info;
 }

@@ -44,17 +44,22 @@
 #ifndef TCPCSUM_LOAD_CPOL
 #define TCPCSUM_LOAD_CPOL -1
 #endif
-//   TCPCSUM_XCD_REMAP        1 (the product's): a one-tile-per-wave uniform launch whose grid is a
-//                            whole number of XCD rounds takes its tiles XCD by XCD (block b, on
+//   TCPCSUM_XCD_REMAP        1 (the product's): a wave-tile launch whose grid covers its batch in
+//                            whole XCD rounds takes its tiles XCD by XCD (xcd_block: block b, on
 //                            XCD b % 8 under round-robin dispatch, takes tile run (b % 8) * B/8 +
 //                            b / 8), so each XCD sweeps one contiguous eighth of the batch;
 //                            0: block b takes tile run b
 #ifndef TCPCSUM_XCD_REMAP
 #define TCPCSUM_XCD_REMAP 1
 #endif
+//   TCPCSUM_XCD_CHUNK        > 0: with the XCD order, the XCDs take runs of this many workgroups
+//                            in turn instead of one contiguous eighth each; 0 (the product's)
+#ifndef TCPCSUM_XCD_CHUNK
+#define TCPCSUM_XCD_CHUNK 0
+#endif
 #if !TCPCSUM_MEASUREMENT_BUILD && \
     (TCPCSUM_TUNING_VARIANTS != 0 || TCPCSUM_TX_KNOCKOUT != 0 || TCPCSUM_WIRE_WAVES != 1 || TCPCSUM_TX_WAVES != 1 || \
-     TCPCSUM_LINE_CPOL != 17 || TCPCSUM_LOAD_CPOL != -1 || TCPCSUM_XCD_REMAP != 1)
+     TCPCSUM_LINE_CPOL != 17 || TCPCSUM_LOAD_CPOL != -1 || TCPCSUM_XCD_REMAP != 1 || TCPCSUM_XCD_CHUNK != 0)
 #error "tuning / knock-out / waves knobs are for measurement builds only (-DTCPCSUM_MEASUREMENT_BUILD=1), never a product library"
 #endif
 // Environment variables a context reads at creation (tcpcsum_build_info "runtime_knobs"):

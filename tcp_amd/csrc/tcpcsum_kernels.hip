@@ -172,6 +172,12 @@ __device__ __forceinline__ uint64_t combine(uint64_t start, uint64_t W, uint64_t
 __device__ __forceinline__ uint64_t xcd_block(uint64_t blocks_needed) {
     const uint32_t nb = gridDim.x, bx = blockIdx.x;
     const bool remap = TCPCSUM_XCD_REMAP && nb % 8u == 0u && (uint64_t)nb >= blocks_needed;
+#if TCPCSUM_XCD_CHUNK > 0   // measurement builds: XCDs take runs of CHUNK blocks in turn
+    if (remap && (nb / 8u) % TCPCSUM_XCD_CHUNK == 0u) {
+        const uint64_t j = bx / 8u;
+        return ((j / TCPCSUM_XCD_CHUNK) * 8u + bx % 8u) * TCPCSUM_XCD_CHUNK + j % TCPCSUM_XCD_CHUNK;
+    }
+#endif
     return remap ? (uint64_t)(bx % 8u) * (nb / 8u) + bx / 8u : (uint64_t)bx;
 }
 
@@ -1807,8 +1813,8 @@ __global__ __launch_bounds__(256) void k_synth_pseudo(uint32_t* __restrict__ ss,
 // Read-only stream with the checksum kernels' access shape (each wave reads
 // contiguous 1 KiB per load instruction, C in flight per lane; by default one
 // 4 KiB tile per wave in XCD order, as the uniform kernel's plan), summed so it
-// cannot be dead-code eliminated. Each block adds its partial into slot
-// blockIdx % kProbeSlots (one atomic per block; a few per slot at most — 2048
+// cannot be dead-code eliminated. Each wave adds its partial into slot
+// wave % kProbeSlots (one atomic per wave, spread over the slots — 2048
 // same-address atomics would cost ~25 us on this chip).
 //
 // WR (TCPCSUM_TUNE_PROBE_WRITE): also write back, through (sc0 sc1, as the wire
@@ -1819,7 +1825,6 @@ __global__ __launch_bounds__(256) void k_synth_pseudo(uint32_t* __restrict__ ss,
 template <int C, bool WR>
 __global__ __launch_bounds__(256) void k_probe(const uint8_t* __restrict__ src, uint64_t nchunks,
                                                uint64_t* __restrict__ partials, uint32_t period) {
-    __shared__ uint64_t wsum[4];
     const int lane = threadIdx.x & 63;
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
     const uint64_t ntiles = (nchunks + 64 * C - 1) / (64 * C);
@@ -1844,13 +1849,12 @@ __global__ __launch_bounds__(256) void k_probe(const uint8_t* __restrict__ src, 
             }
         }
     }
+    // each wave adds its own partial (no workgroup barrier: a wave retires as soon as its
+    // tile is summed, as the checksum kernels' waves do) into slot wave % kProbeSlots
     acc = group_sum64<64>(acc);
-    if (lane == 0) wsum[threadIdx.x >> 6] = acc;
-    __syncthreads();
-    // a grid wider than the slots folds into them: a handful of vector atomics per slot
-    if (threadIdx.x == 0)
-        atomicAdd((unsigned long long*)&partials[blockIdx.x % (uint32_t)kProbeSlots],
-                  (unsigned long long)(wsum[0] + wsum[1] + wsum[2] + wsum[3]));
+    if (lane == 0)
+        atomicAdd((unsigned long long*)&partials[((uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6)) % (uint64_t)kProbeSlots],
+                  (unsigned long long)acc);
 }
 
 }  // namespace tcpcsum
@@ -2468,7 +2472,7 @@ int launch_probe(const uint8_t* src, uint64_t nbytes, uint64_t* partials, hipStr
     const int max_blocks = tu.max_blocks > 0 ? tu.max_blocks : (1 << 24);
     const uint64_t nchunks = nbytes / 16;
     const unsigned g = grid_for((nchunks + 64u * C - 1) / (64u * C), max_blocks);
-    const int used = (int)(g < (unsigned)kProbeSlots ? g : (unsigned)kProbeSlots);
+    const int used = (int)(4ull * g < (uint64_t)kProbeSlots ? 4ull * g : (uint64_t)kProbeSlots);
     // write-back probe: the wire FILL's traffic, shape = line period
     const uint32_t period = wr ? (tu.shape > 0 ? (uint32_t)tu.shape : 12u) : 1u;
 #define TC_P(CC)                                                                                              \

@@ -296,8 +296,8 @@ def test_stream_probe_sums(dev):
         finally:
             tcp_amd.set_tuning(0, 0, -1, 0)
         assert int(parts[:k].sum().item()) == want
-    # 192 MiB: 12288 workgroups by default, more than the slots (partials fold into slot
-    # blockIdx % PROBE_SLOTS); the expected sum from torch on the device
+    # 192 MiB: 49152 waves by default, more than the slots (partials fold into slot
+    # wave % PROBE_SLOTS); the expected sum from torch on the device
     g = torch.Generator(device=dev).manual_seed(9)
     w = torch.randint(0, 2**32, (48 << 20,), dtype=torch.int64, device=dev, generator=g)
     want = int(((w & 0xFFFF) + (w >> 16)).sum().item())
