@@ -429,7 +429,7 @@ def run_wire(steps: int, warmup: int, device) -> dict:
         res["fill"]["hbm_traffic_GB/s"] = round((rd + wr) / (res["fill"]["kernel_avg_ms"] * 1e-3) / 1e9, 1)
         res["verify"]["hbm_traffic_GB/s"] = round(
             (rd + t["write_bytes_per_launch_verify"]) / (res["verify"]["kernel_avg_ms"] * 1e-3) / 1e9, 1)
-        res["traffic_source"] = "profiles/traffic.json wire_fill_1Mx1500 (rocprofv3 --pmc, round 4)"
+        res["traffic_source"] = "profiles/traffic.json wire_fill_1Mx1500 (rocprofv3 --pmc, round 5)"
     except Exception:
         pass
     # the write-back probe rewrote the lines it read: the packets are still the builder's
