@@ -368,9 +368,10 @@ def run_wire(steps: int, warmup: int, device) -> dict:
     # 128-B line per 1536-B slot written back through, bytes unchanged — the FILL's HBM traffic
     # without its arithmetic; TCPCSUM_TUNE_PROBE_WRITE, period 12 lines)
     pout = torch.zeros(tcp_amd.api.PROBE_SLOTS, dtype=torch.int64, device=device)
-    # shape: the fastest of 9 grid x unroll shapes on the box (8192 workgroups, 8 loads per lane:
-    # profiles/r05_probe_rw_sweep.jsonl)
-    probe_rw = tcp_amd.make_tuning(8192, 1, slot // 128, tcp_amd.TUNE_PROBE_WRITE)
+    # shape: one 4 KiB tile per wave in XCD order, the fastest found (0.2783 ms against 0.2834 for
+    # the best grid-stride shape, 8192 workgroups; profiles/r05_probe_rw_sweep.jsonl,
+    # r05_probe_rw_xcd.jsonl)
+    probe_rw = tcp_amd.make_tuning(0, 0, slot // 128, tcp_amd.TUNE_PROBE_WRITE)
     modes = (("fill", tcp_amd.IPV4_FILL), ("verify", tcp_amd.IPV4_VERIFY), ("copy_probe", None),
              ("read_probe", None))
 
@@ -413,8 +414,9 @@ def run_wire(steps: int, warmup: int, device) -> dict:
         gbs = n * tcp_len / (ms * 1e-3) / 1e9
         res[name] = {"kernel_avg_ms": round(ms, 5), "kernel_ms_rounds": [round(t, 4) for t in times[name]],
                      "achieved_GB/s": round(gbs, 1), "roofline_frac": round(gbs / HBM_PEAK_GBS, 4)}
-    res["copy_probe"]["what"] = ("k_probe<8,WR>, 8192 workgroups: every line of the 1.61 GB region read, one "
-                                 "128-B line per 1536-B slot written back through (sc0 sc1), bytes unchanged")
+    res["copy_probe"]["what"] = ("k_probe<4,WR>, one 4 KiB tile per wave in XCD order: every line of the 1.61 GB "
+                                 "region read, one 128-B line per 1536-B slot written back through (sc0 sc1), "
+                                 "bytes unchanged")
     res["read_probe"]["what"] = "k_probe<4>, one 4 KiB tile per wave in XCD order: every line of the region read"
     res["fill_over_verify"] = round(res["fill"]["kernel_avg_ms"] / res["verify"]["kernel_avg_ms"], 3)
     res["fill_over_copy_probe"] = round(res["fill"]["kernel_avg_ms"] / res["copy_probe"]["avg_ms"], 3)

@@ -1822,10 +1822,14 @@ __global__ __launch_bounds__(256) void k_synth_pseudo(uint32_t* __restrict__ ss,
 // With period 12 over 1536-B slots that is the wire FILL's HBM traffic (every line
 // read, one whole line written per packet) without its arithmetic: the ceiling the
 // FILL is held to.
-template <int C, bool WR>
+// G: lanes per group — a group reads its own contiguous C x G x 16 bytes, G x 16 per
+// instruction (G = 64: one contiguous 1 KiB per instruction; G = 32: two 512-B pieces,
+// as the uniform kernel's (32, C) lane groups read two segments)
+template <int C, bool WR, int G = 64>
 __global__ __launch_bounds__(256) void k_probe(const uint8_t* __restrict__ src, uint64_t nchunks,
                                                uint64_t* __restrict__ partials, uint32_t period) {
     const int lane = threadIdx.x & 63;
+    const int q = lane / G, gl = lane % G;
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
     const uint64_t ntiles = (nchunks + 64 * C - 1) / (64 * C);
     uint64_t acc = 0;
@@ -1833,7 +1837,7 @@ __global__ __launch_bounds__(256) void k_probe(const uint8_t* __restrict__ src, 
         u32x4 v[C];
 #pragma unroll
         for (int k = 0; k < C; ++k) {
-            const uint64_t idx = t * (64 * C) + (uint64_t)(k * 64 + lane);
+            const uint64_t idx = t * (64 * C) + (uint64_t)(q * G * C + k * G + gl);
             v[k] = idx < nchunks ? ld16(src + idx * 16u) : u32x4{0u, 0u, 0u, 0u};
         }
         uint32_t w = 0;
@@ -1843,7 +1847,7 @@ __global__ __launch_bounds__(256) void k_probe(const uint8_t* __restrict__ src, 
         if constexpr (WR) {
 #pragma unroll
             for (int k = 0; k < C; ++k) {
-                const uint64_t idx = t * (64 * C) + (uint64_t)(k * 64 + lane);
+                const uint64_t idx = t * (64 * C) + (uint64_t)(q * G * C + k * G + gl);
                 if (idx < nchunks && (idx >> 3) % period == 0u)
                     stg_wt16_at(const_cast<uint8_t*>(src) + idx * 16u, v[k], (uint64_t)(uintptr_t)src);
             }
@@ -2465,7 +2469,7 @@ void launch_synth_pseudo(uint32_t* ss, uint64_t seg0, uint64_t n, uint32_t seg_l
 int launch_probe(const uint8_t* src, uint64_t nbytes, uint64_t* partials, hipStream_t s, const Tuning& tu) {
     // chunks per lane per wave tile, C: by unroll 0 / 1 / 2 / >= 4 -> 4 (the default: one 4 KiB
     // tile per wave, the uniform plan's tile) / 8 / 16 / 32; a read-only probe also takes
-    // shape 2 or 3 as C (tile-size sweeps)
+    // shape 2 or 3 as C, and shape 10 / 11 / 12 as 32-lane groups with C = 2 / 3 / 4 (sweeps)
     const bool wr = (tu.flags & TCPCSUM_TUNE_PROBE_WRITE) != 0;
     int C = tu.unroll == 0 ? 4 : tu.unroll == 1 ? 8 : tu.unroll == 2 ? 16 : 32;
     if (!wr && (tu.shape == 2 || tu.shape == 3)) C = tu.shape;
@@ -2480,6 +2484,14 @@ int launch_probe(const uint8_t* src, uint64_t nbytes, uint64_t* partials, hipStr
         if (wr) hipLaunchKernelGGL((k_probe<CC, true>), dim3(g), dim3(256), 0, s, src, nchunks, partials, period); \
         else hipLaunchKernelGGL((k_probe<CC, false>), dim3(g), dim3(256), 0, s, src, nchunks, partials, period);   \
     } while (0)
+    if (!wr && tu.shape >= 10 && tu.shape <= 12) {   // 32-lane groups (two 512-B pieces per instruction), C = 2..4
+        const unsigned C2 = (unsigned)tu.shape - 8u;
+        const unsigned g2 = grid_for((nchunks + 64u * C2 - 1) / (64u * C2), max_blocks);
+        if (C2 == 2) hipLaunchKernelGGL((k_probe<2, false, 32>), dim3(g2), dim3(256), 0, s, src, nchunks, partials, 1u);
+        else if (C2 == 3) hipLaunchKernelGGL((k_probe<3, false, 32>), dim3(g2), dim3(256), 0, s, src, nchunks, partials, 1u);
+        else hipLaunchKernelGGL((k_probe<4, false, 32>), dim3(g2), dim3(256), 0, s, src, nchunks, partials, 1u);
+        return (int)(4ull * g2 < (uint64_t)kProbeSlots ? 4ull * g2 : (uint64_t)kProbeSlots);
+    }
     switch (C) {
         case 2: hipLaunchKernelGGL((k_probe<2, false>), dim3(g), dim3(256), 0, s, src, nchunks, partials, 1u); break;
         case 3: hipLaunchKernelGGL((k_probe<3, false>), dim3(g), dim3(256), 0, s, src, nchunks, partials, 1u); break;

@@ -37,8 +37,11 @@ def main():
     st = torch.cuda.current_stream()
     runs = {"fill": lambda: tcp_amd.ipv4_batch(reg, doff, n, slot, 0, out, sta),
             "verify": lambda: tcp_amd.ipv4_batch(reg, doff, n, slot, 1, out, sta)}
-    for mb in (512, 2048, 8192):
-        for u in (1, 2, 4):
+    # PROBE_GRIDS / PROBE_UNROLLS: comma lists (grid 0 = one tile per wave, XCD order; unroll 0 = C 4)
+    grids = [int(x) for x in os.environ.get("PROBE_GRIDS", "512,2048,8192").split(",")]
+    unrolls = [int(x) for x in os.environ.get("PROBE_UNROLLS", "1,2,4").split(",")]
+    for mb in grids:
+        for u in unrolls:
             for wr in (0, 1):
                 t = (mb, u, 12 if wr else -1, tcp_amd.TUNE_PROBE_WRITE if wr else 0)
                 runs[f"{'rw' if wr else 'rd'}_mb{mb}_u{u}"] = (lambda t=t: tcp_amd.stream_probe(reg, n * slot, pout, tune=t))
