@@ -347,7 +347,9 @@ __global__ __launch_bounds__(256) void k_uniform_long(const uint8_t* __restrict_
                                                       uint16_t* __restrict__ out, uint64_t n) {
     const int lane = threadIdx.x & 63;
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
-    uint64_t seg = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);   // block order (xcd_block: unmeasured here)
+    // block order: XCD order measured no better for one segment per wave (byte-granular
+    // 12301 / 20001 B, profiles/r05_xcd_kernels_ab.jsonl); the 64 KiB config's grid loops
+    uint64_t seg = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
     if (seg >= n) return;
     uint32_t r = 0;
     uint64_t W = 0, O = 0;
@@ -566,7 +568,8 @@ __global__ __launch_bounds__(256) void k_desc(const uint8_t* __restrict__ base,
     const int q = lane / G, gl = lane % G;
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
     const uint64_t ntiles = (n + SPT - 1) / SPT;
-    // block order: XCD order inconclusive on ragged batches (profiles/r05_xcd_kernels_ab.jsonl)
+    // block order: XCD order measured 0.7-2 % slower on ragged batches in two runs
+    // (profiles/r05_xcd_kernels_ab.jsonl)
     uint64_t t = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
     // one 16-B load per descriptor; slots past n read zeros (len 0)
     auto load_desc = [&](uint64_t tile, u32x4 (&dst)[U]) {
@@ -2244,7 +2247,8 @@ void launch_desc(const uint8_t* base, const tcpcsum_desc_t* d, uint64_t n, uint3
         // segments leaves too few waves: 64K x 64 KiB 1.385 ms with 64 per tile
         // against 0.635 for lane groups (tools/desc_sweep.py,
         // profiles/r02_desc_sweep.jsonl)
-        uint32_t spw = 64;
+        // (a forced unroll u divides it: at most 64 / u per tile — tile-size sweeps)
+        uint32_t spw = tu.unroll ? 64u / (uint32_t)tu.unroll : 64u;
         while (spw > 1 && (uint64_t)spw * nch > 8192u) spw >>= 1;
         // and, chosen automatically, at least 4096 wave tiles where the batch allows
         // (16 waves per CU: 16K x 1500-B descriptors 0.0361 -> 0.0082 ms; a forced
