@@ -355,13 +355,17 @@ int tcpcsum_stream_probe_dev(const void *d_src, uint64_t nbytes, uint64_t *d_par
  * tiles (contiguous 1 KiB per load instruction; 1-32 KiB segments, 4-B
  * aligned, stride >= len), 13 = split segments (a workgroup of four waves
  * per segment, 4*unroll chunk loads per thread per round);
- * unroll: segments in flight per lane group; max_blocks: resident grid. */
+ * unroll: segments in flight per lane group; max_blocks: resident grid
+ * (1 << 24: one wave tile per wave, the grid rounded to whole XCD rounds and
+ * the tiles taken XCD by XCD — the default for lane-group shapes, with a tile
+ * of at most ~4.5 KiB). */
 int tcpcsum_plan_uniform(uint64_t base, uint64_t stride, uint32_t len, uint64_t n,
                          const tcpcsum_tuning_t *tune, int *mode, int *shape, int *unroll, int *max_blocks);
 
 /* tcpcsum_tuning_t.shape, read per entry point: uniform 0..13 (a forced shape
  * that cannot cover the segments is ignored), ragged 0..6 = (G,C) (4,1) (8,1) (16,1) (32,1) (32,3) (64,4) (64,8)
- * and 7..8 = balanced chunk space (4 / 8 loads per lane in flight),
+ * and 7..8 = balanced chunk space (4 / 8 loads per lane in flight; a nonzero
+ * unroll u caps its tile at 64 / u segments),
  * wire 0..7 = (8,1) (32,3) (64,4) (16,2) (16,6) (8,12) (8,2) (8,4) and 8..9 =
  * balanced (4 / 8 loads per lane), builder 0..4. tcpcsum_tuning_t.flags: */
 /* PIPE_* and NT_* take effect only in a library built with TUNING_VARIANTS=1 */
