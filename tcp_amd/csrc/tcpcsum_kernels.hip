@@ -1690,9 +1690,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TCPCSUM_TX_
     const int q0 = lane / G, gl = lane % G;
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
     const uint64_t ntiles = (n + SPT - 1) / SPT;
-    // block order: XCD order measured no faster (0.6200 vs 0.6198 ms, 1M x 1456-B payloads;
-    // profiles/r05_xcd_kernels_ab.jsonl)
-    uint64_t t = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
+    uint64_t t = xcd_block((ntiles + 3) / 4) * 4u + (threadIdx.x >> 6);   // covering grids only
     TxRec rn[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) rn[u] = tx_load(segs, t * SPT + (uint64_t)(u * GPW + q0), n);
