@@ -211,6 +211,31 @@ def test_plan_uniform(base, stride, length, n, expect):
     assert unroll in (1, 2, 4, 8) and (1 <= blocks <= 32768 or blocks == 1 << 24)
 
 
+@pytest.mark.parametrize("stride,length,unroll", [
+    (1500, 1500, 1),    # 32-lane groups, two segments per wave: 3000 B
+    (64, 64, 4),        # 4-lane groups, 16 per instruction x 4: 4096 B
+    (128, 128, 4), (256, 256, 4), (512, 512, 4), (1024, 1024, 4),
+    (2048, 2048, 2),    # 64-lane groups, one per instruction x 2: 4096 B
+    (3000, 3000, 1), (4096, 4096, 1), (6000, 6000, 1),
+    (1536, 1500, 1),    # the span is the stride
+    (576, 576, 8),      # 64-lane groups, one per instruction x 8: 4608 B, the limit
+])
+def test_plan_tile_of_at_most_4608_bytes(stride, length, unroll):
+    """The lane-group plan (profiles/r05_tile_sweep_xcd.jsonl): one wave tile per wave
+    (grid cap 1 << 24, tiles in XCD order) of the most segments in flight whose span fits 4608 B."""
+    mode, shape, u, blocks = api.plan_uniform(0, stride, length, 1 << 20)
+    assert mode in (0, 1) and shape <= 8
+    assert (u, blocks) == (unroll, 1 << 24)
+
+
+def test_plan_byte_granular_keeps_its_grid():
+    """Byte-granular batches keep 16384 looping workgroups and at most 4 in flight: the tile plan in
+    XCD order measured 1-11 % slower for them (profiles/r05_plan_ab.jsonl)."""
+    for length in (99, 577, 1499, 3001):
+        mode, shape, u, blocks = api.plan_uniform(1, length, length, 1 << 20)
+        assert mode == 2 and shape <= 8 and u <= 4 and blocks == 16384
+
+
 def test_plan_respects_overrides():
     try:
         api.set_tuning(100, 1, -1, 0)
