@@ -58,15 +58,19 @@ def main():
         shapes = [int(x) for x in os.environ.get("TX_SHAPES", "0,1,2,3,4").split(",")]
         blocks = [int(x) for x in os.environ.get("TX_BLOCKS", "1024,4096,8192,16384,32768").split(",")]
         unrolls = [int(x) for x in os.environ.get("TX_UNROLLS", "1,2").split(",")]
-        for sh in shapes:
-          for mb in blocks:
-            for un in unrolls:
-                tcp_amd.set_tuning(mb, un, sh, 0)
-                tt = timeit(lambda: tcp_amd.tx_build(payload, dsegs, n, L, out, 0, chk), 20)
-                print(json.dumps({"sweep": "tx_build", "len": L, "n": n, "shape": sh, "max_blocks": mb, "unroll": un,
-                                  "ms": round(tt * 1e3, 4),
-                                  "GB/s": round((n * L + n * (L + 44) + n * 48) / tt / 1e9, 1)}), flush=True)
+        # TX_ROUNDS interleaved rounds over every variant, median per variant (shape -1: the plan's)
+        variants = [(sh, mb, un) for sh in shapes for mb in blocks for un in unrolls]
+        ts = {v: [] for v in variants}
+        for _ in range(int(os.environ.get("TX_ROUNDS", "1"))):
+            for v in variants:
+                tcp_amd.set_tuning(v[1], v[2], v[0], 0)
+                ts[v].append(timeit(lambda: tcp_amd.tx_build(payload, dsegs, n, L, out, 0, chk), 20))
         tcp_amd.set_tuning(0, 0, -1, 0)
+        for (sh, mb, un), tl in ts.items():
+            tt = sorted(tl)[len(tl) // 2]
+            print(json.dumps({"sweep": "tx_build", "len": L, "n": n, "shape": sh, "max_blocks": mb, "unroll": un,
+                              "ms": round(tt * 1e3, 4), "rounds": len(tl),
+                              "GB/s": round((n * L + n * (L + 44) + n * 48) / tt / 1e9, 1)}), flush=True)
     # store policy: default vs non-temporal payload stores, interleaved rounds
     moved = n * L + n * (L + 44) + n * 48
     pol = {0: [], 128: [], 1024: []}
