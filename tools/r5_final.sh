@@ -1,7 +1,7 @@
 # Round 5 final rehearsal (one run): every GPU test, smoke(), the default bench, the bench under
 # rocprofv3 --kernel-trace --stats, and the headline FETCH_SIZE pass.
 set -o pipefail
-O=gpurun_out/r5final
+O=${R5_OUT:-gpurun_out/r5final}
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 600 python3 -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests/ > $O/gputest.txt 2>&1 || exit $?
