@@ -57,9 +57,14 @@
 #ifndef TCPCSUM_XCD_CHUNK
 #define TCPCSUM_XCD_CHUNK 0
 #endif
+//   TCPCSUM_UNIFORM_WPB      waves per workgroup of the uniform kernel: 4 (the product's), 1 or 2
+#ifndef TCPCSUM_UNIFORM_WPB
+#define TCPCSUM_UNIFORM_WPB 4
+#endif
 #if !TCPCSUM_MEASUREMENT_BUILD && \
     (TCPCSUM_TUNING_VARIANTS != 0 || TCPCSUM_TX_KNOCKOUT != 0 || TCPCSUM_WIRE_WAVES != 1 || TCPCSUM_TX_WAVES != 1 || \
-     TCPCSUM_LINE_CPOL != 17 || TCPCSUM_LOAD_CPOL != -1 || TCPCSUM_XCD_REMAP != 1 || TCPCSUM_XCD_CHUNK != 0)
+     TCPCSUM_LINE_CPOL != 17 || TCPCSUM_LOAD_CPOL != -1 || TCPCSUM_XCD_REMAP != 1 || TCPCSUM_XCD_CHUNK != 0 || \
+     TCPCSUM_UNIFORM_WPB != 4)
 #error "tuning / knock-out / waves knobs are for measurement builds only (-DTCPCSUM_MEASUREMENT_BUILD=1), never a product library"
 #endif
 // Environment variables a context reads at creation (tcpcsum_build_info "runtime_knobs"):

@@ -266,14 +266,15 @@ __global__ __launch_bounds__(256) void k_uniform(const uint8_t* __restrict__ bas
                                                  uint32_t ss_scalar, uint16_t* __restrict__ out,
                                                  uint64_t n, int blocked) {
     using Tile = UniformTile<G, C, U, MODE, NT>;
+    constexpr uint32_t WPB = TCPCSUM_UNIFORM_WPB;   // waves per workgroup
     const int lane = threadIdx.x & 63;
     const int q = lane / G, gl = lane % G;
-    const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
+    const uint64_t nwaves = (uint64_t)gridDim.x * WPB;
     const uint64_t ntiles = (n + Tile::SPT - 1) / Tile::SPT;
     // tiles XCD by XCD (xcd_block): 1M x 1500 B 0.34 / 0.38 % faster at eight segments in
     // flight, HBM bytes unchanged (profiles/r05_xcd_remap_ab.jsonl); with it smaller tiles
     // win (plan_uniform)
-    const uint64_t wave = xcd_block((ntiles + 3) / 4) * 4u + (threadIdx.x >> 6);
+    const uint64_t wave = xcd_block((ntiles + WPB - 1) / WPB) * WPB + (threadIdx.x >> 6);
     uint64_t t = wave;
     if constexpr (!PIPE) {
         Tile a;
@@ -1898,8 +1899,10 @@ void launch_uniform_t(const uint8_t* base, uint64_t stride, uint32_t len, const 
     constexpr int UE = (C * U > LIM) ? (LIM / C > 0 ? LIM / C : 1) : U;
     constexpr int SPT = (64 / G) * UE;
     const uint64_t ntiles = (n + SPT - 1) / SPT;
-    hipLaunchKernelGGL((k_uniform<G, C, UE, MODE, PIPE, NT>), dim3(grid_for(ntiles, max_blocks)), dim3(256), 0,
-                       s, base, stride, len, ss, ss0, out, n, blocked);
+    // grid_for counts four waves per workgroup; TCPCSUM_UNIFORM_WPB (measurement builds) other sizes
+    const uint64_t waves = TCPCSUM_UNIFORM_WPB == 4 ? ntiles : (ntiles * 4u + TCPCSUM_UNIFORM_WPB - 1) / TCPCSUM_UNIFORM_WPB;
+    hipLaunchKernelGGL((k_uniform<G, C, UE, MODE, PIPE, NT>), dim3(grid_for(waves, max_blocks)),
+                       dim3(64 * TCPCSUM_UNIFORM_WPB), 0, s, base, stride, len, ss, ss0, out, n, blocked);
 }
 
 template <int C, int MODE, bool PIPE, bool NT>
