@@ -342,7 +342,10 @@ int tcpcsum_synth_pseudo_dev(uint32_t *d_sum_start, uint64_t seg0, uint64_t n, u
  * writable. d_partials: TCPCSUM_PROBE_SLOTS u64 entries; the launch ADDS into
  * the first *n_partials of them (wave w into slot w % TCPCSUM_PROBE_SLOTS),
  * so when they were zero, their sum on completion is the sum of the lo16+hi16
- * halves of every u32 word of d_src. nbytes multiple of 16, d_src 16-B aligned. */
+ * halves of every u32 word of d_src. nbytes multiple of 16, d_src 16-B aligned.
+ * Tuning: unroll 0 / 1 / 2 / 4 = 4 / 8 / 16 / 32 chunks per lane per tile; for the
+ * read-only probe, shape 2 or 3 = that many chunks, 10 / 11 / 12 = 32-lane groups
+ * with 2 / 3 / 4 (tile-shape sweeps); max_blocks caps the grid. */
 #define TCPCSUM_PROBE_SLOTS 8192
 int tcpcsum_stream_probe_dev(const void *d_src, uint64_t nbytes, uint64_t *d_partials,
                              int *n_partials, void *stream, const tcpcsum_tuning_t *tune);

@@ -2009,7 +2009,9 @@ namespace tcpcsum {
 
 // Segment-group shapes: shape k covers up to kShapeChunks[k] 16-B chunks per
 // segment. Defaults per shape (measured on MI355X, tools/sweep.py; see
-// DESIGN.md): segments-in-flight per group and the resident grid.
+// DESIGN.md): segments-in-flight per group and the resident grid — for the
+// lane-group shapes 0..8 only where the tile plan in plan_uniform does not
+// apply (byte-granular batches; forced max_blocks).
 // Shapes 10/11 are the thin lane groups (1 or 2 lanes per segment) for tiny
 // segments; shape 9 (one wave per segment) has no chunk limit.
 // Shape 12 is the flat tile (segments of 1 KiB .. 32 KiB, 4-byte aligned, stride
