@@ -2313,10 +2313,13 @@ static void launch_ipv4_t(uint8_t* pkts, const uint64_t* off, const uint32_t* pl
 void launch_ipv4(uint8_t* pkts, const uint64_t* off, const uint32_t* plen, uint64_t n, uint32_t cap, uint64_t limit,
                  uint64_t footprint, int mode, uint16_t* out, uint8_t* status, uint16_t* ipout, hipStream_t s,
                  const Tuning& tu) {
-    // 32768 workgroups (at most one or two tiles per wave): 1M x 9000-B jumbo
-    // packets VERIFY 1.46 -> 1.41 ms, FILL 1.62 -> 1.59 against 8192
-    // (profiles/r02_wire_jumbo_sweep.jsonl); MTU slots 16384-32768 alike
-    const int max_blocks = tu.max_blocks > 0 ? tu.max_blocks : 32768;
+    // caps up to 4 KiB: one tile per wave, so the tiles go XCD by XCD at any batch size
+    // (2M MTU packets in 1536-B slots: FILL 0.6345 -> 0.6065 ms, VERIFY 0.4824 -> 0.4674
+    // against 32768 looping workgroups; 1M and fewer already covered;
+    // profiles/r05_wire_grid_xcd.jsonl). Jumbo caps: 32768 workgroups (at most one or two
+    // tiles per wave): 1M x 9000-B packets VERIFY 1.46 -> 1.41 ms, FILL 1.62 -> 1.59 against
+    // 8192 (profiles/r02_wire_jumbo_sweep.jsonl)
+    const int max_blocks = tu.max_blocks > 0 ? tu.max_blocks : cap <= 4096u ? (1 << 24) : 32768;
     const int unroll = tu.unroll ? tu.unroll : 1;
     const bool nt = (tu.flags & TCPCSUM_TUNE_WIRE_CACHED) == 0;
     const uint32_t amask = (tu.flags & TCPCSUM_TUNE_WIN16) ? 15u : 127u;

@@ -5,7 +5,7 @@ variant's FILL must reproduce the builder's checks and its VERIFY must give 0. J
 
   python tools/wire_sweep.py [--slot 1536] [--rounds 5] [--steps 20] blocks:unroll:shape ...
 
-A variant "0:0:-1" is the built-in plan."""
+A variant "0:0:-1" is the built-in plan. WIRE_N: packets (default 1M)."""
 import argparse
 import json
 import os
@@ -28,7 +28,7 @@ def main():
     import torch
     import tcp_amd
     dev = torch.device("cuda:0")
-    n, slot, tot = 1 << 20, args.slot, args.tot
+    n, slot, tot = int(os.environ.get("WIRE_N", 1 << 20)), args.slot, args.tot
     tcp_len = tot - 20
     payload = torch.empty(1 << 26, dtype=torch.uint8, device=dev)
     tcp_amd.synth_fill(payload, 0, payload.numel())
@@ -71,7 +71,7 @@ def main():
                 torch.cuda.synchronize()
                 times[(v, name)].append(e0.elapsed_time(e1) / args.steps)
     for (v, name), ts in times.items():
-        print(json.dumps({"slot": slot, "max_blocks": v[0], "unroll": v[1], "shape": v[2], "mode": name,
+        print(json.dumps({"n": n, "slot": slot, "max_blocks": v[0], "unroll": v[1], "shape": v[2], "mode": name,
                           "med_ms": round(statistics.median(ts), 5), "min_ms": round(min(ts), 5),
                           "ok": ok[(v, name)]}), flush=True)
 
