@@ -61,10 +61,15 @@
 #ifndef TCPCSUM_UNIFORM_WPB
 #define TCPCSUM_UNIFORM_WPB 4
 #endif
+//   TCPCSUM_DESC_LB_WAVES    minimum waves per SIMD asked of the balanced ragged kernel
+//                            (amdgpu_waves_per_eu): 1 = the compiler's choice (the product's)
+#ifndef TCPCSUM_DESC_LB_WAVES
+#define TCPCSUM_DESC_LB_WAVES 1
+#endif
 #if !TCPCSUM_MEASUREMENT_BUILD && \
     (TCPCSUM_TUNING_VARIANTS != 0 || TCPCSUM_TX_KNOCKOUT != 0 || TCPCSUM_WIRE_WAVES != 1 || TCPCSUM_TX_WAVES != 1 || \
      TCPCSUM_LINE_CPOL != 17 || TCPCSUM_LOAD_CPOL != -1 || TCPCSUM_XCD_REMAP != 1 || TCPCSUM_XCD_CHUNK != 0 || \
-     TCPCSUM_UNIFORM_WPB != 4)
+     TCPCSUM_UNIFORM_WPB != 4 || TCPCSUM_DESC_LB_WAVES != 1)
 #error "tuning / knock-out / waves knobs are for measurement builds only (-DTCPCSUM_MEASUREMENT_BUILD=1), never a product library"
 #endif
 // Environment variables a context reads at creation (tcpcsum_build_info "runtime_knobs"):

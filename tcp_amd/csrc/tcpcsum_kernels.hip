@@ -848,7 +848,7 @@ __device__ __forceinline__ void wave_seg_sums(const uint8_t* a, uint32_t len, bo
 // Ragged descriptors, balanced: 64 descriptors per wave tile. Segments longer
 // than 1 MiB (chunk space kept < 2^32) are summed one at a time by the wave.
 template <int C>
-__global__ __launch_bounds__(256) void k_desc_lb(const uint8_t* __restrict__ base,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TCPCSUM_DESC_LB_WAVES, 8))) void k_desc_lb(const uint8_t* __restrict__ base,
                                                  const tcpcsum_desc_t* __restrict__ desc, uint64_t n,
                                                  uint16_t* __restrict__ out, uint32_t spw) {
     // spw: segments per wave tile (1..64; lanes >= spw hold no segment) — fewer
