@@ -26,7 +26,8 @@ SRC_HASH := $(shell cat $(HASH_SRCS) | sha256sum | cut -c1-64)
 
 PRELOAD := tcp_amd/libtcpcsum_preload.so
 
-all: $(LIB) $(PRELOAD) $(WRAP) oracle tests/c/abi_smoke tests/c/mmsg_loop tests/c/mmsg_loop_wrap tests/c/raw_echo tools/mmsg_bench
+all: $(LIB) $(PRELOAD) $(WRAP) oracle tests/c/abi_smoke tests/c/mmsg_loop tests/c/mmsg_loop_wrap \
+	tests/c/mmsg_loop_wrap_nopool tests/c/raw_echo tools/mmsg_bench
 
 $(OBJDIR)/%.o: tcp_amd/csrc/%.hip $(HDRS) Makefile
 	@mkdir -p $(OBJDIR)
@@ -49,18 +50,27 @@ $(LIB): $(OBJDIR)/tcpcsum_kernels.o $(OBJDIR)/tcpcsum_api.o $(OBJDIR)/tcpcsum_ho
 $(PRELOAD): tcp_amd/csrc/preload_mmsg.c tcp_amd/csrc/preload_arena.h tcp_amd/csrc/rx_compact.h include/tcpcsum.h $(LIB)
 	$(CC) -O2 -fPIC -shared -Wall -Wextra -Iinclude -o $@ $< -Ltcp_amd -ltcpcsum -ldl -lpthread -Wl,-rpath,'$$ORIGIN'
 
-# the same seam as a static archive for the link-time form (-Wl,--wrap=sendmmsg,...)
+# the same seam as a static archive for the link-time form (-Wl,--wrap=sendmmsg,...): two
+# members, the seams and the arena's allocation wraps (pulled in only by --wrap=malloc ...)
 WRAP := tcp_amd/libtcpcsum_wrap.a
 $(WRAP): tcp_amd/csrc/preload_mmsg.c tcp_amd/csrc/preload_arena.h tcp_amd/csrc/rx_compact.h include/tcpcsum.h
 	@mkdir -p $(OBJDIR)
-	$(CC) -O2 -fPIC -Wall -Wextra -Iinclude -DTCPCSUM_WRAP -c $< -o $(OBJDIR)/wrap_mmsg.o
-	ar rcs $@ $(OBJDIR)/wrap_mmsg.o
+	$(CC) -O2 -fPIC -Wall -Wextra -Iinclude -DTCPCSUM_WRAP -DTCPCSUM_WRAP_PART=1 -c $< -o $(OBJDIR)/wrap_mmsg.o
+	$(CC) -O2 -fPIC -Wall -Wextra -Iinclude -DTCPCSUM_WRAP -DTCPCSUM_WRAP_PART=2 -c $< -o $(OBJDIR)/wrap_alloc.o
+	rm -f $@
+	ar rcs $@ $(OBJDIR)/wrap_mmsg.o $(OBJDIR)/wrap_alloc.o
 
-WRAP_LDFLAGS := -Wl,--wrap=sendmmsg,--wrap=recvmmsg,--wrap=malloc,--wrap=calloc,--wrap=free,--wrap=realloc
+WRAP_MMSG := -Wl,--wrap=sendmmsg,--wrap=recvmmsg
+WRAP_LDFLAGS := $(WRAP_MMSG),--wrap=malloc,--wrap=calloc,--wrap=free,--wrap=realloc
 
 # tests/c/mmsg_loop linked with the seam at build time instead of LD_PRELOAD
 tests/c/mmsg_loop_wrap: tests/c/mmsg_loop.c include/tcpcsum.h $(LIB) $(WRAP)
 	$(CC) -O2 -Wall -Wextra -Iinclude -o $@ $< $(WRAP_LDFLAGS) $(WRAP) -Ltcp_amd -ltcpcsum -ldl -lpthread \
+		-Wl,-rpath,'$$ORIGIN/../../tcp_amd'
+
+# the same with the two mmsg wraps only (no pool): the allocation member stays out of the link
+tests/c/mmsg_loop_wrap_nopool: tests/c/mmsg_loop.c include/tcpcsum.h $(LIB) $(WRAP)
+	$(CC) -O2 -Wall -Wextra -Iinclude -o $@ $< $(WRAP_MMSG) $(WRAP) -Ltcp_amd -ltcpcsum -ldl -lpthread \
 		-Wl,-rpath,'$$ORIGIN/../../tcp_amd'
 
 oracle: oracle/build/liboracle.so oracle/build/liboracle_O0.so
@@ -87,6 +97,7 @@ tools/mmsg_bench: tools/mmsg_bench.c include/tcpcsum.h $(LIB)
 
 clean:
 	rm -rf build oracle/build $(LIB) $(PRELOAD) $(WRAP) tests/c/abi_smoke tests/c/mmsg_loop tests/c/mmsg_loop_wrap \
+		tests/c/mmsg_loop_wrap_nopool \
 		tests/c/raw_echo tools/mmsg_bench
 
 .PHONY: all oracle clean

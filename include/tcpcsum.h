@@ -50,12 +50,12 @@ extern "C" {
 #define TCPCSUM_EHIP (-3)     /* a HIP call failed (tcpcsum_last_hip_error) */
 #define TCPCSUM_ENOMEM (-4)   /* allocation failed */
 
-#define TCPCSUM_ABI_VERSION 4
+#define TCPCSUM_ABI_VERSION 5
 
 /* Launch-shape override, passed per call (NULL = the built-in shapes measured
  * on MI355X). Fields: max_blocks (0 = per-shape default, else
  * the resident grid), unroll in {0,1,2,4,8} (0 = default; segments in flight
- * per lane group), shape in {-1, 0..13} (-1 = auto; meaning per entry point,
+ * per lane group), shape in {-1, 0..14} (-1 = auto; meaning per entry point,
  * see TCPCSUM_TUNE_* below), flags = TCPCSUM_TUNE_* bits (0 = defaults).
  * Every entry point taking one returns TCPCSUM_EINVAL for an invalid value. */
 typedef struct tcpcsum_tuning {
@@ -289,6 +289,14 @@ int tcpcsum_ctx_get_stats(tcpcsum_ctx_t *ctx, tcpcsum_ctx_stats_t *out);
  * in place over PCIe, with no copy. NULL on failure. */
 void *tcpcsum_host_alloc(size_t bytes);
 void tcpcsum_host_free(void *p);
+/* The same, allocated for GPU `device` (its NUMA node; the calling thread's current
+ * device is restored): one loop process per GPU (ABI v5). NULL on failure. */
+void *tcpcsum_host_alloc_on(int device, size_t bytes);
+
+/* 1 on a thread the library started (its copy threads), else 0 (ABI v5): an
+ * allocator in front of the library (the interposer's arena) serves the
+ * application's threads only. */
+int tcpcsum_on_library_thread(void);
 
 /* Uniform layout in host memory; h_out[i] as tcpcsum_batch_uniform_dev.
  * h_sum_start may be NULL (then sum_start is used for every segment).
@@ -340,7 +348,7 @@ int tcpcsum_synth_pseudo_dev(uint32_t *d_sum_start, uint64_t seg0, uint64_t n, u
  * them. With TCPCSUM_TUNE_PROBE_WRITE it also writes lines back (the wire
  * FILL's ceiling); d_src is then written (its bytes unchanged) and must be
  * writable. d_partials: TCPCSUM_PROBE_SLOTS u64 entries; the launch ADDS into
- * the first *n_partials of them (wave w into slot w % TCPCSUM_PROBE_SLOTS),
+ * (since ABI v5; v4 overwrote per-block slots — zero them before reuse) the first *n_partials of them (wave w into slot w % TCPCSUM_PROBE_SLOTS),
  * so when they were zero, their sum on completion is the sum of the lo16+hi16
  * halves of every u32 word of d_src. nbytes multiple of 16, d_src 16-B aligned.
  * Tuning: unroll 0 / 1 / 2 / 4 = 4 / 8 / 16 / 32 chunks per lane per tile; for the
@@ -357,7 +365,9 @@ int tcpcsum_stream_probe_dev(const void *d_src, uint64_t nbytes, uint64_t *d_par
  * 10 / 11 = one / two lanes per segment (up to 5 / 8 chunks), 12 = flat
  * tiles (contiguous 1 KiB per load instruction; 1-32 KiB segments, 4-B
  * aligned, stride >= len), 13 = split segments (a workgroup of four waves
- * per segment, 4*unroll chunk loads per thread per round);
+ * per segment, 4*unroll chunk loads per thread per round), 14 = a workgroup
+ * per segment, segments taken XCD by XCD (unroll 1 / 2 / 4 / 8 = 16 waves x 4
+ * loads, 8 x 8, 16 x 2, 4 x 16 per lane per round; 4- or 16-B aligned only);
  * unroll: segments in flight per lane group; max_blocks: resident grid
  * (1 << 24: one wave tile per wave, the grid rounded to whole XCD rounds and
  * the tiles taken XCD by XCD — the default for lane-group shapes, with a tile
@@ -365,7 +375,7 @@ int tcpcsum_stream_probe_dev(const void *d_src, uint64_t nbytes, uint64_t *d_par
 int tcpcsum_plan_uniform(uint64_t base, uint64_t stride, uint32_t len, uint64_t n,
                          const tcpcsum_tuning_t *tune, int *mode, int *shape, int *unroll, int *max_blocks);
 
-/* tcpcsum_tuning_t.shape, read per entry point: uniform 0..13 (a forced shape
+/* tcpcsum_tuning_t.shape, read per entry point: uniform 0..14 (a forced shape
  * that cannot cover the segments is ignored), ragged 0..6 = (G,C) (4,1) (8,1) (16,1) (32,1) (32,3) (64,4) (64,8)
  * and 7..8 = balanced chunk space (4 / 8 loads per lane in flight; a nonzero
  * unroll u caps its tile at 64 / u segments),

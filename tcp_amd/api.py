@@ -160,6 +160,8 @@ SIGNATURES = {
     "tcpcsum_ctx_get_stats": (ctypes.c_int, [vp, vp]),
     "tcpcsum_host_alloc": (vp, [ctypes.c_size_t]),
     "tcpcsum_host_free": (None, [vp]),
+    "tcpcsum_host_alloc_on": (vp, [ctypes.c_int, ctypes.c_size_t]),
+    "tcpcsum_on_library_thread": (ctypes.c_int, []),
     "tcpcsum_batch_uniform_host": (ctypes.c_int, [vp, vp, u64, u32, vp, u32, vp, u64]),
     "tcpcsum_ipv4_batch_host": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp, u64, u32, ctypes.c_int, vp, vp]),
     "tcpcsum_ipv4_batch_ptrs_host": (ctypes.c_int, [vp, vp, vp, u64, ctypes.c_int, vp, vp]),

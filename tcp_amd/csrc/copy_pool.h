@@ -27,6 +27,11 @@
 
 namespace tcpcsum {
 
+// Set on the library's own threads (the copy pool's workers) for their whole life:
+// tcpcsum_on_library_thread() reports it, so the interposer's arena never serves a
+// packet block to an allocation the library makes.
+inline thread_local int t_library_thread = 0;
+
 inline uint64_t now_ns() {
     return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
                std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -140,6 +145,7 @@ private:
     // the FILL write-back), microseconds apart, and a condition-variable
     // wake-up costs about as long as one of them.
     void loop() {
+        t_library_thread = 1;
         uint64_t seen = 0;
         for (;;) {
             const uint64_t t0 = now_ns();

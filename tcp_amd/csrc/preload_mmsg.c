@@ -101,14 +101,31 @@
  *                                           for TCPCSUM_PRELOAD_POOL: all four, or none)
  *     tcp_amd/libtcpcsum_wrap.a -ltcpcsum -ldl -lpthread
  * and the same entry points become __wrap_sendmmsg / __wrap_recvmmsg (the real
- * calls __real_*). Its arena then serves only the wrapped objects' own mallocs —
- * the loop's, never the HIP runtime's. The environment variables are the same.
+ * calls __real_*). The archive holds two members: the seams
+ * (TCPCSUM_WRAP_PART=1) and the arena's allocation wraps with the pool's
+ * constructor (TCPCSUM_WRAP_PART=2), which the linker pulls in only when
+ * --wrap=malloc makes the loop reference __wrap_malloc — so the two mmsg wraps
+ * alone link too (tests/c/mmsg_loop_wrap_nopool). The arena then serves only the
+ * wrapped objects' own mallocs — the loop's, never the HIP runtime's. The
+ * environment variables are the same.
+ *
+ * Allocations the arena never serves (the LD_PRELOAD build, where every malloc
+ * of the process passes through it): those of a thread inside a library call
+ * (t_guard: the constructor's HIP start-up, a GPU batch), of a thread the
+ * library started (tcpcsum_on_library_thread: its copy threads), and of a
+ * thread created by the GPU runtime or by a guarded thread (pthread_create is
+ * interposed while the pool is on: HIP's worker and host-callback threads are
+ * marked for life). And a process whose interposer started HIP refuses to exec
+ * (execve and its family fail with EPERM: on this hardware an exec after the GPU
+ * was opened takes the machine down); its forked children may exec.
  */
 #define _GNU_SOURCE
 #include <dirent.h>
 #include <dlfcn.h>
 #include <errno.h>
+#include <alloca.h>
 #include <pthread.h>
+#include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -120,6 +137,29 @@
 #include "preload_arena.h"
 #include "rx_compact.h"
 #include "tcpcsum.h"
+
+/* The preload build is one object with everything; the wrap build two archive members
+ * (above) that share the arena, the guard flag and the HIP owner's pid by name. */
+#ifndef TCPCSUM_WRAP
+#define PART_SEAMS 1
+#define PART_ALLOC 1
+#define SHARED static
+#elif TCPCSUM_WRAP_PART == 1
+#define PART_SEAMS 1
+#define PART_ALLOC 0
+#define SHARED
+#elif TCPCSUM_WRAP_PART == 2
+#define PART_SEAMS 0
+#define PART_ALLOC 1
+#define SHARED extern
+#else
+#error "TCPCSUM_WRAP builds need TCPCSUM_WRAP_PART=1 (seams) or 2 (allocation wraps)"
+#endif
+#ifdef TCPCSUM_WRAP
+#define g_arena tcpcsum_wrap_arena
+#define t_guard tcpcsum_wrap_guard
+#define g_hip_pid tcpcsum_wrap_hip_pid
+#endif
 
 typedef int (*sendmmsg_fn)(int, struct mmsghdr *, unsigned int, int);
 typedef int (*recvmmsg_fn)(int, struct mmsghdr *, unsigned int, int, struct timespec *);
@@ -133,6 +173,7 @@ struct tcpcsum_preload_stats {
     unsigned long long errors;
 };
 
+#if PART_SEAMS
 static pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;
 static pthread_once_t g_once = PTHREAD_ONCE_INIT;
 static sendmmsg_fn real_sendmmsg;
@@ -144,6 +185,7 @@ static int g_forked;        /* a forked child of a process that had started HIP 
 static uint16_t *g_out;     /* pinned: the kernel writes results straight here */
 static uint8_t *g_status;
 static struct tcpcsum_preload_stats g_st;
+#endif
 
 /* ------------------------------------------------------------------ the arena
  * TCPCSUM_PRELOAD_POOL: malloc(kPoolBlock) served from page-locked memory the
@@ -151,8 +193,18 @@ static struct tcpcsum_preload_stats g_st;
  * (the constructor's HIP start-up, a GPU batch) — its allocations of the block
  * size are the runtime's, not the loop's, and go to libc. */
 enum { kPoolBlock = 1024 * 32 };   /* loop.c:181-182 */
-static arena_t g_arena = ARENA_INIT;
-static __thread int t_guard __attribute__((tls_model("initial-exec")));
+#if PART_SEAMS
+SHARED arena_t g_arena = ARENA_INIT;
+SHARED __thread int t_guard __attribute__((tls_model("initial-exec")));
+SHARED pid_t g_hip_pid;     /* the process whose interposer started HIP (it must not exec) */
+#else
+SHARED arena_t g_arena;
+SHARED __thread int t_guard __attribute__((tls_model("initial-exec")));
+SHARED pid_t g_hip_pid;
+#endif
+#if PART_ALLOC
+static int g_pool_on;       /* the pool was wanted in this process: mark runtime threads */
+#endif
 
 extern void *__libc_malloc(size_t);
 extern void __libc_free(void *);
@@ -175,14 +227,23 @@ int __real_recvmmsg(int, struct mmsghdr *, unsigned int, int, struct timespec *)
 #define UNDER(fn) __libc_##fn
 #endif
 
+#if PART_ALLOC
 static const arena_libc_t k_libc = {UNDER(malloc), UNDER(free), UNDER(realloc)};
 
+/* Whether a request of the block size comes from the library's or the runtime's side
+ * (never served): asked only for that size, once the arena is on. */
+static int guarded(void) {
+    return t_guard || tcpcsum_on_library_thread();
+}
+
 void *SEAM(malloc)(size_t n) {
-    return arena_route_malloc(&g_arena, n, t_guard, &k_libc);
+    return arena_route_malloc(&g_arena, n, n == arena_block(&g_arena) && guarded(), &k_libc);
 }
 
 void *SEAM(calloc)(size_t nmemb, size_t size) {
-    return arena_route_calloc(&g_arena, nmemb, size, t_guard, UNDER(calloc));
+    size_t n;
+    const int big = !__builtin_mul_overflow(nmemb, size, &n) && n == arena_block(&g_arena);
+    return arena_route_calloc(&g_arena, nmemb, size, big && guarded(), UNDER(calloc));
 }
 
 void SEAM(free)(void *p) {
@@ -237,14 +298,24 @@ static int pool_wanted(const char *v) {
 __attribute__((constructor)) static void pool_ctor(void) {
     if (!pool_wanted(getenv("TCPCSUM_PRELOAD_POOL"))) return;
     unsetenv("TCPCSUM_PRELOAD_POOL");   /* children (an exec'd shell, say) never start HIP for it */
+    /* the GPU the batches will run on (TCPCSUM_PRELOAD_DEVICE, read again by the seams):
+     * the block is allocated for it, on its NUMA node */
+    const char *dv = getenv("TCPCSUM_PRELOAD_DEVICE");
+    const int dev = dv && *dv ? atoi(dv) : 0;
+    g_pool_on = 1;
+    __atomic_store_n(&g_hip_pid, getpid(), __ATOMIC_RELEASE);   /* from here on HIP may be up: no exec */
     t_guard = 1;
-    void *mem = tcpcsum_host_alloc((size_t) kPoolBlock * ARENA_MAX_BLOCKS);
+    void *mem = tcpcsum_host_alloc_on(dev, (size_t) kPoolBlock * ARENA_MAX_BLOCKS);
     t_guard = 0;
     if (!mem || arena_publish(&g_arena, mem, kPoolBlock, ARENA_MAX_BLOCKS)) {
-        fprintf(stderr, "tcpcsum_preload: TCPCSUM_PRELOAD_POOL: no page-locked pool (%s); the loop's buffers stay "
-                        "malloc'd and are copied into staging\n", mem ? "publish failed" : tcpcsum_strerror(TCPCSUM_ENOMEM));
+        fprintf(stderr, "tcpcsum_preload: TCPCSUM_PRELOAD_POOL: no page-locked pool on device %d (%s); the loop's "
+                        "buffers stay malloc'd and are copied into staging\n", dev,
+                mem ? "publish failed" : tcpcsum_strerror(TCPCSUM_ENOMEM));
     }
 }
+#endif /* PART_ALLOC */
+
+#if PART_SEAMS
 
 /* fork: the handlers hold the interposer's locks across it, so the child never
  * inherits one taken mid-update; the child then gives up the GPU path and the arena
@@ -276,6 +347,150 @@ static void fork_child(void) {
 __attribute__((constructor)) static void fork_ctor(void) {
     pthread_atfork(fork_prepare, fork_parent, fork_child);
 }
+
+#ifndef TCPCSUM_WRAP
+/* ------------------------------------------------------------------ exec guard
+ * A process whose interposer started HIP (the pool's constructor, or the first GPU
+ * batch) must not replace itself with another program: on this hardware that takes
+ * the machine down. LD_PRELOAD exported in a shell reaches wrappers (timeout, env,
+ * a shell) that exec; with TCPCSUM_PRELOAD_POOL=1 they would start HIP and then exec.
+ * Every exec entry point of this process fails with EPERM instead; a forked child
+ * (another pid) may exec as usual. */
+static int exec_refused(const char *what) {
+    if (__atomic_load_n(&g_hip_pid, __ATOMIC_ACQUIRE) != getpid()) return 0;
+    fprintf(stderr, "tcpcsum_preload: %s refused: this process started HIP for the GPU checksum path and must not "
+                    "exec (fork first; put LD_PRELOAD on the loop binary, not on a wrapper)\n", what);
+    errno = EPERM;
+    return 1;
+}
+
+static void *next_sym(void **slot, const char *name) {
+    void *f = __atomic_load_n(slot, __ATOMIC_ACQUIRE);
+    if (!f) {
+        f = dlsym(RTLD_NEXT, name);
+        __atomic_store_n(slot, f, __ATOMIC_RELEASE);
+    }
+    return f;
+}
+#define NEXT(type, name) ((type) next_sym(&next_##name, #name))
+static void *next_execve, *next_execv, *next_execvp, *next_execvpe, *next_fexecve, *next_execveat;
+typedef int (*execve_fn)(const char *, char *const[], char *const[]);
+typedef int (*execv_fn)(const char *, char *const[]);
+typedef int (*fexecve_fn)(int, char *const[], char *const[]);
+typedef int (*execveat_fn)(int, const char *, char *const[], char *const[], int);
+
+int execve(const char *path, char *const argv[], char *const envp[]) {
+    return exec_refused("execve") ? -1 : NEXT(execve_fn, execve)(path, argv, envp);
+}
+int execv(const char *path, char *const argv[]) {
+    return exec_refused("execv") ? -1 : NEXT(execv_fn, execv)(path, argv);
+}
+int execvp(const char *file, char *const argv[]) {
+    return exec_refused("execvp") ? -1 : NEXT(execv_fn, execvp)(file, argv);
+}
+int execvpe(const char *file, char *const argv[], char *const envp[]) {
+    return exec_refused("execvpe") ? -1 : NEXT(execve_fn, execvpe)(file, argv, envp);
+}
+int fexecve(int fd, char *const argv[], char *const envp[]) {
+    return exec_refused("fexecve") ? -1 : NEXT(fexecve_fn, fexecve)(fd, argv, envp);
+}
+int execveat(int dirfd, const char *path, char *const argv[], char *const envp[], int flags) {
+    return exec_refused("execveat") ? -1 : NEXT(execveat_fn, execveat)(dirfd, path, argv, envp, flags);
+}
+
+/* execl / execlp / execle: glibc's call execve internally (not through this
+ * library), so they are answered here: the list becomes a vector. */
+#define EXECL_ARGV(arg, ap, argv, envp_out)                                  \
+    size_t n_ = 1;                                                           \
+    {                                                                        \
+        va_list c_;                                                          \
+        va_copy(c_, ap);                                                     \
+        while (va_arg(c_, const char *)) ++n_;                               \
+        va_end(c_);                                                          \
+    }                                                                        \
+    char **argv = alloca((n_ + 1) * sizeof(char *));                         \
+    argv[0] = (char *) (arg);                                                \
+    for (size_t i_ = 1; i_ <= n_; ++i_) argv[i_] = va_arg(ap, char *);       \
+    envp_out
+
+int execl(const char *path, const char *arg, ...) {
+    if (exec_refused("execl")) return -1;
+    va_list ap;
+    va_start(ap, arg);
+    EXECL_ARGV(arg, ap, argv, ;);
+    va_end(ap);
+    return NEXT(execv_fn, execv)(path, argv);
+}
+int execlp(const char *file, const char *arg, ...) {
+    if (exec_refused("execlp")) return -1;
+    va_list ap;
+    va_start(ap, arg);
+    EXECL_ARGV(arg, ap, argv, ;);
+    va_end(ap);
+    return NEXT(execv_fn, execvp)(file, argv);
+}
+int execle(const char *path, const char *arg, ...) {
+    if (exec_refused("execle")) return -1;
+    va_list ap;
+    va_start(ap, arg);
+    EXECL_ARGV(arg, ap, argv, char *const *envp = va_arg(ap, char *const *););
+    va_end(ap);
+    return NEXT(execve_fn, execve)(path, argv, envp);
+}
+
+/* ------------------------------------------------------------------ runtime threads
+ * While the pool is on, a thread created by a guarded thread (inside a library call:
+ * the copy threads, HIP's threads started with it) or by the GPU runtime itself (HIP's
+ * host-callback and worker threads, whenever they start) is guarded for life: its
+ * allocations of the block size are the runtime's, not the loop's. */
+typedef int (*pthread_create_fn)(pthread_t *, const pthread_attr_t *, void *(*)(void *), void *);
+static void *next_pthread_create;
+struct guarded_start {
+    void *(*fn)(void *);
+    void *arg;
+};
+
+static void *guarded_thread(void *p) {
+    struct guarded_start st = *(struct guarded_start *) p;
+    __libc_free(p);
+    t_guard = 1;
+    return st.fn(st.arg);
+}
+
+static int runtime_caller(const void *ra) {
+    static const char *const libs[] = {"libamdhip64", "libhsa-runtime64", "libhsakmt", "libtcpcsum.",
+                                       "librocprofiler", "libroctracer", "libamd_comgr"};
+    Dl_info di;
+    if (!ra || !dladdr(ra, &di) || !di.dli_fname) return 0;
+    const char *b = strrchr(di.dli_fname, '/');
+    b = b ? b + 1 : di.dli_fname;
+    for (size_t i = 0; i < sizeof libs / sizeof libs[0]; ++i)
+        if (!strncmp(b, libs[i], strlen(libs[i]))) return 1;
+    return 0;
+}
+
+int pthread_create(pthread_t *th, const pthread_attr_t *attr, void *(*fn)(void *), void *arg) {
+    pthread_create_fn real = NEXT(pthread_create_fn, pthread_create);
+    if (__atomic_load_n(&g_pool_on, __ATOMIC_ACQUIRE) &&
+        (t_guard || runtime_caller(__builtin_extract_return_addr(__builtin_return_address(0))))) {
+        struct guarded_start *st = (struct guarded_start *) __libc_malloc(sizeof *st);
+        if (st) {
+            st->fn = fn;
+            st->arg = arg;
+            const int rc = real(th, attr, guarded_thread, st);
+            if (rc) __libc_free(st);
+            return rc;
+        }
+    }
+    return real(th, attr, fn, arg);
+}
+
+/* Exported for tests: whether the calling thread's block-size allocations are kept
+ * from the arena. */
+int tcpcsum_preload_thread_guarded(void) {
+    return t_guard || tcpcsum_on_library_thread();
+}
+#endif /* !TCPCSUM_WRAP */
 
 /* ------------------------------------------------------------------ seams */
 static int env_mode(const char *name, int dflt) {
@@ -395,6 +610,7 @@ static int ensure_ctx(void) {
     }
     if (g_ctx_failed) return -1;
     if (!g_ctx) {
+        __atomic_store_n(&g_hip_pid, getpid(), __ATOMIC_RELEASE);   /* HIP starts here: no exec from now on */
         int rc = tcpcsum_ctx_create(g_device, 0, &g_ctx);
         const char *w = getenv("TCPCSUM_PRELOAD_WAIT");
         if (!rc && !(w && !strcmp(w, "spin"))) rc = tcpcsum_ctx_set_flags(g_ctx, TCPCSUM_CTX_BLOCKING_WAIT);
@@ -563,3 +779,4 @@ int SEAM(recvmmsg)(int fd, struct mmsghdr *vec, unsigned int vlen, int flags, st
     }
     return r;
 }
+#endif /* PART_SEAMS */

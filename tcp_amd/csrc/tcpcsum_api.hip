@@ -53,7 +53,7 @@ int get_tuning(const tcpcsum_tuning_t* t, tcpcsum::Tuning* out) {
     if (t) {
         const int u = t->unroll;
         if (t->max_blocks < 0 || !(u == 0 || u == 1 || u == 2 || u == 4 || u == 8) || t->shape < -1 ||
-            t->shape > 13 || (t->flags & ~8191) || (t->flags & 3) == 3 || (t->flags & 12) == 12)
+            t->shape > 14 || (t->flags & ~8191) || (t->flags & 3) == 3 || (t->flags & 12) == 12)
             return TCPCSUM_EINVAL;
         r.max_blocks = t->max_blocks;
         r.unroll = t->unroll;

@@ -372,8 +372,8 @@ hipError_t sleep_on_event(tcpcsum_ctx* c, hipEvent_t ev, uint64_t nap_ns, uint64
 //
 // The sleeping wait predicts when the work ends: expect_ns (the caller's estimate
 // from its bytes) times a ratio this context learns per size class. It naps until
-// the prediction, then polls every poll_ns until twice the prediction, then backs
-// off. When the work was already done at the end of the nap, the nap may have been
+// the prediction, then polls every poll_ns for as long again (at most 200 us), then
+// backs off. When the work was already done at the end of the nap, the nap may have been
 // too long: the ratio shrinks by 1/32. When it took polls, the ratio moves an
 // eighth of the way to what the wait took (at most one poll interval late). A wake
 // that comes late (a busy host) therefore never lengthens the next nap. Round 4
@@ -388,7 +388,9 @@ hipError_t wait_stream(tcpcsum_ctx* c, hipStream_t st, uint64_t expect_ns) {
             uint32_t& ratio = c->wait_ratio[expect_ns < 1000000u ? 0 : 1];   // predicted / expected, x1024
             const uint64_t pred = std::min<uint64_t>(expect_ns * ratio / 1024u, 200000000u);
             int sleeps = 0;
-            e = sleep_on_event(c, c->done_ev, pred, 100000u, t0 + 2 * pred, &sleeps);
+            // fixed-step polls for at most min(pred, 200 us) past the prediction, then back
+            // off: a bulk batch (pred up to 200 ms) that overruns is not polled every 5 us
+            e = sleep_on_event(c, c->done_ev, pred, 100000u, t0 + pred + std::min<uint64_t>(pred, 200000u), &sleeps);
             const uint64_t took = tcpcsum::now_ns() - t0;
             if (e == hipSuccess && expect_ns) {
                 if (sleeps <= 1)   // done by the end of the nap: try a shorter one
@@ -719,6 +721,21 @@ void* tcpcsum_host_alloc(size_t bytes) {
 void tcpcsum_host_free(void* p) {
     if (p) hipHostFree(p);
 }
+
+void* tcpcsum_host_alloc_on(int device, size_t bytes) {
+    int cur = -1;
+    if (!bytes || hipGetDevice(&cur) != hipSuccess) return nullptr;
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) {
+        tcpcsum::note_hip_error((int)e);
+        return nullptr;
+    }
+    void* p = tcpcsum_host_alloc(bytes);
+    (void)hipSetDevice(cur);
+    return p;
+}
+
+int tcpcsum_on_library_thread(void) { return tcpcsum::t_library_thread; }
 
 // Page-locked input: batches under two 16 MiB pieces are read in place by one
 // launch over PCIe; larger ones go to HBM by DMA straight from the caller's

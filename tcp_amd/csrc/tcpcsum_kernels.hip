@@ -475,6 +475,55 @@ __global__ __launch_bounds__(256) void k_uniform_split(const uint8_t* __restrict
     }
 }
 
+// One workgroup of WPB waves per segment, the headline's tile plan carried to long
+// segments (shape 14): each wave reads one contiguous tile of C KiB per round — wave v,
+// load k, lane l reads chunk r*WPB*64*C + v*64*C + k*64 + l — so at 64 KiB with (16, 4)
+// every wave holds exactly one 4 KiB tile and the workgroup the whole segment in one
+// round. Segments are taken XCD by XCD (xcd_block), one per workgroup, so each XCD
+// sweeps one contiguous eighth of the batch. All C loads of a round are unconditional
+// (zsel) and in flight together; u32 lane partials per round (C*8 words of <= 0xffff)
+// flushed to u64; the WPB wave totals meet in LDS. Exact for any length <= INT32_MAX.
+template <int WPB, int C, int MODE>
+__global__ __launch_bounds__(WPB * 64) void k_uniform_wg(const uint8_t* __restrict__ base, uint64_t stride,
+                                                         uint32_t len, uint32_t rounds,
+                                                         const uint32_t* __restrict__ ss, uint32_t ss_scalar,
+                                                         uint16_t* __restrict__ out, uint64_t n) {
+    static_assert(MODE != M1, "byte-granular segments keep one wave per segment");
+    __shared__ uint64_t part[WPB];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint64_t first = xcd_block(n);
+    for (uint64_t seg = first; seg < n; seg += gridDim.x) {
+        const uint8_t* p = base + seg * stride;
+        const uint32_t m = (uint32_t)((uintptr_t)p & 15u);
+        const uint8_t* a0 = p - m;
+        const uint32_t nch = (uint32_t)(((uint64_t)m + len + 15u) >> 4);
+        uint64_t W = 0;
+        for (uint32_t r = 0; r < rounds; ++r) {
+            u32x4 v[C];
+            const uint32_t c0 = r * (uint32_t)(WPB * 64 * C) + (uint32_t)(wv * 64 * C + lane);
+#pragma unroll
+            for (int k = 0; k < C; ++k) {
+                const uint32_t idx = c0 + (uint32_t)(k * 64);
+                v[k] = ld16(zsel(idx < nch, a0 + (uint64_t)idx * 16u));
+            }
+            uint32_t w = 0;
+#pragma unroll
+            for (int k = 0; k < C; ++k) w += chunk_w<MODE>(v[k], (c0 + (uint32_t)(k * 64)) * 16u - m, len);
+            W += w;
+        }
+        W = group_sum64<64>(W);
+        if (lane == 0) part[wv] = W;
+        __syncthreads();
+        if (tid == 0) {
+            uint64_t Wt = 0;
+#pragma unroll
+            for (int i = 0; i < WPB; ++i) Wt += part[i];
+            out[seg] = fold_ref((ss ? ss[seg] : ss_scalar) + Wt);
+        }
+        if (seg + gridDim.x < n) __syncthreads();
+    }
+}
+
 // Flat tiles (segments of >= 1 KiB, 4-byte aligned): a wave takes SPT
 // consecutive segments and reads their byte span as one contiguous stream —
 // lane l loads chunk c0 + 64k + l, so every load instruction is one contiguous
@@ -1948,6 +1997,32 @@ void launch_split(const uint8_t* base, uint64_t stride, uint32_t len, const uint
 #undef TC_S
 }
 
+// a workgroup per segment (shape 14): unroll selects (waves per workgroup, loads per lane per
+// round) = 1: (16, 4) one 4 KiB tile per wave; 2: (8, 8); 4: (16, 2); 8: (4, 16). The grid
+// covers the batch in whole XCD rounds (segments XCD by XCD) unless max_blocks caps it.
+template <int MODE>
+void launch_wg(const uint8_t* base, uint64_t stride, uint32_t len, const uint32_t* ss, uint32_t ss0,
+               uint16_t* out, uint64_t n, hipStream_t s, int max_blocks, int unroll) {
+    uint64_t nch = 0;
+    for (uint64_t i = 0; i < 16 && i < n; ++i) {
+        const uint64_t c = ((((uintptr_t)base + i * stride) & 15u) + len + 15u) >> 4;
+        if (c > nch) nch = c;
+    }
+    if (nch == 0) return;
+    uint64_t gb = xcd_rounds(n);
+    if (max_blocks > 0 && gb > (uint64_t)max_blocks) gb = (uint64_t)max_blocks;
+    if (gb > kMaxGrid) gb = kMaxGrid & ~(uint64_t)7u;
+    const unsigned g = (unsigned)gb;
+#define TC_W(WPB, CC)                                                                                        \
+    hipLaunchKernelGGL((k_uniform_wg<WPB, CC, MODE>), dim3(g), dim3(WPB * 64), 0, s, base, stride, len,      \
+                       (uint32_t)((nch + WPB * 64u * CC - 1) / (WPB * 64u * CC)), ss, ss0, out, n)
+    if (unroll <= 1) TC_W(16, 4);
+    else if (unroll == 2) TC_W(8, 8);
+    else if (unroll == 4) TC_W(16, 2);
+    else TC_W(4, 16);
+#undef TC_W
+}
+
 // flat tiles: unroll selects C (8 * unroll chunks per lane, 8 KiB * unroll per wave tile)
 inline void launch_flat(const uint8_t* base, uint64_t stride, uint32_t len, const uint32_t* ss, uint32_t ss0,
                         uint16_t* out, uint64_t n, hipStream_t s, int max_blocks, int unroll) {
@@ -1991,6 +2066,9 @@ void launch_uniform_mode(int shape, int unroll, const uint8_t* base, uint64_t st
         case 8: TC_U4(64, 8); break;   // <= 512
         case 12: launch_flat(base, stride, len, ss, ss0, out, n, s, max_blocks, unroll); break;
         case 13: launch_split<MODE>(base, stride, len, ss, ss0, out, n, s, max_blocks, unroll); break;
+        case 14:
+            if constexpr (MODE != M1) launch_wg<MODE>(base, stride, len, ss, ss0, out, n, s, max_blocks, unroll);
+            break;
         case 10: TC_U4(1, 5); break;   // <= 5: one lane per segment, no cross-lane reduction
         case 11: TC_U4(2, 4); break;   // <= 8: two lanes per segment
         default:                       // one wave per segment, 8*unroll chunks per lane per round
@@ -2017,12 +2095,14 @@ namespace tcpcsum {
 // Shape 12 is the flat tile (segments of 1 KiB .. 32 KiB, 4-byte aligned, stride
 // >= len), only used when forced or when kFlatAuto says so.
 // Shape 13 is the split segment (a workgroup of four waves per segment, no chunk limit).
-static const uint32_t kShapeChunks[14] = {4, 8, 16, 32, 64, 96, 128, 256, 512, 0xffffffffu, 5, 8, 2048, 0xffffffffu};
-static const int kShapeUnroll[14] = {4, 8, 8, 8, 8, 8, 8, 8, 4, 2, 2, 2, 2, 2};
-static const int kShapeBlocks[14] = {4096, 512, 4096, 4096, 4096, 512, 4096, 1024, 2048, 256, 2048, 2048, 512, 1 << 24};
-static const bool kShapePipe[14] = {false, false, false, false, false, false, false, false, false, false, false, false,
-                                    false, false};
-static const bool kShapeNt[14] = {true, true, true, true, true, true, true, true, true, true, true, true, true, true};
+static const uint32_t kShapeChunks[15] = {4, 8, 16, 32, 64, 96, 128, 256, 512, 0xffffffffu, 5, 8, 2048, 0xffffffffu,
+                                         0xffffffffu};
+static const int kShapeUnroll[15] = {4, 8, 8, 8, 8, 8, 8, 8, 4, 2, 2, 2, 2, 2, 1};
+static const int kShapeBlocks[15] = {4096, 512, 4096, 4096, 4096, 512, 4096, 1024, 2048, 256, 2048, 2048, 512, 1 << 24,
+                                     1 << 24};
+static const bool kShapePipe[15] = {false, false, false, false, false, false, false, false, false, false, false, false,
+                                    false, false, false};
+static const bool kShapeNt[15] = {true, true, true, true, true, true, true, true, true, true, true, true, true, true, true};
 
 static bool flat_ok(uintptr_t b, uint64_t stride, uint32_t len, int mode) {
     return mode != M1 && stride >= 1024 && stride >= len && stride + 46u <= 32u * 1024u && len >= 1024 &&
@@ -2060,6 +2140,8 @@ UniformPlan plan_uniform(uintptr_t b, uint64_t stride, uint32_t len, uint64_t n,
     // a forced shape is honoured only if it covers the segment
     if (tu.shape == 12) {
         if (flat_ok(b, stride, len, p.mode)) p.shape = 12;
+    } else if (tu.shape == 14) {
+        if (p.mode != M1) p.shape = 14;
     } else if (tu.shape >= 0 && tu.shape <= 13 && nch <= kShapeChunks[tu.shape]) {
         p.shape = tu.shape;
     }

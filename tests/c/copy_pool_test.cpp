@@ -60,6 +60,16 @@ int main() {
             for (size_t i = lo; i < hi; ++i) out[i] = (uint32_t)(i * 2654435761u);
         });
         for (size_t i = 0; i < out.size(); ++i) EXPECT(out[i] == (uint32_t)(i * 2654435761u));
+        // the workers are the library's threads for life (tcpcsum_on_library_thread: the
+        // interposer's arena never serves them), the caller is not
+        std::atomic<int> marked{0}, unmarked{0};
+        const std::thread::id me = std::this_thread::get_id();
+        for (int rep = 0; rep < 20; ++rep)
+            pool.run(4096, 1, [&](size_t, size_t) {
+                if (std::this_thread::get_id() != me) (tcpcsum::t_library_thread ? marked : unmarked)++;
+            });
+        EXPECT(marked.load() > 0 && unmarked.load() == 0);
+        EXPECT(tcpcsum::t_library_thread == 0);
         // the streaming-store copy, every destination head / tail alignment, source at
         // an aligned and an odd offset (wire staging: 64-B destination starts, packets
         // anywhere in the caller's buffers)

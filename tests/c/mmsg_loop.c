@@ -32,6 +32,10 @@
  * packet through the seam, and prints "fork child parent_owned=<0|1|-1>
  * child_owned=<..> send=<r> errno=<e>" (owned: whether the interposer's pool holds
  * the block, -1 without the interposer); the parent waits for it (exit 6 if it failed).
+ * "threads": before the loop allocates its buffers, a thread of its own and a HIP
+ * host callback (the GPU runtime's thread) each malloc one 32 KiB buffer and free it;
+ * prints "threads app_owned=<0|1> cb_owned=<0|1> cb_guarded=<0|1>" (the pool should
+ * serve the loop's thread, never the runtime's; exit 8 if the callback did not run).
  * Under TCPCSUM_PRELOAD_RX=drop the receiver expects exactly the packets the
  * mode makes unverifiable to go missing (corrupt / forge: i % 7 == 3, with iov2
  * only those of at most 800 bytes; trunc: those longer than 600 bytes). Sends them with sendmmsg in batches
@@ -43,7 +47,9 @@
  */
 #define _GNU_SOURCE
 #include <arpa/inet.h>
+#include <dlfcn.h>
 #include <errno.h>
+#include <pthread.h>
 #include <netinet/in.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -61,6 +67,43 @@ enum { NBUF = 1024, SLOT = 1024 * 32, IOV2_FIRST = 800 };   /* loop.c:180-183 */
 
 /* the interposer's (preload or --wrap build); absent when the loop runs without it */
 extern int tcpcsum_preload_pool_owns(const void *p) __attribute__((weak));
+extern int tcpcsum_preload_thread_guarded(void) __attribute__((weak));
+
+/* "threads": who gets a block of the loop's size */
+struct probe_alloc {
+    int ran, owned, guarded;
+};
+
+static void *probe_alloc_run(void *arg) {
+    struct probe_alloc *pa = (struct probe_alloc *) arg;
+    uint8_t *p = malloc(SLOT);
+    if (p) memset(p, 1, SLOT);
+    pa->owned = p && tcpcsum_preload_pool_owns ? tcpcsum_preload_pool_owns(p) : 0;
+    pa->guarded = tcpcsum_preload_thread_guarded ? tcpcsum_preload_thread_guarded() : -1;
+    free(p);
+    pa->ran = 1;
+    return NULL;
+}
+
+static void probe_alloc_cb(void *arg) {
+    probe_alloc_run(arg);
+}
+
+/* the loop's own thread, then a HIP host callback (hipLaunchHostFunc on the null
+ * stream, found in the HIP runtime libtcpcsum brought in) */
+static int threads_check(void) {
+    struct probe_alloc app = {0, 0, 0}, cb = {0, 0, 0};
+    pthread_t th;
+    if (pthread_create(&th, NULL, probe_alloc_run, &app) || pthread_join(th, NULL)) return 8;
+    typedef int (*launch_host_fn)(void *, void (*)(void *), void *);
+    typedef int (*sync_fn)(void *);
+    launch_host_fn lh = (launch_host_fn) dlsym(RTLD_DEFAULT, "hipLaunchHostFunc");
+    sync_fn sy = (sync_fn) dlsym(RTLD_DEFAULT, "hipStreamSynchronize");
+    if (!lh || !sy || lh(NULL, probe_alloc_cb, &cb) || sy(NULL) || !cb.ran) return 8;
+    printf("threads app_owned=%d cb_owned=%d cb_guarded=%d\n", app.owned, cb.owned, cb.guarded);
+    fflush(stdout);
+    return 0;
+}
 
 static uint64_t rng = 0x9E3779B97F4A7C15ull;
 static uint32_t next32(void) {
@@ -115,6 +158,10 @@ int main(int argc, char **argv) {
     int pinned = argc > 4 && !strcmp(argv[4], "pinned");
     int iov2 = argc > 4 && !strcmp(argv[4], "iov2");
     int forkm = argc > 4 && !strcmp(argv[4], "fork");
+    if (argc > 4 && !strcmp(argv[4], "threads")) {
+        const int rc = threads_check();
+        if (rc) return rc;
+    }
     int cpu_checks = corrupt || trunc || forge || (argc > 3 && !strcmp(argv[3], "cpu-checks"));
     const char *rxm = getenv("TCPCSUM_PRELOAD_RX");
     const int rx_drop = rxm && !strcmp(rxm, "drop");

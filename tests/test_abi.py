@@ -165,7 +165,7 @@ def test_argument_errors_need_no_device():
     ng = ctypes.c_int()
     assert L.tcpcsum_stream_probe_dev(1 << 20, 17, 1 << 20, ctypes.byref(ng), None, None) == api.EINVAL
     T = api.Tuning
-    for bad in (T(-1, 0, -1, 0), T(0, 3, -1, 0), T(0, 0, 14, 0), T(0, 0, -2, 0),
+    for bad in (T(-1, 0, -1, 0), T(0, 3, -1, 0), T(0, 0, 15, 0), T(0, 0, -2, 0),
                 T(0, 0, -1, 3),      # PIPE_ON | PIPE_OFF
                 T(0, 0, -1, 12),     # NT_ON | NT_OFF
                 T(0, 0, -1, 8192)):   # past the last TCPCSUM_TUNE_* bit

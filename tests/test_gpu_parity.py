@@ -100,7 +100,7 @@ def test_forced_shapes(dev):
     host = rng.integers(0, 256, 1 << 21, dtype=np.uint8)
     d = to_dev(host, dev)
     try:
-        for shape in range(14):
+        for shape in range(15):
             for unroll, flags in ((1, 0), (8, 0), (2, 1 | 8), (8, 1 | 4), (4, 2 | 8), (8, 16), (1, 16 | 8)):
                 tcp_amd.set_tuning(0, unroll, shape, flags)
                 for length, off in ((1500, 0), (1499, 1), (64, 4), (3000, 2), (64, 0), (60, 3), (100, 0),
@@ -113,9 +113,12 @@ def test_forced_shapes(dev):
         tcp_amd.set_tuning(0, 0, -1, 0)
 
 
-def test_split_segments_round_edges(dev):
-    """Shape 13 (four waves per segment): lengths at the edges of its rounds (256*C chunks per
-    round, C = 4..32), every start alignment mod 16, a capped grid (grid-stride over segments)."""
+@pytest.mark.parametrize("shape", [13, 14])
+def test_split_segments_round_edges(dev, shape):
+    """Shape 13 (four waves per segment) and 14 (a workgroup of 4..16 waves per segment, segments
+    XCD by XCD): lengths at the edges of their rounds (256*C chunks per round, C = 4..32; 1024*4,
+    512*8, 1024*2, 256*16), every start alignment mod 16, a capped grid (grid-stride over
+    segments, block order)."""
     import tcp_amd
     rng = np.random.default_rng(23)
     host = rng.integers(0, 256, 6 << 20, dtype=np.uint8)
@@ -124,8 +127,8 @@ def test_split_segments_round_edges(dev):
     dss = to_dev(ss.view(np.int32), dev)
     try:
         for unroll in (1, 2, 4, 8):
-            for max_blocks in (0, 3):
-                tcp_amd.set_tuning(max_blocks, unroll, 13, 0)
+            for max_blocks in (0, 3, 16):
+                tcp_amd.set_tuning(max_blocks, unroll, shape, 0)
                 for length in (8204, 16384, 16380, 16400, 32768, 32772, 65536, 131072 + 4, 262144):
                     for off in (0, 4, 12):
                         n = min(4096, ((6 << 20) - 16) // (length + 16))
@@ -167,6 +170,11 @@ def test_long_segments_and_big_sums(dev):
             got = u16(tcp_amd.batch_uniform(d, length, length - off, n, 0xFFFFFFFF, offset=off))
             want = oracle.batch_uniform(host, length, length - off, n, 0xFFFFFFFF, offset=off)
             assert np.array_equal(got, want), (length, off)
+        # a workgroup per segment (shape 14), every variant: u32 lane partials per round, u64 above
+        for unroll in (1, 2, 4, 8):
+            got = u16(tcp_amd.batch_uniform(d, length, length, n, 0xFFFFFFFF,
+                                            tune=tcp_amd.make_tuning(0, unroll, 14, 0)))
+            assert np.array_equal(got, oracle.batch_uniform(host, length, length, n, 0xFFFFFFFF)), (length, unroll)
 
 
 def _desc(off, lens, ss):

@@ -12,6 +12,7 @@ import re
 import socket
 import struct
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -21,17 +22,18 @@ import oracle
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EXE = os.path.join(REPO, "tests", "c", "mmsg_loop")
 EXE_WRAP = os.path.join(REPO, "tests", "c", "mmsg_loop_wrap")   # the seam linked in (-Wl,--wrap=...)
+EXE_WRAP_NOPOOL = os.path.join(REPO, "tests", "c", "mmsg_loop_wrap_nopool")   # --wrap=sendmmsg,recvmmsg only
 PRELOAD = os.path.join(REPO, "tcp_amd", "libtcpcsum_preload.so")
 
 
 def _ensure_built():
-    if not (os.path.exists(EXE) and os.path.exists(PRELOAD) and os.path.exists(EXE_WRAP)):
+    if not all(os.path.exists(p) for p in (EXE, PRELOAD, EXE_WRAP, EXE_WRAP_NOPOOL)):
         subprocess.run(["make", "-C", REPO, "tests/c/mmsg_loop", "tests/c/mmsg_loop_wrap",
-                        "tcp_amd/libtcpcsum_preload.so"], check=True)
+                        "tests/c/mmsg_loop_wrap_nopool", "tcp_amd/libtcpcsum_preload.so"], check=True)
 
 
 def run_loop(tmp_path, n, env_extra, cpu_checks=False, corrupt=False, trunc=False, forge=False, pinned=False,
-             iov2=False, wrap=False, fork=False):
+             iov2=False, wrap=False, fork=False, threads=False, exe=None):
     """Run mmsg_loop under the LD_PRELOAD interposer, or (wrap) its build with the seam linked in."""
     _ensure_built()
     out = tmp_path / "mm.bin"
@@ -42,8 +44,8 @@ def run_loop(tmp_path, n, env_extra, cpu_checks=False, corrupt=False, trunc=Fals
     env.update(env_extra)
     mode = ("trunc" if trunc else "corrupt" if corrupt else "forge" if forge else
             "cpu-checks" if cpu_checks else "plain")
-    args = [EXE_WRAP if wrap else EXE, str(n), str(out), mode] + (
-        ["pinned"] if pinned else ["iov2"] if iov2 else ["fork"] if fork else [])
+    args = [exe or (EXE_WRAP if wrap else EXE), str(n), str(out), mode] + (
+        ["pinned"] if pinned else ["iov2"] if iov2 else ["fork"] if fork else ["threads"] if threads else [])
     r = subprocess.run(args, env=env, capture_output=True, text=True, timeout=120)
     pkts = []
     if r.returncode == 0:
@@ -136,6 +138,50 @@ def test_wrap_seam_passthrough_and_refusal(tmp_path):
     if tcp_amd.device_check()[0] != 0:
         r, _, _ = run_loop(tmp_path, 10, {"TCPCSUM_PRELOAD_TX": "fill"}, wrap=True)
         assert r.returncode == 3 and "No such device or address" in r.stderr
+
+
+def test_wrap_mmsg_wraps_alone_link_and_run(tmp_path):
+    """the archive's seams link with only -Wl,--wrap=sendmmsg,--wrap=recvmmsg (the allocation
+    member, which needs __real_malloc & co, stays out of the link): the loop runs, TX off passes every
+    packet through, and without a GPU FILL refuses loudly."""
+    import tcp_amd
+    r, pkts, stats = run_loop(tmp_path, 150, {"TCPCSUM_PRELOAD_TX": "off"}, wrap=True, exe=EXE_WRAP_NOPOOL)
+    assert r.returncode == 0, r.stderr
+    assert len(pkts) == 150 and all(b == g for b, g in pkts) and stats["tx_packets"] == 0
+    nm = subprocess.run(["nm", EXE_WRAP_NOPOOL], capture_output=True, text=True).stdout
+    assert "__wrap_sendmmsg" in nm and "__wrap_malloc" not in nm
+    if tcp_amd.device_check()[0] != 0:
+        r, _, _ = run_loop(tmp_path, 10, {"TCPCSUM_PRELOAD_TX": "fill"}, wrap=True, exe=EXE_WRAP_NOPOOL)
+        assert r.returncode == 3 and "No such device or address" in r.stderr
+
+
+@pytest.mark.parametrize("call", ["os.execv('/bin/echo', ['echo', 'EXECED'])",
+                                  "os.execve('/bin/echo', ['echo', 'EXECED'], dict(os.environ))",
+                                  "os.execvp('echo', ['echo', 'EXECED'])"])
+def test_exec_refused_once_the_pool_started_hip(tmp_path, call):
+    """with TCPCSUM_PRELOAD_POOL=1 the constructor starts HIP in whatever process loads the
+    interposer, and a process that has must not exec. Every exec entry point then fails with EPERM
+    (here in Python, which calls execv / execve from libc); without the pool the same exec runs. A
+    forked child may still exec (subprocess from the same process works). CPU only: on a GPU box the
+    refused call would be an exec after HIP started if the guard failed."""
+    import tcp_amd
+    if tcp_amd.device_check()[0] == 0 or os.path.exists("/dev/kfd"):
+        pytest.skip("a GPU is present: never exec after HIP started, guarded or not")
+    _ensure_built()
+    prog = ("import os, subprocess, sys\n"
+            "print(subprocess.run(['/bin/echo', 'CHILD'], capture_output=True, text=True).stdout.strip(), flush=True)\n"
+            "try:\n"
+            f"    {call}\n"
+            "except PermissionError as e:\n"
+            "    print('REFUSED', e.errno)\n")
+    env = {k: v for k, v in os.environ.items() if not k.startswith("TCPCSUM_PRELOAD") and k != "LD_PRELOAD"}
+    env["LD_PRELOAD"] = PRELOAD
+    on = subprocess.run([sys.executable, "-c", prog], env=dict(env, TCPCSUM_PRELOAD_POOL="1"),
+                        capture_output=True, text=True, timeout=120)
+    assert on.stdout.split() == ["CHILD", "REFUSED", str(errno.EPERM)], (on.stdout, on.stderr)
+    assert "refused: this process started HIP" in on.stderr
+    off = subprocess.run([sys.executable, "-c", prog], env=env, capture_output=True, text=True, timeout=120)
+    assert off.stdout.split() == ["CHILD", "EXECED"], (off.stdout, off.stderr)
 
 
 def fork_child_line(r):
@@ -237,6 +283,40 @@ def test_pool_fork_child(tmp_path, wrap):
     assert "forked child of a process that started HIP" in r.stderr
     assert r.stderr.count("tcpcsum_preload: tx batches=") == 1
     assert stats["pool_served"] == 2048 and stats["pool_released"] == 2048 and stats["ctx_staged"] == 0
+
+
+@pytest.mark.gpu
+def test_pool_guards_runtime_threads(tmp_path):
+    """under the pool a thread of the loop's own gets a block of the loop's size from the
+    arena, a HIP host callback (the GPU runtime's thread) never does, and the loop's 2 x 1024 buffers
+    are then all served and every batch runs in place (the library's copy threads are marked too:
+    tcpcsum_on_library_thread, tests/c/copy_pool_test.cpp)."""
+    n = 2100
+    r, pkts, stats = run_loop(tmp_path, n, {"TCPCSUM_PRELOAD_TX": "fill", "TCPCSUM_PRELOAD_RX": "verify",
+                                            "TCPCSUM_PRELOAD_POOL": "mmsg_loop"}, threads=True)
+    assert r.returncode == 0, r.stderr
+    m = re.search(r"threads app_owned=(\d) cb_owned=(\d) cb_guarded=(-?\d)", r.stdout)
+    assert m and m.groups() == ("1", "0", "1"), (r.stdout, r.stderr)
+    assert len(pkts) == n and all(got == oracle_fill(built) for built, got in pkts)
+    assert stats["pool_served"] == 2049 and stats["pool_released"] == 2049 and stats["pool_full"] == 0
+    assert stats["ctx_in_place"] == 2 * n and stats["ctx_staged"] == 0
+
+
+@pytest.mark.gpu
+def test_pool_on_the_named_device(tmp_path):
+    """the pool's block is allocated for TCPCSUM_PRELOAD_DEVICE's GPU (tcpcsum_host_alloc_on),
+    the device the seams then use; a device that does not exist gets no pool (said once) and its
+    seams refuse (ENXIO), never a block placed for another GPU."""
+    n = 1500
+    r, pkts, stats = run_loop(tmp_path, n, {"TCPCSUM_PRELOAD_TX": "fill", "TCPCSUM_PRELOAD_POOL": "mmsg_loop",
+                                            "TCPCSUM_PRELOAD_DEVICE": "0"})
+    assert r.returncode == 0, r.stderr
+    assert len(pkts) == n and all(got == oracle_fill(built) for built, got in pkts)
+    assert stats["pool_served"] == 2048 and stats["ctx_staged"] == 0 and stats["pool_device"] == 0
+    r, _, stats = run_loop(tmp_path, 10, {"TCPCSUM_PRELOAD_TX": "fill", "TCPCSUM_PRELOAD_POOL": "mmsg_loop",
+                                          "TCPCSUM_PRELOAD_DEVICE": "64"})
+    assert "no page-locked pool on device 64" in r.stderr
+    assert r.returncode == 3 and "No such device or address" in r.stderr
 
 
 @pytest.mark.gpu

@@ -1,0 +1,75 @@
+#!/usr/bin/env bash
+# Round-6 GPU runs, one function per experiment; outputs under gpurun_out/r6/:
+#   bash tools/r6_runs.sh <function> [args] [-- <function> [args] ...]
+# Several functions may be chained with "--"; the first failure ends the call.
+# Every GPU step runs under its own timeout.
+set -o pipefail
+O=gpurun_out/r6
+mkdir -p $O
+export TMPDIR=/tmp
+
+# GPU tests of the files named (default: all), one pytest process
+tests() {
+  timeout -k 10 900 python3 -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu "${@:-tests}" \
+    > $O/gputest.txt 2>&1; local rc=$?
+  tail -5 $O/gputest.txt; return $rc
+}
+
+smoke() {
+  timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1; local rc=$?
+  tail -3 $O/smoke.txt; return $rc
+}
+
+# bench.py exactly as the driver runs it (python3 bench.py --gpus 1 --steps 20 --warmup 5), or with
+# the flags given; output $O/bench_<tag>.json, tag = $BTAG or "driver"
+bench() {
+  local tag=${BTAG:-driver}
+  local args=("$@"); [ ${#args[@]} = 0 ] && args=(--gpus 1 --steps 20 --warmup 5)
+  timeout -k 10 600 python3 -u bench.py "${args[@]}" > $O/bench_$tag.json 2> $O/bench_$tag.err; local rc=$?
+  tail -c 400 $O/bench_$tag.err
+  python3 tools/bench_summary.py $O/bench_$tag.json
+  return $rc
+}
+
+# run length / first read / probe order on the 64-B and 1500-B configs (tools/runlen_ab.py)
+runlen() {
+  timeout -k 10 600 python3 -u tools/runlen_ab.py > $O/runlen.jsonl 2> $O/runlen.err; local rc=$?
+  cat $O/runlen.jsonl; tail -5 $O/runlen.err; return $rc
+}
+
+# any python tool under tools/ with its args: output $O/<name>.jsonl
+py() {
+  local name=$(basename $1 .py)
+  timeout -k 10 ${PYT:-600} python3 -u "$@" > $O/$name.jsonl 2> $O/$name.err; local rc=$?
+  cat $O/$name.jsonl; tail -5 $O/$name.err; return $rc
+}
+
+# rocprofv3 kernel trace + stats of the driver's bench command
+prof() {
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o bench -- \
+    python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-host-path --no-cpu-baseline \
+    > $O/bench_under_rocprof.json 2> $O/rocprof.err; local rc=$?
+  tail -3 $O/rocprof.err; return $rc
+}
+
+# one PMC pass (counters $1) over the bench with flags $2...: $O/pmc_<tag>/
+pmc() {
+  local ctr=$1; shift
+  local tag=${PTAG:-$ctr}
+  timeout -s KILL 180 rocprofv3 --pmc $ctr --output-format csv -d $O/pmc_$tag -o pmc -- python3 "$@" \
+    > $O/pmc_$tag.out 2> $O/pmc_$tag.err; local rc=$?
+  tail -2 $O/pmc_$tag.err; return $rc
+}
+
+# run the chained functions: f1 args -- f2 args -- ...
+cmd=()
+for a in "$@"; do
+  if [ "$a" = "--" ]; then
+    "${cmd[@]}" || exit $?
+    cmd=()
+  else
+    cmd+=("$a")
+  fi
+done
+[ ${#cmd[@]} -gt 0 ] && { "${cmd[@]}" || exit $?; }
+exit 0

@@ -54,6 +54,10 @@ def main():
         bufs.append(d)
         sss.append(s)
     out = torch.empty(per, dtype=torch.int16, device=dev)
+    # every variant's results of rotation 0 must equal the built-in plan's
+    tcp_amd.set_tuning(0, 0, -1, 0)
+    tcp_amd.batch_uniform(bufs[0], L, L, per, sss[0], out=out)
+    want = out.clone()
     variants = []
     for fl in [int(x) for x in args.flags.split(",")]:
         for sh in [int(x) for x in args.shapes.split(",")]:
@@ -61,6 +65,7 @@ def main():
                 for u in [int(x) for x in args.unrolls.split(",")]:
                     variants.append((b, u, sh, fl))
     times = {v: [] for v in variants}
+    same = {}
     ptimes = {}
     pshapes = [tuple(int(y) for y in (x + ":-1").split(":")[:3]) for x in args.probe_shapes.split(",")]
     st = torch.cuda.current_stream()
@@ -76,6 +81,9 @@ def main():
             e1.record(st)
             torch.cuda.synchronize()
             times[v].append(e0.elapsed_time(e1) / args.steps)
+            out.zero_()
+            tcp_amd.batch_uniform(bufs[0], L, L, per, sss[0], out=out)
+            same[v] = same.get(v, True) and bool(torch.equal(out, want))
         if args.probe:
             po = torch.zeros(tcp_amd.api.PROBE_SLOTS, dtype=torch.int64, device=dev)
             for ps in pshapes:
@@ -92,7 +100,8 @@ def main():
     for v in variants:
         med, mn = statistics.median(times[v]), min(times[v])
         res.append({"max_blocks": v[0], "unroll": v[1], "shape": v[2], "flags": v[3], "med_ms": round(med, 5), "min_ms": round(mn, 5),
-                    "GB/s_med": round(nbytes / med / 1e6, 1), "GB/s_best": round(nbytes / mn / 1e6, 1)})
+                    "GB/s_med": round(nbytes / med / 1e6, 1), "GB/s_best": round(nbytes / mn / 1e6, 1),
+                    "same_results": same[v]})
         print(json.dumps({"config": args.config, **res[-1]}), flush=True)
     for ps, ts in ptimes.items():
         med = statistics.median(ts)
