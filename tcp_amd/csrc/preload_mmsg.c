@@ -122,8 +122,9 @@
 #define _GNU_SOURCE
 #include <dirent.h>
 #include <dlfcn.h>
-#include <errno.h>
 #include <alloca.h>
+#include <errno.h>
+#include <execinfo.h>
 #include <pthread.h>
 #include <stdarg.h>
 #include <stdint.h>
@@ -230,10 +231,42 @@ int __real_recvmmsg(int, struct mmsghdr *, unsigned int, int, struct timespec *)
 #if PART_ALLOC
 static const arena_libc_t k_libc = {UNDER(malloc), UNDER(free), UNDER(realloc)};
 
+#ifndef TCPCSUM_WRAP
+/* Whether code address ra lies in the GPU runtime or in libtcpcsum itself. */
+static int runtime_caller(const void *ra) {
+    static const char *const libs[] = {"libamdhip64", "libhsa-runtime64", "libhsakmt", "libtcpcsum.",
+                                       "librocprofiler", "libroctracer", "libamd_comgr"};
+    Dl_info di;
+    if (!ra || !dladdr(ra, &di) || !di.dli_fname) return 0;
+    const char *b = strrchr(di.dli_fname, '/');
+    b = b ? b + 1 : di.dli_fname;
+    for (size_t i = 0; i < sizeof libs / sizeof libs[0]; ++i)
+        if (!strncmp(b, libs[i], strlen(libs[i]))) return 1;
+    return 0;
+}
+
+/* Whether any of the caller's frames (up to 16; through operator new and the like)
+ * lies in the runtime: an allocation the GPU runtime makes on an application thread,
+ * inside a HIP call the application made itself. */
+static int runtime_on_stack(void) {
+    void *fr[16];
+    const int n = backtrace(fr, 16);
+    for (int i = 2; i < n; ++i)
+        if (runtime_caller(fr[i])) return 1;
+    return 0;
+}
+#endif
+
 /* Whether a request of the block size comes from the library's or the runtime's side
- * (never served): asked only for that size, once the arena is on. */
+ * (never served): asked only for that size, once the arena is on. The preload sees
+ * every allocation of the process, the runtime's made on the application's threads
+ * too; the wrap build only the wrapped objects' own. */
 static int guarded(void) {
+#ifndef TCPCSUM_WRAP
+    return t_guard || tcpcsum_on_library_thread() || runtime_on_stack();
+#else
     return t_guard || tcpcsum_on_library_thread();
+#endif
 }
 
 void *SEAM(malloc)(size_t n) {
@@ -303,6 +336,10 @@ __attribute__((constructor)) static void pool_ctor(void) {
     const char *dv = getenv("TCPCSUM_PRELOAD_DEVICE");
     const int dev = dv && *dv ? atoi(dv) : 0;
     g_pool_on = 1;
+#ifndef TCPCSUM_WRAP
+    void *fr[2];
+    (void) backtrace(fr, 2);   /* the unwinder is loaded now, never first inside a malloc */
+#endif
     __atomic_store_n(&g_hip_pid, getpid(), __ATOMIC_RELEASE);   /* from here on HIP may be up: no exec */
     t_guard = 1;
     void *mem = tcpcsum_host_alloc_on(dev, (size_t) kPoolBlock * ARENA_MAX_BLOCKS);
@@ -455,18 +492,6 @@ static void *guarded_thread(void *p) {
     __libc_free(p);
     t_guard = 1;
     return st.fn(st.arg);
-}
-
-static int runtime_caller(const void *ra) {
-    static const char *const libs[] = {"libamdhip64", "libhsa-runtime64", "libhsakmt", "libtcpcsum.",
-                                       "librocprofiler", "libroctracer", "libamd_comgr"};
-    Dl_info di;
-    if (!ra || !dladdr(ra, &di) || !di.dli_fname) return 0;
-    const char *b = strrchr(di.dli_fname, '/');
-    b = b ? b + 1 : di.dli_fname;
-    for (size_t i = 0; i < sizeof libs / sizeof libs[0]; ++i)
-        if (!strncmp(b, libs[i], strlen(libs[i]))) return 1;
-    return 0;
 }
 
 int pthread_create(pthread_t *th, const pthread_attr_t *attr, void *(*fn)(void *), void *arg) {

@@ -124,7 +124,8 @@ const char* tcpcsum_build_info(void) {
         ", \"TCPCSUM_XCD_REMAP\": " TCPCSUM_STR(TCPCSUM_XCD_REMAP)
         ", \"TCPCSUM_XCD_CHUNK\": " TCPCSUM_STR(TCPCSUM_XCD_CHUNK)
         ", \"TCPCSUM_UNIFORM_WPB\": " TCPCSUM_STR(TCPCSUM_UNIFORM_WPB)
-        ", \"TCPCSUM_DESC_LB_WAVES\": " TCPCSUM_STR(TCPCSUM_DESC_LB_WAVES) "}"
+        ", \"TCPCSUM_DESC_LB_WAVES\": " TCPCSUM_STR(TCPCSUM_DESC_LB_WAVES)
+        ", \"TCPCSUM_SS_LOAD\": " TCPCSUM_STR(TCPCSUM_SS_LOAD) "}"
         ", \"runtime_knobs\": [" TCPCSUM_RUNTIME_KNOBS_JSON "]}";
     return info;
 }

@@ -198,13 +198,23 @@ template <int G, int C, int U, int MODE, bool NT>
 struct UniformTile {
     static constexpr int GPW = 64 / G;
     static constexpr int SPT = GPW * U;
+    // start values: one dword per group lane 0 (0, 1: non-temporal), or one coalesced dword per
+    // lane for the whole tile, handed to each group by ds_bpermute (2, 3: non-temporal)
+    static constexpr int SSL = (TCPCSUM_SS_LOAD >= 2 && SPT <= 64) ? TCPCSUM_SS_LOAD : (TCPCSUM_SS_LOAD & 1);
     u32x4 v[U][C];
     uint32_t st[U], mm[U];
+    uint32_t sv;
 
     // issue every load of tile t (chunks, and the start values for lane 0 of each group)
     __device__ __forceinline__ void load(uint64_t t, const uint8_t* __restrict__ base, uint64_t stride,
                                          uint32_t len, const uint32_t* __restrict__ ss, uint32_t ss_scalar,
                                          uint64_t n, int q, int gl) {
+        if constexpr (SSL >= 2) {
+            const uint64_t sl = t * SPT + (uint64_t)(q * G + gl);
+            const bool in = ss && (q * G + gl) < SPT && sl < n;
+            if constexpr (SSL == 3) sv = in ? __builtin_nontemporal_load((gptr<const uint32_t>)(ss + sl)) : ss_scalar;
+            else sv = in ? ss[sl] : ss_scalar;
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint64_t seg = t * SPT + (uint64_t)(u * GPW + q);
@@ -214,7 +224,10 @@ struct UniformTile {
             const uint8_t* a0 = p - m;
             const uint32_t nch = (m + len + 15u) >> 4;
             mm[u] = m;
-            st[u] = (live && gl == 0) ? (ss ? ss[seg] : ss_scalar) : 0u;
+            if constexpr (SSL == 1)
+                st[u] = (live && gl == 0) ? (ss ? __builtin_nontemporal_load((gptr<const uint32_t>)(ss + seg)) : ss_scalar) : 0u;
+            else if constexpr (SSL == 0)
+                st[u] = (live && gl == 0) ? (ss ? ss[seg] : ss_scalar) : 0u;
 #pragma unroll
             for (int k = 0; k < C; ++k) {
                 const uint32_t idx = (uint32_t)(k * G + gl);
@@ -253,7 +266,10 @@ struct UniformTile {
             }
             w = group_sum32<G>(w);
             if constexpr (MODE == M1) o = group_sum32<G>(o);
-            if (gl == 0 && seg < n) out[seg] = fold_ref(combine(st[u], w, o, odd));
+            uint32_t s0;
+            if constexpr (SSL >= 2) s0 = (uint32_t)__shfl((int)sv, u * GPW + q, 64);
+            else s0 = st[u];
+            if (gl == 0 && seg < n) out[seg] = fold_ref(combine(s0, w, o, odd));
         }
     }
 };
@@ -1998,7 +2014,8 @@ void launch_split(const uint8_t* base, uint64_t stride, uint32_t len, const uint
 }
 
 // a workgroup per segment (shape 14): unroll selects (waves per workgroup, loads per lane per
-// round) = 1: (16, 4) one 4 KiB tile per wave; 2: (8, 8); 4: (16, 2); 8: (4, 16). The grid
+// round) = 1: one 4 KiB tile per wave, as many waves as the segment fills — (16, 4) past
+// 32 KiB, (8, 4) past 16 KiB, else (4, 4); 2: (8, 8); 4: (16, 2); 8: (4, 16). The grid
 // covers the batch in whole XCD rounds (segments XCD by XCD) unless max_blocks caps it.
 template <int MODE>
 void launch_wg(const uint8_t* base, uint64_t stride, uint32_t len, const uint32_t* ss, uint32_t ss0,
@@ -2016,8 +2033,11 @@ void launch_wg(const uint8_t* base, uint64_t stride, uint32_t len, const uint32_
 #define TC_W(WPB, CC)                                                                                        \
     hipLaunchKernelGGL((k_uniform_wg<WPB, CC, MODE>), dim3(g), dim3(WPB * 64), 0, s, base, stride, len,      \
                        (uint32_t)((nch + WPB * 64u * CC - 1) / (WPB * 64u * CC)), ss, ss0, out, n)
-    if (unroll <= 1) TC_W(16, 4);
-    else if (unroll == 2) TC_W(8, 8);
+    if (unroll <= 1) {
+        if (nch > 2048u) TC_W(16, 4);
+        else if (nch > 1024u) TC_W(8, 4);
+        else TC_W(4, 4);
+    } else if (unroll == 2) TC_W(8, 8);
     else if (unroll == 4) TC_W(16, 2);
     else TC_W(4, 16);
 #undef TC_W

@@ -44,6 +44,28 @@ py() {
   cat $O/$name.jsonl; tail -5 $O/$name.err; return $rc
 }
 
+# uniform kernel shapes -1 (the plan), 13 (split) and 14 (workgroup per segment) x unroll at
+# each length given (default: the long-segment sizes), ~1.5 GB batches: $O/sweeplens.jsonl
+sweeplens() {
+  [ $# -gt 0 ] && LENS="$*"
+  : > $O/sweeplens.jsonl
+  for L in ${LENS:-8192 9000 12300 16384 20004 32768 65536 131072}; do
+    timeout -k 10 300 python3 -u tools/sweep.py --len $L --shapes=-1,13,14 --blocks 0 --unrolls 1,2,4,8 \
+      --rounds 3 --steps 20 >> $O/sweeplens.jsonl 2>> $O/sweeplens.err || return $?
+  done
+  python3 - << 'PY'
+import json, collections
+rows = [json.loads(l) for l in open("gpurun_out/r6/sweeplens.jsonl") if l.strip()]
+by = collections.defaultdict(list)
+for r in rows: by[r["config"]].append(r)
+for c, rs in by.items():
+    rs.sort(key=lambda r: r["med_ms"])
+    plan = [r for r in rs if r["shape"] == -1 and r["unroll"] == 1]
+    print(c, "best", [(r["shape"], r["unroll"], r["med_ms"], r["same_results"]) for r in rs[:3]],
+          "plan(u1)", [(r["med_ms"]) for r in plan], "all_same", all(r["same_results"] for r in rs))
+PY
+}
+
 # rocprofv3 kernel trace + stats of the driver's bench command
 prof() {
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o bench -- \

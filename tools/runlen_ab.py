@@ -145,7 +145,7 @@ def first_read_parts(config, device, variant):
 
 
 def main():
-    if os.environ.get("RUNLEN_ONLY") == "parts":
+    if os.environ.get("RUNLEN_ONLY") == "parts" or "--parts" in sys.argv:
         device = torch.device("cuda", 0)
         for rep in range(3):
             for v in ("base", "scalar", "ss_warm", "data_warm", "both_warm"):
