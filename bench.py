@@ -73,10 +73,10 @@ def max_over_ranks(x: float, dist, device) -> float:
     return float(t.item())
 
 
-def timed_region(step, steps: int, warmup: int, dist, sync, on_start=None, on_end=None) -> float:
+def timed_region(step, steps: int, warmup: int, dist, sync, on_start=None, on_end=None, after_first=None) -> float:
     """W untimed steps, then EXACTLY `steps` steps between barrier+sync on both sides.
-    on_start/on_end run right after/before the syncs (HIP event records).
-    Returns this rank's wall seconds for the timed steps."""
+    on_start/on_end run right after/before the syncs (HIP event records); after_first right after
+    the first timed step is enqueued. Returns this rank's wall seconds for the timed steps."""
     for _ in range(warmup):
         step()
     sync()
@@ -86,8 +86,10 @@ def timed_region(step, steps: int, warmup: int, dist, sync, on_start=None, on_en
     t0 = time.perf_counter()
     if on_start:
         on_start()
-    for _ in range(steps):
+    for i in range(steps):
         step()
+        if i == 0 and after_first:
+            after_first()
     if on_end:
         on_end()
     sync()
@@ -172,18 +174,27 @@ def cpu_baseline(seconds: float) -> dict:
         nseg = (1 << 20) if L <= 1500 else (3 << 29) // L
         if th == 1 and L > 64:
             nseg //= 4
+        c0 = cgroup_cpu_stat()
         r = oracle.cpu_bench(th, L, nseg, seconds * share, opt)
+        c1 = cgroup_cpu_stat()
         key = f"{L}B_{opt}_{'1thread' if th == 1 else f'{th}threads'}"
         figures[key] = {"best": round(r["best"], 3), "median": round(r["median"], 3), "passes": r["passes"],
-                        "sample": f"{nseg} x {L} B"}
+                        "sample": f"{nseg} x {L} B", **cgroup_delta(c0, c1)}
         digests.setdefault((L, nseg), set()).add(r["digest"])   # same batch -> same results at any -O / threads
     head = figures[f"1500B_O2_{'1thread' if T == 1 else f'{T}threads'}"]
+    thr = head.get("throttled_ms")
     return {
         "value": head["median"], "unit": "GiB/s", "cores": T, "kind": "port",
         "sample": (f"1M x 1500-byte segments (Appendix B stream, 1.5 GB in host DRAM, first touched by the "
                    f"thread that reads it), gcc -O2, {T} threads = the CPUs this job may use; median of "
                    f"{head['passes']} passes (best {head['best']})"),
         "threads": T,
+        # whether the job's cgroup throttled the figure (cpu.stat deltas around it)
+        "quota_limited_threads": T, "throttled_ms": thr, "nr_throttled": head.get("nr_throttled"),
+        "throttle_note": (None if thr is None else
+                          f"throttled {thr} ms in {head.get('nr_throttled')} of {head.get('nr_periods')} quota periods "
+                          "while this figure ran" if thr > 0 else
+                          "not throttled while this figure ran: its median/best spread is not the CPU quota"),
         "figures": figures,
         "digests_agree": all(len(v) == 1 for v in digests.values()),
         **info,
@@ -276,9 +287,15 @@ def run_config(config: str, steps: int, warmup: int, rank: int, world: int, dist
         else:
             tcp_amd.batch_uniform(bufs[r], L, L, cnt, sss[r], out=outs[j], stream=sts[j])
 
-    # HIP events on the launch stream(s) bracket the kernels of the timed region
+    # HIP events on the launch stream(s) bracket the kernels of the timed region. The kernel's
+    # average duration is taken over launches 2..K (from an event right after the first launch):
+    # the first timed launch starts on an idle GPU only once the host has enqueued it, a gap
+    # that is no part of any kernel (the host enqueues a launch in ~5 us, the 64-B kernel runs
+    # 12.4 us: launches 2..K run back to back; profiles/r06_runlen.jsonl "cpu_enqueue").
+    # window_ms_per_launch keeps the whole window / K beside it.
     ev0 = [torch.cuda.Event(enable_timing=True) for _ in sts]
     ev1 = [torch.cuda.Event(enable_timing=True) for _ in sts]
+    evA = torch.cuda.Event(enable_timing=True)
 
     def rec(evs):
         for e, st in zip(evs, sts):
@@ -286,10 +303,17 @@ def run_config(config: str, steps: int, warmup: int, rank: int, world: int, dist
     # torch creates a HIP event on its first record: do that here, not inside the timed region
     rec(ev0)
     rec(ev1)
+    evA.record(sts[0])
     torch.cuda.synchronize()
-    wall = timed_region(step, steps, warmup, dist, torch.cuda.synchronize,
-                        on_start=lambda: rec(ev0), on_end=lambda: rec(ev1))
-    kernel_ms = max(ev0[0].elapsed_time(e) for e in ev1) / steps
+    # warm-up: at least one launch over every rotation, so no timed launch is the first read of
+    # a batch just generated — that read costs the 64-B config ~2 us per launch, all of it in the
+    # freshly written start values (profiles/r06_first_read_parts.jsonl, r06_ss_ab.jsonl)
+    warm = max(warmup, rot if not multi else len(marr))
+    wall = timed_region(step, steps, warm, dist, torch.cuda.synchronize,
+                        on_start=lambda: rec(ev0), on_end=lambda: rec(ev1),
+                        after_first=(lambda: evA.record(sts[0])) if streams == 1 and steps > 1 else None)
+    window_ms = max(ev0[0].elapsed_time(e) for e in ev1) / steps
+    kernel_ms = evA.elapsed_time(ev1[0]) / (steps - 1) if streams == 1 and steps > 1 else window_ms
     wall_max = max_over_ranks(wall, dist, device)
     kernel_ms_max = max_over_ranks(kernel_ms, dist, device)
     if multi:   # batch 0 of group 0 is rotation 0 = the Appendix B batch
@@ -302,86 +326,66 @@ def run_config(config: str, steps: int, warmup: int, rank: int, world: int, dist
         check = check and mcheck
     r = {"config": config, "desc": desc, "L": L, "cnt": cnt, "rot": rot, "batch_bytes": batch_bytes,
          "check": check, "wall_max": wall_max, "kernel_ms": kernel_ms, "kernel_ms_max": kernel_ms_max,
-         "streams": streams, "multi": multi}
+         "window_ms": window_ms, "warmup_launches": warm, "streams": streams, "multi": multi}
     return r, bufs, rot
 
 
 def time_probe(bufs, nbytes: int, steps: int, device) -> float:
     """Average ms of the read-only probe (k_probe: the kernels' access shape, every byte read once)
-    over the same rotation of batches a config's kernel was timed on, HIP events on the stream."""
+    over the same rotation of batches a config's kernel was timed on, HIP events on the stream —
+    as the kernel is timed: warm-up launches over every rotation, the same K launches, the
+    average over launches 2..K."""
     import torch
     import tcp_amd
     pout = torch.zeros(tcp_amd.api.PROBE_SLOTS, dtype=torch.int64, device=device)
     nb = (nbytes // 16) * 16
-    for _ in range(3):
-        tcp_amd.stream_probe(bufs[0], nb, pout, tune=(0, 0, -1, 0))
+    for i in range(max(3, len(bufs))):
+        tcp_amd.stream_probe(bufs[i % len(bufs)], nb, pout, tune=(0, 0, -1, 0))
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream()
-    pe0, pe1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    pe0.record(stream)
+    pe1, peA = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for i in range(steps):
         tcp_amd.stream_probe(bufs[i % len(bufs)], nb, pout, tune=(0, 0, -1, 0))
+        if i == 0:
+            peA.record(stream)
     pe1.record(stream)
     torch.cuda.synchronize()
-    return pe0.elapsed_time(pe1) / steps
+    return peA.elapsed_time(pe1) / max(steps - 1, 1)
 
 
-def run_wire(steps: int, warmup: int, device) -> dict:
-    """The reference's own operation on wire packets, device-resident, beside the headline:
-    1M IPv4/TCP packets of 1500 B (1480 TCP bytes) framed as context.c:169-206 frames them, one
-    per 1536-B slot, checks filled in place (context.c:208-209, tcpcsum_ipv4_batch_dev FILL) and
-    verified (VERIFY). Built on the GPU by the fused builder, whose own checks are the anchor:
-    FILL must reproduce them for every packet and VERIFY must then give 0 (a self-consistency
-    check across two kernels, not a parity test — tests/ does that against the oracle).
-    Algorithmic bytes = the 1480 TCP bytes each packet's checksum reads."""
-    import numpy as np
+def time_wire(reg, doff, n: int, cap: int, tcp_bytes: int, built, period: int, steps: int, warmup: int,
+              device) -> dict:
+    """FILL and VERIFY (tcpcsum_ipv4_batch_dev) of the n packets at reg + doff[i], interleaved over 5
+    rounds (3 untimed + `steps` timed launches each) with the same box's ceilings for their traffic
+    over the same region: the read-only probe (every line read, as VERIFY) and the write-back probe
+    (every line read and one whole 128-B line in `period` written back through, bytes unchanged —
+    the FILL's HBM traffic without its arithmetic; TCPCSUM_TUNE_PROBE_WRITE). Median per mode: the
+    first window after the build runs slow on some boxes (0.29 vs 0.245 ms VERIFY,
+    tools/wire_fresh.py), which one window per mode would report as the kernel's rate. FILL must
+    reproduce `built` (the fused builder's checks) for every packet, VERIFY must give 0."""
     import torch
     import tcp_amd
-
-    n, slot, tot = 1 << 20, 1536, 1500
-    tcp_len = tot - 20
-    payload = torch.empty(1 << 26, dtype=torch.uint8, device=device)
-    tcp_amd.synth_fill(payload, 0, payload.numel())
-    segs = np.zeros(n, tcp_amd.TXSEG_DTYPE)
-    segs["payload_off"] = (np.arange(n, dtype=np.uint64) * 4096) % np.uint64(payload.numel() - 65536)
-    segs["out_off"] = np.arange(n, dtype=np.uint64) * slot
-    segs["saddr_be"] = 0x0100007F
-    segs["daddr_be"] = np.arange(n, dtype=np.uint32)
-    segs["sport"], segs["dport"], segs["len"], segs["flags"] = 4000, 45001, tcp_len - 24, 1 | 16
-    reg = torch.zeros(n * slot, dtype=torch.uint8, device=device)
-    built = torch.empty(n, dtype=torch.int16, device=device)
-    dsegs = torch.from_numpy(segs.view(np.uint8)).to(device)
-    tcp_amd.tx_build(payload, dsegs, n, tcp_len, reg, 0, built)
-    del dsegs, payload
-    doff = torch.from_numpy((np.arange(n, dtype=np.uint64) * slot).view(np.int64)).to(device)
     out = torch.empty(n, dtype=torch.int16, device=device)
     sta = torch.empty(n, dtype=torch.uint8, device=device)
     stream = torch.cuda.current_stream()
-    res = {"workload": "1M x 1500-B IPv4/TCP packets (context.c:169-206 framing) in 1536-B slots, "
-                       "device-resident, checks filled / verified in place (tcpcsum_ipv4_batch_dev)",
-           "algorithmic_bytes_per_launch": n * tcp_len}
-    # FILL and VERIFY interleaved over 5 rounds (3 untimed + `steps` timed launches each), median
-    # per mode: the first window after the build runs slow on some boxes (0.29 vs 0.245 ms VERIFY,
-    # tools/wire_fresh.py), which one window per mode would report as the kernel's rate
-    # Beside them, the same box's ceilings for their traffic, over the same region: the read-only
-    # probe (every line read, as VERIFY) and the write-back probe (every line read and one whole
-    # 128-B line per 1536-B slot written back through, bytes unchanged — the FILL's HBM traffic
-    # without its arithmetic; TCPCSUM_TUNE_PROBE_WRITE, period 12 lines)
+    region = reg.numel()
     pout = torch.zeros(tcp_amd.api.PROBE_SLOTS, dtype=torch.int64, device=device)
-    # shape: one 4 KiB tile per wave in XCD order, the fastest found (0.2783 ms against 0.2834 for
-    # the best grid-stride shape, 8192 workgroups; profiles/r05_probe_rw_sweep.jsonl,
+    # probe shape: one 4 KiB tile per wave in XCD order, the fastest found (0.2783 ms against 0.2834
+    # for the best grid-stride shape, 8192 workgroups; profiles/r05_probe_rw_sweep.jsonl,
     # r05_probe_rw_xcd.jsonl)
-    probe_rw = tcp_amd.make_tuning(0, 0, slot // 128, tcp_amd.TUNE_PROBE_WRITE)
+    probe_rw = tcp_amd.make_tuning(0, 0, period, tcp_amd.TUNE_PROBE_WRITE)
+    nb = (region // 16) * 16
     modes = (("fill", tcp_amd.IPV4_FILL), ("verify", tcp_amd.IPV4_VERIFY), ("copy_probe", None),
              ("read_probe", None))
 
     def launch(name, mode):
         if name == "copy_probe":
-            tcp_amd.stream_probe(reg, n * slot, pout, tune=probe_rw)
+            tcp_amd.stream_probe(reg, nb, pout, tune=probe_rw)
         elif name == "read_probe":
-            tcp_amd.stream_probe(reg, n * slot, pout, tune=(0, 0, -1, 0))
+            tcp_amd.stream_probe(reg, nb, pout, tune=(0, 0, -1, 0))
         else:
-            tcp_amd.ipv4_batch(reg, doff, n, slot, mode, out, sta)
+            tcp_amd.ipv4_batch(reg, doff, n, cap, mode, out, sta)
+    res = {"algorithmic_bytes_per_launch": tcp_bytes}
     times = {name: [] for name, _ in modes}
     fill_ok = verify_ok = True
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -389,7 +393,7 @@ def run_wire(steps: int, warmup: int, device) -> dict:
     e1.record(stream)
     torch.cuda.synchronize()
     for _ in range(warmup):
-        tcp_amd.ipv4_batch(reg, doff, n, slot, tcp_amd.IPV4_FILL, out, sta)
+        tcp_amd.ipv4_batch(reg, doff, n, cap, tcp_amd.IPV4_FILL, out, sta)
     for _ in range(5):
         for name, mode in modes:
             for _ in range(3):
@@ -407,20 +411,72 @@ def run_wire(steps: int, warmup: int, device) -> dict:
     for name, _ in modes:
         ms = statistics.median(times[name])
         if name.endswith("probe"):
-            moved = n * slot + (n * 128 if name == "copy_probe" else 0)
+            moved = nb + (nb // (128 * period) * 128 if name == "copy_probe" else 0)
             res[name] = {"avg_ms": round(ms, 5), "ms_rounds": [round(t, 4) for t in times[name]],
                          "bytes_moved_per_launch": moved, "GB/s": round(moved / (ms * 1e-3) / 1e9, 1)}
             continue
-        gbs = n * tcp_len / (ms * 1e-3) / 1e9
+        gbs = tcp_bytes / (ms * 1e-3) / 1e9
         res[name] = {"kernel_avg_ms": round(ms, 5), "kernel_ms_rounds": [round(t, 4) for t in times[name]],
                      "achieved_GB/s": round(gbs, 1), "roofline_frac": round(gbs / HBM_PEAK_GBS, 4)}
-    res["copy_probe"]["what"] = ("k_probe<4,WR>, one 4 KiB tile per wave in XCD order: every line of the 1.61 GB "
-                                 "region read, one 128-B line per 1536-B slot written back through (sc0 sc1), "
-                                 "bytes unchanged")
+    res["copy_probe"]["what"] = (f"k_probe<4,WR>, one 4 KiB tile per wave in XCD order: every line of the "
+                                 f"{region / 1e9:.2f} GB region read, one 128-B line in {period} written back "
+                                 "through (sc0 sc1), bytes unchanged")
     res["read_probe"]["what"] = "k_probe<4>, one 4 KiB tile per wave in XCD order: every line of the region read"
     res["fill_over_verify"] = round(res["fill"]["kernel_avg_ms"] / res["verify"]["kernel_avg_ms"], 3)
     res["fill_over_copy_probe"] = round(res["fill"]["kernel_avg_ms"] / res["copy_probe"]["avg_ms"], 3)
     res["verify_over_read_probe"] = round(res["verify"]["kernel_avg_ms"] / res["read_probe"]["avg_ms"], 3)
+    # the write-back probe rewrote the lines it read: the packets are still the builder's
+    tcp_amd.ipv4_batch(reg, doff, n, cap, tcp_amd.IPV4_VERIFY, out, sta)
+    torch.cuda.synchronize()
+    verify_ok = verify_ok and bool((out == 0).all()) and bool((sta == tcp_amd.PKT_OK).all())
+    res["check"] = fill_ok and verify_ok
+    return res
+
+
+def build_wire(segs, region_bytes: int, max_len: int, device):
+    """The packets of TXSEG_DTYPE records `segs`, built on the GPU by the fused builder
+    (context.c:150-213 on the device) from an Appendix B payload stream into a zeroed region:
+    (region, device offsets, the builder's own checks, summed TCP bytes)."""
+    import numpy as np
+    import torch
+    import tcp_amd
+    n = len(segs)
+    payload = torch.empty(1 << 26, dtype=torch.uint8, device=device)
+    tcp_amd.synth_fill(payload, 0, payload.numel())
+    reg = torch.zeros(region_bytes, dtype=torch.uint8, device=device)
+    built = torch.empty(n, dtype=torch.int16, device=device)
+    dsegs = torch.from_numpy(segs.view(np.uint8)).to(device)
+    tcp_amd.tx_build(payload, dsegs, n, max_len, reg, 0, built)
+    del dsegs, payload
+    doff = torch.from_numpy(segs["out_off"].astype(np.uint64).view(np.int64)).to(device)
+    tcp_bytes = int((24 + segs["len"].astype(np.int64) * ((segs["flags"] & tcp_amd.api.TXF_DATA) != 0)).sum())
+    return reg, doff, built, tcp_bytes
+
+
+def run_wire(steps: int, warmup: int, device) -> dict:
+    """The reference's own operation on wire packets, device-resident, beside the headline:
+    1M IPv4/TCP packets of 1500 B (1480 TCP bytes) framed as context.c:169-206 frames them, one
+    per 1536-B slot, checks filled in place (context.c:208-209, tcpcsum_ipv4_batch_dev FILL) and
+    verified (VERIFY). Built on the GPU by the fused builder, whose own checks are the anchor:
+    FILL must reproduce them for every packet and VERIFY must then give 0 (a self-consistency
+    check across two kernels, not a parity test — tests/ does that against the oracle).
+    Algorithmic bytes = the 1480 TCP bytes each packet's checksum reads."""
+    import numpy as np
+    import tcp_amd
+
+    n, slot, tot = 1 << 20, 1536, 1500
+    tcp_len = tot - 20
+    segs = np.zeros(n, tcp_amd.TXSEG_DTYPE)
+    segs["payload_off"] = (np.arange(n, dtype=np.uint64) * 4096) % np.uint64((1 << 26) - 65536)
+    segs["out_off"] = np.arange(n, dtype=np.uint64) * slot
+    segs["saddr_be"] = 0x0100007F
+    segs["daddr_be"] = np.arange(n, dtype=np.uint32)
+    segs["sport"], segs["dport"], segs["len"], segs["flags"] = 4000, 45001, tcp_len - 24, 1 | 16
+    reg, doff, built, tcp_bytes = build_wire(segs, n * slot, tcp_len - 24, device)
+    assert tcp_bytes == n * tcp_len
+    res = {"workload": "1M x 1500-B IPv4/TCP packets (context.c:169-206 framing) in 1536-B slots, "
+                       "device-resident, checks filled / verified in place (tcpcsum_ipv4_batch_dev)"}
+    res.update(time_wire(reg, doff, n, slot, tcp_bytes, built, slot // 128, steps, warmup, device))
     # HBM bytes actually moved (committed PMC pass: whole 128-B lines read, FILL's check lines
     # written back whole) per launch time — the FILL is a read+write stream, whose measured
     # ceiling is a plain copy's ~6.1 TB/s (tools/copy_probe.hip), not the 8 TB/s read peak
@@ -434,11 +490,55 @@ def run_wire(steps: int, warmup: int, device) -> dict:
         res["traffic_source"] = "profiles/traffic.json wire_fill_1Mx1500 (rocprofv3 --pmc, round 5)"
     except Exception:
         pass
-    # the write-back probe rewrote the lines it read: the packets are still the builder's
-    tcp_amd.ipv4_batch(reg, doff, n, slot, tcp_amd.IPV4_VERIFY, out, sta)
-    torch.cuda.synchronize()
-    verify_ok = verify_ok and bool((out == 0).all()) and bool((sta == tcp_amd.PKT_OK).all())
-    res["check"] = fill_ok and verify_ok
+    return res
+
+
+def wire_mix_segments(n: int):
+    """The flush releaseSend (loop.c:27-94) hands sendmmsg on an echo server, as TXSEG_DTYPE records:
+    of every 8 packets, 3 pure ACKs (context.c:558), one SYN-ACK (context.c:324, resent at :94) or
+    FIN-ACK (:368) in turn — 44-B packets, a 24-B TCP header with the window-scale option — and 4
+    data segments (socket.c:17) with 0..1456-B payloads (1500-B MTU), hash-spread. Packed back to
+    back, each packet starting 16-B aligned as a malloc'd out-buffer does (loop.c:180-183)."""
+    import numpy as np
+    import tcp_amd
+    i = np.arange(n, dtype=np.uint64)
+    h = ((i + np.uint64(1)) * np.uint64(0x9E3779B97F4A7C15)) >> np.uint64(40)
+    kind = (i % np.uint64(8)).astype(np.int64)
+    data = kind >= 4
+    plen = np.where(data, (h % np.uint64(1457)).astype(np.int64), 0)
+    flags = np.where(data, tcp_amd.api.TXF_DATA | tcp_amd.api.TXF_ACK,
+                     np.where(kind == 3, np.where((i // np.uint64(8)) % np.uint64(2) == 0,
+                                                  tcp_amd.api.TXF_SYN | tcp_amd.api.TXF_ACK,
+                                                  tcp_amd.api.TXF_FIN | tcp_amd.api.TXF_ACK), tcp_amd.api.TXF_ACK))
+    size = 44 + plen
+    span = (size + 15) // 16 * 16
+    segs = np.zeros(n, tcp_amd.TXSEG_DTYPE)
+    segs["out_off"] = np.concatenate([[0], np.cumsum(span)[:-1]]).astype(np.uint64)
+    segs["payload_off"] = (i * np.uint64(4096)) % np.uint64((1 << 26) - 65536)
+    segs["saddr_be"] = 0x0100007F
+    segs["daddr_be"] = i.astype(np.uint32)
+    segs["seq"] = (h & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+    segs["ack"] = (i * np.uint64(7919)).astype(np.uint32)
+    segs["sport"], segs["dport"] = 4000, 45001
+    segs["len"], segs["flags"] = plen, flags
+    return segs, int(span.sum())
+
+
+def run_wire_mix(steps: int, warmup: int, device) -> dict:
+    """the reference's real flush, not uniform MTU packets — 1M IPv4/TCP packets of
+    the wire_mix_segments mix, device-resident, FILL and VERIFY in place (tcpcsum_ipv4_batch_dev:
+    the balanced kernel k_ipv4_lb takes large batches of small or mixed packets), with the read
+    and write-back probes over the same region. Algorithmic bytes = each packet's TCP bytes."""
+    n = 1 << 20
+    segs, region = wire_mix_segments(n)
+    reg, doff, built, tcp_bytes = build_wire(segs, region, 1456, device)
+    ctl = int((segs["len"] == 0).sum())
+    res = {"workload": (f"1M IPv4/TCP packets as releaseSend flushes them: {ctl} 44-B control segments (pure ACK, "
+                        f"SYN-ACK, FIN-ACK) and {n - ctl} data segments of 0-1456-B payload, packed 16-B aligned "
+                        f"({region / 1e6:.1f} MB, mean {region / n:.0f} B per packet), checks filled / verified "
+                        "in place (tcpcsum_ipv4_batch_dev)")}
+    res.update(time_wire(reg, doff, n, 1500, tcp_bytes, built, max(1, round(region / n / 128)), steps, warmup,
+                         device))
     return res
 
 
@@ -522,6 +622,27 @@ def node_free_gib() -> dict | None:
         return out or None
     except Exception:
         return None
+
+
+def cgroup_cpu_stat() -> dict | None:
+    """The job's cgroup cpu.stat counters (nr_periods, nr_throttled, throttled_usec, usage_usec), or None."""
+    try:
+        out = {}
+        for line in open("/sys/fs/cgroup/cpu.stat"):
+            k, v = line.split()
+            out[k] = int(v)
+        return out
+    except Exception:
+        return None
+
+
+def cgroup_delta(c0, c1) -> dict:
+    """Throttling between two cgroup_cpu_stat() reads: throttled ms, throttled periods, periods."""
+    if not c0 or not c1:
+        return {}
+    d = {k: c1.get(k, 0) - c0.get(k, 0) for k in ("nr_periods", "nr_throttled", "throttled_usec", "usage_usec")}
+    return {"throttled_ms": round(d["throttled_usec"] / 1e3, 1), "nr_throttled": d["nr_throttled"],
+            "nr_periods": d["nr_periods"], "cpu_usage_s": round(d["usage_usec"] / 1e6, 2)}
 
 
 def cgroup_throttled_us() -> int | None:
@@ -690,6 +811,81 @@ def run_host_path(steps: int, warmup: int, rank: int, world: int, local: int, di
     return r
 
 
+SEAM_VARIANTS = (
+    # name, mmsg_bench args, interposer env (None: no interposer), what
+    ("tx_reference_cpu", ["cpu"], None,
+     "the reference: csum_continue(getPseudoHeaderSum(...)) per packet on one core (context.c:208, -O2)"),
+    ("tx_staged", ["gpu"], {"TCPCSUM_PRELOAD_TX": "fill", "TCPCSUM_PRELOAD_POOL": "0"},
+     "sendmmsg seam, loop.c unedited: the loop's malloc'd out-buffers copied into pinned staging, GPU FILL, "
+     "checks stored back"),
+    ("tx_pool", ["gpu"], {"TCPCSUM_PRELOAD_TX": "fill", "TCPCSUM_PRELOAD_POOL": "mmsg_bench"},
+     "sendmmsg seam, loop.c unedited, TCPCSUM_PRELOAD_POOL: the loop's mallocs served from the interposer's "
+     "page-locked arena, GPU FILL in place"),
+    ("rx_plain", ["rx"], None, "recvmmsg of the 1024 datagrams alone"),
+    ("rx_drop_staged", ["rx"], {"TCPCSUM_PRELOAD_TX": "off", "TCPCSUM_PRELOAD_RX": "drop",
+                                "TCPCSUM_PRELOAD_POOL": "0"},
+     "recvmmsg seam, rx drop: GPU VERIFY of every segment (staged), failing ones removed"),
+    ("rx_drop_pool", ["rx"], {"TCPCSUM_PRELOAD_TX": "off", "TCPCSUM_PRELOAD_RX": "drop",
+                              "TCPCSUM_PRELOAD_POOL": "mmsg_bench"},
+     "the same, in place in the arena's in-buffers"),
+    ("rx_cpu_verify", ["rxcpu"], None, "recvmmsg, then the reference's arithmetic verifying every segment on one core"),
+)
+
+
+def run_seam(iters: int = 300) -> dict:
+    """the seam in the record — tools/mmsg_bench over UDP loopback (no root), 1024 x
+    1500-B packets per batch in the reference's buffer layout (loop.c:180-183), every variant a child
+    process of its own (started before this process makes any GPU call), the interposer preloaded
+    on the child alone. Medians of `iters` batches: wall us and core-us (the whole child's CPU time:
+    caller, copy threads, HIP's threads) per sendmmsg / recvmmsg of 1024 packets (loop.c:75 / :24)."""
+    import re
+    import subprocess
+    exe = os.path.join(REPO, "tools", "mmsg_bench")
+    pre = os.path.join(REPO, "tcp_amd", "libtcpcsum_preload.so")
+    if not (os.path.exists(exe) and os.path.exists(pre)):
+        return {"error": "tools/mmsg_bench or tcp_amd/libtcpcsum_preload.so not built (make)"}
+    base_env = {k: v for k, v in os.environ.items() if not k.startswith("TCPCSUM_PRELOAD") and k != "LD_PRELOAD"}
+    out = {"batch": "1024 x 1500-B IPv4/TCP packets, one per 32 KiB malloc'd buffer (loop.c:180-183), UDP loopback",
+           "iters": iters}
+    for name, args, env_extra, what in SEAM_VARIANTS:
+        env = dict(base_env)
+        if env_extra is not None:
+            env.update({"LD_PRELOAD": pre, "TCPCSUM_PRELOAD_ANY_SOCKET": "1", "TCPCSUM_PRELOAD_STATS": "1",
+                        **env_extra})
+        try:
+            r = subprocess.run([exe] + args + [str(iters)], env=env, capture_output=True, text=True, timeout=120)
+            d = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else {}
+        except Exception as e:   # a failed variant is reported, never fatal to the bench
+            out[name] = {"error": repr(e)[:200]}
+            continue
+        if r.returncode != 0:
+            out[name] = {"error": f"exit {r.returncode}", "stderr_tail": r.stderr[-300:]}
+            continue
+        v = {"what": what, "median_us": d.get("median_us"), "min_us": d.get("min_us"),
+             "core_us_median": d.get("cpu_us_median"), "first_us": d.get("first_us")}
+        if d.get("call_errors"):
+            out[name] = {"error": f"{d['call_errors']} of {iters} calls failed (no GPU path: ENXIO)",
+                         "stderr_tail": r.stderr[-300:]}
+            continue
+        if "checks_match_cpu" in d:
+            v["checks_match_cpu"] = d["checks_match_cpu"]
+        if "batches_not_all_verified" in d:
+            v["batches_not_all_verified"] = d["batches_not_all_verified"]
+            v["short_batches"] = d.get("short_batches")
+        m = re.search(r"in_place=(\d+) staged=(\d+)", r.stderr)
+        if m:
+            v["packets_in_place"], v["packets_staged"] = int(m.group(1)), int(m.group(2))
+        m = re.search(r"pool on=(\d) served=(\d+)", r.stderr)
+        if m and env_extra and env_extra.get("TCPCSUM_PRELOAD_POOL", "0") != "0":
+            v["pool_on"], v["pool_served"] = int(m.group(1)), int(m.group(2))
+        out[name] = v
+    ref = (out.get("tx_reference_cpu") or {}).get("median_us")
+    for k in ("tx_staged", "tx_pool"):
+        if ref and (out.get(k) or {}).get("median_us"):
+            out[k]["speedup_vs_reference_cpu"] = round(ref / out[k]["median_us"], 2)
+    return out
+
+
 def spawn_ranks(args, argv, script=None) -> int:
     """`bench.py --gpus N` with no launcher: start ranks 0..N-1 as child processes (this process
     has made no GPU call), rendezvous on 127.0.0.1, relay rank 0's JSON line, return the worst
@@ -790,6 +986,9 @@ def main(argv=None) -> int:
     ap.add_argument("--host-path-first", action="store_true",
                     help="run the host-memory leg before the device configs (A/B: DESIGN.md §7, 'Order')")
     ap.add_argument("--host-path-last", action="store_true", help=argparse.SUPPRESS)   # the default
+    ap.add_argument("--no-seam", action="store_true",
+                    help="skip the sendmmsg / recvmmsg seam leg (tools/mmsg_bench children, N=1)")
+    ap.add_argument("--seam-iters", type=int, default=300)
     args = ap.parse_args(argv)
 
     rank, world, local = dist_env()
@@ -798,6 +997,8 @@ def main(argv=None) -> int:
     if world != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         return 2
+    # the seam's children run before this process makes any GPU call (N=1 only)
+    seam = run_seam(args.seam_iters) if world == 1 and not args.no_seam and not args.host_path_only else None
 
     import numpy as np
     import torch
@@ -893,6 +1094,8 @@ def main(argv=None) -> int:
             extra[cfg] = {"workload": e["desc"], "GiB/s": round(e["batch_bytes"] * steps / e["wall_max"] / (1 << 30), 2),
                           "kernel_avg_ms": round(e["kernel_ms"], 5), "achieved_GB/s": round(gbs, 1),
                           "roofline_frac": round(gbs / HBM_PEAK_GBS, 4), "steps": steps,
+                          "window_ms_per_launch": round(e["window_ms"], 5),
+                          "warmup_launches": e["warmup_launches"],
                           "rotating_batches": e["rot"], "digest_check": e["check"],
                           "traffic": load_traffic(cfg)}
             if epms:
@@ -927,9 +1130,13 @@ def main(argv=None) -> int:
                     "achieved_GB/s": round(gbs3, 1), "roofline_frac": round(gbs3 / HBM_PEAK_GBS, 4),
                     "digest_check": e3["check"], "traffic": load_traffic(cfg + "_multi")}
                 torch.cuda.empty_cache()
-        # the reference's own call site on wire packets (context.c:208): FILL and VERIFY in place
+        # the reference's own call site on wire packets (context.c:208): FILL and VERIFY in place,
+        # on MTU packets and on the flush mix of control and data segments
         if not args.other or "wire" in args.other.split(","):
             extra["wire_1500"] = run_wire(max(10, min(args.steps, 100)), min(args.warmup, 5), device)
+            torch.cuda.empty_cache()
+        if not args.other or "wire_mix" in args.other.split(","):
+            extra["wire_mix"] = run_wire_mix(max(10, min(args.steps, 100)), min(args.warmup, 5), device)
             torch.cuda.empty_cache()
 
     # end to end from host memory, every rank at once (PCIe and host DRAM bound; never `value`)
@@ -970,6 +1177,9 @@ def main(argv=None) -> int:
                                             "committed, not measured in this run") if traffic else None,
                          "kernel": "tcpcsum::k_uniform (tcpcsum_batch_uniform_dev)",
                          "kernel_avg_ms": round(kernel_ms, 5), "kernel_avg_ms_max_rank": round(kernel_ms_max, 5),
+                         "kernel_avg_over": "HIP events, launches 2..K of the timed window (the first waits on "
+                                            "the host's enqueue)",
+                         "window_ms_per_launch": round(r["window_ms"], 5),
                          "algorithmic_bytes_per_launch": batch_bytes},
             "digest_check": check,
         }
@@ -983,6 +1193,8 @@ def main(argv=None) -> int:
         if host_path or host_first:
             line["host_path"] = host_path or host_first
             line["host_path_order"] = "before the device configs" if host_first else "after the device configs"
+        if seam:
+            line["seam"] = seam
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         print(json.dumps(line), flush=True)

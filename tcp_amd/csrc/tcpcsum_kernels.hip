@@ -2153,6 +2153,13 @@ UniformPlan plan_uniform(uintptr_t b, uint64_t stride, uint32_t len, uint64_t n,
     // split, three same-process runs (profiles/r02_k64_check.jsonl).
     const bool huge = p.mode == M16 && len >= 65536u && (double)n * len >= 4.0 * (1u << 30);
     if (p.shape == 9 && p.mode != M1 && !huge) p.shape = 13;
+    // Dword- or chunk-aligned segments past 32 KiB up to 128 KiB: a workgroup per segment,
+    // one 4 KiB tile per wave (16 waves), segments XCD by XCD (shape 14) — the headline's tile
+    // plan. Same process against the plan before it (split / resident one-wave grid), ~1.5 GB
+    // batches: 48 KiB -2.6 %, 64 KiB -3.3 %, 128 KiB -1.5 %; the 16 GiB 64 KiB config 2.279 vs
+    // 2.393 ms (-4.8 %) (profiles/r06_sweeplens.jsonl, r06_sweep64k.jsonl). At 12-32 KiB it was
+    // within +-2.5 % either way and 256 KiB even, so those keep theirs.
+    if (p.mode != M1 && nch > 2048u && nch <= 8193u) p.shape = 14;
     // 8 KiB chunk-aligned segments (exactly 512 chunks): the split is 9 % ahead of
     // (64,8) (0.208 vs 0.228 ms per 1.5 GB); 6.4-8 KiB otherwise within 2 % of the
     // best shape (tools/uniform_size_sweep*.sh, profiles/r02_uniform_size_sweep.jsonl)

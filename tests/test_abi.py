@@ -71,7 +71,7 @@ def test_library_is_a_product_build_of_this_tree():
                              "TCPCSUM_WIRE_WAVES": 1, "TCPCSUM_TX_WAVES": 1, "TCPCSUM_LINE_CPOL": 17,
                              "TCPCSUM_LOAD_CPOL": -1, "TCPCSUM_XCD_REMAP": 1,
                              "TCPCSUM_XCD_CHUNK": 0, "TCPCSUM_UNIFORM_WPB": 4,
-                             "TCPCSUM_DESC_LB_WAVES": 1, "TCPCSUM_SS_LOAD": 0}
+                             "TCPCSUM_DESC_LB_WAVES": 1, "TCPCSUM_SS_LOAD": 2}
     # the only environment a product context reads
     assert info["runtime_knobs"] == ["TCPCSUM_HOST_THREADS", "TCPCSUM_HOST_NUMA", "TCPCSUM_HOST_SPIN_US",
                                      "LOCAL_WORLD_SIZE"]
@@ -196,8 +196,11 @@ def test_no_device_is_reported_not_faked():
 @pytest.mark.parametrize("base,stride,length,n,expect", [
     (0, 1500, 1500, 1 << 20, (1, 5)),       # 1M x 1500: 4-B aligned, 95 chunks -> 32 lanes x 3
     (0, 64, 64, 1 << 20, (0, 0)),           # 1M x 64: 16-B aligned, 4 lanes
-    (0, 65536, 65536, 1 << 18, (0, 9)),     # 16 GiB of 64 KiB: resident one-wave-per-segment grid
-    (0, 65536, 65536, 1 << 14, (0, 13)),    # 1 GiB of 64 KiB: four waves per segment (split)
+    (0, 65536, 65536, 1 << 18, (0, 14)),    # 16 GiB of 64 KiB: a workgroup per segment, 4 KiB per wave
+    (0, 65536, 65536, 1 << 14, (0, 14)),    # 1 GiB of 64 KiB: the same
+    (4, 131072, 131072, 1 << 12, (1, 14)),  # 128 KiB, dword aligned (8193 chunks): the same
+    (0, 32768, 32768, 1 << 14, (0, 13)),    # 32 KiB: four waves per segment (split)
+    (0, 262144, 262144, 1 << 14, (0, 9)),   # 4 GiB of 256 KiB: resident one-wave-per-segment grid
     (0, 9000, 9000, 1 << 17, (1, 13)),      # jumbo, dword aligned: split
     (3, 1501, 1501, 100, (2, 5)),           # byte-granular
     (0, 1500, 1500, 1, (1, 5)),
