@@ -787,9 +787,73 @@ __device__ __forceinline__ void chunk_masked(u32x4 v, int32_t rel, int32_t len, 
 // IPv4/TCP packets of 4-B multiples, IMIX) — dword-granular masks, no byte
 // masks. A template parameter, not a branch in the sweep: a branch there joins
 // after the masks, and the join waits for every load of the round.
+// Inclusive max-scan over the 64 lanes (values >= 0; 0 where nothing came before), DPP as
+// wave_scan_incl.
+__device__ __forceinline__ uint32_t wave_max_scan_incl(uint32_t x) {
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false));   // row_shr:1
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false));   // row_shr:2
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false));   // row_shr:4
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false));   // row_shr:8
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false));   // row_bcast:15
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false));   // row_bcast:31
+    return x;
+}
+
+// One round of the balanced sweep: for each of its C windows of 64 chunks, every lane's owner
+// segment, the owner's first chunk, the chunk's index in the owner's hull, and the chunk itself
+// (its load issued here, consumed by lb_consume).
+template <int C>
+struct LbRound {
+    uint32_t own[C], pc[C], po[C];
+    u32x4 v[C];
+};
+
+// The owner search of window [W0, W0 + 64). LB_OWNER 0: a scalar loop over the segments that
+// start in the window (a ballot), one readlane each; 1: the starting lanes mark their first
+// chunk's lane in a per-wave LDS row (ids + 1, zero elsewhere) and a max-scan carries each id
+// to the lanes after it — no loop, whatever the number of starts (small packets: ~20 per window).
+template <int OWNER>
+__device__ __forceinline__ uint32_t lb_owner(uint32_t W0, uint32_t P, uint32_t nj, uint32_t lane, uint32_t& carry,
+                                             uint32_t* mark) {
+    uint32_t o;
+    if constexpr (OWNER == 0) {
+        // segments starting inside [W0, W0 + 64), in lane (= start) order
+        uint64_t M = __ballot(nj != 0 && P - W0 < 64u && P >= W0);
+        o = carry;
+        while (M) {
+            const int j = __builtin_ctzll(M);
+            M &= M - 1;
+            const uint32_t st = (uint32_t)__builtin_amdgcn_readlane((int)P, j) - W0;
+            o = lane >= st ? (uint32_t)j : o;
+        }
+    } else {
+        // one wave's LDS row, in program order within the wave: clear, mark, read
+        mark[lane] = 0u;
+        if (nj != 0 && P - W0 < 64u && P >= W0) mark[P - W0] = lane + 1u;
+        const uint32_t m = wave_max_scan_incl(mark[lane]);
+        o = m ? m - 1u : carry;
+    }
+    carry = (uint32_t)__builtin_amdgcn_readlane((int)o, 63);
+    return o;
+}
+
+// Per-lane segment [a, a + len) (len <= 1 MiB: the chunk space stays < 2^32),
+// hole (the same segment-relative offset for every segment, kNoHole: none) as
+// above. On return accW[lane] / accO[lane] hold the lane's segment sums W and O
+// (O only when want_odd, wave-uniform). acc: the wave's 2 x 64 u64 LDS slots;
+// mark: its 64 u32 LDS slots (owner search 1).
+// A4: every segment of the tile 4-B aligned in start and length (packed
+// IPv4/TCP packets of 4-B multiples, IMIX) — dword-granular masks, no byte
+// masks. A template parameter, not a branch in the sweep: a branch there joins
+// after the masks, and the join waits for every load of the round.
+// TCPCSUM_LB_VARIANT bit 0: owner search 1 (lb_owner); bit 1: software-pipelined rounds — the
+// owner search and the loads of round r + 1 are issued before round r is summed (two LbRound
+// register sets), so a round's loads no longer wait for the previous round's scans and atomics.
 template <int C, bool A4>
 __device__ __forceinline__ void lb_sums_t(const uint8_t* a, uint32_t len, uint32_t hole, bool want_odd,
-                                          uint64_t* accW, uint64_t* accO) {
+                                          uint64_t* accW, uint64_t* accO, uint32_t* mark) {
+    constexpr int OWNER = TCPCSUM_LB_VARIANT & 1;
+    constexpr bool PIPE = (TCPCSUM_LB_VARIANT & 2) != 0;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t m = (uint32_t)((uintptr_t)a & 15u);
     const uint32_t nj = len ? (m + len + 15u) >> 4 : 0u;   // chunks of the aligned hull
@@ -802,36 +866,27 @@ __device__ __forceinline__ void lb_sums_t(const uint8_t* a, uint32_t len, uint32
     accW[lane] = 0;
     if (want_odd) accO[lane] = 0;
     uint32_t carry = 0;   // segment owning the next window's first chunk
-    for (uint32_t R = 0; R < T; R += 64u * C) {
-        uint32_t own[C], pc[C], po[C];
-        u32x4 v[C];
+    auto issue = [&](LbRound<C>& r, uint32_t R) {
 #pragma unroll
         for (int k = 0; k < C; ++k) {
             const uint32_t W0 = R + 64u * k;
             const uint32_t g = W0 + lane;
-            // segments starting inside [W0, W0 + 64), in lane (= start) order
-            uint64_t M = __ballot(nj != 0 && P - W0 < 64u && P >= W0);
-            uint32_t o = carry;
-            while (M) {
-                const int j = __builtin_ctzll(M);
-                M &= M - 1;
-                const uint32_t st = (uint32_t)__builtin_amdgcn_readlane((int)P, j) - W0;
-                o = lane >= st ? (uint32_t)j : o;
-            }
-            carry = (uint32_t)__builtin_amdgcn_readlane((int)o, 63);
-            own[k] = o;
-            po[k] = bperm(P, o);
-            pc[k] = g - po[k];   // chunk index inside the owner's hull
+            const uint32_t o = lb_owner<OWNER>(W0, P, nj, lane, carry, mark);
+            r.own[k] = o;
+            r.po[k] = bperm(P, o);
+            r.pc[k] = g - r.po[k];   // chunk index inside the owner's hull
             const uint64_t base = (uint64_t)bperm(a_lo, o) | ((uint64_t)bperm(a_hi, o) << 32);
-            v[k] = ld16(zsel(g < T, reinterpret_cast<const uint8_t*>(base + (uint64_t)pc[k] * 16u)));
+            r.v[k] = ld16(zsel(g < T, reinterpret_cast<const uint8_t*>(base + (uint64_t)r.pc[k] * 16u)));
         }
+    };
+    auto consume = [&](const LbRound<C>& r, uint32_t R) {
         uint32_t w[C], od[C], sr[C];
         bool end[C];
 #pragma unroll
         for (int k = 0; k < C; ++k) {
             const uint32_t W0 = R + 64u * k;
             const uint32_t g = W0 + lane;
-            const uint32_t o = own[k];
+            const uint32_t o = r.own[k];
             const uint32_t lmo = bperm(lm, o);
             const uint32_t lo = lmo & ((1u << 27) - 1u), mo = lmo >> 27;
             const uint32_t no = (mo + lo + 15u) >> 4;
@@ -839,18 +894,18 @@ __device__ __forceinline__ void lb_sums_t(const uint8_t* a, uint32_t len, uint32
             od[k] = 0;
             // lanes past the chunk space (g >= T) loaded the zero buffer: they sum 0
             if constexpr (A4) {
-                const uint32_t rel = pc[k] * 16u - mo;   // dwords at rel + 4j: inside iff < lo (unsigned)
-                const u32x4 x = v[k];
+                const uint32_t rel = r.pc[k] * 16u - mo;   // dwords at rel + 4j: inside iff < lo (unsigned)
+                const u32x4 x = r.v[k];
                 uint32_t t = sad16(rel < lo ? x.x : 0u, 0u);
                 t = sad16(rel + 4u < lo ? x.y : 0u, t);
                 t = sad16(rel + 8u < lo ? x.z : 0u, t);
                 w[k] = sad16(rel + 12u < lo ? x.w : 0u, t);
             } else {
-                chunk_masked(v[k], (int32_t)(pc[k] * 16u) - (int32_t)mo, (int32_t)lo, (int32_t)hole, want_odd, w[k],
-                             od[k]);
+                chunk_masked(r.v[k], (int32_t)(r.pc[k] * 16u) - (int32_t)mo, (int32_t)lo, (int32_t)hole, want_odd,
+                             w[k], od[k]);
             }
-            end[k] = g < T && (pc[k] + 1u == no || lane == 63u || g + 1u == T);
-            sr[k] = po[k] > W0 ? po[k] - W0 : 0u;   // the run's first lane in this window
+            end[k] = g < T && (r.pc[k] + 1u == no || lane == 63u || g + 1u == T);
+            sr[k] = r.po[k] > W0 ? r.po[k] - W0 : 0u;   // the run's first lane in this window
         }
         // the C windows' scans interleaved (their DPP steps fill each other's wait states)
         wave_scan_incl_n<C>(w);
@@ -858,7 +913,7 @@ __device__ __forceinline__ void lb_sums_t(const uint8_t* a, uint32_t len, uint32
         for (int k = 0; k < C; ++k) {
             const uint32_t Xp = bperm(w[k], sr[k] ? sr[k] - 1u : 0u);
             if (end[k])
-                atomicAdd(reinterpret_cast<unsigned long long*>(accW + own[k]),
+                atomicAdd(reinterpret_cast<unsigned long long*>(accW + r.own[k]),
                           (unsigned long long)(w[k] - (sr[k] ? Xp : 0u)));
         }
         if (want_odd) {   // wave-uniform
@@ -867,9 +922,27 @@ __device__ __forceinline__ void lb_sums_t(const uint8_t* a, uint32_t len, uint32
             for (int k = 0; k < C; ++k) {
                 const uint32_t Yp = bperm(od[k], sr[k] ? sr[k] - 1u : 0u);
                 if (end[k])
-                    atomicAdd(reinterpret_cast<unsigned long long*>(accO + own[k]),
+                    atomicAdd(reinterpret_cast<unsigned long long*>(accO + r.own[k]),
                               (unsigned long long)(od[k] - (sr[k] ? Yp : 0u)));
             }
+        }
+    };
+    constexpr uint32_t STEP = 64u * C;
+    if constexpr (!PIPE) {
+        for (uint32_t R = 0; R < T; R += STEP) {
+            LbRound<C> r;
+            issue(r, R);
+            consume(r, R);
+        }
+    } else {
+        LbRound<C> ra, rb;
+        if (T) issue(ra, 0);
+        for (uint32_t R = 0; R < T; R += 2u * STEP) {
+            if (R + STEP < T) issue(rb, R + STEP);
+            consume(ra, R);
+            if (R + STEP >= T) break;
+            if (R + 2u * STEP < T) issue(ra, R + 2u * STEP);
+            consume(rb, R + STEP);
         }
     }
     __builtin_amdgcn_wave_barrier();
@@ -877,12 +950,12 @@ __device__ __forceinline__ void lb_sums_t(const uint8_t* a, uint32_t len, uint32
 
 template <int C>
 __device__ __forceinline__ void lb_sums(const uint8_t* a, uint32_t len, uint32_t hole, bool want_odd,
-                                        uint64_t* accW, uint64_t* accO) {
+                                        uint64_t* accW, uint64_t* accO, uint32_t* mark) {
     const bool a4 = __ballot(len != 0 && (((uint32_t)(uintptr_t)a | len) & 3u) != 0) == 0 && hole == kNoHole;
     if (a4)
-        lb_sums_t<C, true>(a, len, hole, want_odd, accW, accO);
+        lb_sums_t<C, true>(a, len, hole, want_odd, accW, accO, mark);
     else
-        lb_sums_t<C, false>(a, len, hole, want_odd, accW, accO);
+        lb_sums_t<C, false>(a, len, hole, want_odd, accW, accO, mark);
 }
 
 // One segment summed by the whole wave (wave-uniform a, len): 64 chunks per
@@ -919,7 +992,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TCPCSUM_DES
     // spw: segments per wave tile (1..64; lanes >= spw hold no segment) — fewer
     // for long segments, so a batch of them still spreads over enough waves
     __shared__ uint64_t acc[4][2][64];
+    __shared__ uint32_t marks[(TCPCSUM_LB_VARIANT & 1) ? 4 : 1][64];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint32_t* mark = marks[(TCPCSUM_LB_VARIANT & 1) ? wv : 0];
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
     const uint64_t ntiles = (n + spw - 1) / spw;
     for (uint64_t t = (uint64_t)blockIdx.x * 4u + wv; t < ntiles; t += nwaves) {   // block order, as k_desc
@@ -941,7 +1016,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TCPCSUM_DES
             wave_seg_sums(reinterpret_cast<const uint8_t*>(pj), lj, any_odd, W, O);
             if (lane == j) { bw = W; bo = O; }
         }
-        lb_sums<C>(p, big ? 0u : len, kNoHole, any_odd, acc[wv][0], acc[wv][1]);
+        lb_sums<C>(p, big ? 0u : len, kNoHole, any_odd, acc[wv][0], acc[wv][1], mark);
         const uint64_t W = big ? bw : acc[wv][0][lane];
         const uint64_t O = !any_odd ? 0 : big ? bo : acc[wv][1][lane];
         if (mine) out[seg] = fold_ref(combine((uint64_t)d.w, W, O, odd));
@@ -1441,7 +1516,9 @@ __global__ __launch_bounds__(256) void k_ipv4_lb(uint8_t* __restrict__ pkts, con
                                                  uint16_t* __restrict__ ipout, uint32_t spw) {
     // spw: packets per wave tile (1..64; lanes >= spw hold none), as in k_desc_lb
     __shared__ uint64_t acc[4][2][64];
+    __shared__ uint32_t marks[(TCPCSUM_LB_VARIANT & 1) ? 4 : 1][64];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint32_t* mark = marks[(TCPCSUM_LB_VARIANT & 1) ? wv : 0];
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
     const uint64_t ntiles = (n + spw - 1) / spw;
     const bool verify = (mode & TCPCSUM_IPV4_VERIFY) != 0;
@@ -1483,7 +1560,7 @@ __global__ __launch_bounds__(256) void k_ipv4_lb(uint8_t* __restrict__ pkts, con
         uint8_t* tcp = ip + th;
         const bool odd = ((uintptr_t)ip & 1u) != 0;   // th is even
         const bool any_odd = __ballot(ok && odd) != 0;
-        lb_sums<C>(tcp, len, kNoHole, any_odd, acc[wv][0], acc[wv][1]);
+        lb_sums<C>(tcp, len, kNoHole, any_odd, acc[wv][0], acc[wv][1], mark);
         if (!live) continue;
         if (!ok) {
             if (out) out[i] = 0;

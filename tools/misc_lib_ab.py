@@ -57,8 +57,11 @@ def main():
                               "GB_per_s": round(algo_bytes / (ms * 1e-3) / 1e9, 1), "same": same[k]}), flush=True)
 
     # tx_build: 1M x 1456-B payloads -> 1500-B packets, packed
+    only = os.environ.get("MISC_AB_ONLY", "")
     n, L = 1 << 20, 1456
-    payload = torch.empty(n * L, dtype=torch.uint8, device=dev)
+    if only and "tx_build_1Mx1456" not in only.split(","):
+        n = 0
+    payload = torch.empty(max(n, 1) * L, dtype=torch.uint8, device=dev)
     tcp_amd.synth_fill(payload, 0, n * L)
     segs = np.zeros(n, tcp_amd.TXSEG_DTYPE)
     segs["payload_off"] = np.arange(n, dtype=np.uint64) * L
@@ -71,13 +74,17 @@ def main():
     calls = {k: (lambda k=k: libs[k].tcpcsum_tx_build_dev(payload.data_ptr(), dsegs.data_ptr(), n, L,
                                                            pk[k].data_ptr(), 0, ck[k].data_ptr(), h, None))
              for k in libs}
-    run("tx_build_1Mx1456", calls, {k: (pk[k], ck[k]) for k in libs}, 20, n * (2 * L + 44))
+    if n:
+        run("tx_build_1Mx1456", calls, {k: (pk[k], ck[k]) for k in libs}, 20, n * (2 * L + 44))
     del payload, dsegs, pk, ck
     torch.cuda.empty_cache()
 
     # ragged descriptor batches
     rng = np.random.default_rng(5)
-    for name, lo, hi in (("desc_imix_40_1500", 40, 1500), ("desc_mtu_1400_1500", 1400, 1500)):
+    for name, lo, hi in (("desc_imix_40_1500", 40, 1500), ("desc_mtu_1400_1500", 1400, 1500),
+                         ("desc_small_40_200", 40, 200)):
+        if only and name not in only.split(","):
+            continue
         lens = rng.integers(lo, hi + 1, 1 << 22).astype(np.uint32)
         total = np.cumsum(lens.astype(np.uint64))
         m = int(np.searchsorted(total, 1572864000))

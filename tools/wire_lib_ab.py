@@ -57,12 +57,23 @@ def main():
               (n // 8) * 9216, 9216),
              ("2Mx576_packed", np.arange(2 * n, dtype=np.uint64) * 576, np.full(2 * n, 556, np.uint32), 2 * n * 576,
               576)]   # small packets: the balanced kernel (k_ipv4_lb)
+    # the flush mix of bench.py's wire_mix leg (control segments and data, packed 16-B aligned)
+    import bench
+    mix_segs, mix_region = bench.wire_mix_segments(n)
+    works.append(("1M_flush_mix", mix_segs, None, mix_region, 1500))
     only = os.environ.get("WIRE_AB_ONLY")
     rounds = int(os.environ.get("WIRE_AB_ROUNDS", "5"))
     for name, offs, tl, rb, cap in works:
         if only and name not in only.split(","):
             continue
-        reg0 = build(offs, tl, rb)
+        if tl is None:   # ready TXSEG records
+            segs = offs
+            m = segs.size
+            reg0 = torch.zeros(rb, dtype=torch.uint8, device=dev)
+            tcp_amd.tx_build(payload, torch.from_numpy(segs.view(np.uint8)).to(dev), m, 1456, reg0, 0, None)
+            offs = segs["out_off"].astype(np.uint64)
+        else:
+            reg0 = build(offs, tl, rb)
         m = offs.size
         doff = torch.from_numpy(offs.view(np.int64)).to(dev)
         regs = {k: reg0.clone() for k in libs}
