@@ -827,10 +827,16 @@ __device__ __forceinline__ uint32_t lb_owner(uint32_t W0, uint32_t P, uint32_t n
             o = lane >= st ? (uint32_t)j : o;
         }
     } else {
-        // one wave's LDS row, in program order within the wave: clear, mark, read
-        mark[lane] = 0u;
-        if (nj != 0 && P - W0 < 64u && P >= W0) mark[P - W0] = lane + 1u;
-        const uint32_t m = wave_max_scan_incl(mark[lane]);
+        // one wave's LDS row: clear, mark, read. Other lanes' writes are read back, so the
+        // accesses are volatile (never forwarded from this lane's own store) and a wave
+        // barrier orders them
+        volatile uint32_t* vm = mark;
+        vm[lane] = 0u;
+        __builtin_amdgcn_wave_barrier();
+        if (nj != 0 && P - W0 < 64u && P >= W0) vm[P - W0] = lane + 1u;
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t m = wave_max_scan_incl(vm[lane]);
+        __builtin_amdgcn_wave_barrier();
         o = m ? m - 1u : carry;
     }
     carry = (uint32_t)__builtin_amdgcn_readlane((int)o, 63);
@@ -1523,31 +1529,54 @@ __global__ __launch_bounds__(256) void k_ipv4_lb(uint8_t* __restrict__ pkts, con
     const uint64_t ntiles = (n + spw - 1) / spw;
     const bool verify = (mode & TCPCSUM_IPV4_VERIFY) != 0;
     const bool iphdr = (mode & TCPCSUM_IPV4_IPHDR) != 0;
-    // block order: XCD order measured 1 % slower on 2M packed 576-B packets
-    // (profiles/r05_xcd_kernels_ab.jsonl)
-    for (uint64_t t = (uint64_t)blockIdx.x * 4u + wv; t < ntiles; t += nwaves) {
+    // A tile's packet offsets (and PL lengths), then the header dwords under them: two
+    // dependent loads before its sweep. TCPCSUM_LB_VARIANT bit 2: a grid-stride loop that
+    // issues tile t + 2's offsets and tile t + 1's header loads before tile t is swept.
+    struct Off {
+        uint64_t o;
+        uint32_t pl;
+    };
+    auto load_off = [&](uint64_t t) {
         const uint64_t i = t * spw + (uint64_t)lane;
         const bool live = (uint32_t)lane < spw && i < n;
-        const uint64_t o = ldg<uint64_t>(zsel(live, reinterpret_cast<const uint8_t*>(off + i)));
-        uint32_t room = 0;   // PL: readable bytes at the packet (region end, its own length)
-        bool hdr;
+        Off r;
+        r.o = ldg<uint64_t>(zsel(live, reinterpret_cast<const uint8_t*>(off + i)));
+        r.pl = PL ? ldg<uint32_t>(zsel(live, reinterpret_cast<const uint8_t*>(plen + i))) : 0u;
+        return r;
+    };
+    // the readable bytes at the packet (PL: region end and its own length) and whether the
+    // 20-byte header is among them
+    auto room_of = [&](uint64_t t, const Off& f, uint32_t& room) {
+        const uint64_t i = t * spw + (uint64_t)lane;
+        const bool live = (uint32_t)lane < spw && i < n;
         if constexpr (PL) {
-            const uint32_t pl = ldg<uint32_t>(zsel(live, reinterpret_cast<const uint8_t*>(plen + i)));
-            const uint64_t rr = live && o < limit ? limit - o : 0u;
-            room = (uint32_t)(rr < (uint64_t)pl ? rr : (uint64_t)pl);
-            hdr = room >= 20u;
+            const uint64_t rr = live && f.o < limit ? limit - f.o : 0u;
+            room = (uint32_t)(rr < (uint64_t)f.pl ? rr : (uint64_t)f.pl);
+            return room >= 20u;
         } else {
-            hdr = live && o < limit && limit - o >= 20u;
+            room = 0;
+            return live && f.o < limit && limit - f.o >= 20u;
         }
+    };
+    // the dwords under header bytes [0, 20): D[5] only when ip is not 4-B aligned
+    // (an aligned dword holding a needed byte never crosses a page)
+    auto load_hdr = [&](uint64_t t, const Off& f, uint32_t (&D)[6]) {
+        uint32_t room;
+        const bool hdr = room_of(t, f, room);
+        const uint8_t* ip = PL ? reinterpret_cast<const uint8_t*>((uintptr_t)pkts + f.o) : pkts + f.o;
+        const uint32_t sh = (uint32_t)((uintptr_t)ip & 3u);
+#pragma unroll
+        for (int k = 0; k < 6; ++k) D[k] = ldg<uint32_t>(zsel(hdr && (k < 5 || sh != 0), ip - sh + 4 * k));
+    };
+    auto process = [&](uint64_t t, const Off& f, const uint32_t (&D)[6]) {
+        const uint64_t i = t * spw + (uint64_t)lane;
+        const bool live = (uint32_t)lane < spw && i < n;
+        const uint64_t o = f.o;
+        uint32_t room;
+        const bool hdr = room_of(t, f, room);
         uint8_t* ip = PL ? reinterpret_cast<uint8_t*>((uintptr_t)pkts + o) : pkts + o;
         const uint32_t sh = (uint32_t)((uintptr_t)ip & 3u);
         const uint8_t* d0 = ip - sh;
-        // the dwords under header bytes [0, 20): D[5] only when ip is not 4-B aligned
-        // (an aligned dword holding a needed byte never crosses a page)
-        uint32_t D[6];
-#pragma unroll
-        for (int k = 0; k < 6; ++k)
-            D[k] = ldg<uint32_t>(zsel(hdr && (k < 5 || sh != 0), d0 + 4 * k));
         auto rel4 = [&](int k) { return __builtin_amdgcn_alignbyte(D[k + 1], D[k], sh); };   // bytes [4k, 4k+4)
         const uint32_t h0 = rel4(0), h8 = rel4(2), sa = rel4(3), da = rel4(4);
         const uint32_t ver = (h0 >> 4) & 15u, ihl = h0 & 15u;
@@ -1561,11 +1590,11 @@ __global__ __launch_bounds__(256) void k_ipv4_lb(uint8_t* __restrict__ pkts, con
         const bool odd = ((uintptr_t)ip & 1u) != 0;   // th is even
         const bool any_odd = __ballot(ok && odd) != 0;
         lb_sums<C>(tcp, len, kNoHole, any_odd, acc[wv][0], acc[wv][1], mark);
-        if (!live) continue;
+        if (!live) return;
         if (!ok) {
             if (out) out[i] = 0;
             if (status) status[i] = TCPCSUM_PKT_SKIPPED;
-            continue;
+            return;
         }
         const uint32_t len_be = ((len & 0xffu) << 8) | ((len >> 8) & 0xffu);   // htons
         // context.c:104-119 closed form
@@ -1599,6 +1628,32 @@ __global__ __launch_bounds__(256) void k_ipv4_lb(uint8_t* __restrict__ pkts, con
         if (!verify) store_u16(tcp + 16, c);   // native u16 store, as context.c:208
         if (out) out[i] = c;
         if (status) status[i] = (uint8_t)st;
+    };
+    // block order: XCD order measured 1 % slower on 2M packed 576-B packets
+    // (profiles/r05_xcd_kernels_ab.jsonl)
+    uint64_t t = (uint64_t)blockIdx.x * 4u + wv;
+    if constexpr ((TCPCSUM_LB_VARIANT & 4) == 0) {
+        for (; t < ntiles; t += nwaves) {
+            const Off f = load_off(t);
+            uint32_t D[6];
+            load_hdr(t, f, D);
+            process(t, f, D);
+        }
+    } else {
+        if (t >= ntiles) return;
+        Off f1 = load_off(t), f2 = load_off(t + nwaves);   // past the end: zero loads, no packet
+        uint32_t D1[6];
+        load_hdr(t, f1, D1);
+        for (; t < ntiles; t += nwaves) {
+            const Off f3 = load_off(t + 2 * nwaves);
+            uint32_t D2[6];
+            load_hdr(t + nwaves, f2, D2);
+            process(t, f1, D1);
+            f1 = f2;
+            f2 = f3;
+#pragma unroll
+            for (int k = 0; k < 6; ++k) D1[k] = D2[k];
+        }
     }
 }
 
@@ -2568,12 +2623,15 @@ void launch_ipv4(uint8_t* pkts, const uint64_t* off, const uint32_t* plen, uint6
     if (sh == 8 || sh == 9) {
         // 64 packets per wave tile; chosen automatically, at least 4096 tiles where
         // the batch allows (16 waves per CU; profiles/r02_wire_lb_small_batches.jsonl)
-        uint32_t spw = 64;
+        // (a forced unroll u caps the tile at 64 / u packets — tile-size sweeps)
+        uint32_t spw = tu.unroll ? 64u / (uint32_t)tu.unroll : 64u;
         if (auto_shape)
             while (spw > 1 && (n + spw - 1) / spw < 4096u) spw >>= 1;
         // one tile per wave by default (4M packed 84-B packets 0.116 -> 0.112 ms
-        // against 8192 blocks; profiles/r02_lb_grid_sweep.jsonl)
-        const dim3 grid(grid_for((n + spw - 1) / spw, tu.max_blocks > 0 ? tu.max_blocks : 1 << 24));
+        // against 8192 blocks; profiles/r02_lb_grid_sweep.jsonl); the prefetching loop of
+        // measurement variant 4 wants several tiles per wave: 1536 workgroups
+        const int lb_blocks = (TCPCSUM_LB_VARIANT & 4) ? 1536 : 1 << 24;
+        const dim3 grid(grid_for((n + spw - 1) / spw, tu.max_blocks > 0 ? tu.max_blocks : lb_blocks));
         if (sh == 8 && plen)
             hipLaunchKernelGGL((k_ipv4_lb<4, true>), grid, dim3(256), 0, s, pkts, off, plen, n, cap, limit, mode, out,
                                status, ipout, spw);
