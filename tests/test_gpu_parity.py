@@ -138,10 +138,13 @@ def test_split_segments_round_edges(dev, shape):
                         assert np.array_equal(got, want), (unroll, max_blocks, length, off)
     finally:
         tcp_amd.set_tuning(0, 0, -1, 0)
-    # the default plan takes the split for aligned long segments and matches too
-    assert tcp_amd.api.plan_uniform(0, 65536, 65536, 64)[1] == 13
-    got = u16(tcp_amd.batch_uniform(d, 65536, 65536, 64, 7))
-    assert np.array_equal(got, oracle.batch_uniform(host, 65536, 65536, 64, 7))
+    # the default plan takes the split for aligned segments up to 32 KiB, a workgroup per segment
+    # past that up to 128 KiB, and matches too
+    for length, shape in ((16384, 13), (32768, 13), (32772, 14), (65536, 14), (131072, 14)):
+        n = ((6 << 20) - 64) // length
+        assert tcp_amd.api.plan_uniform(0, length, length, n)[1] == shape, length
+        got = u16(tcp_amd.batch_uniform(d, length, length, n, 7))
+        assert np.array_equal(got, oracle.batch_uniform(host, length, length, n, 7)), length
 
 
 def test_two_fold_semantics_above_4g(dev):

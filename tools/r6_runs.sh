@@ -69,7 +69,7 @@ PY
 # rocprofv3 kernel trace + stats of the driver's bench command
 prof() {
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o bench -- \
-    python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-host-path --no-cpu-baseline \
+    python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-host-path --no-cpu-baseline --no-seam \
     > $O/bench_under_rocprof.json 2> $O/rocprof.err; local rc=$?
   tail -3 $O/rocprof.err; return $rc
 }
@@ -81,6 +81,33 @@ pmc() {
   timeout -s KILL 180 rocprofv3 --pmc $ctr --output-format csv -d $O/pmc_$tag -o pmc -- python3 "$@" \
     > $O/pmc_$tag.out 2> $O/pmc_$tag.err; local rc=$?
   tail -2 $O/pmc_$tag.err; return $rc
+}
+
+# bench.py at N ranks on this one GPU (TCPCSUM_BENCH_SHARE_DEVICE=1): the launcher, barriers,
+# every rank's shard digest, per-rank throttling and copy-thread budget — not the scaling
+shared() {
+  local n=${1:-8}
+  TCPCSUM_BENCH_SHARE_DEVICE=1 timeout -k 10 900 python3 -u bench.py --gpus $n --steps ${2:-20} --warmup 3 \
+    > $O/bench_n${n}_shared.json 2> $O/bench_n${n}_shared.err; local rc=$?
+  tail -c 400 $O/bench_n${n}_shared.err
+  python3 tools/bench_summary.py $O/bench_n${n}_shared.json
+  return $rc
+}
+
+# the round's one closing rehearsal, the driver's own commands: every GPU test, smoke(), the
+# bench as the driver runs it, then the same bench under rocprofv3 --kernel-trace --stats, and
+# the PMC passes (FETCH_SIZE of the headline; WRITE_SIZE / FETCH_SIZE of the wire FILL), each
+# pass its own run
+final() {
+  tests || return $?
+  smoke || return $?
+  bench || return $?
+  prof || return $?
+  python3 tools/trace_runs.py $O/prof/bench_kernel_trace.csv > $O/trace_runs.jsonl
+  PTAG=fetch_headline pmc FETCH_SIZE bench.py --gpus 1 --steps 20 --warmup 5 --no-other-configs --no-host-path \
+    --no-cpu-baseline --no-seam || return $?
+  PTAG=write_wire pmc WRITE_SIZE tools/wire_fill_pmc.py || return $?
+  PTAG=fetch_wire pmc FETCH_SIZE tools/wire_fill_pmc.py || return $?
 }
 
 # run the chained functions: f1 args -- f2 args -- ...

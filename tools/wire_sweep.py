@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--tot", type=int, default=1500)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--mix", action="store_true", help="bench.py's wire_mix workload (the flush mix) instead")
     ap.add_argument("variants", nargs="+")
     args = ap.parse_args()
     import numpy as np
@@ -32,18 +33,24 @@ def main():
     tcp_len = tot - 20
     payload = torch.empty(1 << 26, dtype=torch.uint8, device=dev)
     tcp_amd.synth_fill(payload, 0, payload.numel())
-    segs = np.zeros(n, tcp_amd.TXSEG_DTYPE)
-    segs["payload_off"] = (np.arange(n, dtype=np.uint64) * 4096) % np.uint64(payload.numel() - 65536)
-    segs["out_off"] = np.arange(n, dtype=np.uint64) * slot
-    segs["saddr_be"] = 0x0100007F
-    segs["daddr_be"] = np.arange(n, dtype=np.uint32)
-    segs["sport"], segs["dport"], segs["len"], segs["flags"] = 4000, 45001, tcp_len - 24, 1 | 16
-    reg = torch.zeros(n * slot, dtype=torch.uint8, device=dev)
+    if args.mix:
+        import bench
+        segs, region = bench.wire_mix_segments(n)
+        slot = 1500   # the cap
+    else:
+        segs = np.zeros(n, tcp_amd.TXSEG_DTYPE)
+        segs["payload_off"] = (np.arange(n, dtype=np.uint64) * 4096) % np.uint64(payload.numel() - 65536)
+        segs["out_off"] = np.arange(n, dtype=np.uint64) * slot
+        segs["saddr_be"] = 0x0100007F
+        segs["daddr_be"] = np.arange(n, dtype=np.uint32)
+        segs["sport"], segs["dport"], segs["len"], segs["flags"] = 4000, 45001, tcp_len - 24, 1 | 16
+        region = n * slot
+    reg = torch.zeros(region, dtype=torch.uint8, device=dev)
     built = torch.empty(n, dtype=torch.int16, device=dev)
     dsegs = torch.from_numpy(segs.view(np.uint8)).to(dev)
-    tcp_amd.tx_build(payload, dsegs, n, tcp_len, reg, 0, built)
+    tcp_amd.tx_build(payload, dsegs, n, 1456, reg, 0, built)
     del dsegs, payload
-    doff = torch.from_numpy((np.arange(n, dtype=np.uint64) * slot).view(np.int64)).to(dev)
+    doff = torch.from_numpy(segs["out_off"].astype(np.uint64).view(np.int64)).to(dev)
     out = torch.empty(n, dtype=torch.int16, device=dev)
     sta = torch.empty(n, dtype=torch.uint8, device=dev)
     st = torch.cuda.current_stream()
@@ -71,7 +78,7 @@ def main():
                 torch.cuda.synchronize()
                 times[(v, name)].append(e0.elapsed_time(e1) / args.steps)
     for (v, name), ts in times.items():
-        print(json.dumps({"n": n, "slot": slot, "max_blocks": v[0], "unroll": v[1], "shape": v[2], "mode": name,
+        print(json.dumps({"n": n, "workload": "flush_mix" if args.mix else f"slots{slot}", "max_blocks": v[0], "unroll": v[1], "shape": v[2], "mode": name,
                           "med_ms": round(statistics.median(ts), 5), "min_ms": round(min(ts), 5),
                           "ok": ok[(v, name)]}), flush=True)
 
