@@ -126,8 +126,7 @@ const char* tcpcsum_build_info(void) {
         ", \"TCPCSUM_UNIFORM_WPB\": " TCPCSUM_STR(TCPCSUM_UNIFORM_WPB)
         ", \"TCPCSUM_DESC_LB_WAVES\": " TCPCSUM_STR(TCPCSUM_DESC_LB_WAVES)
         ", \"TCPCSUM_SS_LOAD\": " TCPCSUM_STR(TCPCSUM_SS_LOAD)
-        ", \"TCPCSUM_LB_VARIANT\": " TCPCSUM_STR(TCPCSUM_LB_VARIANT)
-        ", \"TCPCSUM_LB_CHK\": " TCPCSUM_STR(TCPCSUM_LB_CHK) "}"
+        ", \"TCPCSUM_LB_VARIANT\": " TCPCSUM_STR(TCPCSUM_LB_VARIANT) "}"
         ", \"runtime_knobs\": [" TCPCSUM_RUNTIME_KNOBS_JSON "]}";
     return info;
 }

@@ -855,13 +855,9 @@ __device__ __forceinline__ uint32_t lb_owner(uint32_t W0, uint32_t P, uint32_t n
 // TCPCSUM_LB_VARIANT bit 0: owner search 1 (lb_owner); bit 1: software-pipelined rounds — the
 // owner search and the loads of round r + 1 are issued before round r is summed (two LbRound
 // register sets), so a round's loads no longer wait for the previous round's scans and atomics.
-// accC (nullable): the wire FILL's check words — the segment-relative bytes [16, 18) of
-// every segment, taken from the register that swept them (chunk 1 of the segment's hull),
-// so the FILL needs no load of its own after the sweep; 0xFFFFFFFF where the word
-// straddles into chunk 2 (a hull starting at byte 15 of a chunk: the FILL loads it).
 template <int C, bool A4>
 __device__ __forceinline__ void lb_sums_t(const uint8_t* a, uint32_t len, uint32_t hole, bool want_odd,
-                                          uint64_t* accW, uint64_t* accO, uint32_t* mark, uint32_t* accC) {
+                                          uint64_t* accW, uint64_t* accO, uint32_t* mark) {
     constexpr int OWNER = TCPCSUM_LB_VARIANT & 1;
     constexpr bool PIPE = (TCPCSUM_LB_VARIANT & 2) != 0;
     const uint32_t lane = threadIdx.x & 63;
@@ -875,7 +871,6 @@ __device__ __forceinline__ void lb_sums_t(const uint8_t* a, uint32_t len, uint32
     const uint32_t a_lo = (uint32_t)a0, a_hi = (uint32_t)(a0 >> 32);
     accW[lane] = 0;
     if (want_odd) accO[lane] = 0;
-    if (accC) ((volatile uint32_t*)accC)[lane] = 0xFFFFFFFFu;
     uint32_t carry = 0;   // segment owning the next window's first chunk
     auto issue = [&](LbRound<C>& r, uint32_t R) {
 #pragma unroll
@@ -917,13 +912,6 @@ __device__ __forceinline__ void lb_sums_t(const uint8_t* a, uint32_t len, uint32
             }
             end[k] = g < T && (r.pc[k] + 1u == no || lane == 63u || g + 1u == T);
             sr[k] = r.po[k] > W0 ? r.po[k] - W0 : 0u;   // the run's first lane in this window
-            if (accC && r.pc[k] == 1u && g < T && mo <= 14u) {   // bytes [mo, mo + 2) of chunk 1
-                const u32x4 x = r.v[k];
-                const uint32_t q = mo >> 2;
-                const uint32_t lo = q == 0 ? x.x : q == 1 ? x.y : q == 2 ? x.z : x.w;
-                const uint32_t hi = q == 0 ? x.y : q == 1 ? x.z : q == 2 ? x.w : 0u;
-                ((volatile uint32_t*)accC)[r.own[k]] = __builtin_amdgcn_alignbyte(hi, lo, mo & 3u) & 0xffffu;
-            }
         }
         // the C windows' scans interleaved (their DPP steps fill each other's wait states)
         wave_scan_incl_n<C>(w);
@@ -968,12 +956,12 @@ __device__ __forceinline__ void lb_sums_t(const uint8_t* a, uint32_t len, uint32
 
 template <int C>
 __device__ __forceinline__ void lb_sums(const uint8_t* a, uint32_t len, uint32_t hole, bool want_odd,
-                                        uint64_t* accW, uint64_t* accO, uint32_t* mark, uint32_t* accC = nullptr) {
+                                        uint64_t* accW, uint64_t* accO, uint32_t* mark) {
     const bool a4 = __ballot(len != 0 && (((uint32_t)(uintptr_t)a | len) & 3u) != 0) == 0 && hole == kNoHole;
     if (a4)
-        lb_sums_t<C, true>(a, len, hole, want_odd, accW, accO, mark, accC);
+        lb_sums_t<C, true>(a, len, hole, want_odd, accW, accO, mark);
     else
-        lb_sums_t<C, false>(a, len, hole, want_odd, accW, accO, mark, accC);
+        lb_sums_t<C, false>(a, len, hole, want_odd, accW, accO, mark);
 }
 
 // One segment summed by the whole wave (wave-uniform a, len): 64 chunks per
@@ -1535,7 +1523,6 @@ __global__ __launch_bounds__(256) void k_ipv4_lb(uint8_t* __restrict__ pkts, con
     // spw: packets per wave tile (1..64; lanes >= spw hold none), as in k_desc_lb
     __shared__ uint64_t acc[4][2][64];
     __shared__ uint32_t marks[(TCPCSUM_LB_VARIANT & 1) ? 4 : 1][64];
-    __shared__ uint32_t chk[TCPCSUM_LB_CHK ? 4 : 1][64];   // the FILL's check words (lb_sums_t)
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     uint32_t* mark = marks[(TCPCSUM_LB_VARIANT & 1) ? wv : 0];
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
@@ -1602,8 +1589,7 @@ __global__ __launch_bounds__(256) void k_ipv4_lb(uint8_t* __restrict__ pkts, con
         uint8_t* tcp = ip + th;
         const bool odd = ((uintptr_t)ip & 1u) != 0;   // th is even
         const bool any_odd = __ballot(ok && odd) != 0;
-        uint32_t* cw_lds = (TCPCSUM_LB_CHK && !verify) ? chk[TCPCSUM_LB_CHK ? wv : 0] : nullptr;
-        lb_sums<C>(tcp, len, kNoHole, any_odd, acc[wv][0], acc[wv][1], mark, cw_lds);
+        lb_sums<C>(tcp, len, kNoHole, any_odd, acc[wv][0], acc[wv][1], mark);
         if (!live) return;
         if (!ok) {
             if (out) out[i] = 0;
@@ -1616,11 +1602,9 @@ __global__ __launch_bounds__(256) void k_ipv4_lb(uint8_t* __restrict__ pkts, con
         uint64_t S = combine(ps, acc[wv][0][lane], any_odd ? acc[wv][1][lane] : 0, odd);
         // FILL sums with the check as zero (context.c:182): TCP+16 is an even offset,
         // so its native word (L2-hot: just summed) contributes exactly its value
-        if (!verify) {
-            uint32_t cw = cw_lds ? ((volatile uint32_t*)cw_lds)[lane] : 0xFFFFFFFFu;
-            if (cw > 0xffffu) cw = (uint32_t)ldg<uint8_t>(tcp + 16) | ((uint32_t)ldg<uint8_t>(tcp + 17) << 8);
-            S -= cw;
-        }
+        // (taking it from the sweep's registers instead, via LDS, measured slower: flush mix
+        // FILL 0.1163 vs 0.1001 ms, VERIFY too, profiles/r06_wire_lb_chk_ab.jsonl)
+        if (!verify) S -= (uint32_t)ldg<uint8_t>(tcp + 16) | ((uint32_t)ldg<uint8_t>(tcp + 17) << 8);
         const uint16_t c = fold_ref(S);
         uint32_t st = TCPCSUM_PKT_OK;
         if (verify && c != 0) {   // rare: was the check left as the bare pseudo-header sum?
