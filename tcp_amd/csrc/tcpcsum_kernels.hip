@@ -954,14 +954,32 @@ __device__ __forceinline__ void lb_sums_t(const uint8_t* a, uint32_t len, uint32
     __builtin_amdgcn_wave_barrier();
 }
 
+// Every segment of the tile starting 4-B aligned (TCP segments of packets in malloc'd or
+// 16-B packed buffers: TCP at ip + 20): the sweep takes the dword-granular A4 path over each
+// segment's first len & ~3 bytes, and its last len & 3 bytes (at an even offset: low bytes
+// of their words) come from one aligned dword per segment, loaded before the sweep. The
+// byte-granular masks of the A4 = false path cost ~45 VALU per 1 KiB window: the flush mix
+// VERIFY ran at 133 VALU instructions per KiB (rocprofv3 SQ_INSTS_VALU,
+// profiles/r06_wire_mix_pmc.json).
 template <int C>
 __device__ __forceinline__ void lb_sums(const uint8_t* a, uint32_t len, uint32_t hole, bool want_odd,
                                         uint64_t* accW, uint64_t* accO, uint32_t* mark) {
-    const bool a4 = __ballot(len != 0 && (((uint32_t)(uintptr_t)a | len) & 3u) != 0) == 0 && hole == kNoHole;
-    if (a4)
+    const bool a4 = __ballot(len != 0 && ((uint32_t)(uintptr_t)a & 3u) != 0) == 0 && hole == kNoHole;
+    if (a4 && __ballot((len & 3u) != 0) == 0) {   // lengths too: nothing left over
         lb_sums_t<C, true>(a, len, hole, want_odd, accW, accO, mark);
-    else
+    } else if (a4) {
+        const uint32_t body = len & ~3u, tail = len & 3u;
+        // the dword holding the tail bytes: inside the segment's last aligned dword, so on a
+        // page the segment is on
+        const uint32_t td = ldg<uint32_t>(zsel(tail != 0u, a + body));
+        lb_sums_t<C, true>(a, body, hole, want_odd, accW, accO, mark);
+        if (tail)
+            atomicAdd(reinterpret_cast<unsigned long long*>(accW + (threadIdx.x & 63)),
+                      (unsigned long long)sad16(td & ((1u << (8u * tail)) - 1u), 0u));
+        __builtin_amdgcn_wave_barrier();
+    } else {
         lb_sums_t<C, false>(a, len, hole, want_odd, accW, accO, mark);
+    }
 }
 
 // One segment summed by the whole wave (wave-uniform a, len): 64 chunks per

@@ -82,14 +82,16 @@ def main():
     # ragged descriptor batches
     rng = np.random.default_rng(5)
     for name, lo, hi in (("desc_imix_40_1500", 40, 1500), ("desc_mtu_1400_1500", 1400, 1500),
-                         ("desc_small_40_200", 40, 200)):
+                         ("desc_small_40_200", 40, 200), ("desc_imix_a16_40_1500", 40, 1500)):
         if only and name not in only.split(","):
             continue
         lens = rng.integers(lo, hi + 1, 1 << 22).astype(np.uint32)
-        total = np.cumsum(lens.astype(np.uint64))
+        # a16: every segment starting 16-B aligned (packets in malloc'd / 16-B packed buffers)
+        span = (lens.astype(np.uint64) + 15) // 16 * 16 if "_a16_" in name else lens.astype(np.uint64)
+        total = np.cumsum(span)
         m = int(np.searchsorted(total, 1572864000))
         lens = lens[:m]
-        offs = np.concatenate([[0], np.cumsum(lens.astype(np.uint64))[:-1]]).astype(np.uint64)
+        offs = np.concatenate([[0], np.cumsum(span[:m])[:-1]]).astype(np.uint64)
         data = torch.empty(int(offs[-1] + lens[-1]) + 64, dtype=torch.uint8, device=dev)
         tcp_amd.synth_fill(data, 0, data.numel())
         d = np.zeros(m, tcp_amd.DESC_DTYPE)
