@@ -779,26 +779,6 @@ __device__ __forceinline__ void chunk_masked(u32x4 v, int32_t rel, int32_t len, 
     }
 }
 
-// Per-lane segment [a, a + len) (len <= 1 MiB: the chunk space stays < 2^32),
-// hole (the same segment-relative offset for every segment, kNoHole: none) as
-// above. On return accW[lane] / accO[lane] hold the lane's segment sums W and O
-// (O only when want_odd, wave-uniform). acc: the wave's 2 x 64 u64 LDS slots.
-// A4: every segment of the tile 4-B aligned in start and length (packed
-// IPv4/TCP packets of 4-B multiples, IMIX) — dword-granular masks, no byte
-// masks. A template parameter, not a branch in the sweep: a branch there joins
-// after the masks, and the join waits for every load of the round.
-// Inclusive max-scan over the 64 lanes (values >= 0; 0 where nothing came before), DPP as
-// wave_scan_incl.
-__device__ __forceinline__ uint32_t wave_max_scan_incl(uint32_t x) {
-    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false));   // row_shr:1
-    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false));   // row_shr:2
-    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false));   // row_shr:4
-    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false));   // row_shr:8
-    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false));   // row_bcast:15
-    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false));   // row_bcast:31
-    return x;
-}
-
 // One round of the balanced sweep: for each of its C windows of 64 chunks, every lane's owner
 // segment, the owner's first chunk, the chunk's index in the owner's hull, and the chunk itself
 // (its load issued here, consumed by lb_consume).
@@ -808,57 +788,54 @@ struct LbRound {
     u32x4 v[C];
 };
 
-// The owner search of window [W0, W0 + 64). LB_OWNER 0: a scalar loop over the segments that
-// start in the window (a ballot), one readlane each; 1: the starting lanes mark their first
-// chunk's lane in a per-wave LDS row (ids + 1, zero elsewhere) and a max-scan carries each id
-// to the lanes after it — no loop, whatever the number of starts (small packets: ~20 per window).
-template <int OWNER>
-__device__ __forceinline__ uint32_t lb_owner(uint32_t W0, uint32_t P, uint32_t nj, uint32_t lane, uint32_t& carry,
-                                             uint32_t* mark) {
-    uint32_t o;
-    if constexpr (OWNER == 0) {
-        // segments starting inside [W0, W0 + 64), in lane (= start) order
-        uint64_t M = __ballot(nj != 0 && P - W0 < 64u && P >= W0);
-        o = carry;
-        while (M) {
-            const int j = __builtin_ctzll(M);
-            M &= M - 1;
-            const uint32_t st = (uint32_t)__builtin_amdgcn_readlane((int)P, j) - W0;
-            o = lane >= st ? (uint32_t)j : o;
-        }
-    } else {
-        // one wave's LDS row: clear, mark, read. Other lanes' writes are read back, so the
-        // accesses are volatile (never forwarded from this lane's own store) and a wave
-        // barrier orders them
-        volatile uint32_t* vm = mark;
-        vm[lane] = 0u;
-        __builtin_amdgcn_wave_barrier();
-        if (nj != 0 && P - W0 < 64u && P >= W0) vm[P - W0] = lane + 1u;
-        __builtin_amdgcn_wave_barrier();
-        const uint32_t m = wave_max_scan_incl(vm[lane]);
-        __builtin_amdgcn_wave_barrier();
-        o = m ? m - 1u : carry;
+// The owner search of window [W0, W0 + 64): a scalar loop over the segments that start in the
+// window (a ballot), one readlane each — ~12 instructions per start, most of them scalar.
+__device__ __forceinline__ uint32_t lb_owner_loop(uint32_t W0, uint32_t P, uint32_t nj, uint32_t lane,
+                                                  uint32_t& carry) {
+    // segments starting inside [W0, W0 + 64), in lane (= start) order
+    uint64_t M = __ballot(nj != 0 && P - W0 < 64u && P >= W0);
+    uint32_t o = carry;
+    while (M) {
+        const int j = __builtin_ctzll(M);
+        M &= M - 1;
+        const uint32_t st = (uint32_t)__builtin_amdgcn_readlane((int)P, j) - W0;
+        o = lane >= st ? (uint32_t)j : o;
     }
     carry = (uint32_t)__builtin_amdgcn_readlane((int)o, 63);
     return o;
+}
+
+// The loop-free owner search (measurement variant, TCPCSUM_LB_VARIANT bit 0): once per tile the
+// segments' first chunks are marked in a per-wave LDS bitmap over the chunk space (T <= 8192
+// bits) and a permute makes `inv`: rank among the non-empty segments -> lane. Per window one
+// broadcast LDS read gives the 64 start bits S; chunk W0 + l belongs to the segment of rank
+// base + popcount(S & bits [0, l]) - 1 (base: starts in the windows before), found by one
+// bpermute. No loop, whatever the number of starts (small packets: ~20 per window).
+__device__ __forceinline__ uint32_t lb_owner_bitmap(uint32_t W0, uint32_t lane, uint32_t inv, uint32_t& base,
+                                                    const uint32_t* bm) {
+    const uint64_t S = *(const volatile uint64_t*)(bm + (W0 >> 5));   // W0 % 64 == 0: 8-B aligned
+    const uint64_t pre = S & ((2ull << lane) - 1ull);                  // lane 63: every bit
+    const uint32_t rank = base + (uint32_t)__builtin_popcountll(pre) - 1u;
+    base += (uint32_t)__builtin_popcountll(S);
+    return bperm(inv, rank);
 }
 
 // Per-lane segment [a, a + len) (len <= 1 MiB: the chunk space stays < 2^32),
 // hole (the same segment-relative offset for every segment, kNoHole: none) as
 // above. On return accW[lane] / accO[lane] hold the lane's segment sums W and O
 // (O only when want_odd, wave-uniform). acc: the wave's 2 x 64 u64 LDS slots;
-// mark: its 64 u32 LDS slots (owner search 1).
+// mark: its 256 u32 LDS slots (the bitmap owner search).
 // A4: every segment of the tile 4-B aligned in start and length (packed
 // IPv4/TCP packets of 4-B multiples, IMIX) — dword-granular masks, no byte
 // masks. A template parameter, not a branch in the sweep: a branch there joins
 // after the masks, and the join waits for every load of the round.
-// TCPCSUM_LB_VARIANT bit 0: owner search 1 (lb_owner); bit 1: software-pipelined rounds — the
+// TCPCSUM_LB_VARIANT bit 0: the bitmap owner search; bit 1: software-pipelined rounds — the
 // owner search and the loads of round r + 1 are issued before round r is summed (two LbRound
 // register sets), so a round's loads no longer wait for the previous round's scans and atomics.
 template <int C, bool A4>
 __device__ __forceinline__ void lb_sums_t(const uint8_t* a, uint32_t len, uint32_t hole, bool want_odd,
                                           uint64_t* accW, uint64_t* accO, uint32_t* mark) {
-    constexpr int OWNER = TCPCSUM_LB_VARIANT & 1;
+    constexpr bool BITMAP = (TCPCSUM_LB_VARIANT & 1) != 0;
     constexpr bool PIPE = (TCPCSUM_LB_VARIANT & 2) != 0;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t m = (uint32_t)((uintptr_t)a & 15u);
@@ -871,13 +848,30 @@ __device__ __forceinline__ void lb_sums_t(const uint8_t* a, uint32_t len, uint32
     const uint32_t a_lo = (uint32_t)a0, a_hi = (uint32_t)(a0 >> 32);
     accW[lane] = 0;
     if (want_odd) accO[lane] = 0;
-    uint32_t carry = 0;   // segment owning the next window's first chunk
+    uint32_t carry = 0;   // segment owning the next window's first chunk (loop search)
+    uint32_t base = 0, inv = 0;   // bitmap search
+    const bool bitmap = BITMAP && T <= 8192u;
+    if (bitmap) {
+        volatile uint32_t* bm = mark;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) bm[lane * 4u + q] = 0u;
+        __builtin_amdgcn_wave_barrier();
+        if (nj != 0) atomicOr(mark + (P >> 5), 1u << (P & 31u));
+        __builtin_amdgcn_wave_barrier();
+        const uint64_t NZ = __ballot(nj != 0);
+        const uint32_t below =
+            __builtin_amdgcn_mbcnt_hi((uint32_t)(NZ >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)NZ, 0u));
+        const uint32_t K = (uint32_t)__builtin_popcountll(NZ);
+        // a permutation: non-empty segments to their ranks, empty ones after them
+        const uint32_t dest = nj != 0 ? below : K + (lane - below);
+        inv = (uint32_t)__builtin_amdgcn_ds_permute((int)(dest << 2), (int)lane);
+    }
     auto issue = [&](LbRound<C>& r, uint32_t R) {
 #pragma unroll
         for (int k = 0; k < C; ++k) {
             const uint32_t W0 = R + 64u * k;
             const uint32_t g = W0 + lane;
-            const uint32_t o = lb_owner<OWNER>(W0, P, nj, lane, carry, mark);
+            const uint32_t o = bitmap ? lb_owner_bitmap(W0, lane, inv, base, mark) : lb_owner_loop(W0, P, nj, lane, carry);
             r.own[k] = o;
             r.po[k] = bperm(P, o);
             r.pc[k] = g - r.po[k];   // chunk index inside the owner's hull
@@ -1016,7 +1010,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TCPCSUM_DES
     // spw: segments per wave tile (1..64; lanes >= spw hold no segment) — fewer
     // for long segments, so a batch of them still spreads over enough waves
     __shared__ uint64_t acc[4][2][64];
-    __shared__ uint32_t marks[(TCPCSUM_LB_VARIANT & 1) ? 4 : 1][64];
+    __shared__ __attribute__((aligned(8))) uint32_t marks[(TCPCSUM_LB_VARIANT & 1) ? 4 : 1][(TCPCSUM_LB_VARIANT & 1) ? 256 : 2];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     uint32_t* mark = marks[(TCPCSUM_LB_VARIANT & 1) ? wv : 0];
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
@@ -1540,7 +1534,7 @@ __global__ __launch_bounds__(256) void k_ipv4_lb(uint8_t* __restrict__ pkts, con
                                                  uint16_t* __restrict__ ipout, uint32_t spw) {
     // spw: packets per wave tile (1..64; lanes >= spw hold none), as in k_desc_lb
     __shared__ uint64_t acc[4][2][64];
-    __shared__ uint32_t marks[(TCPCSUM_LB_VARIANT & 1) ? 4 : 1][64];
+    __shared__ __attribute__((aligned(8))) uint32_t marks[(TCPCSUM_LB_VARIANT & 1) ? 4 : 1][(TCPCSUM_LB_VARIANT & 1) ? 256 : 2];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     uint32_t* mark = marks[(TCPCSUM_LB_VARIANT & 1) ? wv : 0];
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
