@@ -532,7 +532,8 @@ def run_wire_mix(steps: int, warmup: int, device) -> dict:
     n = 1 << 20
     segs, region = wire_mix_segments(n)
     reg, doff, built, tcp_bytes = build_wire(segs, region, 1456, device)
-    ctl = int((segs["len"] == 0).sum())
+    import tcp_amd
+    ctl = int(((segs["flags"] & tcp_amd.api.TXF_DATA) == 0).sum())
     res = {"workload": (f"1M IPv4/TCP packets as releaseSend flushes them: {ctl} 44-B control segments (pure ACK, "
                         f"SYN-ACK, FIN-ACK) and {n - ctl} data segments of 0-1456-B payload, packed 16-B aligned "
                         f"({region / 1e6:.1f} MB, mean {region / n:.0f} B per packet), checks filled / verified "
