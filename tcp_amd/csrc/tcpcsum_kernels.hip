@@ -871,7 +871,11 @@ __device__ __forceinline__ void lb_sums_t(const uint8_t* a, uint32_t len, uint32
         for (int k = 0; k < C; ++k) {
             const uint32_t W0 = R + 64u * k;
             const uint32_t g = W0 + lane;
+#if TCPCSUM_LB_VARIANT & 8   // knock-out (results WRONG): no owner search, what it costs
+            const uint32_t o = carry;
+#else
             const uint32_t o = bitmap ? lb_owner_bitmap(W0, lane, inv, base, mark) : lb_owner_loop(W0, P, nj, lane, carry);
+#endif
             r.own[k] = o;
             r.po[k] = bperm(P, o);
             r.pc[k] = g - r.po[k];   // chunk index inside the owner's hull
