@@ -61,8 +61,8 @@
 #ifndef TCPCSUM_UNIFORM_WPB
 #define TCPCSUM_UNIFORM_WPB 4
 #endif
-//   TCPCSUM_DESC_LB_WAVES    minimum waves per SIMD asked of the balanced ragged kernel
-//                            (amdgpu_waves_per_eu): 1 = the compiler's choice (the product's)
+//   TCPCSUM_DESC_LB_WAVES    minimum waves per SIMD asked of the balanced kernels (ragged and
+//                            wire; amdgpu_waves_per_eu): 1 = the compiler's choice (the product's)
 #ifndef TCPCSUM_DESC_LB_WAVES
 #define TCPCSUM_DESC_LB_WAVES 1
 #endif

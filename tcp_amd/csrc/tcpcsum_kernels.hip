@@ -1531,7 +1531,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(wire_waves(
 // does). The IPv4 header checksum (IPHDR) is summed per lane from the
 // header dwords: relative dwords, so its u16 halves are the reference's words.
 template <int C, bool PL>
-__global__ __launch_bounds__(256) void k_ipv4_lb(uint8_t* __restrict__ pkts, const uint64_t* __restrict__ off,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TCPCSUM_DESC_LB_WAVES, 8))) void k_ipv4_lb(uint8_t* __restrict__ pkts, const uint64_t* __restrict__ off,
                                                  const uint32_t* __restrict__ plen,
                                                  uint64_t n, uint32_t cap, uint64_t limit, int mode,
                                                  uint16_t* __restrict__ out, uint8_t* __restrict__ status,
