@@ -96,18 +96,24 @@ shared() {
 
 # the round's one closing rehearsal, the driver's own commands: every GPU test, smoke(), the
 # bench as the driver runs it, then the same bench under rocprofv3 --kernel-trace --stats, and
-# the PMC passes (FETCH_SIZE of the headline; WRITE_SIZE / FETCH_SIZE of the wire FILL), each
-# pass its own run
+# the PMC passes, each its own run: FETCH_SIZE of the headline, 64 KiB and 64-B configs (the
+# probe in each pass calibrates it), FETCH_SIZE / WRITE_SIZE of the wire FILL / VERIFY on MTU
+# packets and on the flush mix
 final() {
   tests || return $?
   smoke || return $?
   bench || return $?
   prof || return $?
   python3 tools/trace_runs.py $O/prof/bench_kernel_trace.csv > $O/trace_runs.jsonl
-  PTAG=fetch_headline pmc FETCH_SIZE bench.py --gpus 1 --steps 20 --warmup 5 --no-other-configs --no-host-path \
-    --no-cpu-baseline --no-seam || return $?
+  local common="--gpus 1 --warmup 5 --no-other-configs --no-host-path --no-cpu-baseline --no-seam"
+  PTAG=fetch_1500 pmc FETCH_SIZE bench.py --steps 20 $common || return $?
+  PTAG=fetch_64k pmc FETCH_SIZE bench.py --config 64k --steps 10 $common || return $?
+  PTAG=fetch_64 pmc FETCH_SIZE bench.py --config 64 --steps 50 $common || return $?
   PTAG=write_wire pmc WRITE_SIZE tools/wire_fill_pmc.py || return $?
   PTAG=fetch_wire pmc FETCH_SIZE tools/wire_fill_pmc.py || return $?
+  PTAG=fetch_mix pmc FETCH_SIZE tools/wire_mix_pmc.py || return $?
+  PTAG=write_mix pmc WRITE_SIZE tools/wire_mix_pmc.py || return $?
+  ls $O/pmc_*/
 }
 
 # run the chained functions: f1 args -- f2 args -- ...
