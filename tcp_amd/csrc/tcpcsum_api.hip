@@ -126,7 +126,8 @@ const char* tcpcsum_build_info(void) {
         ", \"TCPCSUM_UNIFORM_WPB\": " TCPCSUM_STR(TCPCSUM_UNIFORM_WPB)
         ", \"TCPCSUM_DESC_LB_WAVES\": " TCPCSUM_STR(TCPCSUM_DESC_LB_WAVES)
         ", \"TCPCSUM_SS_LOAD\": " TCPCSUM_STR(TCPCSUM_SS_LOAD)
-        ", \"TCPCSUM_LB_VARIANT\": " TCPCSUM_STR(TCPCSUM_LB_VARIANT) "}"
+        ", \"TCPCSUM_LB_VARIANT\": " TCPCSUM_STR(TCPCSUM_LB_VARIANT)
+        ", \"TCPCSUM_LB_HEAD\": " TCPCSUM_STR(TCPCSUM_LB_HEAD) "}"
         ", \"runtime_knobs\": [" TCPCSUM_RUNTIME_KNOBS_JSON "]}";
     return info;
 }

@@ -79,10 +79,17 @@
 #ifndef TCPCSUM_LB_VARIANT
 #define TCPCSUM_LB_VARIANT 0
 #endif
+//   TCPCSUM_LB_HEAD          1: the balanced wire kernel takes 4-B aligned packets' first 64 bytes
+//                            in registers and sweeps only the rest (the product's); 0: it reads
+//                            the header apart and sweeps every TCP byte
+#ifndef TCPCSUM_LB_HEAD
+#define TCPCSUM_LB_HEAD 1
+#endif
 #if !TCPCSUM_MEASUREMENT_BUILD && \
     (TCPCSUM_TUNING_VARIANTS != 0 || TCPCSUM_TX_KNOCKOUT != 0 || TCPCSUM_WIRE_WAVES != 1 || TCPCSUM_TX_WAVES != 1 || \
      TCPCSUM_LINE_CPOL != 17 || TCPCSUM_LOAD_CPOL != -1 || TCPCSUM_XCD_REMAP != 1 || TCPCSUM_XCD_CHUNK != 0 || \
-     TCPCSUM_UNIFORM_WPB != 4 || TCPCSUM_DESC_LB_WAVES != 1 || TCPCSUM_SS_LOAD != 2 || TCPCSUM_LB_VARIANT != 0)
+     TCPCSUM_UNIFORM_WPB != 4 || TCPCSUM_DESC_LB_WAVES != 1 || TCPCSUM_SS_LOAD != 2 || TCPCSUM_LB_VARIANT != 0 || \
+     TCPCSUM_LB_HEAD != 1)
 #error "tuning / knock-out / waves knobs are for measurement builds only (-DTCPCSUM_MEASUREMENT_BUILD=1), never a product library"
 #endif
 // Environment variables a context reads at creation (tcpcsum_build_info "runtime_knobs"):

@@ -1647,12 +1647,99 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TCPCSUM_DES
         if (out) out[i] = c;
         if (status) status[i] = (uint8_t)st;
     };
+    // Tiles whose packets all start 4-B aligned (any real packet buffer), without IPHDR: the
+    // packet's first 64 bytes from its 16-B aligned start come in with four 16-B loads — the
+    // header fields, the first TCP bytes (a 44-B control segment entirely) and the FILL's
+    // check word, all from registers — and only the rest of each segment, from the next 16-B
+    // boundary past those 64 bytes, is swept. The sweep then never re-reads the header's
+    // line (the separate header loads made the flush mix read 1.125 x its region, PMC
+    // FETCH_SIZE, profiles/r06_wire_mix_pmc.json) and a control segment never enters it.
+    auto process_head = [&](uint64_t t, const Off& f) {
+        const uint64_t i = t * spw + (uint64_t)lane;
+        const bool live = (uint32_t)lane < spw && i < n;
+        const uint64_t o = f.o;
+        uint32_t room;
+        const bool hdr = room_of(t, f, room);
+        const uint64_t readable = !hdr ? 0u : PL ? (uint64_t)room : limit - o;
+        uint8_t* ip = PL ? reinterpret_cast<uint8_t*>((uintptr_t)pkts + o) : pkts + o;
+        const uint32_t sh = (uint32_t)((uintptr_t)ip & 15u);   // 0, 4, 8 or 12
+        const uint8_t* al = ip - sh;
+        u32x4 H[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)   // a 16-B chunk holding a readable byte never crosses a page
+            H[k] = ldg<u32x4>(zsel(hdr && 16u * k < sh + readable, al + 16 * k));
+        // dword j (0..15) of the 64 loaded bytes: register selects only
+        auto dw = [&](uint32_t j) {
+            const u32x4 c = j < 4u ? H[0] : j < 8u ? H[1] : j < 12u ? H[2] : H[3];
+            const uint32_t r = j & 3u;
+            return r == 0u ? c.x : r == 1u ? c.y : r == 2u ? c.z : c.w;
+        };
+        const uint32_t q = sh >> 2;
+        const uint32_t h0 = dw(q), h8 = dw(q + 2u), sa = dw(q + 3u), da = dw(q + 4u);
+        const uint32_t ver = (h0 >> 4) & 15u, ihl = h0 & 15u;
+        const uint32_t tot = ((h0 >> 8) & 0xff00u) | (h0 >> 24);
+        const uint32_t proto = (h8 >> 8) & 0xffu;
+        const bool fits = PL ? tot <= room : o + tot <= limit;
+        const bool ok = hdr && ver == 4u && proto == 6u && ihl >= 5u && tot >= ihl * 4u + 20u && tot <= cap && fits;
+        const uint32_t th = ihl * 4u;
+        const uint32_t len = ok ? tot - th : 0u;
+        uint8_t* tcp = ip + th;
+        // the TCP bytes among the 64 loaded: relative dwords [th / 4, in_regs / 4), the last
+        // one cut at tot
+        const uint32_t in_regs = 64u - sh;   // bytes of the packet in H
+        const uint32_t head_end = ok ? (tot < in_regs ? tot : in_regs) : 0u;
+        uint32_t wh = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const uint32_t rel = 4u * (uint32_t)j - sh;   // wraps for dwords before the packet
+            const uint32_t d = j < 4 ? (j == 0 ? H[0].x : j == 1 ? H[0].y : j == 2 ? H[0].z : H[0].w)
+                             : j < 8 ? (j == 4 ? H[1].x : j == 5 ? H[1].y : j == 6 ? H[1].z : H[1].w)
+                             : j < 12 ? (j == 8 ? H[2].x : j == 9 ? H[2].y : j == 10 ? H[2].z : H[2].w)
+                                      : (j == 12 ? H[3].x : j == 13 ? H[3].y : j == 14 ? H[3].z : H[3].w);
+            const uint32_t keep = head_end - rel;   // bytes of this dword before head_end
+            const uint32_t m = keep >= 4u ? 0xffffffffu : (1u << (8u * keep)) - 1u;
+            wh = sad16(rel >= th && rel < head_end ? d & m : 0u, wh);
+        }
+        // the rest of the segment, from the first 16-B boundary past the loaded bytes
+        const uint32_t bstart = th > in_regs ? th : in_regs;
+        const uint32_t blen = ok && tot > bstart ? tot - bstart : 0u;
+        lb_sums<C>(ip + bstart, blen, kNoHole, false, acc[wv][0], acc[wv][1], mark);
+        if (!live) return;
+        if (!ok) {
+            if (out) out[i] = 0;
+            if (status) status[i] = TCPCSUM_PKT_SKIPPED;
+            return;
+        }
+        const uint32_t len_be = ((len & 0xffu) << 8) | ((len >> 8) & 0xffu);   // htons
+        // context.c:104-119 closed form
+        const uint64_t ps = (sa & 0xffffu) + (sa >> 16) + (da & 0xffffu) + (da >> 16) + 0x0600u + len_be;
+        uint64_t S = ps + wh + acc[wv][0][lane];
+        // the check word (TCP+16, an even offset: its native u16), from the registers when
+        // it lies among the loaded bytes
+        const uint32_t cpos = th + 16u;
+        const uint32_t cw = cpos + 2u <= in_regs ? (dw(q + (cpos >> 2)) & 0xffffu)
+                                                 : ((uint32_t)ldg<uint8_t>(tcp + 16) | ((uint32_t)ldg<uint8_t>(tcp + 17) << 8));
+        if (!verify) S -= cw;   // FILL sums with the check as zero (context.c:182)
+        const uint16_t c = fold_ref(S);
+        uint32_t st = TCPCSUM_PKT_OK;
+        if (verify && c != 0 && cw == (uint32_t)(uint16_t)~fold_ref(ps)) st |= TCPCSUM_PKT_CSUM_PARTIAL;
+        if (!verify) store_u16(tcp + 16, c);   // native u16 store, as context.c:208
+        if (out) out[i] = c;
+        if (status) status[i] = (uint8_t)st;
+    };
     // block order: XCD order measured 1 % slower on 2M packed 576-B packets
     // (profiles/r05_xcd_kernels_ab.jsonl)
     uint64_t t = (uint64_t)blockIdx.x * 4u + wv;
     if constexpr ((TCPCSUM_LB_VARIANT & 4) == 0) {
         for (; t < ntiles; t += nwaves) {
             const Off f = load_off(t);
+            const uint64_t i = t * spw + (uint64_t)lane;
+            const bool live = (uint32_t)lane < spw && i < n;
+            const uintptr_t ipa = PL ? (uintptr_t)pkts + f.o : (uintptr_t)(pkts + f.o);
+            if (TCPCSUM_LB_HEAD && !iphdr && __ballot(live && (ipa & 3u) != 0) == 0) {
+                process_head(t, f);
+                continue;
+            }
             uint32_t D[6];
             load_hdr(t, f, D);
             process(t, f, D);

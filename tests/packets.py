@@ -36,11 +36,16 @@ def ip_packet(rng, payload_len, saddr=None, daddr=None, ihl=5, version=4, proto=
     return ip + opts + tcp
 
 
-def build_batch(rng, n, slot=32768, malformed=False, odd_offsets=False, max_payload=1456):
-    """A region of n packets. Returns (region uint8 array, offsets uint64, payload lengths)."""
+def build_batch(rng, n, slot=32768, malformed=False, odd_offsets=False, max_payload=1456, align=0,
+                control_every=0):
+    """A region of n packets. Returns (region uint8 array, offsets uint64, payload lengths).
+    align > 0: packed, every packet starting at a multiple of `align` (plus 0..2 more of it);
+    control_every = k: every k-th packet has no payload (a 44-B control segment)."""
     pkts, lens = [], []
     for i in range(n):
         pl = int(rng.integers(0, max_payload + 1))
+        if control_every and i % control_every == 0:
+            pl = 0
         kind = i % 11 if malformed else 0
         if kind == 3:
             p = ip_packet(rng, pl, version=6)
@@ -61,14 +66,16 @@ def build_batch(rng, n, slot=32768, malformed=False, odd_offsets=False, max_payl
     offs = []
     pos = 0
     for i, p in enumerate(pkts):
-        if odd_offsets:
+        if align:
+            pos = (pos + align - 1) // align * align + align * int(rng.integers(0, 3))
+        elif odd_offsets:
             pos += int(rng.integers(0, 7))
         else:
             pos = i * slot
         offs.append(pos)
-        if odd_offsets:
+        if odd_offsets or align:
             pos += len(p)
-    size = (offs[-1] + len(pkts[-1]) + 64) if odd_offsets else n * slot
+    size = (offs[-1] + len(pkts[-1]) + 64) if (odd_offsets or align) else n * slot
     region = np.zeros(size, np.uint8)
     for o, p in zip(offs, pkts):
         region[o:o + len(p)] = np.frombuffer(p, np.uint8)

@@ -602,6 +602,46 @@ def test_ipv4_forced_shapes(dev, shape):
         region = ref   # VERIFY runs over the filled packets
 
 
+@pytest.mark.parametrize("shape", [8, 9])
+@pytest.mark.parametrize("align", [4, 16])
+def test_ipv4_balanced_head_path(dev, shape, align):
+    """The balanced wire kernel on tiles of 4-B aligned packets — the path that takes each packet's
+    first 64 bytes in registers (header, first TCP bytes, a control segment whole, the FILL's check
+    word) and sweeps only the rest: control segments beside MTU ones, IHL 5..15 (the TCP start and
+    the check word past the 64 bytes), malformed packets, a packet cut by the region end and an
+    offset with no room for a header; FILL then VERIFY for every tile size, against the oracle, the
+    whole region byte-identical. IPHDR batches take the other path and are checked too."""
+    import tcp_amd
+    from tests.packets import build_batch
+    rng = np.random.default_rng(41 + shape + align)
+    region, off, _ = build_batch(rng, 1200, malformed=True, align=align, control_every=2)
+    cut = int(off[-1]) + 30                   # the last packet runs past the region: skipped
+    off = np.concatenate([off, np.array([cut - 10], np.uint64)])  # no room for a header: skipped
+    region = region[:cut].copy()
+    for mode in (tcp_amd.IPV4_FILL, tcp_amd.IPV4_VERIFY, tcp_amd.IPV4_FILL | tcp_amd.IPV4_IPHDR):
+        ref = np.concatenate([region, np.zeros(64, np.uint8)])
+        want_out, want_st = oracle.ipv4_batch(ref, off, 32768, mode)
+        want_st[-2:] = tcp_amd.PKT_SKIPPED
+        want_out[-2:] = 0
+        ref = ref[:cut]
+        # the oracle filled the cut packet from the padding it read past the region: undo that
+        ref[int(off[-2]):] = region[int(off[-2]):]
+        for un in (1, 2, 4):
+            tcp_amd.set_tuning(0, un, shape, 0)
+            try:
+                dreg = to_dev(region, dev)
+                out = torch.empty(off.size, dtype=torch.int16, device=dev)
+                st = torch.empty(off.size, dtype=torch.uint8, device=dev)
+                tcp_amd.ipv4_batch(dreg, to_dev(off.view(np.int64), dev), off.size, 32768, mode, out, st)
+            finally:
+                tcp_amd.set_tuning(0, 0, -1, 0)
+            assert np.array_equal(host(st), want_st), (mode, un)
+            assert np.array_equal(u16(out), want_out), (mode, un)
+            assert np.array_equal(host(dreg), ref), (mode, un)
+        if mode == tcp_amd.IPV4_FILL:
+            region = ref   # VERIFY runs over the filled packets
+
+
 @pytest.mark.parametrize("shape", range(9))
 def test_desc_forced_shapes(dev, shape):
     """Every ragged lane-group shape (tcpcsum.h: ragged 0..6, balanced 7..8) and tile depth is exact
