@@ -79,9 +79,10 @@
 #ifndef TCPCSUM_LB_VARIANT
 #define TCPCSUM_LB_VARIANT 0
 #endif
-//   TCPCSUM_LB_HEAD          1: the balanced wire kernel takes 4-B aligned packets' first 64 bytes
-//                            in registers and sweeps only the rest (the product's); 0: it reads
-//                            the header apart and sweeps every TCP byte
+//   TCPCSUM_LB_HEAD          1: the balanced wire kernel's FILL (without IPHDR) takes 4-B aligned
+//                            packets' first 64 bytes in registers and sweeps only the rest (the
+//                            product's); 2: VERIFY too; 0: neither (header read apart, every TCP
+//                            byte swept)
 #ifndef TCPCSUM_LB_HEAD
 #define TCPCSUM_LB_HEAD 1
 #endif

@@ -1530,7 +1530,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(wire_waves(
 // summed by lb_sums — FILL then subtracts the check word (what zeroing it
 // does). The IPv4 header checksum (IPHDR) is summed per lane from the
 // header dwords: relative dwords, so its u16 halves are the reference's words.
-template <int C, bool PL>
+template <int C, bool PL, bool HD>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TCPCSUM_DESC_LB_WAVES, 8))) void k_ipv4_lb(uint8_t* __restrict__ pkts, const uint64_t* __restrict__ off,
                                                  const uint32_t* __restrict__ plen,
                                                  uint64_t n, uint32_t cap, uint64_t limit, int mode,
@@ -1700,6 +1700,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TCPCSUM_DES
             const uint32_t m = keep >= 4u ? 0xffffffffu : (1u << (8u * keep)) - 1u;
             wh = sad16(rel >= th && rel < head_end ? d & m : 0u, wh);
         }
+        const uint32_t len_be = ((len & 0xffu) << 8) | ((len >> 8) & 0xffu);   // htons
+        // context.c:104-119 closed form
+        const uint32_t ps = (sa & 0xffffu) + (sa >> 16) + (da & 0xffffu) + (da >> 16) + 0x0600u + len_be;
+        // the check word (TCP+16, an even offset: its native u16), from the registers when
+        // it lies among the loaded bytes — taken before the sweep, so that the 64 loaded bytes
+        // are not held across it
+        const uint32_t cpos = th + 16u;
+        const bool cw_in = cpos + 2u <= in_regs;
+        uint32_t cw = dw(q + ((cw_in ? cpos : 0u) >> 2)) & 0xffffu;
         // the rest of the segment, from the first 16-B boundary past the loaded bytes
         const uint32_t bstart = th > in_regs ? th : in_regs;
         const uint32_t blen = ok && tot > bstart ? tot - bstart : 0u;
@@ -1710,15 +1719,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TCPCSUM_DES
             if (status) status[i] = TCPCSUM_PKT_SKIPPED;
             return;
         }
-        const uint32_t len_be = ((len & 0xffu) << 8) | ((len >> 8) & 0xffu);   // htons
-        // context.c:104-119 closed form
-        const uint64_t ps = (sa & 0xffffu) + (sa >> 16) + (da & 0xffffu) + (da >> 16) + 0x0600u + len_be;
-        uint64_t S = ps + wh + acc[wv][0][lane];
-        // the check word (TCP+16, an even offset: its native u16), from the registers when
-        // it lies among the loaded bytes
-        const uint32_t cpos = th + 16u;
-        const uint32_t cw = cpos + 2u <= in_regs ? (dw(q + (cpos >> 2)) & 0xffffu)
-                                                 : ((uint32_t)ldg<uint8_t>(tcp + 16) | ((uint32_t)ldg<uint8_t>(tcp + 17) << 8));
+        if (!cw_in) cw = (uint32_t)ldg<uint8_t>(tcp + 16) | ((uint32_t)ldg<uint8_t>(tcp + 17) << 8);
+        uint64_t S = (uint64_t)ps + wh + acc[wv][0][lane];
         if (!verify) S -= cw;   // FILL sums with the check as zero (context.c:182)
         const uint16_t c = fold_ref(S);
         uint32_t st = TCPCSUM_PKT_OK;
@@ -1736,7 +1738,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TCPCSUM_DES
             const uint64_t i = t * spw + (uint64_t)lane;
             const bool live = (uint32_t)lane < spw && i < n;
             const uintptr_t ipa = PL ? (uintptr_t)pkts + f.o : (uintptr_t)(pkts + f.o);
-            if (TCPCSUM_LB_HEAD && !iphdr && __ballot(live && (ipa & 3u) != 0) == 0) {
+            if (HD && __ballot(live && (ipa & 3u) != 0) == 0) {
                 process_head(t, f);
                 continue;
             }
@@ -2740,18 +2742,24 @@ void launch_ipv4(uint8_t* pkts, const uint64_t* off, const uint32_t* plen, uint6
         // measurement variant 4 wants several tiles per wave: 1536 workgroups
         const int lb_blocks = (TCPCSUM_LB_VARIANT & 4) ? 1536 : 1 << 24;
         const dim3 grid(grid_for((n + spw - 1) / spw, tu.max_blocks > 0 ? tu.max_blocks : lb_blocks));
-        if (sh == 8 && plen)
-            hipLaunchKernelGGL((k_ipv4_lb<4, true>), grid, dim3(256), 0, s, pkts, off, plen, n, cap, limit, mode, out,
-                               status, ipout, spw);
-        else if (sh == 8)
-            hipLaunchKernelGGL((k_ipv4_lb<4, false>), grid, dim3(256), 0, s, pkts, off, plen, n, cap, limit, mode, out,
-                               status, ipout, spw);
-        else if (plen)
-            hipLaunchKernelGGL((k_ipv4_lb<8, true>), grid, dim3(256), 0, s, pkts, off, plen, n, cap, limit, mode, out,
-                               status, ipout, spw);
-        else
-            hipLaunchKernelGGL((k_ipv4_lb<8, false>), grid, dim3(256), 0, s, pkts, off, plen, n, cap, limit, mode, out,
-                               status, ipout, spw);
+        // the head-in-registers path (k_ipv4_lb) is its own instantiation, for FILL without
+        // IPHDR: it needs 86 VGPRs against 78 (5 waves per SIMD, not 6; asked for 6 the
+        // compiler spills) and VERIFY ran slower with it (flush mix VERIFY 0.0851 vs 0.078 ms),
+        // FILL faster (flush mix 0.0928 vs 0.0962, 2M packed 576-B 0.254 vs 0.290;
+        // profiles/r06_lb_head_ab.jsonl)
+        const bool hd = !(mode & TCPCSUM_IPV4_IPHDR) &&
+                        (TCPCSUM_LB_HEAD == 2 || (TCPCSUM_LB_HEAD == 1 && !(mode & TCPCSUM_IPV4_VERIFY)));
+#define TCPCSUM_LB_WIRE(C_, PL_, HD_)                                                                          \
+    hipLaunchKernelGGL((k_ipv4_lb<C_, PL_, HD_>), grid, dim3(256), 0, s, pkts, off, plen, n, cap, limit, mode, out, \
+                       status, ipout, spw)
+        if (sh == 8) {
+            if (plen) { if (hd) TCPCSUM_LB_WIRE(4, true, true); else TCPCSUM_LB_WIRE(4, true, false); }
+            else { if (hd) TCPCSUM_LB_WIRE(4, false, true); else TCPCSUM_LB_WIRE(4, false, false); }
+        } else {
+            if (plen) { if (hd) TCPCSUM_LB_WIRE(8, true, true); else TCPCSUM_LB_WIRE(8, true, false); }
+            else { if (hd) TCPCSUM_LB_WIRE(8, false, true); else TCPCSUM_LB_WIRE(8, false, false); }
+        }
+#undef TCPCSUM_LB_WIRE
         return;
     }
     switch (sh) {

@@ -80,8 +80,9 @@ def main():
         outs = {k: torch.empty(m, dtype=torch.int16, device=dev) for k in libs}
         stas = {k: torch.empty(m, dtype=torch.uint8, device=dev) for k in libs}
 
-        def call(k, mode):
-            rc = libs[k].tcpcsum_ipv4_batch_dev(regs[k].data_ptr(), rb, doff.data_ptr(), m, cap, mode,
+        def call(k, mode, reg=None):
+            reg = regs[k] if reg is None else reg
+            rc = libs[k].tcpcsum_ipv4_batch_dev(reg.data_ptr(), rb, doff.data_ptr(), m, cap, mode,
                                                 outs[k].data_ptr(), stas[k].data_ptr(), h, None)
             assert rc == 0, (k, rc)
 
@@ -97,16 +98,20 @@ def main():
         torch.cuda.synchronize()
         for k in libs:
             same[k] = same[k] and bool((outs[k] == 0).all().item() and (stas[k] == 0).all().item())
+        # every build is timed on one and the same region (filled: FILL rewrites the same bytes),
+        # so that where a buffer lies in HBM is no difference between builds (a clone per build
+        # made identical kernels differ by up to 5 %)
+        regt = regs["in_tree"]
         res = {(k, md): [] for k in libs for md in (1, 0)}
         for _ in range(rounds):
             for k in libs:
                 for md in (1, 0):
                     for _ in range(3):
-                        call(k, md)
+                        call(k, md, regt)
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record(st)
                     for _ in range(20):
-                        call(k, md)
+                        call(k, md, regt)
                     e1.record(st)
                     torch.cuda.synchronize()
                     res[(k, md)].append(e0.elapsed_time(e1) / 20)
