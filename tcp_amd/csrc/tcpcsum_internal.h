@@ -86,17 +86,11 @@
 #ifndef TCPCSUM_LB_HEAD
 #define TCPCSUM_LB_HEAD 1
 #endif
-//   TCPCSUM_LB_SPAN          the balanced wire kernel's span path for tiles of 4-B aligned
-//                            packets in address order: bit 0 VERIFY, bit 1 FILL, bit 2 the next
-//                            round's loads issued before a round is summed; 0: none
-#ifndef TCPCSUM_LB_SPAN
-#define TCPCSUM_LB_SPAN 0
-#endif
 #if !TCPCSUM_MEASUREMENT_BUILD && \
     (TCPCSUM_TUNING_VARIANTS != 0 || TCPCSUM_TX_KNOCKOUT != 0 || TCPCSUM_WIRE_WAVES != 1 || TCPCSUM_TX_WAVES != 1 || \
      TCPCSUM_LINE_CPOL != 17 || TCPCSUM_LOAD_CPOL != -1 || TCPCSUM_XCD_REMAP != 1 || TCPCSUM_XCD_CHUNK != 0 || \
      TCPCSUM_UNIFORM_WPB != 4 || TCPCSUM_DESC_LB_WAVES != 1 || TCPCSUM_SS_LOAD != 2 || TCPCSUM_LB_VARIANT != 0 || \
-     TCPCSUM_LB_HEAD != 1 || TCPCSUM_LB_SPAN != 0)
+     TCPCSUM_LB_HEAD != 1)
 #error "tuning / knock-out / waves knobs are for measurement builds only (-DTCPCSUM_MEASUREMENT_BUILD=1), never a product library"
 #endif
 // Environment variables a context reads at creation (tcpcsum_build_info "runtime_knobs"):

@@ -1530,7 +1530,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(wire_waves(
 // summed by lb_sums — FILL then subtracts the check word (what zeroing it
 // does). The IPv4 header checksum (IPHDR) is summed per lane from the
 // header dwords: relative dwords, so its u16 halves are the reference's words.
-template <int C, bool PL, int HP>
+template <int C, bool PL, bool HD>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TCPCSUM_DESC_LB_WAVES, 8))) void k_ipv4_lb(uint8_t* __restrict__ pkts, const uint64_t* __restrict__ off,
                                                  const uint32_t* __restrict__ plen,
                                                  uint64_t n, uint32_t cap, uint64_t limit, int mode,
@@ -1729,151 +1729,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TCPCSUM_DES
         if (out) out[i] = c;
         if (status) status[i] = (uint8_t)st;
     };
-    // The span path (HP == 2): tiles of 4-B aligned packets laid out in address order. The
-    // tile's bytes from its first packet's 16-B chunk on are swept as one run of chunks whose
-    // addresses need only that first offset, so the first round's loads go out beside the header
-    // loads instead of after them; a chunk's owner is the last packet starting at or before it
-    // (the packets' start chunks, from the offsets alone), and its dwords count for their packet
-    // when inside that packet's TCP bytes. Kept only when the packets are in increasing order,
-    // each at least 16 B past the one before and not overlapping it, and the run holds at most
-    // 64 B per packet that are not packet bytes; otherwise the tile takes process() and the
-    // first round's loads are dropped.
-    auto process_span = [&](uint64_t t, const Off& f) {
-        const uint64_t i = t * spw + (uint64_t)lane;
-        const bool live = (uint32_t)lane < spw && i < n;
-        uint32_t D[6];
-        load_hdr(t, f, D);
-        const uintptr_t ipa = (uintptr_t)(pkts + f.o);
-        const uint64_t a0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ipa, 0) |
-                             ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(ipa >> 32), 0) << 32)) &
-                            ~(uint64_t)15u;
-        const uint64_t rend = (uint64_t)(uintptr_t)(pkts + limit);
-        const uint64_t lim = rend > a0 ? rend - a0 : 0u;   // readable bytes from a0
-        constexpr uint32_t STEP = 64u * C;
-        u32x4 va[C];
-#pragma unroll
-        for (int k = 0; k < C; ++k) {   // a chunk holding a readable byte never crosses a page
-            const uint64_t c = (uint64_t)(64u * k + lane) * 16u;
-            va[k] = ld16(zsel(c < lim, reinterpret_cast<const uint8_t*>(a0 + c)));
-        }
-        uint32_t room;
-        const bool hdr = room_of(t, f, room);
-        const uint32_t h0 = D[0], h8 = D[2], sa = D[3], da = D[4];   // 4-B aligned: no shift
-        const uint32_t ver = (h0 >> 4) & 15u, ihl = h0 & 15u;
-        const uint32_t tot = ((h0 >> 8) & 0xff00u) | (h0 >> 24);
-        const uint32_t proto = (h8 >> 8) & 0xffu;
-        const bool ok = hdr && ver == 4u && proto == 6u && ihl >= 5u && tot >= ihl * 4u + 20u && tot <= cap &&
-                        f.o + tot <= limit;
-        const uint32_t th = ihl * 4u;
-        const uint64_t d = (uint64_t)ipa - a0;
-        const uint32_t rel = (uint32_t)d;
-        const uint32_t tcpr = ok ? rel + th : rel, endr = ok ? rel + tot : rel;
-        const uint32_t rn = bperm(rel, (uint32_t)lane + 1u);   // lane 63 reads lane 0: unused
-        const bool nxt = (uint32_t)lane + 1u < spw && i + 1u < n;
-        const bool bad = live && (d >= (1ull << 30) || (nxt && (rn < rel + 16u || endr > rn)));
-        const uint64_t okm = __ballot(live && ok);
-        const uint32_t sum_tot = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_incl(live && ok ? tot : 0u), 63);
-        const uint32_t Tend = okm ? (uint32_t)__builtin_amdgcn_readlane((int)endr, 63 - __builtin_clzll(okm)) : 0u;
-        if (__ballot(bad) != 0 || Tend > sum_tot + 64u * spw) {
-            process(t, f, D);
-            return;
-        }
-        const uint32_t T = (Tend + 15u) >> 4;   // chunks of the run
-        const uint32_t P = rel >> 4;            // the packet's first chunk
-        const uint32_t nj = live ? 1u : 0u;
-        // what a chunk's owner o tells about packet o - 1, whose last bytes may share o's first
-        // chunk: the gap from its end to o's start and the distance from its TCP start, both
-        // capped at 16 (lane 0: the packet before is another tile's, none of its bytes count)
-        const uint32_t pe = bperm(endr, (uint32_t)lane - 1u), pt = bperm(tcpr, (uint32_t)lane - 1u);
-        const uint32_t gap = lane == 0 ? 16u : (rel - pe < 16u ? rel - pe : 16u);
-        const uint32_t tcpd = lane == 0 ? 0u : (rel - pt < 16u ? rel - pt : 16u);
-        const uint32_t pack = (tcpr - rel) | ((endr - rel) << 6) | (gap << 22) | (tcpd << 27);
-        uint64_t* accW = acc[wv][0];
-        accW[lane] = 0;
-        uint32_t carry = 0;
-        auto consume = [&](const u32x4 (&v)[C], uint32_t R) {
-            uint32_t w[C], sr[C], own[C];
-            bool end[C];
-#pragma unroll
-            for (int k = 0; k < C; ++k) {
-                const uint32_t W0 = R + 64u * k;
-                const uint32_t g = W0 + lane;
-                const uint32_t o = lb_owner_loop(W0, P, nj, lane, carry);
-                const uint32_t ro = bperm(rel, o), pk = bperm(pack, o);
-                const uint32_t tcpo = ro + (pk & 63u), endo = ro + ((pk >> 6) & 0xffffu);
-                const uint32_t gapo = (pk >> 22) & 31u, tcpdo = pk >> 27;
-                const uint32_t x[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
-                uint32_t wo = 0, wp = 0;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const uint32_t crel = g * 16u + 4u * (uint32_t)j;
-                    const bool mine = crel >= tcpo && crel < endo;
-                    const uint32_t dd = ro - crel;   // bytes to o's start (crel < ro)
-                    const bool prev = crel < ro && dd > gapo && dd <= tcpdo;
-                    const uint32_t keep = mine ? endo - crel : dd - gapo;
-                    const uint32_t msk = keep >= 4u ? 0xffffffffu : (1u << (8u * keep)) - 1u;
-                    wo = sad16(mine ? x[j] & msk : 0u, wo);
-                    wp = sad16(prev ? x[j] & msk : 0u, wp);
-                }
-                if (wp) atomicAdd(reinterpret_cast<unsigned long long*>(accW + o - 1u), (unsigned long long)wp);
-                w[k] = wo;
-                own[k] = o;
-                const uint32_t on = bperm(o, (uint32_t)lane + 1u);
-                end[k] = g < T && (lane == 63 || g + 1u == T || on != o);
-                sr[k] = (ro >> 4) > W0 ? (ro >> 4) - W0 : 0u;   // the run's first lane in this window
-            }
-            wave_scan_incl_n<C>(w);
-#pragma unroll
-            for (int k = 0; k < C; ++k) {
-                const uint32_t Xp = bperm(w[k], sr[k] ? sr[k] - 1u : 0u);
-                if (end[k])
-                    atomicAdd(reinterpret_cast<unsigned long long*>(accW + own[k]),
-                              (unsigned long long)(w[k] - (sr[k] ? Xp : 0u)));
-            }
-        };
-        auto load_round = [&](u32x4 (&v)[C], uint32_t R) {
-#pragma unroll
-            for (int k = 0; k < C; ++k) {
-                const uint32_t g = R + 64u * k + lane;
-                v[k] = ld16(zsel(g < T, reinterpret_cast<const uint8_t*>(a0 + (uint64_t)g * 16u)));
-            }
-        };
-        if constexpr ((TCPCSUM_LB_SPAN & 4) != 0) {   // the next round's loads out before this one is summed
-            for (uint32_t R = 0; R < T; R += STEP) {
-                u32x4 vb[C];
-                if (R + STEP < T) load_round(vb, R + STEP);
-                consume(va, R);
-#pragma unroll
-                for (int k = 0; k < C; ++k) va[k] = vb[k];
-            }
-        } else {
-            for (uint32_t R = 0; R < T; R += STEP) {
-                if (R) load_round(va, R);
-                consume(va, R);
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-        if (!live) return;
-        if (!ok) {
-            if (out) out[i] = 0;
-            if (status) status[i] = TCPCSUM_PKT_SKIPPED;
-            return;
-        }
-        uint8_t* tcp = pkts + f.o + th;
-        const uint32_t len = tot - th;
-        const uint32_t len_be = ((len & 0xffu) << 8) | ((len >> 8) & 0xffu);   // htons
-        // context.c:104-119 closed form
-        const uint64_t ps = (sa & 0xffffu) + (sa >> 16) + (da & 0xffffu) + (da >> 16) + 0x0600u + len_be;
-        uint64_t S = ps + accW[lane];
-        const uint32_t cw = (uint32_t)ldg<uint8_t>(tcp + 16) | ((uint32_t)ldg<uint8_t>(tcp + 17) << 8);
-        if (!verify) S -= cw;   // FILL sums with the check as zero (context.c:182)
-        const uint16_t c = fold_ref(S);
-        uint32_t st = TCPCSUM_PKT_OK;
-        if (verify && c != 0 && cw == (uint32_t)(uint16_t)~fold_ref(ps)) st |= TCPCSUM_PKT_CSUM_PARTIAL;
-        if (!verify) store_u16(tcp + 16, c);   // native u16 store, as context.c:208
-        if (out) out[i] = c;
-        if (status) status[i] = (uint8_t)st;
-    };
+    // Measured and dropped: a span path sweeping a packed tile as one run of chunks (owners from
+    // the offsets alone, the first round's loads issued beside the header loads): parity-exact
+    // but flush mix VERIFY 0.119 ms against 0.078, 2M packed 576 B 0.287 against 0.190 — per-dword
+    // owner masks and one wave per SIMD less cost more than the latency it hid (commit 976945f,
+    // profiles/r06_lb_span_ab.jsonl).
     // block order: XCD order measured 1 % slower on 2M packed 576-B packets
     // (profiles/r05_xcd_kernels_ab.jsonl)
     uint64_t t = (uint64_t)blockIdx.x * 4u + wv;
@@ -1883,15 +1743,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TCPCSUM_DES
             const uint64_t i = t * spw + (uint64_t)lane;
             const bool live = (uint32_t)lane < spw && i < n;
             const uintptr_t ipa = PL ? (uintptr_t)pkts + f.o : (uintptr_t)(pkts + f.o);
-            if (HP == 1 && __ballot(live && (ipa & 3u) != 0) == 0) {
+            if (HD && __ballot(live && (ipa & 3u) != 0) == 0) {
                 process_head(t, f);
                 continue;
-            }
-            if constexpr (HP == 2 && !PL) {
-                if (__ballot(live && (ipa & 3u) != 0) == 0) {
-                    process_span(t, f);
-                    continue;
-                }
             }
             uint32_t D[6];
             load_hdr(t, f, D);
@@ -2898,35 +2752,18 @@ void launch_ipv4(uint8_t* pkts, const uint64_t* off, const uint32_t* plen, uint6
         // compiler spills) and VERIFY ran slower with it (flush mix VERIFY 0.0851 vs 0.078 ms),
         // FILL faster (flush mix 0.0928 vs 0.0962, 2M packed 576-B 0.254 vs 0.290;
         // profiles/r06_lb_head_ab.jsonl)
-        // the span path (TCPCSUM_LB_SPAN bit 0: VERIFY, bit 1: FILL; offsets only) likewise
-        const bool ver = (mode & TCPCSUM_IPV4_VERIFY) != 0, iph = (mode & TCPCSUM_IPV4_IPHDR) != 0;
-        const int hp = iph ? 0
-                       : (!plen && (TCPCSUM_LB_SPAN & (ver ? 1 : 2))) ? 2
-                       : (TCPCSUM_LB_HEAD == 2 || (TCPCSUM_LB_HEAD == 1 && !ver)) ? 1
-                                                                                   : 0;
-#define TCPCSUM_LB_WIRE(C_, PL_, HP_)                                                                          \
-    hipLaunchKernelGGL((k_ipv4_lb<C_, PL_, HP_>), grid, dim3(256), 0, s, pkts, off, plen, n, cap, limit, mode, out, \
+        const bool hd = !(mode & TCPCSUM_IPV4_IPHDR) &&
+                        (TCPCSUM_LB_HEAD == 2 || (TCPCSUM_LB_HEAD == 1 && !(mode & TCPCSUM_IPV4_VERIFY)));
+#define TCPCSUM_LB_WIRE(C_, PL_, HD_)                                                                          \
+    hipLaunchKernelGGL((k_ipv4_lb<C_, PL_, HD_>), grid, dim3(256), 0, s, pkts, off, plen, n, cap, limit, mode, out, \
                        status, ipout, spw)
-#if TCPCSUM_LB_SPAN
-#define TCPCSUM_LB_WIRE_SPAN(C_) TCPCSUM_LB_WIRE(C_, false, 2)
-#else
-#define TCPCSUM_LB_WIRE_SPAN(C_) TCPCSUM_LB_WIRE(C_, false, 0)
-#endif
-#define TCPCSUM_LB_WIRE_HP(C_, PL_)                 \
-    do {                                            \
-        if (hp == 1) TCPCSUM_LB_WIRE(C_, PL_, 1);   \
-        else if (hp == 2) TCPCSUM_LB_WIRE_SPAN(C_); \
-        else TCPCSUM_LB_WIRE(C_, PL_, 0);           \
-    } while (0)
         if (sh == 8) {
-            if (plen) TCPCSUM_LB_WIRE_HP(4, true);
-            else TCPCSUM_LB_WIRE_HP(4, false);
+            if (plen) { if (hd) TCPCSUM_LB_WIRE(4, true, true); else TCPCSUM_LB_WIRE(4, true, false); }
+            else { if (hd) TCPCSUM_LB_WIRE(4, false, true); else TCPCSUM_LB_WIRE(4, false, false); }
         } else {
-            if (plen) TCPCSUM_LB_WIRE_HP(8, true);
-            else TCPCSUM_LB_WIRE_HP(8, false);
+            if (plen) { if (hd) TCPCSUM_LB_WIRE(8, true, true); else TCPCSUM_LB_WIRE(8, true, false); }
+            else { if (hd) TCPCSUM_LB_WIRE(8, false, true); else TCPCSUM_LB_WIRE(8, false, false); }
         }
-#undef TCPCSUM_LB_WIRE_HP
-#undef TCPCSUM_LB_WIRE_SPAN
 #undef TCPCSUM_LB_WIRE
         return;
     }

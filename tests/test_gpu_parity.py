@@ -642,6 +642,53 @@ def test_ipv4_balanced_head_path(dev, shape, align):
             region = ref   # VERIFY runs over the filled packets
 
 
+@pytest.mark.parametrize("layout", ["packed4", "slots1536", "sparse", "shuffled", "repeated", "tiny_hulls"])
+@pytest.mark.parametrize("shape", [8, 9])
+def test_ipv4_balanced_layouts(dev, shape, layout):
+    """Balanced wire kernel over offset layouts a tile may see: packed 4-B aligned, MTU slots,
+    sparse 32 KiB slots, shuffled order, every packet listed twice (VERIFY only) and packets
+    whose offsets lie closer than 16 B (malformed, then valid ones in the same tile). Tiles in
+    address order, non-overlapping and dense may be swept as one run (the span path); every
+    other layout must give the same results through the per-packet sweep."""
+    import tcp_amd
+    from tests.packets import build_batch
+    rng = np.random.default_rng(77 + shape)
+    n = 700
+    if layout == "packed4":
+        region, off, _ = build_batch(rng, n, malformed=True, align=4, control_every=3)
+    elif layout == "slots1536":
+        region, off, _ = build_batch(rng, n, slot=1536, malformed=True)
+    elif layout == "sparse":
+        region, off, _ = build_batch(rng, 96, slot=32768, malformed=True)
+    else:
+        region, off, _ = build_batch(rng, n, malformed=True, align=16, control_every=2)
+        if layout == "shuffled":
+            off = off[rng.permutation(off.size)]
+        elif layout == "repeated":
+            off = np.repeat(off, 2)
+        elif layout == "tiny_hulls":   # offsets 4 and 8 B into a packet: headers that fail to parse
+            extra = off[::5] + np.uint64(8)
+            off = np.sort(np.concatenate([off, extra]))
+    modes = [tcp_amd.IPV4_VERIFY] if layout in ("repeated", "tiny_hulls") else [tcp_amd.IPV4_FILL, tcp_amd.IPV4_VERIFY]
+    for mode in modes:
+        ref = region.copy()
+        want_out, want_st = oracle.ipv4_batch(ref, off, 32768, mode)
+        for un in (1, 2):
+            tcp_amd.set_tuning(0, un, shape, 0)
+            try:
+                dreg = to_dev(region, dev)
+                out = torch.empty(off.size, dtype=torch.int16, device=dev)
+                st = torch.empty(off.size, dtype=torch.uint8, device=dev)
+                tcp_amd.ipv4_batch(dreg, to_dev(off.view(np.int64), dev), off.size, 32768, mode, out, st)
+            finally:
+                tcp_amd.set_tuning(0, 0, -1, 0)
+            assert np.array_equal(host(st), want_st), (mode, un)
+            assert np.array_equal(u16(out), want_out), (mode, un)
+            assert np.array_equal(host(dreg), ref), (mode, un)
+        if mode == tcp_amd.IPV4_FILL:
+            region = ref
+
+
 @pytest.mark.parametrize("shape", range(9))
 def test_desc_forced_shapes(dev, shape):
     """Every ragged lane-group shape (tcpcsum.h: ragged 0..6, balanced 7..8) and tile depth is exact
