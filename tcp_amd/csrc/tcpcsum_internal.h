@@ -86,11 +86,16 @@
 #ifndef TCPCSUM_LB_HEAD
 #define TCPCSUM_LB_HEAD 1
 #endif
+//   TCPCSUM_LB_HDR_X4        1: the balanced wire kernel reads 4-B aligned tiles' headers with one
+//                            dwordx4 and one dword load per packet; 0: five dword loads
+#ifndef TCPCSUM_LB_HDR_X4
+#define TCPCSUM_LB_HDR_X4 1
+#endif
 #if !TCPCSUM_MEASUREMENT_BUILD && \
     (TCPCSUM_TUNING_VARIANTS != 0 || TCPCSUM_TX_KNOCKOUT != 0 || TCPCSUM_WIRE_WAVES != 1 || TCPCSUM_TX_WAVES != 1 || \
      TCPCSUM_LINE_CPOL != 17 || TCPCSUM_LOAD_CPOL != -1 || TCPCSUM_XCD_REMAP != 1 || TCPCSUM_XCD_CHUNK != 0 || \
      TCPCSUM_UNIFORM_WPB != 4 || TCPCSUM_DESC_LB_WAVES != 1 || TCPCSUM_SS_LOAD != 2 || TCPCSUM_LB_VARIANT != 0 || \
-     TCPCSUM_LB_HEAD != 1)
+     TCPCSUM_LB_HEAD != 1 || TCPCSUM_LB_HDR_X4 != 1)
 #error "tuning / knock-out / waves knobs are for measurement builds only (-DTCPCSUM_MEASUREMENT_BUILD=1), never a product library"
 #endif
 // Environment variables a context reads at creation (tcpcsum_build_info "runtime_knobs"):

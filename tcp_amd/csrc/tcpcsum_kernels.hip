@@ -41,6 +41,7 @@
 namespace tcpcsum {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));   // 4-B aligned dwordx4
 
 enum : int { M16 = 0, M4 = 1, M1 = 2 };
 
@@ -1581,6 +1582,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TCPCSUM_DES
         const bool hdr = room_of(t, f, room);
         const uint8_t* ip = PL ? reinterpret_cast<const uint8_t*>((uintptr_t)pkts + f.o) : pkts + f.o;
         const uint32_t sh = (uint32_t)((uintptr_t)ip & 3u);
+        if (TCPCSUM_LB_HDR_X4 && __ballot(hdr && sh != 0) == 0) {
+            // 4-B aligned headers: one dwordx4 and one dword load (the 20 bytes are readable)
+            const uint8_t* hp = zsel(hdr, ip);
+            const u32x4a4 q = *(gptr<const u32x4a4>)(hp);
+            D[0] = q.x;
+            D[1] = q.y;
+            D[2] = q.z;
+            D[3] = q.w;
+            D[4] = ldg<uint32_t>(hp + 16);
+            D[5] = 0;
+            return;
+        }
 #pragma unroll
         for (int k = 0; k < 6; ++k) D[k] = ldg<uint32_t>(zsel(hdr && (k < 5 || sh != 0), ip - sh + 4 * k));
     };
