@@ -127,7 +127,8 @@ const char* tcpcsum_build_info(void) {
         ", \"TCPCSUM_DESC_LB_WAVES\": " TCPCSUM_STR(TCPCSUM_DESC_LB_WAVES)
         ", \"TCPCSUM_SS_LOAD\": " TCPCSUM_STR(TCPCSUM_SS_LOAD)
         ", \"TCPCSUM_LB_VARIANT\": " TCPCSUM_STR(TCPCSUM_LB_VARIANT)
-        ", \"TCPCSUM_LB_HEAD\": " TCPCSUM_STR(TCPCSUM_LB_HEAD) "}"
+        ", \"TCPCSUM_LB_HEAD\": " TCPCSUM_STR(TCPCSUM_LB_HEAD)
+        ", \"TCPCSUM_LB_HDR_X4\": " TCPCSUM_STR(TCPCSUM_LB_HDR_X4) "}"
         ", \"runtime_knobs\": [" TCPCSUM_RUNTIME_KNOBS_JSON "]}";
     return info;
 }

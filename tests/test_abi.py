@@ -71,7 +71,8 @@ def test_library_is_a_product_build_of_this_tree():
                              "TCPCSUM_WIRE_WAVES": 1, "TCPCSUM_TX_WAVES": 1, "TCPCSUM_LINE_CPOL": 17,
                              "TCPCSUM_LOAD_CPOL": -1, "TCPCSUM_XCD_REMAP": 1,
                              "TCPCSUM_XCD_CHUNK": 0, "TCPCSUM_UNIFORM_WPB": 4,
-                             "TCPCSUM_DESC_LB_WAVES": 1, "TCPCSUM_SS_LOAD": 2, "TCPCSUM_LB_VARIANT": 0, "TCPCSUM_LB_HEAD": 1}
+                             "TCPCSUM_DESC_LB_WAVES": 1, "TCPCSUM_SS_LOAD": 2, "TCPCSUM_LB_VARIANT": 0, "TCPCSUM_LB_HEAD": 1,
+                             "TCPCSUM_LB_HDR_X4": 1}
     # the only environment a product context reads
     assert info["runtime_knobs"] == ["TCPCSUM_HOST_THREADS", "TCPCSUM_HOST_NUMA", "TCPCSUM_HOST_SPIN_US",
                                      "LOCAL_WORLD_SIZE"]
