@@ -1664,9 +1664,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TCPCSUM_DES
     // packet's first 64 bytes from its 16-B aligned start come in with four 16-B loads — the
     // header fields, the first TCP bytes (a 44-B control segment entirely) and the FILL's
     // check word, all from registers — and only the rest of each segment, from the next 16-B
-    // boundary past those 64 bytes, is swept. The sweep then never re-reads the header's
-    // line (the separate header loads made the flush mix read 1.125 x its region, PMC
-    // FETCH_SIZE, profiles/r06_wire_mix_pmc.json) and a control segment never enters it.
+    // boundary past those 64 bytes, is swept: a control segment never enters the sweep and
+    // the check word needs no load of its own. Taken by FILL only (its own instantiation,
+    // see the launcher): 2M packed 576-B FILL -12.5 %, flush mix FILL -4 %.
     auto process_head = [&](uint64_t t, const Off& f) {
         const uint64_t i = t * spw + (uint64_t)lane;
         const bool live = (uint32_t)lane < spw && i < n;
