@@ -81,8 +81,8 @@
 #endif
 //   TCPCSUM_LB_HEAD          1: the balanced wire kernel's FILL (without IPHDR) takes 4-B aligned
 //                            packets' first 64 bytes in registers and sweeps only the rest (the
-//                            product's); 2: VERIFY too; 3: VERIFY with the first 32 bytes; 0:
-//                            neither (header read apart, every TCP byte swept)
+//                            product's); 2: VERIFY too; 0: neither (header read apart, every TCP
+//                            byte swept)
 #ifndef TCPCSUM_LB_HEAD
 #define TCPCSUM_LB_HEAD 1
 #endif

@@ -1531,7 +1531,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(wire_waves(
 // summed by lb_sums — FILL then subtracts the check word (what zeroing it
 // does). The IPv4 header checksum (IPHDR) is summed per lane from the
 // header dwords: relative dwords, so its u16 halves are the reference's words.
-template <int C, bool PL, int HD>
+template <int C, bool PL, bool HD>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TCPCSUM_DESC_LB_WAVES, 8))) void k_ipv4_lb(uint8_t* __restrict__ pkts, const uint64_t* __restrict__ off,
                                                  const uint32_t* __restrict__ plen,
                                                  uint64_t n, uint32_t cap, uint64_t limit, int mode,
@@ -1667,9 +1667,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TCPCSUM_DES
     // boundary past those 64 bytes, is swept: a control segment never enters the sweep and
     // the check word needs no load of its own. Taken by FILL only (its own instantiation,
     // see the launcher): 2M packed 576-B FILL -12.5 %, flush mix FILL -4 %.
-    // HD: the 16-B loads per packet (4: 64 bytes, FILL; 2: 32 bytes, the header and the first
-    // TCP bytes, measurement builds' VERIFY)
-    constexpr int NH = HD > 0 ? HD : 1;
     auto process_head = [&](uint64_t t, const Off& f) {
         const uint64_t i = t * spw + (uint64_t)lane;
         const bool live = (uint32_t)lane < spw && i < n;
@@ -1680,15 +1677,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TCPCSUM_DES
         uint8_t* ip = PL ? reinterpret_cast<uint8_t*>((uintptr_t)pkts + o) : pkts + o;
         const uint32_t sh = (uint32_t)((uintptr_t)ip & 15u);   // 0, 4, 8 or 12
         const uint8_t* al = ip - sh;
-        u32x4 H[NH];
+        u32x4 H[4];
 #pragma unroll
-        for (int k = 0; k < NH; ++k)   // a 16-B chunk holding a readable byte never crosses a page
+        for (int k = 0; k < 4; ++k)   // a 16-B chunk holding a readable byte never crosses a page
             H[k] = ldg<u32x4>(zsel(hdr && 16u * k < sh + readable, al + 16 * k));
-        // dword j (0..4 NH - 1) of the loaded bytes: register selects only
+        // dword j (0..15) of the 64 loaded bytes: register selects only
         auto dw = [&](uint32_t j) {
-            u32x4 c = H[0];
-#pragma unroll
-            for (int k = 1; k < NH; ++k) c = j >= 4u * k ? H[k] : c;
+            const u32x4 c = j < 4u ? H[0] : j < 8u ? H[1] : j < 12u ? H[2] : H[3];
             const uint32_t r = j & 3u;
             return r == 0u ? c.x : r == 1u ? c.y : r == 2u ? c.z : c.w;
         };
@@ -1704,14 +1699,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TCPCSUM_DES
         uint8_t* tcp = ip + th;
         // the TCP bytes among the 64 loaded: relative dwords [th / 4, in_regs / 4), the last
         // one cut at tot
-        const uint32_t in_regs = 16u * NH - sh;   // bytes of the packet in H
+        const uint32_t in_regs = 64u - sh;   // bytes of the packet in H
         const uint32_t head_end = ok ? (tot < in_regs ? tot : in_regs) : 0u;
         uint32_t wh = 0;
 #pragma unroll
-        for (int j = 0; j < 4 * NH; ++j) {
+        for (int j = 0; j < 16; ++j) {
             const uint32_t rel = 4u * (uint32_t)j - sh;   // wraps for dwords before the packet
-            const u32x4 hk = H[j >> 2];
-            const uint32_t d = (j & 3) == 0 ? hk.x : (j & 3) == 1 ? hk.y : (j & 3) == 2 ? hk.z : hk.w;
+            const uint32_t d = j < 4 ? (j == 0 ? H[0].x : j == 1 ? H[0].y : j == 2 ? H[0].z : H[0].w)
+                             : j < 8 ? (j == 4 ? H[1].x : j == 5 ? H[1].y : j == 6 ? H[1].z : H[1].w)
+                             : j < 12 ? (j == 8 ? H[2].x : j == 9 ? H[2].y : j == 10 ? H[2].z : H[2].w)
+                                      : (j == 12 ? H[3].x : j == 13 ? H[3].y : j == 14 ? H[3].z : H[3].w);
             const uint32_t keep = head_end - rel;   // bytes of this dword before head_end
             const uint32_t m = keep >= 4u ? 0xffffffffu : (1u << (8u * keep)) - 1u;
             wh = sad16(rel >= th && rel < head_end ? d & m : 0u, wh);
@@ -1735,20 +1732,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TCPCSUM_DES
             if (status) status[i] = TCPCSUM_PKT_SKIPPED;
             return;
         }
-        auto load_cw = [&]() {
-            if (!cw_in) cw = (uint32_t)ldg<uint8_t>(tcp + 16) | ((uint32_t)ldg<uint8_t>(tcp + 17) << 8);
-        };
+        if (!cw_in) cw = (uint32_t)ldg<uint8_t>(tcp + 16) | ((uint32_t)ldg<uint8_t>(tcp + 17) << 8);
         uint64_t S = (uint64_t)ps + wh + acc[wv][0][lane];
-        if (!verify) {   // FILL sums with the check as zero (context.c:182)
-            load_cw();
-            S -= cw;
-        }
+        if (!verify) S -= cw;   // FILL sums with the check as zero (context.c:182)
         const uint16_t c = fold_ref(S);
         uint32_t st = TCPCSUM_PKT_OK;
-        if (verify && c != 0) {   // rare: was the check left as the bare pseudo-header sum?
-            load_cw();
-            if (cw == (uint32_t)(uint16_t)~fold_ref(ps)) st |= TCPCSUM_PKT_CSUM_PARTIAL;
-        }
+        if (verify && c != 0 && cw == (uint32_t)(uint16_t)~fold_ref(ps)) st |= TCPCSUM_PKT_CSUM_PARTIAL;
         if (!verify) store_u16(tcp + 16, c);   // native u16 store, as context.c:208
         if (out) out[i] = c;
         if (status) status[i] = (uint8_t)st;
@@ -1767,7 +1756,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TCPCSUM_DES
             const uint64_t i = t * spw + (uint64_t)lane;
             const bool live = (uint32_t)lane < spw && i < n;
             const uintptr_t ipa = PL ? (uintptr_t)pkts + f.o : (uintptr_t)(pkts + f.o);
-            if (HD > 0 && __ballot(live && (ipa & 3u) != 0) == 0) {
+            if (HD && __ballot(live && (ipa & 3u) != 0) == 0) {
                 process_head(t, f);
                 continue;
             }
@@ -2776,29 +2765,18 @@ void launch_ipv4(uint8_t* pkts, const uint64_t* off, const uint32_t* plen, uint6
         // compiler spills) and VERIFY ran slower with it (flush mix VERIFY 0.0851 vs 0.078 ms),
         // FILL faster (flush mix 0.0928 vs 0.0962, 2M packed 576-B 0.254 vs 0.290;
         // profiles/r06_lb_head_ab.jsonl)
-        const bool ver = (mode & TCPCSUM_IPV4_VERIFY) != 0;
-        // 4: 64 bytes in registers, 2: 32 bytes (TCPCSUM_LB_HEAD 3: VERIFY), 0: the header apart
-        const int hd = (mode & TCPCSUM_IPV4_IPHDR) ? 0
-                       : !ver ? (TCPCSUM_LB_HEAD >= 1 ? 4 : 0)
-                              : (TCPCSUM_LB_HEAD == 2 ? 4 : TCPCSUM_LB_HEAD == 3 ? 2 : 0);
+        const bool hd = !(mode & TCPCSUM_IPV4_IPHDR) &&
+                        (TCPCSUM_LB_HEAD == 2 || (TCPCSUM_LB_HEAD == 1 && !(mode & TCPCSUM_IPV4_VERIFY)));
 #define TCPCSUM_LB_WIRE(C_, PL_, HD_)                                                                          \
     hipLaunchKernelGGL((k_ipv4_lb<C_, PL_, HD_>), grid, dim3(256), 0, s, pkts, off, plen, n, cap, limit, mode, out, \
                        status, ipout, spw)
-#if TCPCSUM_LB_HEAD == 3
-#define TCPCSUM_LB_WIRE_HD(C_, PL_) \
-    do { if (hd == 4) TCPCSUM_LB_WIRE(C_, PL_, 4); else if (hd == 2) TCPCSUM_LB_WIRE(C_, PL_, 2); else TCPCSUM_LB_WIRE(C_, PL_, 0); } while (0)
-#else
-#define TCPCSUM_LB_WIRE_HD(C_, PL_) \
-    do { if (hd) TCPCSUM_LB_WIRE(C_, PL_, 4); else TCPCSUM_LB_WIRE(C_, PL_, 0); } while (0)
-#endif
         if (sh == 8) {
-            if (plen) TCPCSUM_LB_WIRE_HD(4, true);
-            else TCPCSUM_LB_WIRE_HD(4, false);
+            if (plen) { if (hd) TCPCSUM_LB_WIRE(4, true, true); else TCPCSUM_LB_WIRE(4, true, false); }
+            else { if (hd) TCPCSUM_LB_WIRE(4, false, true); else TCPCSUM_LB_WIRE(4, false, false); }
         } else {
-            if (plen) TCPCSUM_LB_WIRE_HD(8, true);
-            else TCPCSUM_LB_WIRE_HD(8, false);
+            if (plen) { if (hd) TCPCSUM_LB_WIRE(8, true, true); else TCPCSUM_LB_WIRE(8, true, false); }
+            else { if (hd) TCPCSUM_LB_WIRE(8, false, true); else TCPCSUM_LB_WIRE(8, false, false); }
         }
-#undef TCPCSUM_LB_WIRE_HD
 #undef TCPCSUM_LB_WIRE
         return;
     }
